@@ -1,0 +1,18 @@
+// Common macros for libcordagpu device code.  Everything in the *.h arithmetic
+// headers is written as CG_HD so the exact device algorithm can also be compiled
+// for the host (tests/native/) and checked against the CPU oracle there.
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define CG_HD __host__ __device__ __forceinline__
+#define CG_DEV __device__ __forceinline__
+#define CG_UNROLL _Pragma("unroll")
+#define CG_NOUNROLL _Pragma("unroll 1")
+#else
+#define CG_HD static inline
+#define CG_DEV static inline
+#define CG_UNROLL _Pragma("GCC unroll 16")
+#define CG_NOUNROLL
+#endif

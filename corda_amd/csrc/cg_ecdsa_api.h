@@ -1,0 +1,34 @@
+// Host-side interface of the ECDSA (secp256k1 / secp256r1) kernels (K2-K4).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace cg {
+
+struct EcdsaConsts;  // device-resident curve constants + generator tables
+
+// Device-resident SoA subset of one curve.
+struct EcdsaBatch {
+  uint32_t n = 0;
+  int scheme = 0;
+  uint32_t* index = nullptr;    // positions in the full batch
+  uint32_t* q = nullptr;        // [16][n] X||Y words (little-endian limbs)
+  uint8_t* der = nullptr;       // [n][kDerStride] raw signature bytes
+  uint32_t* der_len = nullptr;  // [n]
+  uint64_t* msg_off = nullptr;  // [n]
+  uint32_t* msg_len = nullptr;  // [n]
+};
+
+constexpr uint32_t kDerStride = 80;  // bytes kept per DER signature on the device
+
+hipError_t ecdsa_consts_create(EcdsaConsts** out);
+void ecdsa_consts_free(EcdsaConsts* c);
+hipError_t ecdsa_batch_stage(EcdsaBatch& b, int scheme, const uint32_t* host_index, uint32_t n,
+                             const uint8_t* pk_raw_dev, size_t pk_stride, const uint8_t* sig_raw_dev,
+                             size_t sig_stride, const uint32_t* sig_len_dev, const uint64_t* msg_off_all_dev,
+                             const uint32_t* msg_len_all_dev, hipStream_t s);
+hipError_t ecdsa_batch_verify(const EcdsaBatch& b, const EcdsaConsts* c, const uint8_t* arena, uint32_t mode,
+                              uint8_t* verdict, hipStream_t s);
+void ecdsa_batch_free(EcdsaBatch& b);
+
+}  // namespace cg

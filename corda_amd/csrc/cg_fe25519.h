@@ -1,0 +1,241 @@
+// GF(2^255 - 19) arithmetic for the Ed25519 kernels (gfx950 VALU, no MFMA).
+//
+// Representation: 10 signed 32-bit limbs, radix 2^25.5 (limb i starts at bit
+// ceil(25.5 i); widths 26,25,26,...).  Products are accumulated in 64 bits, which
+// gfx950 issues as one full-rate v_mad_i64_i32 per limb product (measured
+// profiles/r01_isa_rates.json: mad_u64_u32 at the same rate as any VOP3 integer
+// op), so a multiply is 100 mads + ~55 carry ops and fe_add / fe_sub need no
+// carry at all.  Bounds follow the classic 25.5-bit analysis: reduced limbs are
+// |h| <= 1.01*2^25 (even) / 2^24 (odd); mul/sq inputs may be up to 1.65x the
+// 2^26 / 2^25 limb widths, i.e. any sum/difference of <= 3 reduced values.
+//
+// All functions are CG_HD so tests/native/ compiles the very same code for the
+// host and checks it against the oracle.
+#pragma once
+#include "cg_common.h"
+
+namespace cg {
+
+struct fe {
+  int32_t v[10];
+};
+
+CG_HD void fe_0(fe& h) {
+  CG_UNROLL for (int i = 0; i < 10; ++i) h.v[i] = 0;
+}
+CG_HD void fe_1(fe& h) {
+  fe_0(h);
+  h.v[0] = 1;
+}
+CG_HD void fe_add(fe& h, const fe& f, const fe& g) {
+  CG_UNROLL for (int i = 0; i < 10; ++i) h.v[i] = f.v[i] + g.v[i];
+}
+CG_HD void fe_sub(fe& h, const fe& f, const fe& g) {
+  CG_UNROLL for (int i = 0; i < 10; ++i) h.v[i] = f.v[i] - g.v[i];
+}
+CG_HD void fe_neg(fe& h, const fe& f) {
+  CG_UNROLL for (int i = 0; i < 10; ++i) h.v[i] = -f.v[i];
+}
+// h = c ? g : f   (c is 0/1; branch-free so divergent lanes cost nothing extra)
+CG_HD void fe_select(fe& h, const fe& f, const fe& g, uint32_t c) {
+  const int32_t m = -(int32_t)c;
+  CG_UNROLL for (int i = 0; i < 10; ++i) h.v[i] = f.v[i] ^ ((f.v[i] ^ g.v[i]) & m);
+}
+
+// Signed carry chain (round-to-nearest) on 64-bit column sums -> reduced limbs.
+CG_HD void fe_carry_wide(fe& h, int64_t t[10]) {
+  int64_t c;
+#define CG_C26(k)                      \
+  c = (t[k] + (1LL << 25)) >> 26;      \
+  t[(k) + 1] += c;                     \
+  t[k] -= c * (1LL << 26);
+#define CG_C25(k)                      \
+  c = (t[k] + (1LL << 24)) >> 25;      \
+  t[(k) + 1] += c;                     \
+  t[k] -= c * (1LL << 25);
+  CG_C26(0) CG_C26(4)
+  CG_C25(1) CG_C25(5)
+  CG_C26(2) CG_C26(6)
+  CG_C25(3) CG_C25(7)
+  CG_C26(4) CG_C26(8)
+  c = (t[9] + (1LL << 24)) >> 25;
+  t[0] += c * 19;
+  t[9] -= c * (1LL << 25);
+  CG_C26(0)
+#undef CG_C26
+#undef CG_C25
+  CG_UNROLL for (int i = 0; i < 10; ++i) h.v[i] = (int32_t)t[i];
+}
+
+// Same chain on 32-bit limbs (for values already within ~2^29 per limb).
+CG_HD void fe_reduce(fe& h) {
+  int32_t c;
+#define CG_C26(k)                      \
+  c = (h.v[k] + (1 << 25)) >> 26;      \
+  h.v[(k) + 1] += c;                   \
+  h.v[k] -= c * (1 << 26);
+#define CG_C25(k)                      \
+  c = (h.v[k] + (1 << 24)) >> 25;      \
+  h.v[(k) + 1] += c;                   \
+  h.v[k] -= c * (1 << 25);
+  CG_C26(0) CG_C26(4)
+  CG_C25(1) CG_C25(5)
+  CG_C26(2) CG_C26(6)
+  CG_C25(3) CG_C25(7)
+  CG_C26(4) CG_C26(8)
+  c = (h.v[9] + (1 << 24)) >> 25;
+  h.v[0] += c * 19;
+  h.v[9] -= c * (1 << 25);
+  CG_C26(0)
+#undef CG_C26
+#undef CG_C25
+}
+
+// h = f * g.  Column k collects f_i g_j for i+j = k (and 19 f_i g_j for
+// i+j = k+10); products of two odd limbs carry an extra factor 2 because the
+// odd limbs are 25 bits wide.
+CG_HD void fe_mul(fe& h, const fe& f, const fe& g) {
+  int32_t g19[10], f2[10];
+  CG_UNROLL for (int j = 0; j < 10; ++j) g19[j] = 19 * g.v[j];
+  CG_UNROLL for (int i = 0; i < 10; ++i) f2[i] = (i & 1) ? 2 * f.v[i] : f.v[i];
+  int64_t t[10];
+  CG_UNROLL for (int k = 0; k < 10; ++k) t[k] = 0;
+  CG_UNROLL for (int i = 0; i < 10; ++i) {
+    CG_UNROLL for (int j = 0; j < 10; ++j) {
+      const int k = i + j;
+      const int32_t a = (j & 1) ? f2[i] : f.v[i];
+      const int32_t b = (k >= 10) ? g19[j] : g.v[j];
+      t[k >= 10 ? k - 10 : k] += (int64_t)a * b;
+    }
+  }
+  fe_carry_wide(h, t);
+}
+
+// h = f^2 (DOUBLE ? 2 f^2 : f^2): 55 products using the symmetry f_i f_j = f_j f_i.
+template <bool DOUBLE>
+CG_HD void fe_sq_t(fe& h, const fe& f) {
+  int32_t f19[10];
+  CG_UNROLL for (int j = 0; j < 10; ++j) f19[j] = 19 * f.v[j];
+  int64_t t[10];
+  CG_UNROLL for (int k = 0; k < 10; ++k) t[k] = 0;
+  CG_UNROLL for (int i = 0; i < 10; ++i) {
+    CG_UNROLL for (int j = i; j < 10; ++j) {
+      const int k = i + j;
+      const int m = ((i == j) ? 1 : 2) * (((i & 1) && (j & 1)) ? 2 : 1);
+      const int32_t a = m * f.v[i];
+      const int32_t b = (k >= 10) ? f19[j] : f.v[j];
+      t[k >= 10 ? k - 10 : k] += (int64_t)a * b;
+    }
+  }
+  if (DOUBLE) {
+    CG_UNROLL for (int k = 0; k < 10; ++k) t[k] *= 2;
+  }
+  fe_carry_wide(h, t);
+}
+CG_HD void fe_sq(fe& h, const fe& f) { fe_sq_t<false>(h, f); }
+CG_HD void fe_sq2(fe& h, const fe& f) { fe_sq_t<true>(h, f); }
+
+CG_HD void fe_sqn(fe& h, const fe& f, int n) {
+  fe_sq(h, f);
+  CG_NOUNROLL for (int i = 1; i < n; ++i) fe_sq(h, h);
+}
+
+// 8 little-endian 32-bit words -> limbs.  Bit 255 is ignored and the value is NOT
+// reduced mod p (i2p GroupElement decode semantics).
+CG_HD void fe_frombytes(fe& h, const uint32_t w[8]) {
+  h.v[0] = (int32_t)(w[0] & 0x3ffffff);
+  h.v[1] = (int32_t)((w[0] >> 26 | w[1] << 6) & 0x1ffffff);
+  h.v[2] = (int32_t)((w[1] >> 19 | w[2] << 13) & 0x3ffffff);
+  h.v[3] = (int32_t)((w[2] >> 13 | w[3] << 19) & 0x1ffffff);
+  h.v[4] = (int32_t)((w[3] >> 6) & 0x3ffffff);
+  h.v[5] = (int32_t)(w[4] & 0x1ffffff);
+  h.v[6] = (int32_t)((w[4] >> 25 | w[5] << 7) & 0x3ffffff);
+  h.v[7] = (int32_t)((w[5] >> 19 | w[6] << 13) & 0x1ffffff);
+  h.v[8] = (int32_t)((w[6] >> 12 | w[7] << 20) & 0x3ffffff);
+  h.v[9] = (int32_t)((w[7] >> 6) & 0x1ffffff);
+}
+
+// Canonical little-endian encoding (value fully reduced mod p).
+CG_HD void fe_tobytes(uint32_t w[8], const fe& f) {
+  fe h = f;
+  fe_reduce(h);
+  int32_t q = (19 * h.v[9] + (1 << 24)) >> 25;
+  CG_UNROLL for (int i = 0; i < 10; ++i) q = (h.v[i] + q) >> ((i & 1) ? 25 : 26);
+  h.v[0] += 19 * q;
+  CG_UNROLL for (int i = 0; i < 9; ++i) {
+    const int sh = (i & 1) ? 25 : 26;
+    const int32_t c = h.v[i] >> sh;
+    h.v[i + 1] += c;
+    h.v[i] -= c * (1 << sh);
+  }
+  h.v[9] &= 0x1ffffff;
+  const uint32_t* u = (const uint32_t*)h.v;
+  w[0] = u[0] | u[1] << 26;
+  w[1] = u[1] >> 6 | u[2] << 19;
+  w[2] = u[2] >> 13 | u[3] << 13;
+  w[3] = u[3] >> 19 | u[4] << 6;
+  w[4] = u[5] | u[6] << 25;
+  w[5] = u[6] >> 7 | u[7] << 19;
+  w[6] = u[7] >> 13 | u[8] << 12;
+  w[7] = u[8] >> 20 | u[9] << 6;
+}
+
+CG_HD uint32_t fe_isnegative(const fe& f) {
+  uint32_t w[8];
+  fe_tobytes(w, f);
+  return w[0] & 1;
+}
+
+CG_HD uint32_t fe_iszero(const fe& f) {
+  uint32_t w[8];
+  fe_tobytes(w, f);
+  uint32_t a = 0;
+  CG_UNROLL for (int i = 0; i < 8; ++i) a |= w[i];
+  return a == 0;
+}
+
+// z^(2^250 - 1) and z^11 (shared prefix of the inversion / square-root chains).
+CG_HD void fe_pow2_250_1(fe& out, fe& z11, const fe& z) {
+  fe z2, z9, t, a, b;
+  fe_sq(z2, z);
+  fe_sqn(t, z2, 2);
+  fe_mul(z9, t, z);
+  fe_mul(z11, z9, z2);
+  fe_sq(t, z11);
+  fe_mul(a, t, z9);     // 2^5 - 1
+  fe_sqn(t, a, 5);
+  fe_mul(a, t, a);      // 2^10 - 1
+  fe_sqn(t, a, 10);
+  fe_mul(b, t, a);      // 2^20 - 1
+  fe_sqn(t, b, 20);
+  fe_mul(t, t, b);      // 2^40 - 1
+  fe_sqn(t, t, 10);
+  fe_mul(a, t, a);      // 2^50 - 1
+  fe_sqn(t, a, 50);
+  fe_mul(b, t, a);      // 2^100 - 1
+  fe_sqn(t, b, 100);
+  fe_mul(t, t, b);      // 2^200 - 1
+  fe_sqn(t, t, 50);
+  fe_mul(out, t, a);    // 2^250 - 1
+}
+
+CG_HD void fe_invert(fe& out, const fe& z) {
+  fe t, z11;
+  fe_pow2_250_1(t, z11, z);
+  fe_sqn(t, t, 5);
+  fe_mul(out, t, z11);  // z^(2^255 - 21)
+}
+
+CG_HD void fe_pow22523(fe& out, const fe& z) {
+  fe t, z11;
+  fe_pow2_250_1(t, z11, z);
+  fe_sqn(t, t, 2);
+  fe_mul(out, t, z);    // z^(2^252 - 3)
+}
+
+// Constants (limbs of the canonical values).
+#define CG_FE_D {{56195235, 13857412, 51736253, 6949390, 114729, 24766616, 60832955, 30306712, 48412415, 21499315}}
+#define CG_FE_D2 {{45281625, 27714825, 36363642, 13898781, 229458, 15978800, 54557047, 27058993, 29715967, 9444199}}
+#define CG_FE_SQRTM1 {{34513072, 25610706, 9377949, 3500415, 12389472, 33281959, 41962654, 31548777, 326685, 11406482}}
+
+}  // namespace cg

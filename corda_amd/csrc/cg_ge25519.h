@@ -1,0 +1,157 @@
+// Edwards25519 group operations (a = -1, extended coordinates) for the verify
+// kernels.  All formulas are the unified Hisil-Wong-Carter-Dawson ones, which are
+// complete on this curve (d is a non-square), so every decoded key — including
+// small-order and mixed-order points that i2p accepts — is handled
+// with exact group arithmetic, which is what makes the verdicts match i2p's
+// doubleScalarMultiplyVariableTime bit for bit.
+//
+// Representations (x = X/Z, y = Y/Z, xy = T/Z):
+//   p2      (X:Y:Z)              input of doubling
+//   p3      (X:Y:Z:T)            input of additions
+//   p1p1    x = X/Z, y = Y/T     output of dbl/add, 3 (to p2) or 4 (to p3) mults to convert
+//   cached  (Y+X, Y-X, Z, 2dT)   per-lane table entries of multiples of -A
+//   precomp (y+x, y-x, 2dxy)     affine, shared table of multiples of B
+#pragma once
+#include "cg_fe25519.h"
+
+namespace cg {
+
+struct ge_p2 { fe X, Y, Z; };
+struct ge_p3 { fe X, Y, Z, T; };
+struct ge_p1p1 { fe X, Y, Z, T; };
+struct ge_cached { fe YplusX, YminusX, Z, T2d; };
+struct ge_precomp { fe yplusx, yminusx, xy2d; };
+
+CG_HD void ge_p1p1_to_p2(ge_p2& r, const ge_p1p1& p) {
+  fe_mul(r.X, p.X, p.T);
+  fe_mul(r.Y, p.Y, p.Z);
+  fe_mul(r.Z, p.Z, p.T);
+}
+
+CG_HD void ge_p1p1_to_p3(ge_p3& r, const ge_p1p1& p) {
+  fe_mul(r.X, p.X, p.T);
+  fe_mul(r.Y, p.Y, p.Z);
+  fe_mul(r.Z, p.Z, p.T);
+  fe_mul(r.T, p.X, p.Y);
+}
+
+CG_HD void ge_p3_to_cached(ge_cached& r, const ge_p3& p) {
+  const fe d2 = CG_FE_D2;
+  fe_add(r.YplusX, p.Y, p.X);
+  fe_sub(r.YminusX, p.Y, p.X);
+  r.Z = p.Z;
+  fe_mul(r.T2d, p.T, d2);
+}
+
+// 2P: x = E/G, y = H/F with E = (X+Y)^2 - X^2 - Y^2, G = Y^2 - X^2,
+// H = -(X^2 + Y^2), F = G - 2Z^2  (stored as p1p1 with the signs folded).
+CG_HD void ge_p2_dbl(ge_p1p1& r, const ge_p2& p) {
+  fe t0;
+  fe_sq(r.X, p.X);
+  fe_sq(r.Z, p.Y);
+  fe_sq2(r.T, p.Z);
+  fe_add(r.Y, p.X, p.Y);
+  fe_sq(t0, r.Y);
+  fe_add(r.Y, r.Z, r.X);  // YY + XX
+  fe_sub(r.Z, r.Z, r.X);  // YY - XX
+  fe_sub(r.X, t0, r.Y);   // (X+Y)^2 - YY - XX
+  fe_sub(r.T, r.T, r.Z);  // 2ZZ - (YY - XX)
+}
+
+CG_HD void ge_p3_dbl(ge_p1p1& r, const ge_p3& p) {
+  ge_p2 q;
+  q.X = p.X; q.Y = p.Y; q.Z = p.Z;
+  ge_p2_dbl(r, q);
+}
+
+// P + Q (neg = 0) or P - Q (neg = 1) with Q cached; neg may differ per lane.
+CG_HD void ge_add_cached(ge_p1p1& r, const ge_p3& p, const ge_cached& q, uint32_t neg) {
+  fe a, b, c, d, qa, qb;
+  fe_select(qa, q.YplusX, q.YminusX, neg);
+  fe_select(qb, q.YminusX, q.YplusX, neg);
+  fe_add(a, p.Y, p.X);
+  fe_sub(b, p.Y, p.X);
+  fe_mul(a, a, qa);
+  fe_mul(b, b, qb);
+  fe_mul(c, q.T2d, p.T);
+  fe_mul(d, p.Z, q.Z);
+  fe_add(d, d, d);
+  fe_sub(r.X, a, b);
+  fe_add(r.Y, a, b);
+  fe_add(r.Z, d, c);
+  fe_sub(r.T, d, c);
+  // negation of Q flips the sign of c: swap Z/T
+  fe tz = r.Z;
+  fe_select(r.Z, r.Z, r.T, neg);
+  fe_select(r.T, r.T, tz, neg);
+}
+
+// P + Q (neg = 0) or P - Q (neg = 1) with Q affine precomputed.
+CG_HD void ge_madd(ge_p1p1& r, const ge_p3& p, const ge_precomp& q, uint32_t neg) {
+  fe a, b, c, d, qa, qb;
+  fe_select(qa, q.yplusx, q.yminusx, neg);
+  fe_select(qb, q.yminusx, q.yplusx, neg);
+  fe_add(a, p.Y, p.X);
+  fe_sub(b, p.Y, p.X);
+  fe_mul(a, a, qa);
+  fe_mul(b, b, qb);
+  fe_mul(c, q.xy2d, p.T);
+  fe_add(d, p.Z, p.Z);
+  fe_sub(r.X, a, b);
+  fe_add(r.Y, a, b);
+  fe_add(r.Z, d, c);
+  fe_sub(r.T, d, c);
+  fe tz = r.Z;
+  fe_select(r.Z, r.Z, r.T, neg);
+  fe_select(r.T, r.T, tz, neg);
+}
+
+// Canonical encoding of (X:Y:Z): y with the sign of x in bit 255 (i2p toByteArray).
+CG_HD void ge_tobytes(uint32_t w[8], const fe& X, const fe& Y, const fe& Z) {
+  fe recip, x, y;
+  fe_invert(recip, Z);
+  fe_mul(x, X, recip);
+  fe_mul(y, Y, recip);
+  fe_tobytes(w, y);
+  w[7] ^= fe_isnegative(x) << 31;
+}
+
+// i2p GroupElement(curve, bytes): y from the low 255 bits, NOT
+// range-checked; x = sqrt((y^2-1)/(dy^2+1)); no root -> returns 0 (the key
+// cannot be constructed); x = 0 with the sign bit set is accepted as x = 0.
+CG_HD uint32_t ge_frombytes_i2p(ge_p3& h, const uint32_t w[8]) {
+  const fe d = CG_FE_D, sqrtm1 = CG_FE_SQRTM1;
+  fe u, v, v3, vxx, check, one;
+  fe_1(one);
+  fe_frombytes(h.Y, w);
+  fe_reduce(h.Y);  // same value, limbs brought into the reduced range
+  fe_1(h.Z);
+  fe_sq(u, h.Y);
+  fe_mul(v, u, d);
+  fe_sub(u, u, one);  // y^2 - 1
+  fe_add(v, v, one);  // d y^2 + 1
+  fe_sq(v3, v);
+  fe_mul(v3, v3, v);  // v^3
+  fe_sq(h.X, v3);
+  fe_mul(h.X, h.X, v);
+  fe_mul(h.X, h.X, u);  // u v^7
+  fe_pow22523(h.X, h.X);
+  fe_mul(h.X, h.X, v3);
+  fe_mul(h.X, h.X, u);  // u v^3 (u v^7)^((p-5)/8)
+  fe_sq(vxx, h.X);
+  fe_mul(vxx, vxx, v);
+  fe_sub(check, vxx, u);
+  uint32_t ok = 1;
+  if (!fe_iszero(check)) {
+    fe_add(check, vxx, u);
+    ok = fe_iszero(check);
+    fe_mul(h.X, h.X, sqrtm1);
+  }
+  fe negx;
+  fe_neg(negx, h.X);
+  fe_select(h.X, h.X, negx, fe_isnegative(h.X) ^ (w[7] >> 31));
+  fe_mul(h.T, h.X, h.Y);
+  return ok;
+}
+
+}  // namespace cg

@@ -1,0 +1,141 @@
+// FIPS 180-4 SHA-512 of the Ed25519 challenge preimage R || Abyte || M, one
+// message per lane (i2p EdDSAEngine digest).  64-bit words are kept
+// as uint64_t; on gfx950 rotates become v_alignbit pairs and adds v_add_co/addc.
+#pragma once
+#include "cg_common.h"
+
+namespace cg {
+
+#if defined(__HIPCC__)
+__constant__ static const uint64_t kSha512K[80] = {
+#else
+static const uint64_t kSha512K[80] = {
+#endif
+    0x428a2f98d728ae22ULL, 0x7137449123ef65cdULL, 0xb5c0fbcfec4d3b2fULL, 0xe9b5dba58189dbbcULL,
+    0x3956c25bf348b538ULL, 0x59f111f1b605d019ULL, 0x923f82a4af194f9bULL, 0xab1c5ed5da6d8118ULL,
+    0xd807aa98a3030242ULL, 0x12835b0145706fbeULL, 0x243185be4ee4b28cULL, 0x550c7dc3d5ffb4e2ULL,
+    0x72be5d74f27b896fULL, 0x80deb1fe3b1696b1ULL, 0x9bdc06a725c71235ULL, 0xc19bf174cf692694ULL,
+    0xe49b69c19ef14ad2ULL, 0xefbe4786384f25e3ULL, 0x0fc19dc68b8cd5b5ULL, 0x240ca1cc77ac9c65ULL,
+    0x2de92c6f592b0275ULL, 0x4a7484aa6ea6e483ULL, 0x5cb0a9dcbd41fbd4ULL, 0x76f988da831153b5ULL,
+    0x983e5152ee66dfabULL, 0xa831c66d2db43210ULL, 0xb00327c898fb213fULL, 0xbf597fc7beef0ee4ULL,
+    0xc6e00bf33da88fc2ULL, 0xd5a79147930aa725ULL, 0x06ca6351e003826fULL, 0x142929670a0e6e70ULL,
+    0x27b70a8546d22ffcULL, 0x2e1b21385c26c926ULL, 0x4d2c6dfc5ac42aedULL, 0x53380d139d95b3dfULL,
+    0x650a73548baf63deULL, 0x766a0abb3c77b2a8ULL, 0x81c2c92e47edaee6ULL, 0x92722c851482353bULL,
+    0xa2bfe8a14cf10364ULL, 0xa81a664bbc423001ULL, 0xc24b8b70d0f89791ULL, 0xc76c51a30654be30ULL,
+    0xd192e819d6ef5218ULL, 0xd69906245565a910ULL, 0xf40e35855771202aULL, 0x106aa07032bbd1b8ULL,
+    0x19a4c116b8d2d0c8ULL, 0x1e376c085141ab53ULL, 0x2748774cdf8eeb99ULL, 0x34b0bcb5e19b48a8ULL,
+    0x391c0cb3c5c95a63ULL, 0x4ed8aa4ae3418acbULL, 0x5b9cca4f7763e373ULL, 0x682e6ff3d6b2b8a3ULL,
+    0x748f82ee5defb2fcULL, 0x78a5636f43172f60ULL, 0x84c87814a1f0ab72ULL, 0x8cc702081a6439ecULL,
+    0x90befffa23631e28ULL, 0xa4506cebde82bde9ULL, 0xbef9a3f7b2c67915ULL, 0xc67178f2e372532bULL,
+    0xca273eceea26619cULL, 0xd186b8c721c0c207ULL, 0xeada7dd6cde0eb1eULL, 0xf57d4f7fee6ed178ULL,
+    0x06f067aa72176fbaULL, 0x0a637dc5a2c898a6ULL, 0x113f9804bef90daeULL, 0x1b710b35131c471bULL,
+    0x28db77f523047d84ULL, 0x32caab7b40c72493ULL, 0x3c9ebe0a15c9bebcULL, 0x431d67c49c100d4cULL,
+    0x4cc5d4becb3e42b6ULL, 0x597f299cfc657e2aULL, 0x5fcb6fab3ad6faecULL, 0x6c44198c4a475817ULL};
+
+CG_HD uint64_t rotr64(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+
+CG_HD uint32_t bswap32(uint32_t x) {
+  return (x >> 24) | ((x >> 8) & 0xff00u) | ((x << 8) & 0xff0000u) | (x << 24);
+}
+
+// Big-endian 64-bit word from 8 little-endian-stored bytes held as two u32.
+CG_HD uint64_t be64_from_le32(uint32_t lo_bytes, uint32_t hi_bytes) {
+  return (uint64_t)bswap32(lo_bytes) << 32 | bswap32(hi_bytes);
+}
+
+CG_HD void sha512_init(uint64_t h[8]) {
+  h[0] = 0x6a09e667f3bcc908ULL; h[1] = 0xbb67ae8584caa73bULL;
+  h[2] = 0x3c6ef372fe94f82bULL; h[3] = 0xa54ff53a5f1d36f1ULL;
+  h[4] = 0x510e527fade682d1ULL; h[5] = 0x9b05688c2b3e6c1fULL;
+  h[6] = 0x1f83d9abfb41bd6bULL; h[7] = 0x5be0cd19137e2179ULL;
+}
+
+// One compression.  The schedule is kept as a 16-word ring; rounds run in an
+// outer loop of 5 x 16 so the code stays small (I-cache is shared per CU pair).
+CG_HD void sha512_block(uint64_t h[8], uint64_t w[16]) {
+  uint64_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
+  CG_NOUNROLL for (int r = 0; r < 80; r += 16) {
+    CG_UNROLL for (int j = 0; j < 16; ++j) {
+      if (r > 0) {
+        const uint64_t w15 = w[(j + 1) & 15], w2 = w[(j + 14) & 15];
+        const uint64_t s0 = rotr64(w15, 1) ^ rotr64(w15, 8) ^ (w15 >> 7);
+        const uint64_t s1 = rotr64(w2, 19) ^ rotr64(w2, 61) ^ (w2 >> 6);
+        w[j] += s0 + w[(j + 9) & 15] + s1;
+      }
+      const uint64_t t1 = hh + (rotr64(e, 14) ^ rotr64(e, 18) ^ rotr64(e, 41)) + ((e & f) ^ (~e & g)) +
+                          kSha512K[r + j] + w[j];
+      const uint64_t t2 = (rotr64(a, 28) ^ rotr64(a, 34) ^ rotr64(a, 39)) + ((a & b) ^ (a & c) ^ (b & c));
+      hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+    }
+  }
+  h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
+}
+
+// Loads dword i of a message whose bytes start at `m` (any alignment handled
+// by the caller through `sh`); `m4` is the 4-byte-aligned base.
+CG_HD uint32_t ld32(const uint32_t* m4, int64_t i) { return m4[i]; }
+
+CG_HD uint32_t alignbyte(uint32_t hi, uint32_t lo, uint32_t sh) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_alignbyte(hi, lo, sh);
+#else
+  return sh ? (lo >> (8 * sh)) | (hi << (32 - 8 * sh)) : lo;
+#endif
+}
+
+// SHA-512(prefix64 || M) where prefix64 is given as 8 little-endian u32 words of
+// R followed by 8 of Abyte, M = msg[0..n).  The reader never touches bytes at or
+// beyond m + n rounded up to 4 (callers pad device arenas by 16 bytes anyway).
+// Output: digest as 16 little-endian u32 words (the byte order sc_reduce wants).
+CG_HD void sha512_ed25519(uint32_t out[16], const uint32_t r[8], const uint32_t abyte[8], const uint8_t* msg,
+                          uint32_t n) {
+  uint64_t h[8], w[16];
+  sha512_init(h);
+  const uintptr_t addr = (uintptr_t)msg;
+  const uint32_t* m4 = (const uint32_t*)(addr & ~(uintptr_t)3);
+  const uint32_t sh = (uint32_t)(addr & 3);
+  const uint64_t total = 64 + (uint64_t)n;
+  const uint32_t nb = (uint32_t)((total + 17 + 127) / 128);
+  // dword j of M (relative, may be partially before m when sh != 0) is m4[j]
+  const int64_t ndw = ((int64_t)n + sh + 3) >> 2;  // dwords that hold message bytes
+  CG_NOUNROLL for (uint32_t blk = 0; blk < nb; ++blk) {
+    CG_UNROLL for (int j = 0; j < 16; ++j) {
+      const int64_t off = 128 * (int64_t)blk + 8 * j;  // stream byte offset
+      uint64_t word;
+      if (off < 32) {
+        word = be64_from_le32(r[2 * j], r[2 * j + 1]);
+      } else if (off < 64) {
+        word = be64_from_le32(abyte[2 * (j - 4)], abyte[2 * (j - 4) + 1]);
+      } else {
+        const int64_t q = off - 64;  // message byte offset (multiple of 8)
+        const int64_t c = (int64_t)n - q;
+        if (c <= 0) {
+          word = (c == 0) ? (0x80ULL << 56) : 0;
+        } else {
+          const int64_t d0 = q >> 2;  // first dword index (q is a multiple of 4)
+          const uint32_t x0 = ld32(m4, d0);
+          const uint32_t x1 = (d0 + 1 < ndw) ? ld32(m4, d0 + 1) : 0u;
+          const uint32_t x2 = (d0 + 2 < ndw) ? ld32(m4, d0 + 2) : 0u;
+          const uint32_t lo = alignbyte(x1, x0, sh), hi = alignbyte(x2, x1, sh);
+          word = be64_from_le32(lo, hi);
+          if (c < 8) {
+            const int keep = (int)c * 8;
+            word &= ~((~0ULL) >> keep);            // zero bytes >= n
+            word |= 0x80ULL << (56 - keep);        // padding marker at byte n
+          }
+        }
+      }
+      if (blk == nb - 1 && j == 14) word = 0;
+      if (blk == nb - 1 && j == 15) word = total * 8;
+      w[j] = word;
+    }
+    sha512_block(h, w);
+  }
+  CG_UNROLL for (int i = 0; i < 8; ++i) {
+    // digest bytes are big-endian words; emit as little-endian u32 stream
+    out[2 * i] = bswap32((uint32_t)(h[i] >> 32));
+    out[2 * i + 1] = bswap32((uint32_t)h[i]);
+  }
+}
+
+}  // namespace cg

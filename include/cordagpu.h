@@ -1,0 +1,191 @@
+/*
+ * libcordagpu — C ABI of the MI355X (gfx950) batch signature-verification and
+ * transaction-id engine for Corda's verification hot path.
+ *
+ * Plain C types only (pointers + sizes); no C++/torch types cross this boundary.
+ * Every entry point returns a cg_status (0 = OK, < 0 = error) and never throws,
+ * aborts or exits across the ABI.  Per-element outcomes live only in the verdict
+ * outputs.  A cg_ctx is single-threaded (one context per JVM/host thread; one
+ * process per GPU); different contexts may run concurrently.  The library never
+ * retains caller pointers after a call returns.
+ *
+ * What each entry point replaces in the reference (Kerwong/corda @ 0.14):
+ *
+ *   cg_verify_batch(mode = CG_MODE_IS_VALID)
+ *       a loop of Crypto.isValid(scheme, publicKey, signatureData, clearData)
+ *       core/src/main/kotlin/net/corda/core/crypto/Crypto.kt:534-541
+ *       (JCA Signature.getInstance/initVerify/update/verify; i2p EdDSAEngine for
+ *        EDDSA_ED25519_SHA512, BouncyCastle SHA256withECDSA for ECDSA_SECP256K1_SHA256
+ *        and ECDSA_SECP256R1_SHA256, schemes at Crypto.kt:91-132)
+ *   cg_verify_batch(mode = CG_MODE_DO_VERIFY)
+ *       a loop of Crypto.doVerify(scheme, publicKey, signatureData, clearData)
+ *       Crypto.kt:472-483 (empty sig / empty data -> IllegalArgumentException,
+ *       false -> SignatureException); overloads Crypto.kt:437-456
+ *   cg_der_parse_batch
+ *       BouncyCastle StdDSAEncoder.decode (strict DER) inside DSABase.engineVerify,
+ *       reached from Crypto.kt:537-540
+ *   cg_txid_batch
+ *       WireTransaction.id -> MerkleTree.getMerkleTree(availableComponentHashes)
+ *       core/.../transactions/WireTransaction.kt:39,104;
+ *       core/.../transactions/MerkleTransaction.kt:16-33,74-93;
+ *       core/.../crypto/MerkleTree.kt:27-66; core/.../crypto/SecureHash.kt:25,37,42
+ *   cg_tx_verify_batch
+ *       SignedTransaction signature loop: TransactionWithSignatures.checkSignaturesAreValid
+ *       core/.../transactions/TransactionWithSignatures.kt:58-62 (in order, first
+ *       failure wins), over ids recomputed as cg_txid_batch does.
+ *
+ * Verdict codes (one byte per element) map to the JVM outcomes:
+ *   CG_ACCEPT          isValid -> true / doVerify returns true
+ *   CG_REJECT          isValid -> false / doVerify throws SignatureException("Signature Verification failed!")
+ *   CG_SIG_MALFORMED   the engine throws SignatureException (Ed25519 length != 64; ECDSA DER decode failure)
+ *   CG_KEY_INVALID     the PublicKey object cannot be constructed (Ed25519 point with no square root;
+ *                      ECDSA point off the curve or coordinate >= p): InvalidKeyException /
+ *                      IllegalArgumentException at key decode, before any verify call
+ *   CG_ARG_EMPTY       doVerify only: IllegalArgumentException for an empty signature or empty clear
+ *                      data (Crypto.kt:475-476); isValid does not pre-check these
+ *   CG_UNSUPPORTED     scheme id not one of 2/3/4 (IllegalArgumentException "Unsupported key/algorithm")
+ * Precedence (JVM order): KEY_INVALID > ARG_EMPTY > SIG_MALFORMED > ACCEPT/REJECT.
+ */
+#ifndef CORDAGPU_H_
+#define CORDAGPU_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CG_ABI_VERSION 1
+
+typedef int32_t cg_status;
+enum {
+  CG_OK = 0,
+  CG_E_INVALID_ARGUMENT = -1,
+  CG_E_NO_DEVICE = -2,
+  CG_E_DEVICE = -3,
+  CG_E_OUT_OF_MEMORY = -4,
+  CG_E_MERKLE_EMPTY = -5, /* a transaction with no components: MerkleTreeException (MerkleTree.kt:29-30) */
+};
+
+enum {
+  CG_ACCEPT = 0,
+  CG_REJECT = 1,
+  CG_SIG_MALFORMED = 2,
+  CG_KEY_INVALID = 3,
+  CG_ARG_EMPTY = 4,
+  CG_UNSUPPORTED = 5,
+};
+
+enum { CG_MODE_IS_VALID = 0, CG_MODE_DO_VERIFY = 1 };
+
+/* SignatureScheme.schemeNumberID (Crypto.kt:92,106,120). */
+enum {
+  CG_SCHEME_ECDSA_SECP256K1_SHA256 = 2,
+  CG_SCHEME_ECDSA_SECP256R1_SHA256 = 3,
+  CG_SCHEME_EDDSA_ED25519_SHA512 = 4,
+};
+
+typedef struct cg_ctx cg_ctx;
+typedef struct cg_batch cg_batch;
+
+int cg_abi_version(void);
+/* Number of visible HIP devices (0 when none). */
+int cg_device_count(void);
+/* Opens a context on HIP device `device` (one process per GPU: usually LOCAL_RANK).
+ * Fails with CG_E_NO_DEVICE when no gfx950 device is present — there is no CPU fallback. */
+cg_status cg_open(int device, cg_ctx** out);
+void cg_close(cg_ctx* ctx);
+/* Human-readable description of the last error on this context ("" if none). */
+const char* cg_last_error(const cg_ctx* ctx);
+
+/*
+ * Signature batch input (host memory, element-major; caller-owned):
+ *   scheme_id  n bytes (NULL: every element is CG_SCHEME_EDDSA_ED25519_SHA512)
+ *   pk         n * pk_stride bytes.  Ed25519: the 32-byte key A as carried on the wire
+ *              (Kryo Ed25519PublicKeySerializer, Kryo.kt:330-340).  ECDSA: 64 bytes X||Y,
+ *              big-endian affine coordinates decoded from the X.509 SubjectPublicKeyInfo by the
+ *              caller (Kryo.kt:388-398; corda_amd.keys has a host helper).
+ *   sig        n * sig_stride bytes; element i uses sig_len[i] bytes (sig_len NULL: sig_stride).
+ *              Ed25519: R||S; ECDSA: the DER SEQUENCE{r, s} exactly as produced by the signer.
+ *   msg        the clear-data arena (msg_bytes long); element i's data is
+ *              msg[msg_off[i] .. msg_off[i] + msg_len[i]).
+ * Outputs: verdict_out n bytes (required); accept_bitmap_out ceil(n/32) words (optional;
+ * bit i%32 of word i/32 set iff element i is CG_ACCEPT).
+ */
+cg_status cg_verify_batch(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme_id, const uint8_t* pk,
+                          size_t pk_stride, const uint8_t* sig, size_t sig_stride, const uint32_t* sig_len,
+                          const uint8_t* msg, size_t msg_bytes, const uint64_t* msg_off, const uint32_t* msg_len,
+                          uint8_t* verdict_out, uint32_t* accept_bitmap_out);
+
+/*
+ * Prepared batch: the same inputs staged once into device memory (HBM) in the
+ * library's internal layout, then verified any number of times.  This is how a
+ * notary backlog is fed, and what the benchmark times (inputs resident in HBM).
+ */
+cg_status cg_batch_create(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const uint8_t* pk, size_t pk_stride,
+                          const uint8_t* sig, size_t sig_stride, const uint32_t* sig_len, const uint8_t* msg,
+                          size_t msg_bytes, const uint64_t* msg_off, const uint32_t* msg_len, cg_batch** out);
+/* Verifies a prepared batch.  verdict_out / accept_bitmap_out are host pointers (either may
+ * be NULL); device_bitmap_out, if non-NULL, is a device pointer (e.g. a torch tensor's
+ * data_ptr()) that receives the ceil(n/32)-word accept bitmap on the device, ready for an
+ * RCCL all-gather.  Returns after the results are complete. */
+cg_status cg_batch_verify(cg_ctx* ctx, cg_batch* batch, int mode, uint8_t* verdict_out,
+                          uint32_t* accept_bitmap_out, void* device_bitmap_out);
+size_t cg_batch_size(const cg_batch* batch);
+void cg_batch_destroy(cg_ctx* ctx, cg_batch* batch);
+
+/*
+ * ECDSA DER pre-pass (K4): BouncyCastle-1.57-strict decode of each signature.
+ * rs_out: n * 64 bytes, big-endian r||s (valid when status is 0 or 1);
+ * status_out: n bytes: 0 = parsed and r,s in [1, n-1]; 1 = parsed but out of range (REJECT);
+ * 2 = malformed (CG_SIG_MALFORMED).  scheme_id selects the group order (NULL: all R1).
+ */
+cg_status cg_der_parse_batch(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const uint8_t* sig,
+                             size_t sig_stride, const uint32_t* sig_len, uint8_t* rs_out, uint8_t* status_out);
+
+/*
+ * Transaction ids (K5 + K6).  n_tx transactions; the components of tx t are
+ * comp_start[t] .. comp_start[t+1]-1 (comp_start has n_tx + 1 entries), each a
+ * serialized component (Kryo P2P no-refs bytes) at arena[comp_off[c] .. + comp_len[c]),
+ * in availableComponents order (inputs, attachments, outputs, commands, notary?,
+ * timeWindow?, privacySalt) — the LAST component of every tx is the serialized privacy
+ * salt.  salts: 32 raw salt bytes per tx (used for the nonces).  ids_out: 32 bytes per tx.
+ * Returns CG_E_MERKLE_EMPTY (ids of the other txs still written) when a tx has no component.
+ */
+cg_status cg_txid_batch(cg_ctx* ctx, size_t n_tx, const uint8_t* arena, size_t arena_bytes,
+                        const uint64_t* comp_off, const uint32_t* comp_len, const uint32_t* comp_start,
+                        const uint8_t* salts, uint8_t* ids_out);
+
+/*
+ * Signed-transaction batch (config 4): recompute every tx id on the device, then
+ * verify each tx's signatures over its 32-byte id.  Signatures of tx t are
+ * sig_start[t] .. sig_start[t+1]-1 (n_tx + 1 entries) in the tx's `sigs` order; the
+ * per-signature inputs are laid out as for cg_verify_batch (msg is implied = id).
+ * first_bad_out (n_tx): -1 when every signature of the tx verifies, else the index
+ * (within the tx) of the first failing one — the signature checkSignaturesAreValid
+ * would throw on.  verdict_out (optional, total sigs): per-signature verdicts.
+ * ids_out (optional): 32 bytes per tx.
+ */
+cg_status cg_tx_verify_batch(cg_ctx* ctx, int mode, size_t n_tx, const uint8_t* arena, size_t arena_bytes,
+                             const uint64_t* comp_off, const uint32_t* comp_len, const uint32_t* comp_start,
+                             const uint8_t* salts, const uint32_t* sig_start, const uint8_t* scheme_id,
+                             const uint8_t* pk, size_t pk_stride, const uint8_t* sig, size_t sig_stride,
+                             const uint32_t* sig_len, int32_t* first_bad_out, uint8_t* verdict_out,
+                             uint8_t* ids_out);
+
+/*
+ * Per-kernel device timing (HIP events on the context's stream), accumulated while
+ * profiling is enabled.  Names: "ed25519_prep", "ed25519_msm", "ecdsa_verify",
+ * "der_parse", "merkle_leaf", "merkle_tree", "stage".
+ */
+cg_status cg_set_profiling(cg_ctx* ctx, int enable);
+cg_status cg_kernel_stats(cg_ctx* ctx, const char* kernel, double* total_ms, uint64_t* launches,
+                          uint64_t* items);
+cg_status cg_reset_stats(cg_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CORDAGPU_H_ */

@@ -1,0 +1,143 @@
+"""GPU parity: Ed25519 verdicts of libcordagpu (HIP, gfx950) vs the CPU oracle.
+
+Bar: bit-exact verdict codes (integer work).  Inputs: the committed golden
+fixtures (every adversarial class of SURVEY.md §8d, RFC 8032 KATs, reference test
+keys), seeded random valid + mutated batches checked element-wise against the C
+oracle, and at config scale (1M signatures) size-independent properties
+(every untouched signature accepts; verdict histogram of the mutated 1% equals
+the oracle's on the same subset).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from corda_amd import crypto
+from corda_amd._lib import ACCEPT, MODE_DO_VERIFY, MODE_IS_VALID, ptr
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools", "datagen"))
+import datagen  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+def oracle_verdicts(oracle, w, mode, threads=16):
+    out = np.empty(max(w.n, 1), dtype=np.uint8)
+    oracle.oracle_verify_batch(ptr(w.scheme), ptr(w.pk), ctypes.c_size_t(w.pk_stride), ptr(w.sig),
+                               ctypes.c_size_t(w.sig_stride), ptr(w.sig_len), ptr(w.msg), ptr(w.msg_off),
+                               ptr(w.msg_len), ctypes.c_size_t(w.n), mode, threads, ptr(out))
+    return out[:w.n]
+
+
+def gpu_verdicts(ctx, w, mode):
+    b = crypto.PackedBatch(w.n, w.scheme, w.pk, w.pk_stride, w.sig, w.sig_stride, w.sig_len, w.msg, w.msg_off,
+                           w.msg_len)
+    return crypto.verify_packed(ctx, b, mode)
+
+
+def test_golden_fixtures(gpu_ctx, golden_ed25519):
+    g = golden_ed25519
+    pks = [bytes.fromhex(e["pk"]) for e in g]
+    sigs = [bytes.fromhex(e["sig"]) for e in g]
+    msgs = [bytes.fromhex(e["msg"]) for e in g]
+    for mode, key in ((MODE_IS_VALID, "is_valid"), (MODE_DO_VERIFY, "do_verify")):
+        b = crypto.pack(crypto.EDDSA_ED25519_SHA512, pks, sigs, msgs)
+        v = crypto.verify_packed(gpu_ctx, b, mode)
+        exp = np.array([e[key] for e in g], dtype=np.uint8)
+        bad = np.flatnonzero(v != exp)
+        assert bad.size == 0, [(g[i]["cls"], int(v[i]), int(exp[i])) for i in bad[:10]]
+
+
+def test_random_and_mutated_vs_oracle(gpu_ctx, oracle):
+    w = datagen.make_batch(6000, msg_bytes=97, seed=11, key_base=1000)
+    w = datagen.add_ed25519_adversarial(w, frac=0.25, seed=3)
+    for mode in (MODE_IS_VALID, MODE_DO_VERIFY):
+        exp = oracle_verdicts(oracle, w, mode)
+        got = gpu_verdicts(gpu_ctx, w, mode)
+        bad = np.flatnonzero(got != exp)
+        assert bad.size == 0, [(w.classes[i], int(got[i]), int(exp[i])) for i in bad[:10]]
+    assert (exp == ACCEPT).sum() > 0.7 * w.n
+
+
+def test_message_lengths_and_alignment(gpu_ctx, oracle):
+    # every length 0..300 (SHA-512 block boundaries at 64/111/112/128+...), odd arena offsets
+    lens = list(range(0, 301))
+    rng = np.random.default_rng(5)
+    base = datagen.make_batch(len(lens), msg_bytes=301, seed=99, key_base=50_000)
+    # re-sign at the exact lengths with an unaligned arena
+    n = len(lens)
+    msg_len = np.array(lens, dtype=np.uint32)
+    msg_off = np.zeros(n, dtype=np.uint64)
+    pos = 1
+    for i in range(n):
+        msg_off[i] = pos
+        pos += lens[i] + int(rng.integers(0, 4))
+    arena = np.zeros(pos + 8, dtype=np.uint8)
+    for i in range(n):
+        arena[int(msg_off[i]):int(msg_off[i]) + lens[i]] = base.msg[i * 301:i * 301 + lens[i]]
+    c = datagen.lib()
+    pk = np.zeros((n, 64), np.uint8)
+    sig = np.zeros((n, 72), np.uint8)
+    sl = np.zeros(n, np.uint32)
+    sch = np.full(n, 4, np.uint8)
+    assert c.dg_sign_batch(n, sch.ctypes.data, 77, pk.ctypes.data, 64, sig.ctypes.data, 72, sl.ctypes.data,
+                           arena.ctypes.data, msg_off.ctypes.data, msg_len.ctypes.data, 8) == 0
+    w = datagen.Workload(n, sch, pk, 64, sig, 72, sl, arena, msg_off, msg_len)
+    for mode in (MODE_IS_VALID, MODE_DO_VERIFY):
+        exp = oracle_verdicts(oracle, w, mode)
+        got = gpu_verdicts(gpu_ctx, w, mode)
+        assert np.array_equal(got, exp)
+    assert (gpu_verdicts(gpu_ctx, w, MODE_IS_VALID) == ACCEPT).all()
+
+
+def test_prepared_batch_and_bitmap(gpu_ctx, oracle):
+    w = datagen.make_batch(3000, msg_bytes=32, seed=3, key_base=9)
+    w = datagen.add_ed25519_adversarial(w, frac=0.1, seed=9)
+    exp = oracle_verdicts(oracle, w, MODE_IS_VALID)
+    b = crypto.PackedBatch(w.n, w.scheme, w.pk, w.pk_stride, w.sig, w.sig_stride, w.sig_len, w.msg, w.msg_off,
+                           w.msg_len)
+    pb = crypto.PreparedBatch(gpu_ctx, b)
+    v1 = pb.verify(MODE_IS_VALID)
+    v2 = pb.verify(MODE_IS_VALID)
+    assert np.array_equal(v1, exp) and np.array_equal(v2, exp)
+    v, bm = crypto.verify_packed(gpu_ctx, b, MODE_IS_VALID, bitmap=True)
+    bits = np.unpackbits(bm.view(np.uint8), bitorder="little")[:w.n]
+    assert np.array_equal(bits.astype(bool), exp == ACCEPT)
+    pb.close()
+
+
+def test_do_verify_batch_raises_like_loop(gpu_ctx, golden_ed25519):
+    g = [e for e in golden_ed25519 if e["cls"] == "valid" and e["msg"]][:20]
+    pks = [bytes.fromhex(e["pk"]) for e in g]
+    sigs = [bytes.fromhex(e["sig"]) for e in g]
+    msgs = [bytes.fromhex(e["msg"]) for e in g]
+    assert crypto.do_verify_batch(gpu_ctx, crypto.EDDSA_ED25519_SHA512, pks, sigs, msgs)
+    bad = list(sigs)
+    bad[7] = bytes([bad[7][0] ^ 1]) + bad[7][1:]
+    bad[12] = b""
+    with pytest.raises(crypto.SignatureException) as ei:
+        crypto.do_verify_batch(gpu_ctx, crypto.EDDSA_ED25519_SHA512, pks, bad, msgs)
+    assert ei.value.index == 7
+    bad[3] = b""
+    with pytest.raises(crypto.IllegalArgumentException) as ei:
+        crypto.do_verify_batch(gpu_ctx, crypto.EDDSA_ED25519_SHA512, pks, bad, msgs)
+    assert ei.value.index == 3
+
+
+def test_config2_scale_properties(gpu_ctx, oracle):
+    """1M Ed25519, 1 KB messages, 1% adversarial: untouched elements all accept and
+    the adversarial subset matches the oracle element-wise."""
+    n = 1 << 20
+    w = datagen.make_batch(n, msg_bytes=1024, seed=42, key_base=0)
+    w = datagen.add_ed25519_adversarial(w, frac=0.01, seed=1)
+    got = gpu_verdicts(gpu_ctx, w, MODE_IS_VALID)
+    adv = np.array([c != "valid" for c in w.classes])
+    assert (got[~adv] == ACCEPT).all()
+    sub = w.subset(np.flatnonzero(adv))
+    exp = oracle_verdicts(oracle, sub, MODE_IS_VALID)
+    assert np.array_equal(got[adv], exp)

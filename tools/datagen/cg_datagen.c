@@ -1,0 +1,179 @@
+/* Synthetic workload generator for bench.py and the large GPU tests.
+ *
+ * Produces signature batches in the C-ABI layout (include/cordagpu.h) quickly:
+ * keys from SHA-512("cg-key" || LE64(seed_base + i)), messages from xoshiro256**,
+ * signatures from OpenSSL 3 (EVP Ed25519, deterministic per RFC 8032; ECDSA with
+ * OpenSSL's random nonce), spread over pthreads.  It is neither the oracle (that
+ * decides expected verdicts) nor the product (libcordagpu); it only makes inputs.
+ * SURVEY.md §8(d) config 2/3/5 shapes.
+ */
+#include <openssl/bn.h>
+#include <openssl/ec.h>
+#include <openssl/ecdsa.h>
+#include <openssl/evp.h>
+#include <openssl/obj_mac.h>
+#include <openssl/sha.h>
+#include <pthread.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+static uint64_t rotl(uint64_t x, int k) { return (x << k) | (x >> (64 - k)); }
+
+typedef struct { uint64_t s[4]; } xoshiro;
+
+static uint64_t splitmix(uint64_t* x) {
+  uint64_t z = (*x += 0x9e3779b97f4a7c15ULL);
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+  return z ^ (z >> 31);
+}
+
+static void xo_seed(xoshiro* r, uint64_t seed) {
+  for (int i = 0; i < 4; ++i) r->s[i] = splitmix(&seed);
+}
+
+static uint64_t xo_next(xoshiro* r) {
+  uint64_t* s = r->s;
+  const uint64_t result = rotl(s[1] * 5, 7) * 9;
+  const uint64_t t = s[1] << 17;
+  s[2] ^= s[0]; s[3] ^= s[1]; s[1] ^= s[2]; s[0] ^= s[3];
+  s[2] ^= t; s[3] = rotl(s[3], 45);
+  return result;
+}
+
+/* Fill n bytes with xoshiro256** output seeded by (seed, stream). */
+void dg_fill_bytes(uint8_t* out, size_t n, uint64_t seed) {
+  xoshiro r;
+  xo_seed(&r, seed);
+  size_t i = 0;
+  for (; i + 8 <= n; i += 8) {
+    uint64_t v = xo_next(&r);
+    memcpy(out + i, &v, 8);
+  }
+  if (i < n) {
+    uint64_t v = xo_next(&r);
+    memcpy(out + i, &v, n - i);
+  }
+}
+
+static void key_seed(uint8_t seed32[32], uint64_t idx) {
+  uint8_t buf[14], h[64];
+  memcpy(buf, "cg-key", 6);
+  for (int i = 0; i < 8; ++i) buf[6 + i] = (uint8_t)(idx >> (8 * i));
+  SHA512(buf, sizeof buf, h);
+  memcpy(seed32, h, 32);
+}
+
+typedef struct {
+  int scheme;  /* 2 K1, 3 R1, 4 Ed25519 */
+  size_t lo, hi;
+  uint64_t key_base;
+  uint8_t *pk, *sig;
+  size_t pk_stride, sig_stride;
+  uint32_t* sig_len;
+  const uint8_t* msg;
+  const uint64_t* msg_off;
+  const uint32_t* msg_len;
+  int err;
+} job;
+
+static void* ed_worker(void* arg) {
+  job* j = (job*)arg;
+  EVP_MD_CTX* mctx = EVP_MD_CTX_new();
+  for (size_t i = j->lo; i < j->hi; ++i) {
+    uint8_t seed[32];
+    key_seed(seed, j->key_base + i);
+    EVP_PKEY* k = EVP_PKEY_new_raw_private_key(EVP_PKEY_ED25519, NULL, seed, 32);
+    size_t pl = 32, sl = 64;
+    if (!k || EVP_PKEY_get_raw_public_key(k, j->pk + i * j->pk_stride, &pl) != 1 ||
+        EVP_DigestSignInit(mctx, NULL, NULL, NULL, k) != 1 ||
+        EVP_DigestSign(mctx, j->sig + i * j->sig_stride, &sl, j->msg + j->msg_off[i], j->msg_len[i]) != 1) {
+      j->err = 1;
+    }
+    j->sig_len[i] = (uint32_t)sl;
+    EVP_PKEY_free(k);
+    EVP_MD_CTX_reset(mctx);
+  }
+  EVP_MD_CTX_free(mctx);
+  return NULL;
+}
+
+static void* ec_worker(void* arg) {
+  job* j = (job*)arg;
+  const int nid = j->scheme == 2 ? NID_secp256k1 : NID_X9_62_prime256v1;
+  BN_CTX* bctx = BN_CTX_new();
+  for (size_t i = j->lo; i < j->hi; ++i) {
+    uint8_t seed[32], dig[32];
+    key_seed(seed, j->key_base + i);
+    EC_KEY* k = EC_KEY_new_by_curve_name(nid);
+    const EC_GROUP* g = EC_KEY_get0_group(k);
+    BIGNUM* d = BN_bin2bn(seed, 32, NULL);
+    BIGNUM* order = BN_new();
+    EC_GROUP_get_order(g, order, bctx);
+    BN_mod(d, d, order, bctx);
+    if (BN_is_zero(d)) BN_one(d);
+    EC_POINT* q = EC_POINT_new(g);
+    EC_POINT_mul(g, q, d, NULL, NULL, bctx);
+    EC_KEY_set_private_key(k, d);
+    EC_KEY_set_public_key(k, q);
+    uint8_t oct[65];
+    if (EC_POINT_point2oct(g, q, POINT_CONVERSION_UNCOMPRESSED, oct, 65, bctx) != 65) j->err = 1;
+    memcpy(j->pk + i * j->pk_stride, oct + 1, 64);
+    SHA256(j->msg + j->msg_off[i], j->msg_len[i], dig);
+    unsigned int sl = (unsigned int)j->sig_stride;
+    if (ECDSA_sign(0, dig, 32, j->sig + i * j->sig_stride, &sl, k) != 1) j->err = 1;
+    j->sig_len[i] = sl;
+    EC_POINT_free(q);
+    BN_free(order);
+    BN_free(d);
+    EC_KEY_free(k);
+  }
+  BN_CTX_free(bctx);
+  return NULL;
+}
+
+/* Sign n messages with distinct keys (index key_base + i).  scheme[i] selects the
+ * algorithm (NULL: all Ed25519).  Returns 0 on success. */
+int dg_sign_batch(size_t n, const uint8_t* scheme, uint64_t key_base, uint8_t* pk, size_t pk_stride, uint8_t* sig,
+                  size_t sig_stride, uint32_t* sig_len, const uint8_t* msg, const uint64_t* msg_off,
+                  const uint32_t* msg_len, int n_threads) {
+  if (n_threads < 1) n_threads = 1;
+  int err = 0;
+  /* group by scheme so each worker runs one algorithm over contiguous runs */
+  for (int sc = 2; sc <= 4; ++sc) {
+    size_t cnt = 0;
+    for (size_t i = 0; i < n; ++i) cnt += (scheme ? scheme[i] : 4) == sc;
+    if (!cnt) continue;
+    /* process contiguous runs of this scheme */
+    size_t i = 0;
+    while (i < n) {
+      while (i < n && (scheme ? scheme[i] : 4) != sc) ++i;
+      size_t lo = i;
+      while (i < n && (scheme ? scheme[i] : 4) == sc) ++i;
+      size_t hi = i;
+      if (lo >= hi) break;
+      size_t len = hi - lo;
+      int nt = (size_t)n_threads > len ? (int)len : n_threads;
+      pthread_t* th = calloc((size_t)nt, sizeof(pthread_t));
+      job* jobs = calloc((size_t)nt, sizeof(job));
+      for (int t = 0; t < nt; ++t) {
+        job* j = &jobs[t];
+        j->scheme = sc;
+        j->lo = lo + len * (size_t)t / (size_t)nt;
+        j->hi = lo + len * (size_t)(t + 1) / (size_t)nt;
+        j->key_base = key_base;
+        j->pk = pk; j->sig = sig; j->pk_stride = pk_stride; j->sig_stride = sig_stride;
+        j->sig_len = sig_len; j->msg = msg; j->msg_off = msg_off; j->msg_len = msg_len;
+        pthread_create(&th[t], NULL, sc == 4 ? ed_worker : ec_worker, j);
+      }
+      for (int t = 0; t < nt; ++t) {
+        pthread_join(th[t], NULL);
+        err |= jobs[t].err;
+      }
+      free(th);
+      free(jobs);
+    }
+  }
+  return err ? -1 : 0;
+}

@@ -1,0 +1,136 @@
+"""Synthetic signature workloads in the libcordagpu C-ABI layout.
+
+Config shapes from SURVEY.md §8(d): N distinct keys (SHA-512("cg-key"||LE64(i))),
+xoshiro256** messages, OpenSSL-signed (libcg_datagen.so), and an optional
+adversarial fraction split uniformly over the Ed25519 classes E1–E12 — byte
+mutations (E1–E6, E12) applied in place, the curve-structured classes (E7–E11)
+drawn from the committed golden fixtures (tests/golden/ed25519_golden.json).
+"""
+from __future__ import annotations
+
+import ctypes
+import json
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+LIB = os.path.join(HERE, "libcg_datagen.so")
+L = 2**252 + 27742317777372353535851937790883648493
+
+
+def lib():
+    if not os.path.exists(LIB):
+        import subprocess
+        subprocess.check_call(["make", "-C", HERE], stdout=subprocess.DEVNULL)
+    c = ctypes.CDLL(LIB)
+    c.dg_sign_batch.restype = ctypes.c_int
+    c.dg_sign_batch.argtypes = [ctypes.c_size_t, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_size_t,
+                                ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                ctypes.c_void_p, ctypes.c_int]
+    c.dg_fill_bytes.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64]
+    return c
+
+
+class Workload:
+    """Element-major arrays ready for cg_batch_create / cg_verify_batch."""
+
+    def __init__(self, n, scheme, pk, pk_stride, sig, sig_stride, sig_len, msg, msg_off, msg_len, classes=None):
+        self.n, self.scheme, self.pk, self.pk_stride = n, scheme, pk, pk_stride
+        self.sig, self.sig_stride, self.sig_len = sig, sig_stride, sig_len
+        self.msg, self.msg_off, self.msg_len = msg, msg_off, msg_len
+        self.classes = classes
+
+    def subset(self, idx):
+        """Copy of elements idx (messages re-packed)."""
+        idx = np.asarray(idx, dtype=np.int64)
+        ml = self.msg_len[idx]
+        off = np.zeros(len(idx), dtype=np.uint64)
+        if len(idx) > 1:
+            off[1:] = np.cumsum(ml[:-1], dtype=np.uint64)
+        arena = np.concatenate([self.msg[int(self.msg_off[i]):int(self.msg_off[i]) + int(self.msg_len[i])]
+                                for i in idx] + [np.zeros(1, np.uint8)])
+        return Workload(len(idx), self.scheme[idx].copy(), self.pk[idx].copy(), self.pk_stride, self.sig[idx].copy(),
+                        self.sig_stride, self.sig_len[idx].copy(), arena, off, ml.copy(),
+                        None if self.classes is None else [self.classes[i] for i in idx])
+
+
+def make_batch(n: int, msg_bytes: int = 1024, scheme: int | np.ndarray = 4, seed: int = 42, key_base: int = 0,
+               threads: int | None = None, sig_stride: int = 72) -> Workload:
+    """n signed messages of msg_bytes each (fixed size), all valid."""
+    c = lib()
+    threads = threads or min(16, os.cpu_count() or 1)
+    sch = np.full(n, scheme, dtype=np.uint8) if np.isscalar(scheme) else np.asarray(scheme, dtype=np.uint8)
+    msg = np.empty(n * msg_bytes + 1, dtype=np.uint8)
+    c.dg_fill_bytes(msg.ctypes.data, n * msg_bytes, seed)
+    msg_off = (np.arange(n, dtype=np.uint64) * msg_bytes)
+    msg_len = np.full(n, msg_bytes, dtype=np.uint32)
+    pk = np.zeros((n, 64), dtype=np.uint8)
+    sig = np.zeros((n, sig_stride), dtype=np.uint8)
+    sig_len = np.zeros(n, dtype=np.uint32)
+    rc = c.dg_sign_batch(n, sch.ctypes.data, key_base, pk.ctypes.data, 64, sig.ctypes.data, sig_stride,
+                         sig_len.ctypes.data, msg.ctypes.data, msg_off.ctypes.data, msg_len.ctypes.data, threads)
+    if rc != 0:
+        raise RuntimeError("signature generation failed")
+    return Workload(n, sch, pk, 64, sig, sig_stride, sig_len, msg, msg_off, msg_len, ["valid"] * n)
+
+
+ED_CLASSES = ["E1", "E2", "E3", "E4", "E5", "E6", "E7", "E8", "E9", "E10", "E11", "E12"]
+
+
+def _golden_pool():
+    with open(os.path.join(ROOT, "tests", "golden", "ed25519_golden.json")) as f:
+        g = json.load(f)
+    pool = {}
+    for e in g:
+        for cls in ("E7", "E8", "E9", "E10", "E11"):
+            if e["cls"].startswith(cls + "_"):
+                pool.setdefault(cls, []).append(e)
+    return pool
+
+
+def add_ed25519_adversarial(w: Workload, frac: float = 0.01, seed: int = 7) -> Workload:
+    """Mutates a fraction of an Ed25519 workload in place, uniformly over E1–E12.
+    Structured classes replace the element's key/sig/message with a golden case
+    (its message is written over the element's slot, so msg_len may shrink)."""
+    rng = np.random.default_rng(seed)
+    k = int(round(w.n * frac))
+    idx = rng.choice(w.n, size=k, replace=False)
+    pool = _golden_pool()
+    classes = list(w.classes) if w.classes is not None else ["valid"] * w.n
+    for j, i in enumerate(idx):
+        cls = ED_CLASSES[j % len(ED_CLASSES)]
+        classes[i] = cls
+        o, ln = int(w.msg_off[i]), int(w.msg_len[i])
+        if cls == "E1":
+            w.sig[i, rng.integers(32)] ^= np.uint8(1 << rng.integers(8))
+        elif cls == "E2":
+            w.sig[i, 32 + rng.integers(32)] ^= np.uint8(1 << rng.integers(8))
+        elif cls == "E3":
+            if ln:
+                w.msg[o + rng.integers(ln)] ^= np.uint8(1 << rng.integers(8))
+        elif cls == "E4":
+            w.pk[i, :32] = w.pk[(i + 1) % w.n, :32]
+        elif cls in ("E5", "E6"):
+            s = int.from_bytes(w.sig[i, 32:64].tobytes(), "little")
+            t = s + L
+            if cls == "E6":
+                t = s + 8 * L if s + 8 * L < 2**256 else (2**256 - 1) ^ int(rng.integers(1 << 16))
+            if t < 2**256:
+                w.sig[i, 32:64] = np.frombuffer(t.to_bytes(32, "little"), dtype=np.uint8)
+        elif cls == "E12":
+            w.sig_len[i] = int(rng.choice([0, 63, 65]))
+        else:
+            e = pool[cls][j % len(pool[cls])]
+            pk = bytes.fromhex(e["pk"]); sg = bytes.fromhex(e["sig"]); m = bytes.fromhex(e["msg"])
+            w.pk[i, :] = 0
+            w.pk[i, :32] = np.frombuffer(pk, dtype=np.uint8)
+            w.sig[i, :] = 0
+            w.sig[i, :len(sg)] = np.frombuffer(sg, dtype=np.uint8)
+            w.sig_len[i] = len(sg)
+            m = m[:ln]
+            w.msg[o:o + len(m)] = np.frombuffer(m, dtype=np.uint8)
+            w.msg_len[i] = len(m)
+    w.classes = classes
+    return w

@@ -78,7 +78,20 @@ OP32(add_co_u32, "v_add_co_u32 %0, vcc, %0, %1")
 OP32(addc_co_u32, "v_addc_co_u32 %0, vcc, %0, %1, vcc")
 OP32(mul_f32, "v_mul_f32 %0, %0, %1")
 OP32(cndmask, "v_cndmask_b32 %0, %0, %1, vcc")
+OP32(cndmask_s, "v_cndmask_b32_e64 %0, %0, %1, s[40:41]")
+OP32(bfi_b32, "v_bfi_b32 %0, %1, %0, %1")
+OP32(perm_b32, "v_perm_b32 %0, %0, %1, %1")
+OP32(xor_b32, "v_xor_b32 %0, %0, %1")
+OP32(and_or, "v_and_or_b32 %0, %0, %1, %1")
+OP32(sub_u32, "v_sub_u32 %0, %0, %1")
+OP32(lshlrev_b32, "v_lshlrev_b32 %0, 3, %0")
+OP32(ashrrev_i32, "v_ashrrev_i32 %0, 3, %0")
+OP32(mul_i32_i24, "v_mul_i32_i24 %0, %0, %1")
 OP64(mad_u64_u32, "v_mad_u64_u32 %0, vcc, %1, %1, %0", unsigned long long)
+OP64(mad_i64_i32, "v_mad_i64_i32 %0, vcc, %1, %1, %0", unsigned long long)
+OP64(lshl_add_u64, "v_lshl_add_u64 %0, %0, 0, %0", unsigned long long)
+OP64(ashr_i64, "v_ashrrev_i64 %0, 3, %0", unsigned long long)
+OP64(mov_b64, "v_mov_b64 %0, %0", unsigned long long)
 OP64(lshlrev_b64, "v_lshlrev_b64 %0, 3, %0", unsigned long long)
 OP64(add_f64, "v_add_f64 %0, %0, %2", double)
 OP64(fma_f64, "v_fma_f64 %0, %0, %2, %2", double)
@@ -91,7 +104,7 @@ int main() {
   Entry tab[] = {E(add_u32), E(add3_u32), E(or3_b32), E(alignbit), E(lshl_add), E(bfe_u32),
                  E(mul_lo_u32), E(mul_hi_u32), E(mul_u32_u24), E(mul_hi_u32_u24), E(mad_u32_u24),
                  E(mad_u32_u16), E(pk_mad_u16), E(dot2_u32_u16), E(dot4_u32_u8), E(add_co_u32),
-                 E(addc_co_u32), E(mul_f32), E(cndmask), E(mad_u64_u32), E(lshlrev_b64), E(add_f64),
+                 E(addc_co_u32), E(mul_f32), E(cndmask), E(cndmask_s), E(bfi_b32), E(perm_b32), E(xor_b32), E(and_or), E(sub_u32), E(lshlrev_b32), E(ashrrev_i32), E(mul_i32_i24), E(mad_u64_u32), E(mad_i64_i32), E(lshl_add_u64), E(ashr_i64), E(mov_b64), E(lshlrev_b64), E(add_f64),
                  E(fma_f64), E(mul_f64)};
   hipDeviceProp_t prop;
   CHK(hipGetDeviceProperties(&prop, 0));
