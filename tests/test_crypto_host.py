@@ -1,0 +1,44 @@
+"""Host logic of the Crypto batch mirror (no GPU): packing into the C-ABI
+layout, scheme lookup and the doVerify exception mapping (Crypto.kt:472-483)."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from corda_amd import crypto
+from corda_amd._lib import ACCEPT, ARG_EMPTY, KEY_INVALID, REJECT, SIG_MALFORMED, UNSUPPORTED
+
+
+def test_pack_layout():
+    b = crypto.pack(crypto.EDDSA_ED25519_SHA512, [b"\1" * 32, b"\2" * 32], [b"\3" * 64, b"\4" * 70],
+                    [b"hello", b""])
+    assert b.n == 2 and b.pk_stride == 64 and b.sig_stride == 72
+    assert list(b.scheme) == [4, 4]
+    assert list(b.sig_len) == [64, 70]
+    assert list(b.msg_off) == [0, 5] and list(b.msg_len) == [5, 0]
+    assert bytes(b.msg[:5]) == b"hello"
+    assert bytes(b.pk[1, :32]) == b"\2" * 32 and not b.pk[1, 32:].any()
+
+
+def test_scheme_lookup_like_find_signature_scheme():
+    assert crypto._scheme_id("ECDSA_SECP256R1_SHA256") == 3
+    assert crypto._scheme_id(crypto.ECDSA_SECP256K1_SHA256) == 2
+    with pytest.raises(crypto.IllegalArgumentException):
+        crypto._scheme_id("RSA_SHA256")
+
+
+@pytest.mark.parametrize("code,exc", [(REJECT, crypto.SignatureException), (SIG_MALFORMED, crypto.SignatureException),
+                                      (KEY_INVALID, crypto.InvalidKeyException),
+                                      (ARG_EMPTY, crypto.IllegalArgumentException),
+                                      (UNSUPPORTED, crypto.IllegalArgumentException)])
+def test_exception_mapping(code, exc):
+    with pytest.raises(exc) as ei:
+        crypto.raise_for_verdict(code, 5)
+    assert ei.value.index == 5
+    crypto.raise_for_verdict(ACCEPT, 0)  # no exception
+
+
+def test_mixed_scheme_pack():
+    b = crypto.pack([2, 3, 4], [b"\0" * 64] * 3, [b"\x30\x06\x02\x01\x01\x02\x01\x01", b"", b"\0" * 64], [b"a"] * 3)
+    assert list(b.scheme) == [2, 3, 4]
+    assert np.array_equal(b.sig_len, [8, 0, 64])

@@ -1,0 +1,116 @@
+"""The exact device arithmetic (corda_amd/csrc/cg_*.h), compiled for the host,
+against the oracle: field ops vs Python big ints at and beyond limb bounds,
+Barrett mod L, slide-carry emulation, radix-16 recoding, SHA-512 at every
+alignment, and full verification on the golden fixtures + random batches.
+CPU only; catches limb-bound / carry bugs before a GPU run."""
+from __future__ import annotations
+
+import ctypes
+import hashlib
+import os
+import random
+import subprocess
+
+import pytest
+
+import ed25519_i2p as ED
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SO = os.path.join(ROOT, "tests", "native", "libcg_host.so")
+
+
+@pytest.fixture(scope="module")
+def host():
+    src = os.path.join(ROOT, "tests", "native", "cg_host.cpp")
+    if not os.path.exists(SO) or os.path.getmtime(SO) < max(
+            os.path.getmtime(os.path.join(ROOT, "corda_amd", "csrc", f)) for f in os.listdir(
+                os.path.join(ROOT, "corda_amd", "csrc")) if f.endswith(".h")) or os.path.getmtime(SO) < os.path.getmtime(src):
+        subprocess.check_call(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-I",
+                               os.path.join(ROOT, "corda_amd", "csrc"), src, "-o", SO])
+    lib = ctypes.CDLL(SO)
+    lib.cgh_ed25519_verify.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p,
+                                       ctypes.c_uint32, ctypes.c_uint32]
+    return lib
+
+
+def w8(x):
+    return (ctypes.c_uint32 * 8)(*[(x >> (32 * i)) & 0xFFFFFFFF for i in range(8)])
+
+
+def val(a, n=8):
+    return sum(a[i] << (32 * i) for i in range(n))
+
+
+P, L = ED.P, ED.L
+
+
+def test_field_ops(host):
+    rnd = random.Random(1)
+    out = (ctypes.c_uint32 * 8)()
+    edge = [0, 1, 2, 19, P - 1, P, P + 1, 2**255 - 1, 2**255 - 20, 2**254, 2**26 - 1]
+    for t in range(4000):
+        a = rnd.getrandbits(255) if t % 3 else rnd.choice(edge)
+        b = rnd.getrandbits(255) if t % 5 else rnd.choice(edge)
+        host.cgh_fe_mul(w8(a), w8(b), out)
+        assert val(out) == a * b % P
+        host.cgh_fe_sq(w8(a), out)
+        assert val(out) == a * a % P
+        if t % 20 == 0:
+            host.cgh_fe_invert(w8(a), out)
+            assert val(out) == pow(a, P - 2, P)
+
+
+def test_scalar_ops(host):
+    rnd = random.Random(2)
+    o8 = (ctypes.c_uint32 * 8)()
+    for t in range(4000):
+        x = rnd.getrandbits(512) if t % 4 else rnd.choice([0, L, L - 1, 2 * L, 2**512 - 1])
+        host.cgh_sc_reduce512((ctypes.c_uint32 * 16)(*[(x >> (32 * i)) & 0xFFFFFFFF for i in range(16)]), o8)
+        assert val(o8) == x % L
+        s = rnd.getrandbits(256) | ((t & 1) << 255)
+        if t % 7 == 0:
+            s = (2**256 - 1) ^ (rnd.getrandbits(8) << rnd.randrange(248))
+        sv = ED.slide_value(s.to_bytes(32, "little"))
+        assert bool(host.cgh_slide_drop(w8(s))) == (sv != s)
+        host.cgh_effective_s(w8(s), o8)
+        assert val(o8) == sv % L
+        k = rnd.getrandbits(253) % L
+        host.cgh_recode16(w8(k), o8)
+        pk = val(o8)
+        assert sum((((pk >> (4 * i)) & 15) - 8) * 16**i for i in range(64)) == k
+
+
+def test_sha512_alignment(host):
+    rnd = random.Random(3)
+    buf = rnd.randbytes(1500)
+    mb = (ctypes.c_uint8 * (len(buf) + 16)).from_buffer_copy(buf + bytes(16))
+    o16 = (ctypes.c_uint32 * 16)()
+    for _ in range(300):
+        n, off = rnd.randint(0, 400), rnd.randint(0, 40)
+        r, ab = rnd.randbytes(32), rnd.randbytes(32)
+        host.cgh_sha512_ed25519((ctypes.c_uint32 * 8).from_buffer_copy(r), (ctypes.c_uint32 * 8).from_buffer_copy(ab),
+                                ctypes.byref(mb, off), n, o16)
+        assert bytes(o16) == hashlib.sha512(r + ab + buf[off:off + n]).digest()
+
+
+def test_verify_golden(host, golden_ed25519):
+    for e in golden_ed25519:
+        pk, sig, msg = (bytes.fromhex(e[k]) for k in ("pk", "sig", "msg"))
+        assert host.cgh_ed25519_verify(pk, sig, len(sig), msg, len(msg), 0) == e["is_valid"], e["cls"]
+        assert host.cgh_ed25519_verify(pk, sig, len(sig), msg, len(msg), 1) == e["do_verify"], e["cls"]
+
+
+def test_verify_random_vs_oracle(host, oracle):
+    rnd = random.Random(4)
+    for _ in range(300):
+        seed, msg = rnd.randbytes(32), rnd.randbytes(rnd.randint(0, 130))
+        pk, sig = ED.sign(seed, msg)
+        cases = [(pk, sig), (pk, bytes([sig[0] ^ 4]) + sig[1:])]
+        s = int.from_bytes(sig[32:], "little")
+        for k in (1, 8, 15):
+            if s + k * L < 2**256:
+                cases.append((pk, sig[:32] + (s + k * L).to_bytes(32, "little")))
+        for p, sg in cases:
+            for mode in (0, 1):
+                assert host.cgh_ed25519_verify(p, sg, len(sg), msg, len(msg), mode) == \
+                    oracle.oracle_ed25519_verify(p, sg, len(sg), msg, len(msg), mode)

@@ -1,0 +1,155 @@
+"""The oracle pinned: C restatement vs committed golden fixtures, vs the Python
+twin, vs published known-answer vectors (RFC 8032, RFC 6979) and vs OpenSSL on
+the semantic overlap.  CPU only."""
+from __future__ import annotations
+
+import ctypes
+import hashlib
+import random
+
+import numpy as np
+import pytest
+
+import ecdsa_bc as EC
+import ed25519_i2p as ED
+import merkle_tx as MK
+import openssl_xcheck as OSSL
+
+
+def c_ed(oracle, pk, sig, msg, mode):
+    return oracle.oracle_ed25519_verify(pk, sig, len(sig), msg, len(msg), mode)
+
+
+def c_ec(oracle, scheme, qhex, sig, msg, mode):
+    return oracle.oracle_ecdsa_verify(scheme, bytes.fromhex(qhex), sig, len(sig), msg, len(msg), mode)
+
+
+def test_ed25519_golden(oracle, golden_ed25519):
+    classes = set()
+    for e in golden_ed25519:
+        pk, sig, msg = (bytes.fromhex(e[k]) for k in ("pk", "sig", "msg"))
+        assert c_ed(oracle, pk, sig, msg, 0) == e["is_valid"], e["cls"]
+        assert c_ed(oracle, pk, sig, msg, 1) == e["do_verify"], e["cls"]
+        classes.add(e["cls"].split("_")[0])
+    # every adversarial class of SURVEY.md §8(d) is present
+    assert {f"E{i}" for i in range(1, 13)} <= classes
+
+
+def test_ed25519_golden_python_twin(golden_ed25519):
+    for e in golden_ed25519[::3]:
+        pk, sig, msg = (bytes.fromhex(e[k]) for k in ("pk", "sig", "msg"))
+        assert ED.is_valid(pk, sig, msg) == e["is_valid"]
+        assert ED.do_verify(pk, sig, msg) == e["do_verify"]
+
+
+def test_rfc8032_known_answers(oracle):
+    kat = [("9d61b19deffd5a60ba844af492ec2cc44449c5697b326919703bac031cae7f60", "",
+            "e5564300c360ac729086e2cc806e828a84877f1eb8e5d974d873e065224901555fb8821590a33bacc61e39701cf9b46bd25bf5f0595bbe24655141438e7a100b"),
+           ("4ccd089b28ff96da9db6c346ec114e0f5b8a319f35aba624da8cf6ed4fb8a6fb", "72",
+            "92a009a9f0d4cab8720e820b5f642540a2b27b5416503f8fb3762223ebdb69da085ac1e43e15996e458f3613d0f11d8c387b2eaeb4302aeeb00d291612bb0c00")]
+    for sk, m, sig in kat:
+        pk, s = ED.sign(bytes.fromhex(sk), bytes.fromhex(m))
+        assert s.hex() == sig
+        assert c_ed(oracle, pk, s, bytes.fromhex(m), 0) == ED.ACCEPT
+
+
+def test_ed25519_random_vs_twin_and_openssl(oracle):
+    rnd = random.Random(3)
+    for _ in range(60):
+        seed, msg = rnd.randbytes(32), rnd.randbytes(rnd.randint(1, 150))
+        pk, sig = ED.sign(seed, msg)
+        assert OSSL.ed25519_verify(pk, sig, msg)
+        assert c_ed(oracle, pk, sig, msg, 0) == ED.ACCEPT
+        bad = bytearray(sig)
+        bad[rnd.randrange(64)] ^= 1 << rnd.randrange(8)
+        bad = bytes(bad)
+        v = c_ed(oracle, pk, bad, msg, 0)
+        assert v == ED.is_valid(pk, bad, msg)
+        # overlap: where S < L (OpenSSL's canonical check) the two must agree
+        if int.from_bytes(bad[32:], "little") < ED.L:
+            assert (v == ED.ACCEPT) == OSSL.ed25519_verify(pk, bad, msg)
+
+
+def test_slide_semantics():
+    # S + L is accepted by i2p (no canonical-S check): slide value is S + L
+    s = 12345
+    assert ED.slide_value((s + ED.L).to_bytes(32, "little")) == s + ED.L
+    # a run of ones to bit 255 drops the carry: value is S - 2^256
+    s = 2**256 - 1
+    assert ED.slide_value(s.to_bytes(32, "little")) == s - 2**256
+    assert ED.slide_value((2**255).to_bytes(32, "little")) == 2**255
+
+
+def test_entropy_seed_matches_java_biginteger():
+    assert ED.entropy_seed(20) == bytes([20]) + bytes(31)
+    assert ED.entropy_seed(200) == bytes([0, 200]) + bytes(30)  # toByteArray() sign byte
+
+
+def test_ecdsa_golden(oracle, golden_ecdsa):
+    for e in golden_ecdsa:
+        sig, msg = bytes.fromhex(e["sig"]), bytes.fromhex(e["msg"])
+        assert c_ec(oracle, e["scheme"], e["q"], sig, msg, 0) == e["is_valid"], e["cls"]
+        assert c_ec(oracle, e["scheme"], e["q"], sig, msg, 1) == e["do_verify"], e["cls"]
+
+
+def test_ecdsa_rfc6979_known_answer():
+    d = 0xC9AFA9D845BA75166B5C215767B1D6934E50C3DB36E89B127B8A622B120F6721
+    r, s = EC.sign_rs(3, d, b"sample")
+    assert r == 0xEFD48B2AACB6A8FD1140DD9CD45E81D69D2C877B56AAF991C34D0EA84EAF3716
+    assert s == 0xF7CB1C942D657C41D436C7A1B6E29F65F3E900DBB9AFF4064DC4AB2F843ACDA8
+
+
+def test_ecdsa_openssl_overlap(oracle):
+    rnd = random.Random(8)
+    for scheme in (2, 3):
+        c = EC.CURVES[scheme]
+        for _ in range(15):
+            d = rnd.randrange(1, c.n)
+            q = EC.pubkey(scheme, d)
+            qb = q[0].to_bytes(32, "big") + q[1].to_bytes(32, "big")
+            msg = rnd.randbytes(40)
+            sig = EC.sign(scheme, d, msg)
+            assert OSSL.ecdsa_verify(scheme, qb, sig, hashlib.sha256(msg).digest())
+            assert oracle.oracle_ecdsa_verify(scheme, qb, sig, len(sig), msg, len(msg), 0) == 0
+
+
+def test_der_strictness():
+    r, s = 5, 7
+    good = EC.der_encode(r, s)
+    assert EC.der_decode(good) == (r, s)
+    assert EC.der_decode(good + b"\0") is None                      # trailing data
+    assert EC.der_decode(b"\x30\x81" + good[1:2] + good[2:]) is None  # long form for a short length
+    assert EC.der_decode(b"\x30\x06\x02\x01\x05\x02\x01") is None    # truncated
+    assert EC.der_decode(EC.der_encode(-3, 7)) == (-3, 7)            # negative parses (then range-rejects)
+
+
+def test_merkle_golden(oracle, golden_merkle):
+    for t in golden_merkle["txs"]:
+        comps = [bytes.fromhex(c) for c in t["components"]]
+        salt = bytes.fromhex(t["salt"])
+        assert MK.tx_id(comps, salt).hex() == t["id"]
+        arena = b"".join(comps)
+        offs = np.cumsum([0] + [len(c) for c in comps[:-1]]).astype(np.uint64)
+        lens = np.array([len(c) for c in comps], dtype=np.uint32)
+        start = np.array([0, len(comps)], dtype=np.uint32)
+        out = ctypes.create_string_buffer(32)
+        buf = ctypes.create_string_buffer(arena, len(arena) + 1)
+        assert oracle.oracle_txid_batch(buf, offs.ctypes.data, lens.ctypes.data, start.ctypes.data, salt, 1, out) == 0
+        assert out.raw.hex() == t["id"]
+
+
+def test_merkle_structure_like_reference():
+    # PartialMerkleTreeTest.kt:60-84
+    leaves = [hashlib.sha256(bytes([i])).digest() for i in range(8)]
+    assert MK.merkle_root(leaves[:1]) == leaves[0]
+    h = MK.sha256
+    assert MK.merkle_root(leaves[:3]) == h(h(leaves[0] + leaves[1]) + h(leaves[2] + MK.ZERO_HASH))
+    six = MK.merkle_root(leaves[:6])
+    assert six == MK.merkle_root(leaves[:6] + [MK.ZERO_HASH] * 2)
+    with pytest.raises(MK.MerkleTreeException):
+        MK.merkle_root([])
+
+
+def test_merkle_nonce_is_big_endian_index():
+    salt = bytes(range(32))
+    assert MK.compute_nonce(salt, 1) == hashlib.sha256(salt + b"\0\0\0\1").digest()
