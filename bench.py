@@ -188,11 +188,23 @@ def main():
     achieved = ops_msm * per_launch / avg_msm_s / 1e12 if avg_msm_s > 0 else 0.0
     achieved_prep = ops_prep * per_launch / avg_prep_s / 1e12 if avg_prep_s > 0 else 0.0
     path_ops = OP_MODEL["ed25519_1kb"]["total"]
-    traffic = None
+    traffic, pmc = None, {}
     tpath = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(tpath):
+    if os.path.exists(tpath):  # measured in separate rocprofv3 --pmc passes (tools/pmc_*.sh)
         with open(tpath) as f:
-            traffic = json.load(f).get("ed25519_msm_bytes_per_launch")
+            pmc = json.load(f)
+        traffic = pmc.get("ed25519_msm_bytes_per_launch")
+    hw = None
+    if pmc.get("ed25519_msm_valu_instr_per_verify") and avg_msm_s > 0:
+        # hardware view: VALU lane-instructions actually issued per second (instruction count
+        # per verify from SQ_INSTS_VALU, time from this run's HIP events)
+        lane_ops = pmc["ed25519_msm_valu_instr_per_verify"] * per_launch / avg_msm_s
+        clk = pmc.get("ed25519_msm_effective_clock_GHz")
+        hw = {"valu_instr_per_verify": pmc["ed25519_msm_valu_instr_per_verify"],
+              "valu_lane_ops_T": round(lane_ops / 1e12, 2), "frac_of_peak": round(lane_ops / 1e12 / peak, 3),
+              "pmc_clock_GHz": clk,
+              "frac_of_peak_at_pmc_clock": round(lane_ops / (256 * 64 * clk * 1e9), 3) if clk else None,
+              "source": pmc.get("source")}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -227,7 +239,7 @@ def main():
             "roofline": {"bound": "valu_int32", "kernel": "ed25519_msm", "achieved": round(achieved, 3),
                          "peak": peak, "unit": "TOPS", "frac": round(achieved / peak, 4), "traffic": traffic,
                          "ops_per_unit": ops_msm, "units_per_launch": per_launch,
-                         "avg_launch_ms": round(avg_msm_s * 1e3, 3)},
+                         "avg_launch_ms": round(avg_msm_s * 1e3, 3), "hw_valu": hw},
             "path_frac_of_int32_peak": round(value / world * path_ops / 1e12 / peak, 4),
             "prep_kernel": {"achieved": round(achieved_prep, 3), "avg_launch_ms": round(avg_prep_s * 1e3, 3)},
             "latency": {"p50_device_ms": round(statistics.median(lat_dev) * 1e3, 3) if lat_dev else None,
