@@ -1,4 +1,5 @@
-// Common macros for libcordagpu device code.  Everything in the *.h arithmetic
+// Common macros for libcordagpu device code (CG_HDM: member functions and
+// explicit specializations, which cannot be `static`).  Everything in the *.h arithmetic
 // headers is written as CG_HD so the exact device algorithm can also be compiled
 // for the host (tests/native/) and checked against the CPU oracle there.
 #pragma once
@@ -8,11 +9,13 @@
 #include <hip/hip_runtime.h>
 #define CG_HD __host__ __device__ __forceinline__
 #define CG_DEV __device__ __forceinline__
+#define CG_HDM __host__ __device__ __forceinline__
 #define CG_UNROLL _Pragma("unroll")
 #define CG_NOUNROLL _Pragma("unroll 1")
 #else
 #define CG_HD static inline
 #define CG_DEV static inline
+#define CG_HDM inline
 #define CG_UNROLL _Pragma("GCC unroll 16")
 #define CG_NOUNROLL
 #endif

@@ -1,0 +1,391 @@
+// ECDSA SHA256withECDSA verification with BouncyCastle 1.57 semantics (SURVEY
+// Appendix B) for secp256k1 (scheme 2) and secp256r1 (scheme 3):
+//   B.1 strict DER (StdDSAEncoder.decode + the re-encoding equality check)
+//   B.2 r, s in [1, n-1] (negative INTEGERs parse, then fail the range check)
+//   B.3 e = SHA-256(M) as a 256-bit integer; w = s^-1; u1 = e w, u2 = r w (mod n)
+//   B.4 P = u1 G + u2 Q; infinity -> false
+//   B.5 accept iff x(P) mod n == r (checked projectively: X == r Z^2 or (r+n) Z^2)
+//   B.6 Q affine, x, y < p and on the curve, else the key cannot be built
+// Reference call: Crypto.isValid -> DSABase.engineVerify -> ECDSASigner.verifySignature
+// (/root/reference/core/src/main/kotlin/net/corda/core/crypto/Crypto.kt:534-541).
+// Jacobian arithmetic with explicit infinity flags and exception handling (H == 0),
+// so P = +-T inside the double-scalar loop (reachable with crafted keys) is exact.
+#pragma once
+#include "cg_mp256.h"
+#include "cg_sha256.h"
+
+namespace cg {
+
+enum : uint32_t { DER_OK = 0, DER_RANGE = 1, DER_MALFORMED = 2 };
+
+// ----------------------------------------------------------------- DER
+template <typename Byte>
+CG_HD int der_len(Byte&& b, uint32_t n, uint32_t& i, uint32_t& out) {
+  if (i >= n) return -1;
+  const uint32_t b0 = b(i++);
+  if (b0 < 0x80) {
+    out = b0;
+    return 0;
+  }
+  const uint32_t nb = b0 & 0x7F;
+  if (nb == 0 || nb > 4 || i + nb > n) return -1;
+  if (b(i) == 0) return -1;  // non-minimal
+  uint32_t v = 0;
+  for (uint32_t k = 0; k < nb; ++k) v = v << 8 | b(i++);
+  if (v < 0x80) return -1;
+  out = v;
+  return 0;
+}
+
+// One INTEGER: value into 8 LE words when 0 < v < 2^256; range_bad when v <= 0,
+// v >= 2^256 or v >= order.  Returns -1 on a DER violation.
+template <typename Byte>
+CG_HD int der_int(Byte&& b, uint32_t end, uint32_t& i, const uint32_t order[8], uint32_t out[8], uint32_t& range_bad) {
+  if (i >= end || b(i) != 0x02) return -1;
+  ++i;
+  uint32_t ln;
+  if (der_len(b, end, i, ln) != 0) return -1;
+  if (ln == 0 || ln > end - i) return -1;
+  const uint32_t b0 = b(i), b1 = ln > 1 ? b(i + 1) : 0u;
+  if (ln > 1 && ((b0 == 0x00 && b1 < 0x80) || (b0 == 0xFF && b1 >= 0x80))) return -1;
+  CG_UNROLL for (int k = 0; k < 8; ++k) out[k] = 0;
+  range_bad = 0;
+  if (b0 & 0x80) {
+    range_bad = 1;  // negative
+  } else {
+    uint32_t k = 0;
+    while (k < ln && b(i + k) == 0) ++k;
+    const uint32_t mag = ln - k;
+    if (mag == 0 || mag > 32) {
+      range_bad = 1;
+    } else {
+      for (uint32_t m = 0; m < mag; ++m) {  // big-endian bytes -> LE words
+        const uint32_t pos = mag - 1 - m;    // byte significance
+        const uint32_t byte = b(i + k + m);
+        for (int wi = 0; wi < 8; ++wi)
+          if ((uint32_t)wi == (pos >> 2)) out[wi] |= byte << (8 * (pos & 3));
+      }
+      if (!mp_lt(out, order)) range_bad = 1;
+    }
+  }
+  i += ln;
+  return 0;
+}
+
+// BC StdDSAEncoder.decode as a strict grammar -> DER_OK / DER_RANGE / DER_MALFORMED.
+template <typename Byte>
+CG_HD uint32_t der_parse(Byte&& b, uint32_t n, const uint32_t order[8], uint32_t r[8], uint32_t s[8]) {
+  CG_UNROLL for (int k = 0; k < 8; ++k) { r[k] = 0; s[k] = 0; }
+  if (n < 2 || b(0) != 0x30) return DER_MALFORMED;
+  uint32_t i = 1, ln;
+  if (der_len(b, n, i, ln) != 0) return DER_MALFORMED;
+  if (ln != n - i) return DER_MALFORMED;  // trailing bytes or truncated
+  uint32_t rb, sb;
+  if (der_int(b, n, i, order, r, rb) != 0) return DER_MALFORMED;
+  if (der_int(b, n, i, order, s, sb) != 0) return DER_MALFORMED;
+  if (i != n) return DER_MALFORMED;  // a third element
+  return (rb | sb) ? DER_RANGE : DER_OK;
+}
+
+// ------------------------------------------------------------ points
+struct jpt {
+  uint32_t X[8], Y[8], Z[8];
+  uint32_t inf;
+};
+
+template <class C>
+CG_HD void ec_dbl(jpt& r, const jpt& p) {
+  uint32_t t0[8], t1[8], t2[8], t3[8], x3[8], y3[8], z3[8];
+  if (C::kAMinus3) {
+    // dbl-2001-b: delta = Z^2, gamma = Y^2, beta = X gamma, alpha = 3 (X - delta)(X + delta)
+    uint32_t delta[8], gamma[8], beta[8], alpha[8];
+    fp_sqr<C>(delta, p.Z);
+    fp_sqr<C>(gamma, p.Y);
+    fp_mul<C>(beta, p.X, gamma);
+    fp_sub<C>(t0, p.X, delta);
+    fp_add<C>(t1, p.X, delta);
+    fp_mul<C>(t2, t0, t1);
+    fp_add<C>(alpha, t2, t2);
+    fp_add<C>(alpha, alpha, t2);
+    fp_sqr<C>(x3, alpha);
+    fp_add<C>(t0, beta, beta);   // 2 beta
+    fp_add<C>(t0, t0, t0);       // 4 beta
+    fp_add<C>(t1, t0, t0);       // 8 beta
+    fp_sub<C>(x3, x3, t1);
+    fp_add<C>(t2, p.Y, p.Z);
+    fp_sqr<C>(z3, t2);
+    fp_sub<C>(z3, z3, gamma);
+    fp_sub<C>(z3, z3, delta);
+    fp_sub<C>(t0, t0, x3);       // 4 beta - X3
+    fp_mul<C>(y3, alpha, t0);
+    fp_sqr<C>(t3, gamma);
+    fp_add<C>(t3, t3, t3);
+    fp_add<C>(t3, t3, t3);
+    fp_add<C>(t3, t3, t3);       // 8 gamma^2
+    fp_sub<C>(y3, y3, t3);
+  } else {
+    // dbl-2009-l (a = 0)
+    uint32_t A[8], B[8], Cc[8], D[8], E[8], F[8];
+    fp_sqr<C>(A, p.X);
+    fp_sqr<C>(B, p.Y);
+    fp_sqr<C>(Cc, B);
+    fp_add<C>(t0, p.X, B);
+    fp_sqr<C>(t1, t0);
+    fp_sub<C>(t1, t1, A);
+    fp_sub<C>(t1, t1, Cc);
+    fp_add<C>(D, t1, t1);
+    fp_add<C>(E, A, A);
+    fp_add<C>(E, E, A);
+    fp_sqr<C>(F, E);
+    fp_add<C>(t2, D, D);
+    fp_sub<C>(x3, F, t2);
+    fp_sub<C>(t2, D, x3);
+    fp_mul<C>(y3, E, t2);
+    fp_add<C>(t3, Cc, Cc);
+    fp_add<C>(t3, t3, t3);
+    fp_add<C>(t3, t3, t3);
+    fp_sub<C>(y3, y3, t3);
+    fp_mul<C>(z3, p.Y, p.Z);
+    fp_add<C>(z3, z3, z3);
+  }
+  CG_UNROLL for (int i = 0; i < 8; ++i) { r.X[i] = x3[i]; r.Y[i] = y3[i]; r.Z[i] = z3[i]; }
+  r.inf = p.inf;
+}
+
+// r = p + q (Jacobian + Jacobian, or affine q when AFFINE: q.Z ignored == 1).
+// q_skip: q is the identity (digit 0).  Exact in every case.
+template <class C, bool AFFINE>
+CG_HD void ec_add(jpt& r, const jpt& p, const jpt& q, uint32_t q_skip) {
+  uint32_t z1z1[8], u1[8], u2[8], s1[8], s2[8], t[8], h[8], rr[8], hh[8], hhh[8], v[8], x3[8], y3[8], z3[8];
+  fp_sqr<C>(z1z1, p.Z);
+  if (AFFINE) {
+    CG_UNROLL for (int i = 0; i < 8; ++i) { u1[i] = p.X[i]; s1[i] = p.Y[i]; }
+  } else {
+    uint32_t z2z2[8];
+    fp_sqr<C>(z2z2, q.Z);
+    fp_mul<C>(u1, p.X, z2z2);
+    fp_mul<C>(t, q.Z, z2z2);
+    fp_mul<C>(s1, p.Y, t);
+  }
+  fp_mul<C>(u2, q.X, z1z1);
+  fp_mul<C>(t, p.Z, z1z1);
+  fp_mul<C>(s2, q.Y, t);
+  fp_sub<C>(h, u2, u1);
+  fp_sub<C>(rr, s2, s1);
+  fp_sqr<C>(hh, h);
+  fp_mul<C>(hhh, h, hh);
+  fp_mul<C>(v, u1, hh);
+  fp_sqr<C>(x3, rr);
+  fp_sub<C>(x3, x3, hhh);
+  fp_sub<C>(x3, x3, v);
+  fp_sub<C>(x3, x3, v);
+  fp_sub<C>(t, v, x3);
+  fp_mul<C>(y3, rr, t);
+  fp_mul<C>(t, s1, hhh);
+  fp_sub<C>(y3, y3, t);
+  if (AFFINE) {
+    fp_mul<C>(z3, p.Z, h);
+  } else {
+    fp_mul<C>(t, p.Z, q.Z);
+    fp_mul<C>(z3, t, h);
+  }
+  const uint32_t hz = mp_iszero(h), rz = mp_iszero(rr);
+  jpt out;
+  CG_UNROLL for (int i = 0; i < 8; ++i) { out.X[i] = x3[i]; out.Y[i] = y3[i]; out.Z[i] = z3[i]; }
+  out.inf = 0;
+  const uint32_t live = !p.inf & !q_skip;
+  if (live & hz) {  // P == +-Q: rare (crafted keys only); divergent branch, exact result
+    if (rz) {
+      ec_dbl<C>(out, p);
+    } else {
+      out.inf = 1;
+    }
+  }
+  // P = O -> Q ; Q skipped -> P
+  const uint32_t take_q = p.inf & !q_skip, take_p = q_skip;
+  jpt qq = q;
+  if (AFFINE) {
+    CG_UNROLL for (int i = 0; i < 8; ++i) qq.Z[i] = 0;
+    qq.Z[0] = 1;
+    qq.inf = 0;
+  }
+  mp_select(out.X, out.X, qq.X, take_q);
+  mp_select(out.Y, out.Y, qq.Y, take_q);
+  mp_select(out.Z, out.Z, qq.Z, take_q);
+  out.inf = take_q ? qq.inf : out.inf;
+  mp_select(out.X, out.X, p.X, take_p);
+  mp_select(out.Y, out.Y, p.Y, take_p);
+  mp_select(out.Z, out.Z, p.Z, take_p);
+  out.inf = take_p ? p.inf : out.inf;
+  r = out;
+}
+
+template <class C>
+CG_HD uint32_t ec_on_curve(const uint32_t x[8], const uint32_t y[8]) {
+  uint32_t pp[8], lhs[8], rhs[8], t[8], b[8];
+  C::p(pp);
+  if (!mp_lt(x, pp) || !mp_lt(y, pp)) return 0;
+  fp_sqr<C>(lhs, y);
+  fp_sqr<C>(rhs, x);
+  fp_mul<C>(rhs, rhs, x);
+  if (C::kAMinus3) {
+    fp_add<C>(t, x, x);
+    fp_add<C>(t, t, x);
+    fp_sub<C>(rhs, rhs, t);
+  }
+  C::b(b);
+  fp_add<C>(rhs, rhs, b);
+  return mp_eq(lhs, rhs);
+}
+
+// 8 big-endian bytes-as-LE-words (staged layout) -> LE limbs of a 256-bit BE number
+CG_HD void be_words_to_limbs(uint32_t out[8], const uint32_t w[8]) {
+  CG_UNROLL for (int i = 0; i < 8; ++i) out[i] = bswap32_(w[7 - i]);
+}
+
+// Signed radix-16 digits of k < 2^256 (65 digits, e_i = d_i + 8 packed in nibbles
+// of 9 words; d_64 in {0, 1}).
+CG_HD void recode16_65(uint32_t packed[9], const uint32_t k[8]) {
+  uint32_t carry = 0;
+  CG_UNROLL for (int w = 0; w < 8; ++w) {
+    uint32_t out = 0;
+    CG_UNROLL for (int nib = 0; nib < 8; ++nib) {
+      const uint32_t v = ((k[w] >> (4 * nib)) & 15) + carry;
+      carry = v >= 8;
+      out |= (v + 8 - 16 * carry) << (4 * nib);
+    }
+    packed[w] = out;
+  }
+  packed[8] = carry + 8;
+}
+
+// Phase 1: everything up to the scalars; returns the pre-verdict
+// (V_* codes of cg_ed25519.h: 0 accept .. 4 arg-empty, 0xff compute).
+template <class C>
+CG_HD uint32_t ecdsa_prep(const uint32_t qx[8], const uint32_t qy[8], uint32_t der_status, const uint32_t r[8],
+                          const uint32_t s[8], uint32_t sig_len, const uint8_t* msg, uint32_t msg_len, uint32_t mode,
+                          uint32_t d1[9], uint32_t d2[9]) {
+  if (!ec_on_curve<C>(qx, qy)) return 3;                        // KEY_INVALID
+  if (mode == 1 && (sig_len == 0 || msg_len == 0)) return 4;      // ARG_EMPTY (doVerify)
+  if (der_status == DER_MALFORMED) return 2;                      // SIG_MALFORMED
+  if (der_status == DER_RANGE) return 1;                          // REJECT
+  uint32_t hbe[8], e[8], nn[8], t[8], w[8], u1[8], u2[8];
+  sha256_mem(hbe, msg, msg_len);
+  CG_UNROLL for (int i = 0; i < 8; ++i) e[i] = hbe[7 - i];
+  C::n(nn);
+  const uint32_t bw = mp_sub(t, e, nn);
+  mp_select(e, t, e, bw);  // e mod n (e < 2^256 < 2n)
+  mn_inv<C>(w, s);
+  mn_mulmod<C>(u1, e, w);
+  mn_mulmod<C>(u2, r, w);
+  recode16_65(d1, u1);
+  recode16_65(d2, u2);
+  return 0xff;
+}
+
+// P = u1 G + u2 Q from the packed digits; getQ(k, jpt&) loads k*Q (k = 1..8),
+// getG(k, jpt&) loads affine k*G.
+template <class C, typename GetQ, typename GetG>
+CG_HD void ecdsa_joint(jpt& acc, uint32_t d1[9], uint32_t d2[9], GetQ&& getQ, GetG&& getG) {
+  jpt t;
+  CG_UNROLL for (int i = 0; i < 8; ++i) { acc.X[i] = 0; acc.Y[i] = 0; acc.Z[i] = 0; }
+  acc.inf = 1;
+  CG_NOUNROLL for (int i = 64; i >= 0; --i) {
+    if (i != 64) {
+      CG_NOUNROLL for (int k = 0; k < 4; ++k) ec_dbl<C>(acc, acc);
+    }
+    const uint32_t eg = i == 64 ? (d1[8] & 15) : (d1[7] >> 28);  // digit of u1 (G)
+    const uint32_t eq = i == 64 ? (d2[8] & 15) : (d2[7] >> 28);  // digit of u2 (Q)
+    if (i != 64) {
+      CG_UNROLL for (int w = 7; w > 0; --w) {
+        d1[w] = d1[w] << 4 | d1[w - 1] >> 28;
+        d2[w] = d2[w] << 4 | d2[w - 1] >> 28;
+      }
+      d1[0] <<= 4;
+      d2[0] <<= 4;
+    }
+    // Q part
+    {
+      const uint32_t neg = eq < 8, a = neg ? 8 - eq : eq - 8;
+      getQ(a == 0 ? 1u : a, t);
+      uint32_t ny[8];
+      fp_neg<C>(ny, t.Y);
+      mp_select(t.Y, t.Y, ny, neg);
+      t.inf = 0;
+      ec_add<C, false>(acc, acc, t, a == 0);
+    }
+    // G part (affine)
+    {
+      const uint32_t neg = eg < 8, a = neg ? 8 - eg : eg - 8;
+      getG(a == 0 ? 1u : a, t);
+      uint32_t ny[8];
+      fp_neg<C>(ny, t.Y);
+      mp_select(t.Y, t.Y, ny, neg);
+      t.inf = 0;
+      ec_add<C, true>(acc, acc, t, a == 0);
+    }
+  }
+}
+
+// Phase 2: joint multiplication + the projective x check.  Returns ACCEPT (0) / REJECT (1).
+template <class C, typename GetQ, typename GetG>
+CG_HD uint32_t ecdsa_msm_check(uint32_t d1[9], uint32_t d2[9], const uint32_t r[8], GetQ&& getQ, GetG&& getG) {
+  jpt acc;
+  ecdsa_joint<C>(acc, d1, d2, getQ, getG);
+  if (acc.inf) return 1;
+  // x(P) mod n == r  <=>  X == r Z^2  or  (r + n < p and X == (r + n) Z^2)
+  uint32_t z2[8], rz[8], nn[8], pp[8], rn[8];
+  fp_sqr<C>(z2, acc.Z);
+  fp_mul<C>(rz, r, z2);
+  if (mp_eq(rz, acc.X)) return 0;
+  C::n(nn);
+  C::p(pp);
+  const uint32_t carry = mp_add(rn, r, nn);
+  if (!carry && mp_lt(rn, pp)) {
+    fp_mul<C>(rz, rn, z2);
+    if (mp_eq(rz, acc.X)) return 0;
+  }
+  return 1;
+}
+
+// k*Q, k = 1..8, Jacobian (Q affine, on the curve, prime order: no exceptions).
+template <class C, typename Put>
+CG_HD void ecdsa_q_table(const uint32_t qx[8], const uint32_t qy[8], Put&& put) {
+  jpt q1, cur, t;
+  CG_UNROLL for (int i = 0; i < 8; ++i) { q1.X[i] = qx[i]; q1.Y[i] = qy[i]; q1.Z[i] = 0; }
+  q1.Z[0] = 1;
+  q1.inf = 0;
+  put(1, q1);
+  cur = q1;
+  CG_NOUNROLL for (int k = 2; k <= 8; ++k) {
+    ec_add<C, true>(t, cur, q1, 0);
+    cur = t;
+    put(k, cur);
+  }
+}
+
+// Affine k*G (k = 1..8) for the shared generator table (host-side setup).
+template <class C>
+CG_HD void ecdsa_g_table(jpt tab[9]) {
+  const uint32_t k1x[8] = {0x16F81798u, 0x59F2815Bu, 0x2DCE28D9u, 0x029BFCDBu, 0xCE870B07u, 0x55A06295u, 0xF9DCBBACu, 0x79BE667Eu};
+  const uint32_t k1y[8] = {0xFB10D4B8u, 0x9C47D08Fu, 0xA6855419u, 0xFD17B448u, 0x0E1108A8u, 0x5DA4FBFCu, 0x26A3C465u, 0x483ADA77u};
+  const uint32_t r1x[8] = {0xD898C296u, 0xF4A13945u, 0x2DEB33A0u, 0x77037D81u, 0x63A440F2u, 0xF8BCE6E5u, 0xE12C4247u, 0x6B17D1F2u};
+  const uint32_t r1y[8] = {0x37BF51F5u, 0xCBB64068u, 0x6B315ECEu, 0x2BCE3357u, 0x7C0F9E16u, 0x8EE7EB4Au, 0xFE1A7F9Bu, 0x4FE342E2u};
+  uint32_t gx[8], gy[8];
+  for (int i = 0; i < 8; ++i) {
+    gx[i] = C::kScheme == 2 ? k1x[i] : r1x[i];
+    gy[i] = C::kScheme == 2 ? k1y[i] : r1y[i];
+  }
+  ecdsa_q_table<C>(gx, gy, [&](int k, const jpt& p) {
+    uint32_t zi[8], zi2[8], zi3[8];
+    fp_inv<C>(zi, p.Z);
+    fp_sqr<C>(zi2, zi);
+    fp_mul<C>(zi3, zi2, zi);
+    fp_mul<C>(tab[k].X, p.X, zi2);
+    fp_mul<C>(tab[k].Y, p.Y, zi3);
+    for (int i = 0; i < 8; ++i) tab[k].Z[i] = i == 0;
+    tab[k].inf = 0;
+  });
+}
+
+}  // namespace cg

@@ -1,25 +1,25 @@
 // Host-side interface of the ECDSA (secp256k1 / secp256r1) kernels (K2-K4).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <stdint.h>
 
 namespace cg {
 
-struct EcdsaConsts;  // device-resident curve constants + generator tables
+struct EcdsaConsts;  // per-context: generator tables + scratch
 
-// Device-resident SoA subset of one curve.
+// Device-resident SoA subset of one curve (see ecdsa_kernels.hip for the layout).
 struct EcdsaBatch {
   uint32_t n = 0;
   int scheme = 0;
   uint32_t* index = nullptr;    // positions in the full batch
-  uint32_t* q = nullptr;        // [16][n] X||Y words (little-endian limbs)
-  uint8_t* der = nullptr;       // [n][kDerStride] raw signature bytes
-  uint32_t* der_len = nullptr;  // [n]
+  uint32_t* q = nullptr;        // [16][n]
+  uint32_t* rs = nullptr;       // [16][n]
+  uint32_t* der = nullptr;      // [n] DER status
+  uint32_t* sig_len = nullptr;  // [n]
   uint64_t* msg_off = nullptr;  // [n]
   uint32_t* msg_len = nullptr;  // [n]
 };
-
-constexpr uint32_t kDerStride = 80;  // bytes kept per DER signature on the device
 
 hipError_t ecdsa_consts_create(EcdsaConsts** out);
 void ecdsa_consts_free(EcdsaConsts* c);
@@ -27,8 +27,12 @@ hipError_t ecdsa_batch_stage(EcdsaBatch& b, int scheme, const uint32_t* host_ind
                              const uint8_t* pk_raw_dev, size_t pk_stride, const uint8_t* sig_raw_dev,
                              size_t sig_stride, const uint32_t* sig_len_dev, const uint64_t* msg_off_all_dev,
                              const uint32_t* msg_len_all_dev, hipStream_t s);
-hipError_t ecdsa_batch_verify(const EcdsaBatch& b, const EcdsaConsts* c, const uint8_t* arena, uint32_t mode,
+hipError_t ecdsa_batch_verify(const EcdsaBatch& b, EcdsaConsts* c, const uint8_t* arena, uint32_t mode,
                               uint8_t* verdict, hipStream_t s);
 void ecdsa_batch_free(EcdsaBatch& b);
+// K4 alone: strict DER -> rs [16][cap] LE limbs + status [cap] (0 ok, 1 range, 2 malformed)
+hipError_t launch_der_parse(int scheme, const uint8_t* sig, size_t stride, const uint32_t* sig_len,
+                            uint32_t fill_len, const uint32_t* idx, uint32_t n, uint32_t cap, uint32_t* rs,
+                            uint32_t* der, hipStream_t s);
 
 }  // namespace cg

@@ -500,6 +500,72 @@ cg_status cg_verify_batch(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
   return st;
 }
 
+cg_status cg_der_parse_batch(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const uint8_t* sig,
+                             size_t sig_stride, const uint32_t* sig_len, uint8_t* rs_out, uint8_t* status_out) {
+  if (!ctx) return CG_E_INVALID_ARGUMENT;
+  if (n == 0) return CG_OK;
+  if (!sig || !rs_out || !status_out) return fail(ctx, CG_E_INVALID_ARGUMENT, "null pointer");
+  if (n > 0xFFFFFFF0ull) return fail(ctx, CG_E_INVALID_ARGUMENT, "batch too large");
+  for (size_t i = 0; sig_len && i < n; ++i)
+    if (sig_len[i] > sig_stride) return fail(ctx, CG_E_INVALID_ARGUMENT, "signature longer than sig_stride");
+  if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, CG_E_DEVICE, "hipSetDevice");
+  std::vector<uint32_t> idx[2];
+  for (size_t i = 0; i < n; ++i)
+    idx[(scheme_id && scheme_id[i] == CG_SCHEME_ECDSA_SECP256K1_SHA256) ? 0 : 1].push_back((uint32_t)i);
+  uint8_t* sig_d = nullptr;
+  uint32_t *sl_d = nullptr, *rs_d = nullptr, *st_d = nullptr, *ix_d = nullptr;
+  cg_status st = CG_OK;
+  auto cleanup = [&]() {
+    (void)hipStreamSynchronize(ctx->stream);
+    dfree(sig_d); dfree(sl_d); dfree(rs_d); dfree(st_d); dfree(ix_d);
+  };
+  if ((st = upload(ctx, &sig_d, sig, n * sig_stride, "upload sig")) != CG_OK ||
+      (sig_len && (st = upload(ctx, &sl_d, sig_len, n, "upload sig_len")) != CG_OK) ||
+      (st = dalloc(ctx, &rs_d, 16 * n, "alloc rs")) != CG_OK || (st = dalloc(ctx, &st_d, n, "alloc status")) != CG_OK ||
+      (st = dalloc(ctx, &ix_d, n, "alloc index")) != CG_OK) {
+    cleanup();
+    return st;
+  }
+  // results are written in subset order; scatter back on the host
+  std::vector<uint32_t> rs_h(16 * n), st_h(n);
+  size_t done = 0;
+  for (int c = 0; c < 2; ++c) {
+    const uint32_t m = (uint32_t)idx[c].size();
+    if (!m) continue;
+    hipError_t e = hipMemcpyAsync(ix_d + done, idx[c].data(), (size_t)m * 4, hipMemcpyHostToDevice, ctx->stream);
+    {
+      Timed t(ctx, "der_parse", m);
+      if (e == hipSuccess)
+        e = cg::launch_der_parse(c == 0 ? 2 : 3, sig_d, sig_stride, sl_d, (uint32_t)sig_stride, ix_d + done, m, m,
+                                 rs_d + 16 * done, st_d + done, ctx->stream);
+    }
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(rs_h.data() + 16 * done, rs_d + 16 * done, (size_t)16 * m * 4, hipMemcpyDeviceToHost,
+                         ctx->stream);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(st_h.data() + done, st_d + done, (size_t)m * 4, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) {
+      cleanup();
+      return hip_fail(ctx, e, "der parse");
+    }
+    for (uint32_t j = 0; j < m; ++j) {
+      const size_t dst = idx[c][j];
+      status_out[dst] = (uint8_t)st_h[done + j];
+      for (int half = 0; half < 2; ++half)
+        for (int w = 0; w < 8; ++w) {
+          const uint32_t limb = rs_h[16 * done + (size_t)(8 * half + w) * m + j];
+          uint8_t* o = rs_out + dst * 64 + 32 * half + 4 * (7 - w);  // big-endian bytes
+          o[0] = (uint8_t)(limb >> 24); o[1] = (uint8_t)(limb >> 16); o[2] = (uint8_t)(limb >> 8); o[3] = (uint8_t)limb;
+        }
+    }
+    done += m;
+  }
+  cleanup();
+  collect_timings(ctx);
+  return CG_OK;
+}
+
 cg_status cg_set_profiling(cg_ctx* ctx, int enable) {
   if (!ctx) return CG_E_INVALID_ARGUMENT;
   ctx->profiling = enable != 0;

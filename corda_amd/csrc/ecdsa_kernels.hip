@@ -1,0 +1,274 @@
+// K2 (secp256r1 / P-256) + K3 (secp256k1) ECDSA verification and K4 DER pre-pass
+// for gfx950, BouncyCastle 1.57 semantics (cg_ecdsa.h).
+//
+//   cg_der_parse<C>   staging-time pre-pass: strict DER -> r, s limbs + status
+//   cg_ecdsa_prep<C>  key check, SHA-256(M), s^-1 / u1 / u2 mod n, digits, k*Q table
+//   cg_ecdsa_msm<C>   u1 G + u2 Q (fixed 4-bit window, G table in LDS), x check
+//
+// Device layout (cap = subset size, scap = scratch chunk):
+//   q[w*cap+i] (16 words: the 64-byte big-endian X||Y as staged little-endian
+//   words), rs[w*cap+i] (16 LE limbs: r then s), der[i], sig_len[i], msg_off[i],
+//   msg_len[i]; scratch status[i], digits[w*scap+i] (18 words), qtab[(e*24+w)*scap+i]
+//   (e = k-1 for k*Q, k = 1..8, X|Y|Z).
+#include <vector>
+
+#include "cg_ecdsa.h"
+#include "cg_ecdsa_api.h"
+#include "cg_kernels.h"
+
+using namespace cg;
+
+namespace cg {
+
+struct EcdsaConsts {
+  uint32_t* gtab[2] = {nullptr, nullptr};  // [8][16] affine k*G, K1 then R1
+  uint32_t scap = 0;
+  uint32_t* status = nullptr;
+  uint32_t* digits = nullptr;
+  uint32_t* qtab = nullptr;
+};
+
+}  // namespace cg
+
+namespace {
+
+constexpr uint32_t kEcChunk = 1u << 20;
+constexpr int kQWords = 24;
+
+template <class C>
+__global__ __launch_bounds__(256) void cg_der_parse(const uint8_t* __restrict__ sig, size_t stride,
+                                                    const uint32_t* __restrict__ sig_len, uint32_t fill_len,
+                                                    const uint32_t* __restrict__ idx, uint32_t n, uint32_t cap,
+                                                    uint32_t* __restrict__ rs, uint32_t* __restrict__ der) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const size_t e = idx ? idx[i] : i;
+  const uint8_t* p = sig + e * stride;
+  uint32_t len = sig_len ? sig_len[e] : fill_len;
+  if (len > stride) len = (uint32_t)stride;  // host rejects this case; never read past the slot
+  uint32_t nn[8], r[8], s[8];
+  C::n(nn);
+  const uint32_t st = der_parse([&](uint32_t j) { return (uint32_t)p[j]; }, len, nn, r, s);
+  CG_UNROLL for (int w = 0; w < 8; ++w) {
+    rs[(size_t)w * cap + i] = r[w];
+    rs[(size_t)(8 + w) * cap + i] = s[w];
+  }
+  der[i] = st;
+}
+
+template <class C>
+__global__ __launch_bounds__(256) void cg_ecdsa_prep(const uint32_t* __restrict__ q, const uint32_t* __restrict__ rs,
+                                                     const uint32_t* __restrict__ der,
+                                                     const uint32_t* __restrict__ sig_len,
+                                                     const uint8_t* __restrict__ arena,
+                                                     const uint64_t* __restrict__ msg_off,
+                                                     const uint32_t* __restrict__ msg_len, uint32_t n, uint32_t cap,
+                                                     uint32_t scap, uint32_t mode, uint32_t* __restrict__ status,
+                                                     uint32_t* __restrict__ digits, uint32_t* __restrict__ qtab) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t qw[16], qx[8], qy[8], r[8], s[8], d1[9], d2[9];
+  CG_UNROLL for (int w = 0; w < 16; ++w) qw[w] = q[(size_t)w * cap + i];
+  be_words_to_limbs(qx, qw);
+  be_words_to_limbs(qy, qw + 8);
+  CG_UNROLL for (int w = 0; w < 8; ++w) {
+    r[w] = rs[(size_t)w * cap + i];
+    s[w] = rs[(size_t)(8 + w) * cap + i];
+  }
+  const uint32_t pre =
+      ecdsa_prep<C>(qx, qy, der[i], r, s, sig_len[i], arena + msg_off[i], msg_len[i], mode, d1, d2);
+  status[i] = pre;
+  if (pre != 0xff) return;
+  CG_UNROLL for (int w = 0; w < 9; ++w) {
+    digits[(size_t)w * scap + i] = d1[w];
+    digits[(size_t)(9 + w) * scap + i] = d2[w];
+  }
+  ecdsa_q_table<C>(qx, qy, [&](int k, const jpt& p) {
+    uint32_t* base = qtab + (size_t)(k - 1) * kQWords * scap + i;
+    CG_UNROLL for (int w = 0; w < 8; ++w) {
+      base[(size_t)w * scap] = p.X[w];
+      base[(size_t)(8 + w) * scap] = p.Y[w];
+      base[(size_t)(16 + w) * scap] = p.Z[w];
+    }
+  });
+}
+
+template <class C>
+__global__ __launch_bounds__(256) void cg_ecdsa_msm(const uint32_t* __restrict__ rs,
+                                                    const uint32_t* __restrict__ status,
+                                                    const uint32_t* __restrict__ digits,
+                                                    const uint32_t* __restrict__ qtab,
+                                                    const uint32_t* __restrict__ gtab_g, uint32_t n, uint32_t cap,
+                                                    uint32_t scap, const uint32_t* __restrict__ out_index,
+                                                    uint8_t* __restrict__ verdict) {
+  __shared__ uint32_t gtab[8 * 16];
+  for (int t = threadIdx.x; t < 8 * 16; t += blockDim.x) gtab[t] = gtab_g[t];
+  __syncthreads();
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t dst = out_index[i];
+  const uint32_t st = status[i];
+  if (st != 0xff) {
+    verdict[dst] = (uint8_t)st;
+    return;
+  }
+  uint32_t d1[9], d2[9], r[8];
+  CG_UNROLL for (int w = 0; w < 9; ++w) {
+    d1[w] = digits[(size_t)w * scap + i];
+    d2[w] = digits[(size_t)(9 + w) * scap + i];
+  }
+  CG_UNROLL for (int w = 0; w < 8; ++w) r[w] = rs[(size_t)w * cap + i];
+  const uint32_t v = ecdsa_msm_check<C>(
+      d1, d2, r,
+      [&](uint32_t k, jpt& p) {
+        const uint32_t* base = qtab + (size_t)(k - 1) * kQWords * scap + i;
+        CG_UNROLL for (int w = 0; w < 8; ++w) {
+          p.X[w] = base[(size_t)w * scap];
+          p.Y[w] = base[(size_t)(8 + w) * scap];
+          p.Z[w] = base[(size_t)(16 + w) * scap];
+        }
+        p.inf = 0;
+      },
+      [&](uint32_t k, jpt& p) {
+        const uint32_t* g = gtab + (k - 1) * 16;
+        CG_UNROLL for (int w = 0; w < 8; ++w) {
+          p.X[w] = g[w];
+          p.Y[w] = g[8 + w];
+          p.Z[w] = w == 0;
+        }
+        p.inf = 0;
+      });
+  verdict[dst] = (uint8_t)v;
+}
+
+inline dim3 grid_for(uint32_t n) { return dim3((n + 255) / 256); }
+
+template <class C>
+void g_table_words(uint32_t out[128]) {
+  jpt tab[9];
+  ecdsa_g_table<C>(tab);
+  for (int k = 1; k <= 8; ++k)
+    for (int w = 0; w < 8; ++w) {
+      out[(k - 1) * 16 + w] = tab[k].X[w];
+      out[(k - 1) * 16 + 8 + w] = tab[k].Y[w];
+    }
+}
+
+hipError_t ensure_scratch(EcdsaConsts* c, uint32_t need) {
+  const uint32_t want = need < kEcChunk ? need : kEcChunk;
+  if (c->scap >= want) return hipSuccess;
+  if (c->status) (void)hipFree(c->status);
+  if (c->digits) (void)hipFree(c->digits);
+  if (c->qtab) (void)hipFree(c->qtab);
+  c->status = c->digits = c->qtab = nullptr;
+  c->scap = 0;
+  hipError_t e = hipMalloc((void**)&c->status, (size_t)want * 4);
+  if (e == hipSuccess) e = hipMalloc((void**)&c->digits, (size_t)18 * want * 4);
+  if (e == hipSuccess) e = hipMalloc((void**)&c->qtab, (size_t)8 * kQWords * want * 4);
+  if (e == hipSuccess) c->scap = want;
+  return e;
+}
+
+template <class C>
+hipError_t verify_curve(const EcdsaBatch& b, EcdsaConsts* c, const uint8_t* arena, uint32_t mode, uint8_t* verdict,
+                        hipStream_t s) {
+  hipError_t e = ensure_scratch(c, b.n);
+  if (e != hipSuccess) return e;
+  const uint32_t* gt = c->gtab[C::kScheme == 2 ? 0 : 1];
+  for (uint32_t base = 0; base < b.n; base += c->scap) {
+    const uint32_t cnt = b.n - base < c->scap ? b.n - base : c->scap;
+    hipLaunchKernelGGL(cg_ecdsa_prep<C>, grid_for(cnt), dim3(256), 0, s, b.q + base, b.rs + base, b.der + base,
+                       b.sig_len + base, arena, b.msg_off + base, b.msg_len + base, cnt, b.n, c->scap, mode,
+                       c->status, c->digits, c->qtab);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(cg_ecdsa_msm<C>, grid_for(cnt), dim3(256), 0, s, b.rs + base, c->status, c->digits, c->qtab,
+                       gt, cnt, b.n, c->scap, b.index + base, verdict);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+}  // namespace
+
+namespace cg {
+
+hipError_t ecdsa_consts_create(EcdsaConsts** out) {
+  EcdsaConsts* c = new EcdsaConsts();
+  uint32_t w[2][128];
+  g_table_words<CurveK1>(w[0]);
+  g_table_words<CurveR1>(w[1]);
+  for (int k = 0; k < 2; ++k) {
+    hipError_t e = hipMalloc((void**)&c->gtab[k], sizeof w[k]);
+    if (e == hipSuccess) e = hipMemcpy(c->gtab[k], w[k], sizeof w[k], hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+      ecdsa_consts_free(c);
+      return e;
+    }
+  }
+  *out = c;
+  return hipSuccess;
+}
+
+void ecdsa_consts_free(EcdsaConsts* c) {
+  if (!c) return;
+  for (auto* p : {c->gtab[0], c->gtab[1], c->status, c->digits, c->qtab})
+    if (p) (void)hipFree(p);
+  delete c;
+}
+
+void ecdsa_batch_free(EcdsaBatch& b) {
+  for (void* p : {(void*)b.index, (void*)b.q, (void*)b.rs, (void*)b.der, (void*)b.sig_len, (void*)b.msg_off,
+                  (void*)b.msg_len})
+    if (p) (void)hipFree(p);
+  b = EcdsaBatch();
+}
+
+hipError_t launch_der_parse(int scheme, const uint8_t* sig, size_t stride, const uint32_t* sig_len,
+                            uint32_t fill_len, const uint32_t* idx, uint32_t n, uint32_t cap, uint32_t* rs,
+                            uint32_t* der, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  if (scheme == 2)
+    hipLaunchKernelGGL(cg_der_parse<CurveK1>, grid_for(n), dim3(256), 0, s, sig, stride, sig_len, fill_len, idx, n,
+                       cap, rs, der);
+  else
+    hipLaunchKernelGGL(cg_der_parse<CurveR1>, grid_for(n), dim3(256), 0, s, sig, stride, sig_len, fill_len, idx, n,
+                       cap, rs, der);
+  return hipGetLastError();
+}
+
+hipError_t ecdsa_batch_stage(EcdsaBatch& b, int scheme, const uint32_t* host_index, uint32_t n,
+                             const uint8_t* pk_raw_dev, size_t pk_stride, const uint8_t* sig_raw_dev,
+                             size_t sig_stride, const uint32_t* sig_len_dev, const uint64_t* msg_off_all_dev,
+                             const uint32_t* msg_len_all_dev, hipStream_t s) {
+  b = EcdsaBatch();
+  b.n = n;
+  b.scheme = scheme;
+  hipError_t e = hipMalloc((void**)&b.index, (size_t)n * 4);
+  if (e == hipSuccess) e = hipMalloc((void**)&b.q, (size_t)16 * n * 4);
+  if (e == hipSuccess) e = hipMalloc((void**)&b.rs, (size_t)16 * n * 4);
+  if (e == hipSuccess) e = hipMalloc((void**)&b.der, (size_t)n * 4);
+  if (e == hipSuccess) e = hipMalloc((void**)&b.sig_len, (size_t)n * 4);
+  if (e == hipSuccess) e = hipMalloc((void**)&b.msg_off, (size_t)n * 8);
+  if (e == hipSuccess) e = hipMalloc((void**)&b.msg_len, (size_t)n * 4);
+  if (e == hipSuccess) e = hipMemcpyAsync(b.index, host_index, (size_t)n * 4, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = launch_gather_words(pk_raw_dev, pk_stride, 0, 16, b.index, n, n, b.q, s);
+  if (e == hipSuccess)
+    e = launch_der_parse(scheme, sig_raw_dev, sig_stride, sig_len_dev, (uint32_t)sig_stride, b.index, n, n, b.rs,
+                         b.der, s);
+  if (e == hipSuccess) e = launch_gather_u32(sig_len_dev, b.index, n, b.sig_len, (uint32_t)sig_stride, s);
+  if (e == hipSuccess) e = launch_gather_u64(msg_off_all_dev, b.index, n, b.msg_off, s);
+  if (e == hipSuccess) e = launch_gather_u32(msg_len_all_dev, b.index, n, b.msg_len, 0, s);
+  // host_index must stay valid until the copy completes: callers synchronize before freeing
+  (void)hipStreamSynchronize(s);
+  if (e != hipSuccess) ecdsa_batch_free(b);
+  return e;
+}
+
+hipError_t ecdsa_batch_verify(const EcdsaBatch& b, EcdsaConsts* c, const uint8_t* arena, uint32_t mode,
+                              uint8_t* verdict, hipStream_t s) {
+  if (b.n == 0) return hipSuccess;
+  return b.scheme == 2 ? verify_curve<CurveK1>(b, c, arena, mode, verdict, s)
+                       : verify_curve<CurveR1>(b, c, arena, mode, verdict, s);
+}
+
+}  // namespace cg

@@ -77,3 +77,84 @@ int cgh_ed25519_verify(const uint8_t* pk_bytes, const uint8_t* sig_bytes, uint32
   return memcmp(rc, sig, 32) == 0 ? (int)V_ACCEPT : (int)V_REJECT;
 }
 }
+
+// ------------------------------------------------------------------ ECDSA
+#include "cg_ecdsa.h"
+
+template <class C>
+static void g_table(jpt tab[9]) { ecdsa_g_table<C>(tab); }
+
+template <class C>
+static int ecdsa_verify_host(const uint8_t* q_be, const uint8_t* sig, uint32_t sig_len, const uint8_t* msg,
+                             uint32_t msg_len, uint32_t mode) {
+  static jpt gtab[9];
+  static int init = 0;
+  if (!init) {
+    g_table<C>(gtab);
+    init = 1;
+  }
+  uint32_t qw[16], qx[8], qy[8], r[8], s[8], nn[8], d1[9], d2[9];
+  memcpy(qw, q_be, 64);
+  be_words_to_limbs(qx, qw);
+  be_words_to_limbs(qy, qw + 8);
+  C::n(nn);
+  const uint32_t ds = der_parse([&](uint32_t i) { return (uint32_t)sig[i]; }, sig_len, nn, r, s);
+  const uint32_t pre = ecdsa_prep<C>(qx, qy, ds, r, s, sig_len, msg, msg_len, mode, d1, d2);
+  if (pre != 0xff) return (int)pre;
+  jpt qtab[9];
+  ecdsa_q_table<C>(qx, qy, [&](int k, const jpt& p) { qtab[k] = p; });
+  return (int)ecdsa_msm_check<C>(d1, d2, r, [&](uint32_t k, jpt& p) { p = qtab[k]; },
+                                 [&](uint32_t k, jpt& p) { p = gtab[k]; });
+}
+
+extern "C" {
+int cgh_ecdsa_verify(int scheme, const uint8_t* q_be, const uint8_t* sig, uint32_t sig_len, const uint8_t* msg,
+                     uint32_t msg_len, uint32_t mode) {
+  return scheme == 2 ? ecdsa_verify_host<CurveK1>(q_be, sig, sig_len, msg, msg_len, mode)
+                     : ecdsa_verify_host<CurveR1>(q_be, sig, sig_len, msg, msg_len, mode);
+}
+
+void cgh_fp_mul(int scheme, const uint32_t* a, const uint32_t* b, uint32_t* out) {
+  if (scheme == 2) fp_mul<CurveK1>(out, a, b); else fp_mul<CurveR1>(out, a, b);
+}
+
+void cgh_mn_inv(int scheme, const uint32_t* a, uint32_t* out) {
+  if (scheme == 2) mn_inv<CurveK1>(out, a); else mn_inv<CurveR1>(out, a);
+}
+
+void cgh_mn_mulmod(int scheme, const uint32_t* a, const uint32_t* b, uint32_t* out) {
+  if (scheme == 2) mn_mulmod<CurveK1>(out, a, b); else mn_mulmod<CurveR1>(out, a, b);
+}
+
+uint32_t cgh_der_parse(int scheme, const uint8_t* sig, uint32_t n, uint32_t* r, uint32_t* s) {
+  uint32_t nn[8];
+  if (scheme == 2) CurveK1::n(nn); else CurveR1::n(nn);
+  return der_parse([&](uint32_t i) { return (uint32_t)sig[i]; }, n, nn, r, s);
+}
+}
+
+// u1*G + u2*Q through the device's joint multiplication; returns 0 and affine
+// x||y (LE limbs), or 1 when the result is the point at infinity.
+template <class C>
+static int joint_host(const uint32_t* u1, const uint32_t* u2, const uint32_t* qx, const uint32_t* qy, uint32_t* out) {
+  jpt gtab[9], qtab[9], acc;
+  g_table<C>(gtab);
+  ecdsa_q_table<C>(qx, qy, [&](int k, const jpt& p) { qtab[k] = p; });
+  uint32_t d1[9], d2[9];
+  recode16_65(d1, u1);
+  recode16_65(d2, u2);
+  ecdsa_joint<C>(acc, d1, d2, [&](uint32_t k, jpt& p) { p = qtab[k]; }, [&](uint32_t k, jpt& p) { p = gtab[k]; });
+  if (acc.inf) return 1;
+  uint32_t zi[8], zi2[8], zi3[8];
+  fp_inv<C>(zi, acc.Z);
+  fp_sqr<C>(zi2, zi);
+  fp_mul<C>(zi3, zi2, zi);
+  fp_mul<C>(out, acc.X, zi2);
+  fp_mul<C>(out + 8, acc.Y, zi3);
+  return 0;
+}
+
+extern "C" int cgh_ecdsa_joint(int scheme, const uint32_t* u1, const uint32_t* u2, const uint32_t* qx,
+                               const uint32_t* qy, uint32_t* out) {
+  return scheme == 2 ? joint_host<CurveK1>(u1, u2, qx, qy, out) : joint_host<CurveR1>(u1, u2, qx, qy, out);
+}

@@ -134,3 +134,81 @@ def add_ed25519_adversarial(w: Workload, frac: float = 0.01, seed: int = 7) -> W
             w.msg_len[i] = len(m)
     w.classes = classes
     return w
+
+
+# ---------------------------------------------------------------- ECDSA (D1–D8)
+_N = {2: 0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEBAAEDCE6AF48A03BBFD25E8CD0364141,
+      3: 0xFFFFFFFF00000000FFFFFFFFFFFFFFFFBCE6FAADA7179E84F3B9CAC2FC632551}
+EC_CLASSES = ["D1", "D2", "D3", "D4", "D5", "D6", "D7", "D8"]
+
+
+def _der_len(n: int) -> bytes:
+    if n < 0x80:
+        return bytes([n])
+    raw = n.to_bytes((n.bit_length() + 7) // 8, "big")
+    return bytes([0x80 | len(raw)]) + raw
+
+
+def _der_int(v: int) -> bytes:
+    nb = (v.bit_length() + 8) // 8 if v >= 0 else ((v + 1).bit_length() + 8) // 8
+    body = v.to_bytes(max(nb, 1), "big", signed=True)
+    return b"\x02" + _der_len(len(body)) + body
+
+
+def _der_seq(body: bytes) -> bytes:
+    return b"\x30" + _der_len(len(body)) + body
+
+
+def _parse_rs(sig: bytes):
+    i = 2
+    out = []
+    for _ in range(2):
+        ln = sig[i + 1]
+        out.append(int.from_bytes(sig[i + 2:i + 2 + ln], "big", signed=True))
+        i += 2 + ln
+    return out
+
+
+def add_ecdsa_adversarial(w: Workload, frac: float = 0.01, seed: int = 7) -> Workload:
+    """Mutates a fraction of the ECDSA elements of w uniformly over D1–D8
+    (SURVEY §8d).  Signatures that no longer fit sig_stride are left valid."""
+    rng = np.random.default_rng(seed)
+    ec = np.flatnonzero((w.scheme == 2) | (w.scheme == 3))
+    k = int(round(len(ec) * frac))
+    idx = rng.choice(ec, size=k, replace=False)
+    classes = list(w.classes) if w.classes is not None else ["valid"] * w.n
+    for j, i in enumerate(idx):
+        cls = EC_CLASSES[j % len(EC_CLASSES)]
+        n = _N[int(w.scheme[i])]
+        sig = w.sig[i, :w.sig_len[i]].tobytes()
+        r, s = _parse_rs(sig)
+        new = sig
+        if cls == "D1":
+            if rng.integers(2):
+                b = bytearray(sig); b[6 + rng.integers(len(b) - 6)] ^= 1 << int(rng.integers(8)); new = bytes(b)
+            else:
+                o = int(w.msg_off[i]); w.msg[o + rng.integers(max(int(w.msg_len[i]), 1))] ^= np.uint8(1)
+        elif cls == "D2":
+            new = _der_seq(_der_int(0) + _der_int(s)) if rng.integers(2) else _der_seq(_der_int(r) + _der_int(0))
+        elif cls == "D3":
+            new = _der_seq(_der_int(r + n) + _der_int(s)) if rng.integers(2) else _der_seq(_der_int(r) + _der_int(s + n))
+        elif cls == "D4":
+            new = _der_seq(_der_int(-r) + _der_int(s))
+        elif cls == "D5":
+            ri = _der_int(r)
+            new = _der_seq(b"\x02" + bytes([ri[1] + 1]) + b"\x00" + ri[2:] + _der_int(s))
+        elif cls == "D6":
+            body = _der_int(r) + _der_int(s)
+            new = b"\x30\x81" + bytes([len(body)]) + body
+        elif cls == "D7":
+            new = sig + b"\x00"
+        elif cls == "D8":
+            new = _der_seq(_der_int(r) + _der_int(n - s))
+        if len(new) > w.sig_stride:
+            continue
+        classes[i] = cls
+        w.sig[i, :] = 0
+        w.sig[i, :len(new)] = np.frombuffer(new, dtype=np.uint8)
+        w.sig_len[i] = len(new)
+    w.classes = classes
+    return w
