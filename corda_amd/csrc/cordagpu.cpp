@@ -168,6 +168,7 @@ struct cg_batch {
   uint8_t* verdict = nullptr;   // [n]
   uint32_t* bitmap = nullptr;   // [ceil(n/32)]
   uint8_t* arena = nullptr;     // message arena (+16 pad)
+  bool arena_owned = true;
   uint64_t* msg_off_all = nullptr;
   uint32_t* msg_len_all = nullptr;
   // Ed25519 subset
@@ -188,7 +189,7 @@ void batch_free(cg_batch* b) {
   if (!b) return;
   dfree(b->verdict);
   dfree(b->bitmap);
-  dfree(b->arena);
+  if (b->arena_owned) dfree(b->arena);
   dfree(b->msg_off_all);
   dfree(b->msg_len_all);
   dfree(b->ed_index);
@@ -302,13 +303,21 @@ void cg_close(cg_ctx* ctx) {
 
 const char* cg_last_error(const cg_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
 
-cg_status cg_batch_create(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const uint8_t* pk, size_t pk_stride,
-                          const uint8_t* sig, size_t sig_stride, const uint32_t* sig_len, const uint8_t* msg,
-                          size_t msg_bytes, const uint64_t* msg_off, const uint32_t* msg_len, cg_batch** out) {
+}  // extern "C"
+
+namespace {
+
+// Stages a batch; the message arena comes from host memory (msg) or, for the
+// signed-transaction path, from a device buffer the library owns (msg_dev: the
+// recomputed ids), which the batch then references without owning.
+cg_status create_batch(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const uint8_t* pk, size_t pk_stride,
+                       const uint8_t* sig, size_t sig_stride, const uint32_t* sig_len, const uint8_t* msg,
+                       uint8_t* msg_dev, size_t msg_bytes, const uint64_t* msg_off, const uint32_t* msg_len,
+                       cg_batch** out) {
   if (!out) return fail(ctx, CG_E_INVALID_ARGUMENT, "null out");
   *out = nullptr;
-  cg_status st = check_inputs(ctx, n, scheme_id, pk, pk_stride, sig, sig_stride, sig_len, msg, msg_bytes, msg_off,
-                              msg_len);
+  cg_status st = check_inputs(ctx, n, scheme_id, pk, pk_stride, sig, sig_stride, sig_len,
+                              msg_dev ? (const uint8_t*)msg_dev : msg, msg_bytes, msg_off, msg_len);
   if (st != CG_OK) return st;
   if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, CG_E_DEVICE, "hipSetDevice");
   cg_batch* b = new (std::nothrow) cg_batch();
@@ -340,10 +349,15 @@ cg_status cg_batch_create(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const
   // raw element-major inputs (temporary) + arena (kept)
   uint8_t *pk_raw = nullptr, *sig_raw = nullptr;
   uint32_t* sl_raw = nullptr;
-  if ((st = dalloc(ctx, &b->arena, msg_bytes + 16, "alloc arena")) != CG_OK) return bail(st);
-  if (msg_bytes)
-    CG_TRY(ctx, hipMemcpyAsync(b->arena, msg, msg_bytes, hipMemcpyHostToDevice, ctx->stream), "upload arena");
-  CG_TRY(ctx, hipMemsetAsync(b->arena + msg_bytes, 0, 16, ctx->stream), "pad arena");
+  if (msg_dev) {
+    b->arena = msg_dev;  // caller-owned device arena (padded by the caller)
+    b->arena_owned = false;
+  } else {
+    if ((st = dalloc(ctx, &b->arena, msg_bytes + 16, "alloc arena")) != CG_OK) return bail(st);
+    if (msg_bytes)
+      CG_TRY(ctx, hipMemcpyAsync(b->arena, msg, msg_bytes, hipMemcpyHostToDevice, ctx->stream), "upload arena");
+    CG_TRY(ctx, hipMemsetAsync(b->arena + msg_bytes, 0, 16, ctx->stream), "pad arena");
+  }
   if ((st = upload(ctx, &b->msg_off_all, msg_off, n, "upload msg_off")) != CG_OK) return bail(st);
   if ((st = upload(ctx, &b->msg_len_all, msg_len, n, "upload msg_len")) != CG_OK) return bail(st);
   if ((st = upload(ctx, &pk_raw, pk, n * pk_stride, "upload pk")) != CG_OK) return bail(st);
@@ -411,6 +425,17 @@ cg_status cg_batch_create(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const
   collect_timings(ctx);
   *out = b;
   return CG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+cg_status cg_batch_create(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const uint8_t* pk, size_t pk_stride,
+                          const uint8_t* sig, size_t sig_stride, const uint32_t* sig_len, const uint8_t* msg,
+                          size_t msg_bytes, const uint64_t* msg_off, const uint32_t* msg_len, cg_batch** out) {
+  return create_batch(ctx, n, scheme_id, pk, pk_stride, sig, sig_stride, sig_len, msg, nullptr, msg_bytes, msg_off,
+                      msg_len, out);
 }
 
 cg_status cg_batch_verify(cg_ctx* ctx, cg_batch* b, int mode, uint8_t* verdict_out, uint32_t* accept_bitmap_out,
@@ -588,6 +613,182 @@ cg_status cg_reset_stats(cg_ctx* ctx) {
   collect_timings(ctx);
   ctx->stats.clear();
   return CG_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+// Device buffers of one tx-id computation (K5 + K6).
+struct TxIds {
+  uint8_t* arena = nullptr;
+  uint64_t *slot = nullptr, *leaf_pos = nullptr, *tree_base = nullptr;
+  uint32_t *len = nullptr, *comp_tx = nullptr, *comp_idx = nullptr, *is_salt = nullptr, *salts = nullptr,
+           *comp_start = nullptr, *leaves = nullptr;
+  uint8_t* ids = nullptr;  // 32 B per tx (+16 pad): digest byte order
+  void release() {
+    for (void* p : {(void*)arena, (void*)slot, (void*)leaf_pos, (void*)tree_base, (void*)len, (void*)comp_tx,
+                    (void*)comp_idx, (void*)is_salt, (void*)salts, (void*)comp_start, (void*)leaves, (void*)ids})
+      dfree(p);
+    *this = TxIds();
+  }
+};
+
+cg_status compute_txids(cg_ctx* ctx, size_t n_tx, const uint8_t* arena, size_t arena_bytes, const uint64_t* comp_off,
+                        const uint32_t* comp_len, const uint32_t* comp_start, const uint8_t* salts, TxIds& d,
+                        bool* any_empty) {
+  if (n_tx > 0xFFFFFFF0ull) return fail(ctx, CG_E_INVALID_ARGUMENT, "too many transactions");
+  if (!comp_start || !salts || (comp_start[n_tx] && (!comp_off || !comp_len || !arena)))
+    return fail(ctx, CG_E_INVALID_ARGUMENT, "null pointer");
+  const size_t n_comp = comp_start[n_tx];
+  if (n_comp > 0xFFFFFFF0ull) return fail(ctx, CG_E_INVALID_ARGUMENT, "too many components");
+  // host-side layout: aligned slots with 32 spare bytes for the nonce; trees padded to 2^k
+  std::vector<uint64_t> slot(n_comp), leaf_pos(n_comp), tree_base(n_tx + 1);
+  std::vector<uint32_t> comp_tx(n_comp), comp_idx(n_comp), is_salt(n_comp);
+  uint64_t pos = 0, leaves = 0;
+  *any_empty = false;
+  for (size_t t = 0; t < n_tx; ++t) {
+    if (comp_start[t + 1] < comp_start[t]) return fail(ctx, CG_E_INVALID_ARGUMENT, "comp_start not monotone");
+    const uint32_t k = comp_start[t + 1] - comp_start[t];
+    if (k == 0) *any_empty = true;
+    uint32_t kp = 1;
+    while (kp < k) kp <<= 1;
+    tree_base[t] = leaves;
+    leaves += k ? kp : 1;
+    for (uint32_t i = 0; i < k; ++i) {
+      const size_t c = comp_start[t] + i;
+      if (comp_off[c] + comp_len[c] > arena_bytes)
+        return fail(ctx, CG_E_INVALID_ARGUMENT, "component out of arena bounds");
+      slot[c] = pos;
+      pos += ((uint64_t)comp_len[c] + 32 + 3) & ~3ull;
+      comp_tx[c] = (uint32_t)t;
+      comp_idx[c] = i;
+      is_salt[c] = i == k - 1;
+      leaf_pos[c] = tree_base[t] + i;
+    }
+  }
+  std::vector<uint8_t> slotted(pos + 16, 0);
+  for (size_t c = 0; c < n_comp; ++c) std::memcpy(slotted.data() + slot[c], arena + comp_off[c], comp_len[c]);
+  cg_status st;
+  if ((st = upload(ctx, &d.arena, slotted.data(), slotted.size(), "upload tx arena")) != CG_OK ||
+      (st = upload(ctx, &d.slot, slot.data(), n_comp, "upload slots")) != CG_OK ||
+      (st = upload(ctx, &d.leaf_pos, leaf_pos.data(), n_comp, "upload leaf_pos")) != CG_OK ||
+      (st = upload(ctx, &d.tree_base, tree_base.data(), n_tx, "upload tree_base")) != CG_OK ||
+      (st = upload(ctx, &d.len, comp_len, n_comp, "upload comp_len")) != CG_OK ||
+      (st = upload(ctx, &d.comp_tx, comp_tx.data(), n_comp, "upload comp_tx")) != CG_OK ||
+      (st = upload(ctx, &d.comp_idx, comp_idx.data(), n_comp, "upload comp_idx")) != CG_OK ||
+      (st = upload(ctx, &d.is_salt, is_salt.data(), n_comp, "upload is_salt")) != CG_OK ||
+      (st = upload(ctx, &d.salts, (const uint32_t*)salts, 8 * n_tx, "upload salts")) != CG_OK ||
+      (st = upload(ctx, &d.comp_start, comp_start, n_tx + 1, "upload comp_start")) != CG_OK ||
+      (st = dalloc(ctx, &d.leaves, 8 * leaves, "alloc leaves")) != CG_OK ||
+      (st = dalloc(ctx, &d.ids, 32 * n_tx + 16, "alloc ids")) != CG_OK) {
+    (void)hipStreamSynchronize(ctx->stream);
+    return st;
+  }
+  CG_TRY(ctx, hipMemsetAsync(d.leaves, 0, 32 * leaves, ctx->stream), "zero leaves");
+  CG_TRY(ctx, hipMemsetAsync(d.ids, 0, 32 * n_tx + 16, ctx->stream), "zero ids");
+  {
+    Timed t(ctx, "merkle_leaf", n_comp);
+    CG_TRY(ctx, cg::launch_merkle_nonce(d.arena, d.slot, d.len, d.comp_tx, d.comp_idx, d.is_salt, d.salts,
+                                        (uint32_t)n_comp, ctx->stream), "launch merkle_nonce");
+    CG_TRY(ctx, cg::launch_merkle_leaf(d.arena, d.slot, d.len, d.is_salt, d.leaf_pos, (uint32_t)n_comp, d.leaves,
+                                       ctx->stream), "launch merkle_leaf");
+  }
+  {
+    Timed t(ctx, "merkle_tree", n_tx);
+    CG_TRY(ctx, cg::launch_merkle_tree(d.leaves, d.tree_base, d.comp_start, (uint32_t)n_tx, (uint32_t*)d.ids,
+                                       ctx->stream), "launch merkle_tree");
+  }
+  // the host staging vectors die here: wait for the uploads that read them
+  CG_TRY(ctx, hipStreamSynchronize(ctx->stream), "txid sync");
+  return CG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+cg_status cg_txid_batch(cg_ctx* ctx, size_t n_tx, const uint8_t* arena, size_t arena_bytes,
+                        const uint64_t* comp_off, const uint32_t* comp_len, const uint32_t* comp_start,
+                        const uint8_t* salts, uint8_t* ids_out) {
+  if (!ctx) return CG_E_INVALID_ARGUMENT;
+  if (n_tx == 0) return CG_OK;
+  if (!ids_out) return fail(ctx, CG_E_INVALID_ARGUMENT, "null ids_out");
+  if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, CG_E_DEVICE, "hipSetDevice");
+  TxIds d;
+  bool any_empty = false;
+  cg_status st = compute_txids(ctx, n_tx, arena, arena_bytes, comp_off, comp_len, comp_start, salts, d, &any_empty);
+  if (st == CG_OK) {
+    hipError_t e = hipMemcpyAsync(ids_out, d.ids, 32 * n_tx, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) st = hip_fail(ctx, e, "download ids");
+  }
+  d.release();
+  collect_timings(ctx);
+  if (st == CG_OK && any_empty)
+    return fail(ctx, CG_E_MERKLE_EMPTY, "Cannot calculate Merkle root on empty hash list.");
+  return st;
+}
+
+cg_status cg_tx_verify_batch(cg_ctx* ctx, int mode, size_t n_tx, const uint8_t* arena, size_t arena_bytes,
+                             const uint64_t* comp_off, const uint32_t* comp_len, const uint32_t* comp_start,
+                             const uint8_t* salts, const uint32_t* sig_start, const uint8_t* scheme_id,
+                             const uint8_t* pk, size_t pk_stride, const uint8_t* sig, size_t sig_stride,
+                             const uint32_t* sig_len, int32_t* first_bad_out, uint8_t* verdict_out,
+                             uint8_t* ids_out) {
+  if (!ctx) return CG_E_INVALID_ARGUMENT;
+  if (n_tx == 0) return CG_OK;
+  if (!sig_start || !first_bad_out) return fail(ctx, CG_E_INVALID_ARGUMENT, "null pointer");
+  if (mode != CG_MODE_IS_VALID && mode != CG_MODE_DO_VERIFY) return fail(ctx, CG_E_INVALID_ARGUMENT, "bad mode");
+  if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, CG_E_DEVICE, "hipSetDevice");
+  TxIds d;
+  bool any_empty = false;
+  cg_status st = compute_txids(ctx, n_tx, arena, arena_bytes, comp_off, comp_len, comp_start, salts, d, &any_empty);
+  if (st != CG_OK) {
+    d.release();
+    return st;
+  }
+  const size_t n_sig = sig_start[n_tx];
+  std::vector<uint64_t> moff(n_sig);
+  std::vector<uint32_t> mlen(n_sig, 32);
+  for (size_t t = 0; t < n_tx; ++t) {
+    if (sig_start[t + 1] < sig_start[t]) {
+      d.release();
+      return fail(ctx, CG_E_INVALID_ARGUMENT, "sig_start not monotone");
+    }
+    for (uint32_t s = sig_start[t]; s < sig_start[t + 1]; ++s) moff[s] = 32 * (uint64_t)t;
+  }
+  cg_batch* b = nullptr;
+  if (n_sig) {
+    st = create_batch(ctx, n_sig, scheme_id, pk, pk_stride, sig, sig_stride, sig_len, nullptr, d.ids, 32 * n_tx,
+                      moff.data(), mlen.data(), &b);
+    if (st == CG_OK) st = cg_batch_verify(ctx, b, mode, verdict_out, nullptr, nullptr);
+  }
+  uint32_t* ss_d = nullptr;
+  int32_t* fb_d = nullptr;
+  if (st == CG_OK && (st = upload(ctx, &ss_d, sig_start, n_tx + 1, "upload sig_start")) == CG_OK &&
+      (st = dalloc(ctx, &fb_d, n_tx, "alloc first_bad")) == CG_OK) {
+    uint8_t* verdict_dev = b ? b->verdict : nullptr;
+    hipError_t e = cg::launch_first_bad(verdict_dev, ss_d, (uint32_t)n_tx, fb_d, ctx->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(first_bad_out, fb_d, 4 * n_tx, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess && ids_out) e = hipMemcpyAsync(ids_out, d.ids, 32 * n_tx, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) st = hip_fail(ctx, e, "first_bad");
+  }
+  (void)hipStreamSynchronize(ctx->stream);
+  dfree(ss_d);
+  dfree(fb_d);
+  if (b) cg_batch_destroy(ctx, b);
+  // a tx with no component has no id: report it as -3 (MerkleTreeException)
+  if (st == CG_OK && any_empty) {
+    for (size_t t = 0; t < n_tx; ++t)
+      if (comp_start[t + 1] == comp_start[t]) first_bad_out[t] = -3;
+  }
+  d.release();
+  collect_timings(ctx);
+  if (st == CG_OK && any_empty)
+    return fail(ctx, CG_E_MERKLE_EMPTY, "Cannot calculate Merkle root on empty hash list.");
+  return st;
 }
 
 }  // extern "C"

@@ -1,0 +1,102 @@
+"""GPU parity: WireTransaction ids (K5/K6) and the signed-transaction batch
+(cg_tx_verify_batch) vs the CPU oracle — golden trees (the structure cases of
+PartialMerkleTreeTest.kt:60-84 plus random shapes), config-4 shaped batches
+(ids bit-exact vs oracle_txid_batch; per-tx first failing signature equals a
+sequential checkSignaturesAreValid loop over the oracle's verdicts), and the
+edge cases (empty component list -> MerkleTreeException, empty sigs)."""
+from __future__ import annotations
+
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from corda_amd import transactions as T
+from corda_amd._lib import ACCEPT, MODE_DO_VERIFY, ptr
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools", "datagen"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+import datagen  # noqa: E402
+from test_gpu_ed25519 import oracle_verdicts  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+def test_golden_tx_ids(gpu_ctx, golden_merkle):
+    txs = [T.WireTx([bytes.fromhex(c) for c in t["components"]], bytes.fromhex(t["salt"]))
+           for t in golden_merkle["txs"]]
+    ids = T.tx_ids(gpu_ctx, txs)
+    assert [i.hex() for i in ids] == [t["id"] for t in golden_merkle["txs"]]
+
+
+def test_empty_tx_is_merkle_exception(gpu_ctx):
+    with pytest.raises(T.MerkleTreeException):
+        T.tx_ids(gpu_ctx, [T.WireTx([b"x"], bytes(32)), T.WireTx([], bytes(32))])
+
+
+def oracle_ids(oracle, w):
+    ids = np.zeros(32 * w.n_tx, dtype=np.uint8)
+    oracle.oracle_txid_batch(ptr(w.arena), ptr(w.comp_off), ptr(w.comp_len), ptr(w.comp_start), ptr(w.salts),
+                             w.n_tx, ptr(ids))
+    return ids
+
+
+def run_tx_verify(ctx, w, mode=MODE_DO_VERIFY):
+    n_tx, n_sig = w.n_tx, int(w.sig_start[-1])
+    first_bad = np.zeros(n_tx, dtype=np.int32)
+    verdict = np.zeros(n_sig, dtype=np.uint8)
+    ids = np.zeros(32 * n_tx, dtype=np.uint8)
+    ctx.check(ctx.lib.cg_tx_verify_batch(ctx.h, mode, n_tx, ptr(w.arena), len(w.arena), ptr(w.comp_off),
+                                         ptr(w.comp_len), ptr(w.comp_start), ptr(w.salts), ptr(w.sig_start),
+                                         ptr(w.scheme), ptr(w.pk), 64, ptr(w.sig), 72, ptr(w.sig_len),
+                                         ptr(first_bad), ptr(verdict), ptr(ids)))
+    return first_bad, verdict, ids
+
+
+def test_config4_shape_vs_oracle(gpu_ctx, oracle):
+    w = datagen.make_tx_batch(30_000, seed=8, tamper_frac=0.02)
+    # one bad signature at a random position in some untampered txs
+    rng = np.random.default_rng(2)
+    for t in rng.choice(np.flatnonzero(~w.tampered), size=300, replace=False):
+        s = int(rng.integers(w.sig_start[t], w.sig_start[t + 1]))
+        w.sig[s, 10] ^= 4
+    first_bad, verdict, ids = run_tx_verify(gpu_ctx, w)
+    exp_ids = oracle_ids(oracle, w)
+    assert np.array_equal(ids, exp_ids)
+    # the oracle verifies every signature over the oracle's ids
+    n_sig = int(w.sig_start[-1])
+    msg_off = np.repeat(np.arange(w.n_tx, dtype=np.uint64) * 32, np.diff(w.sig_start))
+    sw = datagen.Workload(n_sig, w.scheme, w.pk, 64, w.sig, 72, w.sig_len, exp_ids, msg_off,
+                          np.full(n_sig, 32, np.uint32))
+    exp_v = oracle_verdicts(oracle, sw, MODE_DO_VERIFY)
+    assert np.array_equal(verdict, exp_v)
+    for t in range(w.n_tx):  # sequential checkSignaturesAreValid
+        a, b = int(w.sig_start[t]), int(w.sig_start[t + 1])
+        bad = [i - a for i in range(a, b) if exp_v[i] != ACCEPT]
+        assert first_bad[t] == (bad[0] if bad else -1)
+    assert (first_bad[w.tampered] == 0).all()
+
+
+def test_python_mirror_raises_like_check_signatures_are_valid(gpu_ctx):
+    w = datagen.make_tx_batch(50, seed=3, tamper_frac=0.0)
+    stxs = []
+    for t in range(w.n_tx):
+        comps = [w.arena[int(w.comp_off[c]):int(w.comp_off[c]) + int(w.comp_len[c])].tobytes()
+                 for c in range(int(w.comp_start[t]), int(w.comp_start[t + 1]))]
+        sigs = [(int(w.scheme[s]), w.pk[s].tobytes(), w.sig[s, :w.sig_len[s]].tobytes())
+                for s in range(int(w.sig_start[t]), int(w.sig_start[t + 1]))]
+        stxs.append(T.SignedTx(T.WireTx(comps, w.salts[32 * t:32 * t + 32].tobytes()), sigs))
+    T.check_signatures_are_valid(gpu_ctx, stxs)  # all valid: no exception
+    ids = T.tx_ids(gpu_ctx, [s.wire for s in stxs])
+    assert b"".join(ids) == w.ids.tobytes()
+    bad = stxs[17]
+    sch, pk, sg = bad.sigs[-1]
+    bad.sigs[-1] = (sch, pk, sg[:-1] + bytes([sg[-1] ^ 1]))
+    with pytest.raises(T.SignatureException) as ei:
+        T.check_signatures_are_valid(gpu_ctx, stxs)
+    assert ei.value.tx_index == 17 and ei.value.sig_index == len(bad.sigs) - 1
+    stxs[5].sigs = []
+    with pytest.raises(T.IllegalArgumentException):
+        T.check_signatures_are_valid(gpu_ctx, stxs)

@@ -66,7 +66,7 @@ static void key_seed(uint8_t seed32[32], uint64_t idx) {
 }
 
 typedef struct {
-  int scheme;  /* 2 K1, 3 R1, 4 Ed25519 */
+  const uint8_t* scheme_arr;  /* 2 K1, 3 R1, 4 Ed25519 (NULL: all Ed25519) */
   size_t lo, hi;
   uint64_t key_base;
   uint8_t *pk, *sig;
@@ -78,58 +78,60 @@ typedef struct {
   int err;
 } job;
 
-static void* ed_worker(void* arg) {
-  job* j = (job*)arg;
-  EVP_MD_CTX* mctx = EVP_MD_CTX_new();
-  for (size_t i = j->lo; i < j->hi; ++i) {
-    uint8_t seed[32];
-    key_seed(seed, j->key_base + i);
-    EVP_PKEY* k = EVP_PKEY_new_raw_private_key(EVP_PKEY_ED25519, NULL, seed, 32);
-    size_t pl = 32, sl = 64;
-    if (!k || EVP_PKEY_get_raw_public_key(k, j->pk + i * j->pk_stride, &pl) != 1 ||
-        EVP_DigestSignInit(mctx, NULL, NULL, NULL, k) != 1 ||
-        EVP_DigestSign(mctx, j->sig + i * j->sig_stride, &sl, j->msg + j->msg_off[i], j->msg_len[i]) != 1) {
-      j->err = 1;
-    }
-    j->sig_len[i] = (uint32_t)sl;
-    EVP_PKEY_free(k);
-    EVP_MD_CTX_reset(mctx);
+static void sign_ed(job* j, size_t i, EVP_MD_CTX* mctx) {
+  uint8_t seed[32];
+  key_seed(seed, j->key_base + i);
+  EVP_PKEY* k = EVP_PKEY_new_raw_private_key(EVP_PKEY_ED25519, NULL, seed, 32);
+  size_t pl = 32, sl = 64;
+  if (!k || EVP_PKEY_get_raw_public_key(k, j->pk + i * j->pk_stride, &pl) != 1 ||
+      EVP_DigestSignInit(mctx, NULL, NULL, NULL, k) != 1 ||
+      EVP_DigestSign(mctx, j->sig + i * j->sig_stride, &sl, j->msg + j->msg_off[i], j->msg_len[i]) != 1) {
+    j->err = 1;
   }
-  EVP_MD_CTX_free(mctx);
-  return NULL;
+  j->sig_len[i] = (uint32_t)sl;
+  EVP_PKEY_free(k);
+  EVP_MD_CTX_reset(mctx);
 }
 
-static void* ec_worker(void* arg) {
+static void sign_ec(job* j, size_t i, int scheme, BN_CTX* bctx) {
+  const int nid = scheme == 2 ? NID_secp256k1 : NID_X9_62_prime256v1;
+  uint8_t seed[32], dig[32];
+  key_seed(seed, j->key_base + i);
+  EC_KEY* k = EC_KEY_new_by_curve_name(nid);
+  const EC_GROUP* g = EC_KEY_get0_group(k);
+  BIGNUM* d = BN_bin2bn(seed, 32, NULL);
+  BIGNUM* order = BN_new();
+  EC_GROUP_get_order(g, order, bctx);
+  BN_mod(d, d, order, bctx);
+  if (BN_is_zero(d)) BN_one(d);
+  EC_POINT* q = EC_POINT_new(g);
+  EC_POINT_mul(g, q, d, NULL, NULL, bctx);
+  EC_KEY_set_private_key(k, d);
+  EC_KEY_set_public_key(k, q);
+  uint8_t oct[65];
+  if (EC_POINT_point2oct(g, q, POINT_CONVERSION_UNCOMPRESSED, oct, 65, bctx) != 65) j->err = 1;
+  memcpy(j->pk + i * j->pk_stride, oct + 1, 64);
+  SHA256(j->msg + j->msg_off[i], j->msg_len[i], dig);
+  unsigned int sl = (unsigned int)j->sig_stride;
+  if (ECDSA_sign(0, dig, 32, j->sig + i * j->sig_stride, &sl, k) != 1) j->err = 1;
+  j->sig_len[i] = sl;
+  EC_POINT_free(q);
+  BN_free(order);
+  BN_free(d);
+  EC_KEY_free(k);
+}
+
+static void* worker(void* arg) {
   job* j = (job*)arg;
-  const int nid = j->scheme == 2 ? NID_secp256k1 : NID_X9_62_prime256v1;
+  EVP_MD_CTX* mctx = EVP_MD_CTX_new();
   BN_CTX* bctx = BN_CTX_new();
   for (size_t i = j->lo; i < j->hi; ++i) {
-    uint8_t seed[32], dig[32];
-    key_seed(seed, j->key_base + i);
-    EC_KEY* k = EC_KEY_new_by_curve_name(nid);
-    const EC_GROUP* g = EC_KEY_get0_group(k);
-    BIGNUM* d = BN_bin2bn(seed, 32, NULL);
-    BIGNUM* order = BN_new();
-    EC_GROUP_get_order(g, order, bctx);
-    BN_mod(d, d, order, bctx);
-    if (BN_is_zero(d)) BN_one(d);
-    EC_POINT* q = EC_POINT_new(g);
-    EC_POINT_mul(g, q, d, NULL, NULL, bctx);
-    EC_KEY_set_private_key(k, d);
-    EC_KEY_set_public_key(k, q);
-    uint8_t oct[65];
-    if (EC_POINT_point2oct(g, q, POINT_CONVERSION_UNCOMPRESSED, oct, 65, bctx) != 65) j->err = 1;
-    memcpy(j->pk + i * j->pk_stride, oct + 1, 64);
-    SHA256(j->msg + j->msg_off[i], j->msg_len[i], dig);
-    unsigned int sl = (unsigned int)j->sig_stride;
-    if (ECDSA_sign(0, dig, 32, j->sig + i * j->sig_stride, &sl, k) != 1) j->err = 1;
-    j->sig_len[i] = sl;
-    EC_POINT_free(q);
-    BN_free(order);
-    BN_free(d);
-    EC_KEY_free(k);
+    const int sc = j->scheme_arr ? j->scheme_arr[i] : 4;
+    if (sc == 4) sign_ed(j, i, mctx);
+    else if (sc == 2 || sc == 3) sign_ec(j, i, sc, bctx);
   }
   BN_CTX_free(bctx);
+  EVP_MD_CTX_free(mctx);
   return NULL;
 }
 
@@ -138,42 +140,62 @@ static void* ec_worker(void* arg) {
 int dg_sign_batch(size_t n, const uint8_t* scheme, uint64_t key_base, uint8_t* pk, size_t pk_stride, uint8_t* sig,
                   size_t sig_stride, uint32_t* sig_len, const uint8_t* msg, const uint64_t* msg_off,
                   const uint32_t* msg_len, int n_threads) {
+  if (n == 0) return 0;
   if (n_threads < 1) n_threads = 1;
-  int err = 0;
-  /* group by scheme so each worker runs one algorithm over contiguous runs */
-  for (int sc = 2; sc <= 4; ++sc) {
-    size_t cnt = 0;
-    for (size_t i = 0; i < n; ++i) cnt += (scheme ? scheme[i] : 4) == sc;
-    if (!cnt) continue;
-    /* process contiguous runs of this scheme */
-    size_t i = 0;
-    while (i < n) {
-      while (i < n && (scheme ? scheme[i] : 4) != sc) ++i;
-      size_t lo = i;
-      while (i < n && (scheme ? scheme[i] : 4) == sc) ++i;
-      size_t hi = i;
-      if (lo >= hi) break;
-      size_t len = hi - lo;
-      int nt = (size_t)n_threads > len ? (int)len : n_threads;
-      pthread_t* th = calloc((size_t)nt, sizeof(pthread_t));
-      job* jobs = calloc((size_t)nt, sizeof(job));
-      for (int t = 0; t < nt; ++t) {
-        job* j = &jobs[t];
-        j->scheme = sc;
-        j->lo = lo + len * (size_t)t / (size_t)nt;
-        j->hi = lo + len * (size_t)(t + 1) / (size_t)nt;
-        j->key_base = key_base;
-        j->pk = pk; j->sig = sig; j->pk_stride = pk_stride; j->sig_stride = sig_stride;
-        j->sig_len = sig_len; j->msg = msg; j->msg_off = msg_off; j->msg_len = msg_len;
-        pthread_create(&th[t], NULL, sc == 4 ? ed_worker : ec_worker, j);
-      }
-      for (int t = 0; t < nt; ++t) {
-        pthread_join(th[t], NULL);
-        err |= jobs[t].err;
-      }
-      free(th);
-      free(jobs);
-    }
+  if ((size_t)n_threads > n) n_threads = (int)n;
+  pthread_t* th = calloc((size_t)n_threads, sizeof(pthread_t));
+  job* jobs = calloc((size_t)n_threads, sizeof(job));
+  for (int t = 0; t < n_threads; ++t) {
+    job* j = &jobs[t];
+    j->scheme_arr = scheme;
+    j->lo = n * (size_t)t / (size_t)n_threads;
+    j->hi = n * (size_t)(t + 1) / (size_t)n_threads;
+    j->key_base = key_base;
+    j->pk = pk; j->sig = sig; j->pk_stride = pk_stride; j->sig_stride = sig_stride;
+    j->sig_len = sig_len; j->msg = msg; j->msg_off = msg_off; j->msg_len = msg_len;
+    pthread_create(&th[t], NULL, worker, j);
   }
+  int err = 0;
+  for (int t = 0; t < n_threads; ++t) {
+    pthread_join(th[t], NULL);
+    err |= jobs[t].err;
+  }
+  free(th);
+  free(jobs);
   return err ? -1 : 0;
+}
+
+/* WireTransaction ids for synthetic transactions (to sign them): the
+ * MerkleTransaction.kt:16-33 / MerkleTree.kt:27-66 construction with OpenSSL's
+ * SHA-256.  Layout as cg_txid_batch. */
+int dg_txid_batch(const uint8_t* arena, const uint64_t* comp_off, const uint32_t* comp_len,
+                  const uint32_t* comp_start, const uint8_t* salts, size_t n_tx, uint8_t* ids_out) {
+  for (size_t t = 0; t < n_tx; ++t) {
+    uint32_t k = comp_start[t + 1] - comp_start[t], kp = 1;
+    if (!k) return -1;
+    while (kp < k) kp <<= 1;
+    uint8_t* lv = calloc(kp, 32);
+    for (uint32_t i = 0; i < k; ++i) {
+      const uint8_t* ser = arena + comp_off[comp_start[t] + i];
+      uint32_t len = comp_len[comp_start[t] + i];
+      if (i == k - 1) {
+        SHA256(ser, len, lv + 32 * i);
+      } else {
+        uint8_t pre[36], nonce[32];
+        memcpy(pre, salts + 32 * t, 32);
+        pre[32] = (uint8_t)(i >> 24); pre[33] = (uint8_t)(i >> 16); pre[34] = (uint8_t)(i >> 8); pre[35] = (uint8_t)i;
+        SHA256(pre, 36, nonce);
+        SHA256_CTX c;
+        SHA256_Init(&c);
+        SHA256_Update(&c, ser, len);
+        SHA256_Update(&c, nonce, 32);
+        SHA256_Final(lv + 32 * i, &c);
+      }
+    }
+    for (uint32_t w = kp; w > 1; w >>= 1)
+      for (uint32_t j = 0; j < w / 2; ++j) SHA256(lv + 64 * j, 64, lv + 32 * j);
+    memcpy(ids_out + 32 * t, lv, 32);
+    free(lv);
+  }
+  return 0;
 }

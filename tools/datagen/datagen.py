@@ -212,3 +212,68 @@ def add_ecdsa_adversarial(w: Workload, frac: float = 0.01, seed: int = 7) -> Wor
         w.sig_len[i] = len(new)
     w.classes = classes
     return w
+
+
+# ---------------------------------------------------------- config 4 (transactions)
+HEADER = b"corda\x00\x00\x01"  # Kryo P2P header (node-api SerializationScheme.kt:216)
+
+
+class TxWorkload:
+    """Config-4 shaped SignedTransaction batch in the cg_tx_verify_batch layout."""
+
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+
+def make_tx_batch(n_tx: int, seed: int = 4, key_base: int = 9_000_000, threads: int | None = None,
+                  tamper_frac: float = 0.01) -> TxWorkload:
+    """Trader-demo / loadtest shapes: inputs U{0..3},
+    attachments U{0..1}, outputs U{1..3}, commands U{1..2}, notary 1,
+    timeWindow p=0.3, salt 1; estimated Kryo sizes; signers = distinct command
+    signers (+ notary when inputs > 0 or a time window); schemes 70/15/15 %
+    Ed25519/R1/K1; signatures over the tx id; tamper_frac of txs get one leaf byte
+    flipped after signing (their id changes, so every signature rejects)."""
+    rng = np.random.default_rng(seed)
+    c = lib()
+    c.dg_txid_batch.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_size_t, ctypes.c_void_p]
+    n_in = rng.integers(0, 4, n_tx); n_att = rng.integers(0, 2, n_tx); n_out = rng.integers(1, 4, n_tx)
+    n_cmd = rng.integers(1, 3, n_tx); has_tw = rng.random(n_tx) < 0.3
+    lens = []
+    for t in range(n_tx):
+        l = list(rng.integers(48, 65, n_in[t])) + [48] * n_att[t] + list(rng.integers(300, 701, n_out[t])) + \
+            list(rng.integers(150, 301, n_cmd[t])) + [int(rng.integers(150, 251))] + ([40] if has_tw[t] else []) + [44]
+        lens.append(l)
+    comp_start = np.zeros(n_tx + 1, dtype=np.uint32)
+    comp_start[1:] = np.cumsum([len(l) for l in lens])
+    comp_len = np.array([x for l in lens for x in l], dtype=np.uint32)
+    comp_off = np.zeros(len(comp_len), dtype=np.uint64)
+    comp_off[1:] = np.cumsum(comp_len[:-1], dtype=np.uint64)
+    arena = np.empty(int(comp_len.sum()) + 1, dtype=np.uint8)
+    c.dg_fill_bytes(arena.ctypes.data, len(arena), seed * 1000 + 1)
+    for o in comp_off:  # every serialized component starts with the Kryo header
+        arena[int(o):int(o) + 8] = np.frombuffer(HEADER, dtype=np.uint8)
+    salts = np.empty(32 * n_tx, dtype=np.uint8)
+    c.dg_fill_bytes(salts.ctypes.data, len(salts), seed * 1000 + 2)
+    ids = np.zeros(32 * n_tx, dtype=np.uint8)
+    assert c.dg_txid_batch(arena.ctypes.data, comp_off.ctypes.data, comp_len.ctypes.data, comp_start.ctypes.data,
+                           salts.ctypes.data, n_tx, ids.ctypes.data) == 0
+    n_sig = n_cmd + ((n_in > 0) | has_tw)
+    sig_start = np.zeros(n_tx + 1, dtype=np.uint32)
+    sig_start[1:] = np.cumsum(n_sig)
+    total = int(sig_start[-1])
+    scheme = rng.choice(np.array([4, 3, 2], dtype=np.uint8), size=total, p=[0.7, 0.15, 0.15])
+    msg_off = np.repeat(np.arange(n_tx, dtype=np.uint64) * 32, n_sig)
+    msg_len = np.full(total, 32, dtype=np.uint32)
+    pk = np.zeros((total, 64), dtype=np.uint8)
+    sig = np.zeros((total, 72), dtype=np.uint8)
+    sig_len = np.zeros(total, dtype=np.uint32)
+    assert c.dg_sign_batch(total, scheme.ctypes.data, key_base, pk.ctypes.data, 64, sig.ctypes.data, 72,
+                           sig_len.ctypes.data, ids.ctypes.data, msg_off.ctypes.data, msg_len.ctypes.data,
+                           threads or min(16, os.cpu_count() or 1)) == 0
+    tampered = rng.random(n_tx) < tamper_frac
+    for t in np.flatnonzero(tampered):
+        c0 = int(comp_start[t])
+        arena[int(comp_off[c0]) + 8] ^= 1  # first component, past the header
+    return TxWorkload(n_tx=n_tx, arena=arena, comp_off=comp_off, comp_len=comp_len, comp_start=comp_start,
+                      salts=salts, ids=ids, sig_start=sig_start, scheme=scheme, pk=pk, sig=sig, sig_len=sig_len,
+                      tampered=tampered)
