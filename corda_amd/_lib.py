@@ -11,7 +11,7 @@ import ctypes
 import os
 from ctypes import POINTER, c_char_p, c_double, c_int, c_size_t, c_uint8, c_uint32, c_uint64, c_void_p
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libcordagpu.so")
+LIB_PATH = os.environ.get("CORDA_AMD_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libcordagpu.so")
 
 # status codes
 CG_OK = 0
@@ -62,12 +62,28 @@ class CordaGpuError(RuntimeError):
         self.status = status
 
 
+def _share_torch_hip_runtime() -> None:
+    """One HIP runtime per process.  The PyTorch-ROCm wheel bundles its own
+    libamdhip64 (SONAME libamdhip64.so.7, but NEEDED by torch under the name
+    libamdhip64.so).  If libcordagpu is loaded first, its libamdhip64.so.7
+    resolves to /opt/rocm and a later ``import torch`` maps a second HIP/HSA
+    runtime that then finds no GPU ("No HIP GPUs are available").  Importing
+    torch first lets the dynamic loader bind libcordagpu's dependency to the
+    runtime torch already mapped.  Without torch (a plain C-ABI host) the system
+    runtime is used."""
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
 def load() -> ctypes.CDLL:
     """Loads the in-tree library (raises OSError if it has not been built)."""
     global _lib
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise OSError(f"{LIB_PATH} not built: run __graft_entry__.build() or make -C corda_amd/csrc")
+        _share_torch_hip_runtime()
         lib = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in PROTOTYPES.items():
             fn = getattr(lib, name)

@@ -3,10 +3,11 @@
 //
 //   phase 1 (prep):  decode A (A.2), canonical Abyte (A.4), h = SHA-512(R||Abyte||M)
 //                    mod L (A.5), S_eff = slide-effective S mod L (A.6/A.7),
-//                    signed radix-16 digits of h and S_eff, table k*(-A), k = 0..8.
-//   phase 2 (msm):   R' = [S_eff]B + [h](-A) by a fixed 4-bit window shared by all
-//                    lanes of a wave (no divergence), canonical encoding, byte
-//                    compare with R (A.8/A.9).
+//                    signed radix-32 digits of h, signed radix-256 digits of
+//                    S_eff, table k*(-A), k = 0..16.
+//   phase 2 (msm):   R' = [S_eff]B + [h](-A) by fixed windows (5 bits for A, 8 bits
+//                    for B) shared by all lanes of a wave (no divergence),
+//                    canonical encoding, byte compare with R (A.8/A.9).
 //
 // Reference call path: Crypto.isValid -> EdDSAEngine.engineVerify
 // (/root/reference/core/src/main/kotlin/net/corda/core/crypto/Crypto.kt:534-541).
@@ -25,6 +26,9 @@ namespace cg {
 enum : uint32_t { V_ACCEPT = 0, V_REJECT = 1, V_SIG_MALFORMED = 2, V_KEY_INVALID = 3, V_ARG_EMPTY = 4, V_COMPUTE = 0xff };
 enum : uint32_t { MODE_IS_VALID = 0, MODE_DO_VERIFY = 1 };
 
+constexpr int kATabEntries = 17;   // A side, w = 5 signed digits: k*(-A), |d| <= 16
+constexpr int kBTabEntries = 129;  // B side, w = 8 signed digits: k*B, |d| <= 128
+
 // Verdict precedence before any curve arithmetic (mirrors the JVM order: the
 // PublicKey object exists before doVerify runs, then Crypto.kt:474-476, then the
 // engine's length check).
@@ -41,7 +45,7 @@ CG_HD void ed25519_abyte(uint32_t ab[8], const ge_p3& A) {
   ab[7] |= fe_isnegative(A.X) << 31;
 }
 
-// Table entry k*P (k = 0..8) in cached form, P given as p3; writes via `put`.
+// Table entry k*P (k = 0..16) in cached form, P given as p3; writes via `put`.
 template <typename Put>
 CG_HD void ed25519_build_table(const ge_p3& P, Put&& put) {
   ge_cached c;
@@ -55,7 +59,7 @@ CG_HD void ed25519_build_table(const ge_p3& P, Put&& put) {
   put(1, p1);
   ge_p3 cur = P;
   ge_p1p1 t;
-  CG_NOUNROLL for (int k = 2; k <= 8; ++k) {
+  CG_NOUNROLL for (int k = 2; k < kATabEntries; ++k) {
     ge_add_cached(t, cur, p1, 0);
     ge_p1p1_to_p3(cur, t);
     ge_p3_to_cached(c, cur);
@@ -63,9 +67,9 @@ CG_HD void ed25519_build_table(const ge_p3& P, Put&& put) {
   }
 }
 
-// Shared table k*B (k = 0..8) in affine precomputed form; computed once on the
-// host at context creation and uploaded (the kernels stage it in LDS).
-CG_HD void ed25519_base_table(ge_precomp tab[9]) {
+// Shared table k*B (k = 0..NB-1) in affine precomputed form; computed once on the
+// host at context creation and uploaded (the MSM kernel stages it in LDS).
+CG_HD void ed25519_base_table(ge_precomp tab[kBTabEntries]) {
   const uint32_t benc[8] = {0x66666658u, 0x66666666u, 0x66666666u, 0x66666666u,
                             0x66666666u, 0x66666666u, 0x66666666u, 0x66666666u};
   const fe d2 = CG_FE_D2;
@@ -77,7 +81,7 @@ CG_HD void ed25519_base_table(ge_precomp tab[9]) {
   fe_1(tab[0].yminusx);
   fe_0(tab[0].xy2d);
   cur = B;
-  for (int k = 1; k <= 8; ++k) {
+  for (int k = 1; k < kBTabEntries; ++k) {
     fe recip, x, y;
     fe_invert(recip, cur.Z);
     fe_mul(x, cur.X, recip);
@@ -97,7 +101,7 @@ CG_HD void ed25519_base_table(ge_precomp tab[9]) {
 // Phase 1 for one signature, everything but the table write.  Returns the
 // pre-verdict (V_COMPUTE when the curve arithmetic must decide).
 CG_HD uint32_t ed25519_prep(const uint32_t pk[8], const uint32_t sig[16], uint32_t sig_len, const uint8_t* msg,
-                            uint32_t msg_len, uint32_t mode, ge_p3& negA, uint32_t hd[8], uint32_t sd[8]) {
+                            uint32_t msg_len, uint32_t mode, ge_p3& negA, uint32_t hd[13], uint32_t sd[8]) {
   ge_p3 A;
   const uint32_t key_ok = ge_frombytes_i2p(A, pk);
   const uint32_t pre = ed25519_precheck(key_ok, sig_len, msg_len, mode);
@@ -107,51 +111,52 @@ CG_HD uint32_t ed25519_prep(const uint32_t pk[8], const uint32_t sig[16], uint32
   sha512_ed25519(dig, sig, ab, msg, msg_len);
   sc_reduce512(h, dig);
   sc_effective_s(s, sig + 8);
-  sc_recode16(hd, h);
-  sc_recode16(sd, s);
+  sc_recode5(hd, h);
+  sc_recode8(sd, s);
   negA = A;
   fe_neg(negA.X, A.X);
   fe_neg(negA.T, A.T);
   return V_COMPUTE;
 }
 
-// Phase 2.  hd/sd: packed digits (consumed, shifted); getA(idx, cached&) loads
-// table entry idx of -A; getB(idx, precomp&) loads entry idx of B's table
-// (k*B, k = 0..8, affine).  Returns the canonical encoding of the result.
+// Phase 2: R' = [S_eff]B + [h](-A) by a bit-position loop shared by every lane
+// of the wave: double at every position, add the A-table entry of the next
+// 5-bit digit at positions = 0 mod 5 and the B-table entry of the next 8-bit digit
+// at positions = 0 mod 8 (both uniform, scalar branches).  hd (13 words) / sd (8)
+// are the MSB-first digit bytes from sc_recode5 / sc_recode8 (consumed).
+// getA(idx, cached&) loads k*(-A) (k = 0..16); getB(idx, precomp&) loads k*B
+// (k = 0..128).  Returns the canonical encoding of R'.
 template <typename GetA, typename GetB>
-CG_HD void ed25519_msm(uint32_t out[8], uint32_t hd[8], uint32_t sd[8], GetA&& getA, GetB&& getB) {
+CG_HD void ed25519_msm(uint32_t out[8], uint32_t hd[13], uint32_t sd[8], GetA&& getA, GetB&& getB) {
   ge_p2 r2;
   ge_p3 r3;
-  ge_p1p1 t;
+  ge_p1p1 t;  // starts as the identity: x = X/Z = 0, y = Y/T = 1
   ge_cached ca;
   ge_precomp pb;
-  fe_0(r3.X);
-  fe_1(r3.Y);
-  fe_1(r3.Z);
-  fe_0(r3.T);
-  CG_NOUNROLL for (int i = 63; i >= 0; --i) {
-    if (i != 63) {
-      CG_NOUNROLL for (int k = 0; k < 3; ++k) {
-        ge_p2_dbl(t, r2);
-        ge_p1p1_to_p2(r2, t);
-      }
-      ge_p2_dbl(t, r2);
+  fe_0(t.X);
+  fe_1(t.Y);
+  fe_1(t.Z);
+  fe_1(t.T);
+  CG_NOUNROLL for (int pos = 250; pos >= 0; --pos) {
+    if (pos != 250) ge_p2_dbl(t, r2);
+    if (pos % 5 == 0) {
+      const uint32_t e = hd[0] & 0xff;
+      CG_UNROLL for (int w = 0; w < 12; ++w) hd[w] = hd[w] >> 8 | hd[w + 1] << 24;
+      hd[12] >>= 8;
+      const uint32_t neg = e < 16, a = neg ? 16 - e : e - 16;
+      getA(a, ca);
       ge_p1p1_to_p3(r3, t);
+      ge_add_cached(t, r3, ca, neg);
     }
-    const uint32_t eh = hd[7] >> 28, es = sd[7] >> 28;
-    CG_UNROLL for (int w = 7; w > 0; --w) {
-      hd[w] = hd[w] << 4 | hd[w - 1] >> 28;
-      sd[w] = sd[w] << 4 | sd[w - 1] >> 28;
+    if (pos % 8 == 0) {
+      const uint32_t e = sd[0] & 0xff;
+      CG_UNROLL for (int w = 0; w < 7; ++w) sd[w] = sd[w] >> 8 | sd[w + 1] << 24;
+      sd[7] >>= 8;
+      const uint32_t neg = e < 128, a = neg ? 128 - e : e - 128;
+      getB(a, pb);
+      ge_p1p1_to_p3(r3, t);
+      ge_madd(t, r3, pb, neg);
     }
-    hd[0] <<= 4;
-    sd[0] <<= 4;
-    const uint32_t nh = eh < 8, ns = es < 8;
-    const uint32_t ah = nh ? 8 - eh : eh - 8, as = ns ? 8 - es : es - 8;
-    getA(ah, ca);
-    ge_add_cached(t, r3, ca, nh);
-    ge_p1p1_to_p3(r3, t);
-    getB(as, pb);
-    ge_madd(t, r3, pb, ns);
     ge_p1p1_to_p2(r2, t);
   }
   ge_tobytes(out, r2.X, r2.Y, r2.Z);

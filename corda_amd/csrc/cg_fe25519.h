@@ -43,16 +43,26 @@ CG_HD void fe_select(fe& h, const fe& f, const fe& g, uint32_t c) {
 }
 
 // Signed carry chain (round-to-nearest) on 64-bit column sums -> reduced limbs.
+// With rounding carries c = (t + 2^(w-1)) >> w, the residue t - c*2^w is exactly
+// the sign-extended low w bits of t, so it costs one v_bfe_i32 instead of a
+// shift + subtract.
+CG_HD int64_t sext_low64(int64_t x, int bits) {
+  return (int64_t)((int32_t)((uint32_t)x << (32 - bits)) >> (32 - bits));
+}
+CG_HD int32_t sext_low32(int32_t x, int bits) {
+  return (int32_t)((uint32_t)x << (32 - bits)) >> (32 - bits);
+}
+
 CG_HD void fe_carry_wide(fe& h, int64_t t[10]) {
   int64_t c;
 #define CG_C26(k)                      \
   c = (t[k] + (1LL << 25)) >> 26;      \
   t[(k) + 1] += c;                     \
-  t[k] -= c * (1LL << 26);
+  t[k] = sext_low64(t[k], 26);
 #define CG_C25(k)                      \
   c = (t[k] + (1LL << 24)) >> 25;      \
   t[(k) + 1] += c;                     \
-  t[k] -= c * (1LL << 25);
+  t[k] = sext_low64(t[k], 25);
   CG_C26(0) CG_C26(4)
   CG_C25(1) CG_C25(5)
   CG_C26(2) CG_C26(6)
@@ -60,7 +70,7 @@ CG_HD void fe_carry_wide(fe& h, int64_t t[10]) {
   CG_C26(4) CG_C26(8)
   c = (t[9] + (1LL << 24)) >> 25;
   t[0] += c * 19;
-  t[9] -= c * (1LL << 25);
+  t[9] = sext_low64(t[9], 25);
   CG_C26(0)
 #undef CG_C26
 #undef CG_C25
@@ -73,11 +83,11 @@ CG_HD void fe_reduce(fe& h) {
 #define CG_C26(k)                      \
   c = (h.v[k] + (1 << 25)) >> 26;      \
   h.v[(k) + 1] += c;                   \
-  h.v[k] -= c * (1 << 26);
+  h.v[k] = sext_low32(h.v[k], 26);
 #define CG_C25(k)                      \
   c = (h.v[k] + (1 << 24)) >> 25;      \
   h.v[(k) + 1] += c;                   \
-  h.v[k] -= c * (1 << 25);
+  h.v[k] = sext_low32(h.v[k], 25);
   CG_C26(0) CG_C26(4)
   CG_C25(1) CG_C25(5)
   CG_C26(2) CG_C26(6)
@@ -85,7 +95,7 @@ CG_HD void fe_reduce(fe& h) {
   CG_C26(4) CG_C26(8)
   c = (h.v[9] + (1 << 24)) >> 25;
   h.v[0] += c * 19;
-  h.v[9] -= c * (1 << 25);
+  h.v[9] = sext_low32(h.v[9], 25);
   CG_C26(0)
 #undef CG_C26
 #undef CG_C25

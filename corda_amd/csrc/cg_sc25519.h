@@ -153,6 +153,33 @@ CG_HD void sc_recode16(uint32_t packed[8], const uint32_t k[8]) {
   }
 }
 
+// Signed radix-2^W digits of k < 2^253, most significant first, one digit per
+// byte (e = d + 2^(W-1)), consumed by the MSM from byte 0 of word 0 onward.
+//   W = 5: 51 digits d in [-16, 15] -> 13 words   (A side: table k*(-A), k = 0..16)
+//   W = 8: 32 digits d in [-128, 127] -> 8 words  (B side: table k*B, k = 0..128)
+template <int W, int NDIG, int NWORDS>
+CG_HD void sc_recode_msb(uint32_t out[NWORDS], const uint32_t k[8]) {
+  uint32_t dig[NDIG];
+  uint32_t carry = 0;
+  CG_UNROLL for (int i = 0; i < NDIG; ++i) {
+    const int bit = W * i;
+    uint32_t chunk = 0;
+    CG_UNROLL for (int b = 0; b < W; ++b) {
+      const int pos = bit + b;
+      if (pos < 256) chunk |= ((k[pos >> 5] >> (pos & 31)) & 1u) << b;
+    }
+    const uint32_t v = chunk + carry;
+    carry = v >= (1u << (W - 1));
+    dig[i] = v + (1u << (W - 1)) - (carry << W);  // d + 2^(W-1)
+  }
+  CG_UNROLL for (int w = 0; w < NWORDS; ++w) out[w] = 0;
+  CG_UNROLL for (int j = 0; j < NDIG; ++j) {  // j-th consumed = digit NDIG-1-j
+    out[j >> 2] |= dig[NDIG - 1 - j] << (8 * (j & 3));
+  }
+}
+CG_HD void sc_recode5(uint32_t out[13], const uint32_t k[8]) { sc_recode_msb<5, 51, 13>(out, k); }
+CG_HD void sc_recode8(uint32_t out[8], const uint32_t k[8]) { sc_recode_msb<8, 32, 8>(out, k); }
+
 // S_eff mod L for i2p's slide semantics.
 CG_HD void sc_effective_s(uint32_t out[8], const uint32_t s[8]) {
   uint32_t x[16];

@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <mutex>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -153,7 +154,7 @@ cg_status ensure_ed_scratch(cg_ctx* ctx, uint32_t need) {
   ctx->ed_scap = 0;
   cg_status st;
   if ((st = dalloc(ctx, &ctx->ed_status, want, "alloc ed25519 status")) != CG_OK) return st;
-  if ((st = dalloc(ctx, &ctx->ed_digits, (size_t)16 * want, "alloc ed25519 digits")) != CG_OK) return st;
+  if ((st = dalloc(ctx, &ctx->ed_digits, cg::ed25519_digit_words() * want, "alloc ed25519 digits")) != CG_OK) return st;
   if ((st = dalloc(ctx, (uint8_t**)&ctx->ed_table, cg::ed25519_table_bytes(want), "alloc ed25519 table")) != CG_OK)
     return st;
   ctx->ed_scap = want;
@@ -271,9 +272,10 @@ cg_status cg_open(int device, cg_ctx** out) {
     delete ctx;
     return CG_E_DEVICE;
   }
-  int32_t bt[270];
-  cg::ed25519_base_table_words(bt);
-  if (dalloc(ctx, &ctx->btab, 270, "alloc base table") != CG_OK ||
+  static int32_t bt[cg::kEdBaseTableWords];
+  static std::once_flag bt_once;
+  std::call_once(bt_once, [] { cg::ed25519_base_table_words(bt); });
+  if (dalloc(ctx, &ctx->btab, cg::kEdBaseTableWords, "alloc base table") != CG_OK ||
       hipMemcpy(ctx->btab, bt, sizeof bt, hipMemcpyHostToDevice) != hipSuccess) {
     cg_close(ctx);
     return CG_E_DEVICE;

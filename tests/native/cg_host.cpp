@@ -41,6 +41,8 @@ uint32_t cgh_slide_drop(const uint32_t* s) { return slide_drops_carry(s); }
 void cgh_effective_s(const uint32_t* s, uint32_t* out) { sc_effective_s(out, s); }
 
 void cgh_recode16(const uint32_t* k, uint32_t* out) { sc_recode16(out, k); }
+void cgh_recode5(const uint32_t* k, uint32_t* out) { sc_recode5(out, k); }
+void cgh_recode8(const uint32_t* k, uint32_t* out) { sc_recode8(out, k); }
 
 void cgh_sha512_ed25519(const uint32_t* r, const uint32_t* ab, const uint8_t* msg, uint32_t n, uint32_t* out) {
   sha512_ed25519(out, r, ab, msg, n);
@@ -53,7 +55,7 @@ int cgh_abyte(const uint32_t* pk, uint32_t* out) {
   return 0;
 }
 
-static ge_precomp g_btab[9];
+static ge_precomp g_btab[kBTabEntries];
 static int g_init;
 
 int cgh_ed25519_verify(const uint8_t* pk_bytes, const uint8_t* sig_bytes, uint32_t sig_len, const uint8_t* msg,
@@ -66,10 +68,10 @@ int cgh_ed25519_verify(const uint8_t* pk_bytes, const uint8_t* sig_bytes, uint32
   memcpy(pk, pk_bytes, 32);
   memcpy(sig, sig_bytes, sig_len < 64 ? sig_len : 64);
   ge_p3 negA;
-  uint32_t hd[8], sd[8];
+  uint32_t hd[13], sd[8];
   const uint32_t pre = ed25519_prep(pk, sig, sig_len, msg, msg_len, mode, negA, hd, sd);
   if (pre != V_COMPUTE) return (int)pre;
-  ge_cached tab[9];
+  ge_cached tab[kATabEntries];
   ed25519_build_table(negA, [&](int k, const ge_cached& c) { tab[k] = c; });
   uint32_t rc[8];
   ed25519_msm(

@@ -65,3 +65,17 @@ def test_product_does_not_link_the_oracle():
     assert "oracle_" not in out
     deps = subprocess.check_output(["readelf", "-d", LIB], text=True)
     assert "liboracle" not in deps and "libcrypto" not in deps
+
+
+def test_single_hip_runtime_per_process():
+    """libcordagpu and torch must share one HIP runtime (two in one process
+    leave the second without a GPU); see corda_amd._lib._share_torch_hip_runtime."""
+    import re
+    import subprocess
+    import sys
+    code = ("from corda_amd import _lib; _lib.load(); import torch, re;"
+            "print(sorted(set(re.findall(r'/\\S*libamdhip64\\S*', open('/proc/self/maps').read()))))")
+    out = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    libs = eval(out.stdout.strip().splitlines()[-1])
+    assert len(libs) == 1, libs

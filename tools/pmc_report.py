@@ -1,0 +1,124 @@
+#!/usr/bin/env python3
+"""Reduce a tools/profile_gpu.sh run into the committed profile summaries.
+
+    python tools/pmc_report.py gpurun_out/prof_r01b r01b [--grid 1048576]
+
+Writes profiles/<tag>_rocprof_kernel_stats.csv (rocprofv3 --stats output),
+profiles/<tag>_rocprof_trace_summary.json, profiles/<tag>_pmc/ (raw counter CSVs),
+profiles/<tag>_pmc_summary.json and refreshes profiles/pmc_traffic.json, which
+bench.py reads for the `traffic` field and the hardware-VALU view.
+
+Conventions (MI355X_MICROARCH.md, HBM / rocprofv3 section):
+  * SQ_INSTS_VALU counts wave instructions; per-lane (= per-verify) count is
+    SQ_INSTS_VALU / SQ_WAVES.
+  * effective clock = GRBM_GUI_ACTIVE / 8 XCDs / dispatch duration.
+  * FETCH_SIZE / WRITE_SIZE are KiB; HBM bytes = (FETCH_SIZE + WRITE_SIZE) * 1024.
+    No 2x correction is applied: these kernels gather 4-16 B per lane, not the
+    16-B streaming loads the correction is calibrated on.
+"""
+from __future__ import annotations
+
+import csv
+import glob
+import json
+import os
+import shutil
+import statistics
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+from prof_summary import short, trace  # noqa: E402
+
+PEAK_LANE_OPS_PER_CLK = 256 * 64  # CUs x lanes (full-rate VOP3 integer)
+
+
+def load_counters(paths, grid):
+    agg = defaultdict(lambda: defaultdict(list))
+    dur = defaultdict(list)
+    for p in paths:
+        for r in csv.DictReader(open(p)):
+            if int(r.get("Grid_Size", 0) or 0) != grid:
+                continue
+            k = short(r["Kernel_Name"])
+            agg[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+            dur[(k, r["Counter_Name"])].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e9)
+    return agg, dur
+
+
+def main():
+    src, tag = sys.argv[1], sys.argv[2]
+    grid = int(sys.argv[sys.argv.index("--grid") + 1]) if "--grid" in sys.argv else 1 << 20
+    prof = os.path.join(ROOT, "profiles")
+    tr = glob.glob(os.path.join(src, "trace", "**", "*kernel_trace.csv"), recursive=True)
+    st = glob.glob(os.path.join(src, "trace", "**", "*kernel_stats.csv"), recursive=True)
+    if st:
+        shutil.copy(st[0], os.path.join(prof, f"{tag}_rocprof_kernel_stats.csv"))
+    trace_rows = trace(tr[0]) if tr else []
+    with open(os.path.join(prof, f"{tag}_rocprof_trace_summary.json"), "w") as f:
+        json.dump({"source": f"rocprofv3 --kernel-trace --stats over bench.py (tools/profile_gpu.sh {tag})",
+                   "kernels": trace_rows}, f, indent=1)
+    pmc_csv = sorted(glob.glob(os.path.join(src, "p*", "**", "*counter_collection.csv"), recursive=True))
+    raw_dir = os.path.join(prof, f"{tag}_pmc")
+    os.makedirs(raw_dir, exist_ok=True)
+    for p in pmc_csv:
+        shutil.copy(p, os.path.join(raw_dir, os.path.basename(p)))
+    agg, dur = load_counters(pmc_csv, grid)
+    kernels = {}
+    for k, cs in agg.items():
+        c = {n: statistics.median(v) for n, v in cs.items()}
+        d = {n: statistics.median(dur[(k, n)]) for n in cs}
+        t_ms = [r["avg_ms"] for r in trace_rows if r["kernel"] == k and r["grid_threads"] == grid]
+        avg_s = t_ms[0] / 1e3 if t_ms else d.get("SQ_INSTS_VALU", 0.0)
+        e = {"grid_threads": grid, "avg_ms_trace": round(avg_s * 1e3, 4)}
+        waves = c.get("SQ_WAVES") or grid / 64
+        if "SQ_INSTS_VALU" in c:
+            per_lane = c["SQ_INSTS_VALU"] / waves
+            lane_ops = per_lane * grid / avg_s
+            e["valu_instr_per_verify"] = round(per_lane)
+            e["valu_lane_ops_per_s_T"] = round(lane_ops / 1e12, 2)
+            e["frac_of_39.3T_nominal"] = round(lane_ops / 39.3e12, 3)
+            if "SQ_INSTS_VALU_INT64" in c:
+                e["int64_instr_per_verify"] = round(c["SQ_INSTS_VALU_INT64"] / waves)
+            if "GRBM_GUI_ACTIVE" in c and d.get("GRBM_GUI_ACTIVE"):
+                clk = c["GRBM_GUI_ACTIVE"] / 8 / d["GRBM_GUI_ACTIVE"]
+                e["effective_clock_GHz"] = round(clk / 1e9, 3)
+                e["frac_of_vop3_peak_at_measured_clock"] = round(
+                    c["SQ_INSTS_VALU"] * 64 / d["SQ_INSTS_VALU"] / (PEAK_LANE_OPS_PER_CLK * clk), 3)
+        if "SQ_ACTIVE_INST_VALU" in c and "SQ_BUSY_CYCLES" in c:
+            e["active_valu_per_busy_cycle"] = round(c["SQ_ACTIVE_INST_VALU"] / c["SQ_BUSY_CYCLES"], 3)
+        if "SQ_WAIT_ANY" in c and "SQ_WAVE_CYCLES" in c:
+            e["wait_any_frac"] = round(c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"], 3)
+            e["wait_inst_any_frac"] = round(c.get("SQ_WAIT_INST_ANY", 0) / c["SQ_WAVE_CYCLES"], 3)
+        if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+            b = (c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024
+            e["hbm_bytes_per_launch"] = round(b)
+            e["hbm_bytes_per_verify"] = round(b / grid, 1)
+            e["hbm_GBps"] = round(b / avg_s / 1e9, 1)
+        if "TCC_HIT_sum" in c:
+            e["l2_hit_rate"] = round(c["TCC_HIT_sum"] / max(c["TCC_HIT_sum"] + c["TCC_MISS_sum"], 1), 4)
+        e["counters"] = c
+        kernels[k] = e
+    summary = {"source": f"rocprofv3 --pmc passes over `python3 bench.py --steps 3` (tools/profile_gpu.sh {tag}); "
+                         f"raw CSVs in profiles/{tag}_pmc/",
+               "notes": __doc__.split("Conventions")[1].strip().splitlines(),
+               "kernels": kernels}
+    with open(os.path.join(prof, f"{tag}_pmc_summary.json"), "w") as f:
+        json.dump(summary, f, indent=1)
+    msm = kernels.get("cg_ed25519_msm", {})
+    prep = kernels.get("cg_ed25519_prep", {})
+    traffic = {"source": f"profiles/{tag}_pmc_summary.json",
+               "ed25519_msm_bytes_per_launch": msm.get("hbm_bytes_per_launch"),
+               "ed25519_prep_bytes_per_launch": prep.get("hbm_bytes_per_launch"),
+               "ed25519_msm_valu_instr_per_verify": msm.get("valu_instr_per_verify"),
+               "ed25519_msm_effective_clock_GHz": msm.get("effective_clock_GHz"),
+               "ed25519_prep_valu_instr_per_verify": prep.get("valu_instr_per_verify")}
+    with open(os.path.join(prof, "pmc_traffic.json"), "w") as f:
+        json.dump(traffic, f, indent=1)
+    print(json.dumps({k: {kk: vv for kk, vv in v.items() if kk != "counters"} for k, v in kernels.items()},
+                     indent=1))
+
+
+if __name__ == "__main__":
+    main()
