@@ -482,9 +482,23 @@ cg_status cg_batch_verify(cg_ctx* ctx, cg_batch* b, int mode, uint8_t* verdict_o
   }
   for (int c = 0; c < 2; ++c) {
     if (!b->ec[c].n) continue;
-    Timed t(ctx, "ecdsa_verify", b->ec[c].n);
-    CG_TRY(ctx, cg::ecdsa_batch_verify(b->ec[c], ctx->ec, b->arena, (uint32_t)mode, b->verdict, ctx->stream),
-           "launch ecdsa");
+    const cg::EcdsaBatch& eb = b->ec[c];
+    const char* prep_name = eb.scheme == 2 ? "ecdsa_k1_prep" : "ecdsa_r1_prep";
+    const char* msm_name = eb.scheme == 2 ? "ecdsa_k1_msm" : "ecdsa_r1_msm";
+    uint32_t chunk = 0;
+    CG_TRY(ctx, cg::ecdsa_scratch(ctx->ec, eb.n, &chunk), "alloc ecdsa scratch");
+    for (uint32_t base = 0; base < eb.n; base += chunk) {
+      const uint32_t cnt = std::min(chunk, eb.n - base);
+      {
+        Timed t(ctx, prep_name, cnt);
+        CG_TRY(ctx, cg::ecdsa_launch_prep(eb, ctx->ec, base, cnt, b->arena, (uint32_t)mode, ctx->stream),
+               "launch ecdsa prep");
+      }
+      {
+        Timed t(ctx, msm_name, cnt);
+        CG_TRY(ctx, cg::ecdsa_launch_msm(eb, ctx->ec, base, cnt, b->verdict, ctx->stream), "launch ecdsa msm");
+      }
+    }
   }
   CG_TRY(ctx, cg::launch_verdict_bitmap(b->verdict, (uint32_t)n, b->bitmap, ctx->stream), "launch bitmap");
   const size_t nwords = (n + 31) / 32;

@@ -170,22 +170,21 @@ hipError_t ensure_scratch(EcdsaConsts* c, uint32_t need) {
 }
 
 template <class C>
-hipError_t verify_curve(const EcdsaBatch& b, EcdsaConsts* c, const uint8_t* arena, uint32_t mode, uint8_t* verdict,
-                        hipStream_t s) {
-  hipError_t e = ensure_scratch(c, b.n);
-  if (e != hipSuccess) return e;
+hipError_t launch_prep(const EcdsaBatch& b, EcdsaConsts* c, uint32_t base, uint32_t cnt, const uint8_t* arena,
+                       uint32_t mode, hipStream_t s) {
+  hipLaunchKernelGGL(cg_ecdsa_prep<C>, grid_for(cnt), dim3(256), 0, s, b.q + base, b.rs + base, b.der + base,
+                     b.sig_len + base, arena, b.msg_off + base, b.msg_len + base, cnt, b.n, c->scap, mode, c->status,
+                     c->digits, c->qtab);
+  return hipGetLastError();
+}
+
+template <class C>
+hipError_t launch_msm(const EcdsaBatch& b, EcdsaConsts* c, uint32_t base, uint32_t cnt, uint8_t* verdict,
+                      hipStream_t s) {
   const uint32_t* gt = c->gtab[C::kScheme == 2 ? 0 : 1];
-  for (uint32_t base = 0; base < b.n; base += c->scap) {
-    const uint32_t cnt = b.n - base < c->scap ? b.n - base : c->scap;
-    hipLaunchKernelGGL(cg_ecdsa_prep<C>, grid_for(cnt), dim3(256), 0, s, b.q + base, b.rs + base, b.der + base,
-                       b.sig_len + base, arena, b.msg_off + base, b.msg_len + base, cnt, b.n, c->scap, mode,
-                       c->status, c->digits, c->qtab);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(cg_ecdsa_msm<C>, grid_for(cnt), dim3(256), 0, s, b.rs + base, c->status, c->digits, c->qtab,
-                       gt, cnt, b.n, c->scap, b.index + base, verdict);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-  }
-  return hipSuccess;
+  hipLaunchKernelGGL(cg_ecdsa_msm<C>, grid_for(cnt), dim3(256), 0, s, b.rs + base, c->status, c->digits, c->qtab, gt,
+                     cnt, b.n, c->scap, b.index + base, verdict);
+  return hipGetLastError();
 }
 
 }  // namespace
@@ -264,11 +263,24 @@ hipError_t ecdsa_batch_stage(EcdsaBatch& b, int scheme, const uint32_t* host_ind
   return e;
 }
 
-hipError_t ecdsa_batch_verify(const EcdsaBatch& b, EcdsaConsts* c, const uint8_t* arena, uint32_t mode,
-                              uint8_t* verdict, hipStream_t s) {
-  if (b.n == 0) return hipSuccess;
-  return b.scheme == 2 ? verify_curve<CurveK1>(b, c, arena, mode, verdict, s)
-                       : verify_curve<CurveR1>(b, c, arena, mode, verdict, s);
+hipError_t ecdsa_scratch(EcdsaConsts* c, uint32_t n, uint32_t* chunk) {
+  const hipError_t e = ensure_scratch(c, n);
+  *chunk = c->scap;
+  return e;
+}
+
+hipError_t ecdsa_launch_prep(const EcdsaBatch& b, EcdsaConsts* c, uint32_t base, uint32_t cnt, const uint8_t* arena,
+                             uint32_t mode, hipStream_t s) {
+  if (cnt == 0) return hipSuccess;
+  return b.scheme == 2 ? launch_prep<CurveK1>(b, c, base, cnt, arena, mode, s)
+                       : launch_prep<CurveR1>(b, c, base, cnt, arena, mode, s);
+}
+
+hipError_t ecdsa_launch_msm(const EcdsaBatch& b, EcdsaConsts* c, uint32_t base, uint32_t cnt, uint8_t* verdict,
+                            hipStream_t s) {
+  if (cnt == 0) return hipSuccess;
+  return b.scheme == 2 ? launch_msm<CurveK1>(b, c, base, cnt, verdict, s)
+                       : launch_msm<CurveR1>(b, c, base, cnt, verdict, s);
 }
 
 }  // namespace cg

@@ -93,15 +93,18 @@ static void sign_ed(job* j, size_t i, EVP_MD_CTX* mctx) {
   EVP_MD_CTX_reset(mctx);
 }
 
-static void sign_ec(job* j, size_t i, int scheme, BN_CTX* bctx) {
+/* One EC_KEY per thread and curve, re-keyed per element (building the group per
+ * signature dominated the generation time). */
+static void sign_ec(job* j, size_t i, int scheme, BN_CTX* bctx, EC_KEY* keys[2]) {
   const int nid = scheme == 2 ? NID_secp256k1 : NID_X9_62_prime256v1;
+  EC_KEY** slot = &keys[scheme == 2 ? 0 : 1];
+  if (!*slot) *slot = EC_KEY_new_by_curve_name(nid);
+  EC_KEY* k = *slot;
   uint8_t seed[32], dig[32];
   key_seed(seed, j->key_base + i);
-  EC_KEY* k = EC_KEY_new_by_curve_name(nid);
   const EC_GROUP* g = EC_KEY_get0_group(k);
   BIGNUM* d = BN_bin2bn(seed, 32, NULL);
-  BIGNUM* order = BN_new();
-  EC_GROUP_get_order(g, order, bctx);
+  const BIGNUM* order = EC_GROUP_get0_order(g);
   BN_mod(d, d, order, bctx);
   if (BN_is_zero(d)) BN_one(d);
   EC_POINT* q = EC_POINT_new(g);
@@ -116,20 +119,21 @@ static void sign_ec(job* j, size_t i, int scheme, BN_CTX* bctx) {
   if (ECDSA_sign(0, dig, 32, j->sig + i * j->sig_stride, &sl, k) != 1) j->err = 1;
   j->sig_len[i] = sl;
   EC_POINT_free(q);
-  BN_free(order);
   BN_free(d);
-  EC_KEY_free(k);
 }
 
 static void* worker(void* arg) {
   job* j = (job*)arg;
   EVP_MD_CTX* mctx = EVP_MD_CTX_new();
   BN_CTX* bctx = BN_CTX_new();
+  EC_KEY* keys[2] = {NULL, NULL};
   for (size_t i = j->lo; i < j->hi; ++i) {
     const int sc = j->scheme_arr ? j->scheme_arr[i] : 4;
     if (sc == 4) sign_ed(j, i, mctx);
-    else if (sc == 2 || sc == 3) sign_ec(j, i, sc, bctx);
+    else if (sc == 2 || sc == 3) sign_ec(j, i, sc, bctx, keys);
   }
+  EC_KEY_free(keys[0]);
+  EC_KEY_free(keys[1]);
   BN_CTX_free(bctx);
   EVP_MD_CTX_free(mctx);
   return NULL;

@@ -30,6 +30,7 @@ def lib():
                                 ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                 ctypes.c_void_p, ctypes.c_int]
     c.dg_fill_bytes.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64]
+    c.dg_txid_batch.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_size_t, ctypes.c_void_p]
     return c
 
 
@@ -41,6 +42,19 @@ class Workload:
         self.sig, self.sig_stride, self.sig_len = sig, sig_stride, sig_len
         self.msg, self.msg_off, self.msg_len = msg, msg_off, msg_len
         self.classes = classes
+
+    def tiled(self, n: int) -> "Workload":
+        """The first n elements of this workload repeated end to end (a bounded
+        pool of distinct signed tuples stretched to a benchmark size).  Every
+        copy owns its message bytes, so later in-place mutations stay local."""
+        reps = -(-n // self.n)
+        m_end = int(self.msg_off[-1]) + int(self.msg_len[-1]) if self.n else 0
+        arena = np.concatenate([np.tile(self.msg[:m_end], reps)[:m_end * reps], np.zeros(16, np.uint8)])
+        off = (self.msg_off[None, :].astype(np.uint64) + np.arange(reps, dtype=np.uint64)[:, None] * np.uint64(m_end))
+        cls = None if self.classes is None else (list(self.classes) * reps)[:n]
+        return Workload(n, np.tile(self.scheme, reps)[:n], np.tile(self.pk, (reps, 1))[:n], self.pk_stride,
+                        np.tile(self.sig, (reps, 1))[:n], self.sig_stride, np.tile(self.sig_len, reps)[:n], arena,
+                        off.ravel()[:n].copy(), np.tile(self.msg_len, reps)[:n], cls)
 
     def subset(self, idx):
         """Copy of elements idx (messages re-packed)."""
@@ -235,23 +249,30 @@ def make_tx_batch(n_tx: int, seed: int = 4, key_base: int = 9_000_000, threads: 
     flipped after signing (their id changes, so every signature rejects)."""
     rng = np.random.default_rng(seed)
     c = lib()
-    c.dg_txid_batch.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_size_t, ctypes.c_void_p]
     n_in = rng.integers(0, 4, n_tx); n_att = rng.integers(0, 2, n_tx); n_out = rng.integers(1, 4, n_tx)
     n_cmd = rng.integers(1, 3, n_tx); has_tw = rng.random(n_tx) < 0.3
-    lens = []
-    for t in range(n_tx):
-        l = list(rng.integers(48, 65, n_in[t])) + [48] * n_att[t] + list(rng.integers(300, 701, n_out[t])) + \
-            list(rng.integers(150, 301, n_cmd[t])) + [int(rng.integers(150, 251))] + ([40] if has_tw[t] else []) + [44]
-        lens.append(l)
+    # components in availableComponents order (MerkleTransaction.kt:74-87), vectorized:
+    # category c of tx t contributes counts[c][t] leaves; a stable sort by tx keeps
+    # the category order inside each tx
+    ones = np.ones(n_tx, dtype=np.int64)
+    cats = [(n_in, lambda k: rng.integers(48, 65, k)), (n_att, lambda k: np.full(k, 48)),
+            (n_out, lambda k: rng.integers(300, 701, k)), (n_cmd, lambda k: rng.integers(150, 301, k)),
+            (ones, lambda k: rng.integers(150, 251, k)), (has_tw.astype(np.int64), lambda k: np.full(k, 40)),
+            (ones, lambda k: np.full(k, 44))]
+    tx_of = np.concatenate([np.repeat(np.arange(n_tx), cnt) for cnt, _ in cats])
+    lens_all = np.concatenate([gen(int(cnt.sum())) for cnt, gen in cats])
+    order = np.argsort(tx_of, kind="stable")
+    comp_len = lens_all[order].astype(np.uint32)
+    per_tx = sum(cnt for cnt, _ in cats)
     comp_start = np.zeros(n_tx + 1, dtype=np.uint32)
-    comp_start[1:] = np.cumsum([len(l) for l in lens])
-    comp_len = np.array([x for l in lens for x in l], dtype=np.uint32)
+    comp_start[1:] = np.cumsum(per_tx)
     comp_off = np.zeros(len(comp_len), dtype=np.uint64)
     comp_off[1:] = np.cumsum(comp_len[:-1], dtype=np.uint64)
     arena = np.empty(int(comp_len.sum()) + 1, dtype=np.uint8)
     c.dg_fill_bytes(arena.ctypes.data, len(arena), seed * 1000 + 1)
-    for o in comp_off:  # every serialized component starts with the Kryo header
-        arena[int(o):int(o) + 8] = np.frombuffer(HEADER, dtype=np.uint8)
+    # every serialized component starts with the Kryo header
+    arena[(comp_off[:, None] + np.arange(8, dtype=np.uint64)).ravel()] = np.tile(
+        np.frombuffer(HEADER, dtype=np.uint8), len(comp_off))
     salts = np.empty(32 * n_tx, dtype=np.uint8)
     c.dg_fill_bytes(salts.ctypes.data, len(salts), seed * 1000 + 2)
     ids = np.zeros(32 * n_tx, dtype=np.uint8)
@@ -277,3 +298,33 @@ def make_tx_batch(n_tx: int, seed: int = 4, key_base: int = 9_000_000, threads: 
     return TxWorkload(n_tx=n_tx, arena=arena, comp_off=comp_off, comp_len=comp_len, comp_start=comp_start,
                       salts=salts, ids=ids, sig_start=sig_start, scheme=scheme, pk=pk, sig=sig, sig_len=sig_len,
                       tampered=tampered)
+
+
+def tile_tx_batch(w: TxWorkload, n_tx: int, tamper_frac: float = 0.01, seed: int = 5) -> TxWorkload:
+    """A pool of signed transactions repeated to n_tx (each copy owns its leaf
+    bytes), then tamper_frac of the txs get one leaf byte flipped (their id
+    changes, so every signature of that tx rejects)."""
+    reps = -(-n_tx // w.n_tx)
+    a_len = int(w.comp_off[-1]) + int(w.comp_len[-1])
+    n_comp = int(w.comp_start[w.n_tx])
+    n_sig = int(w.sig_start[w.n_tx])
+    arena = np.concatenate([np.tile(w.arena[:a_len], reps), np.zeros(1, np.uint8)])
+    comp_off = (w.comp_off[None, :n_comp] + np.arange(reps, dtype=np.uint64)[:, None] * np.uint64(a_len)).ravel()
+    comp_len = np.tile(w.comp_len[:n_comp], reps)
+    comp_start = np.concatenate([np.zeros(1, np.uint32),
+                                 np.cumsum(np.tile(np.diff(w.comp_start), reps), dtype=np.uint64).astype(np.uint32)])
+    sig_start = np.concatenate([np.zeros(1, np.uint32),
+                                np.cumsum(np.tile(np.diff(w.sig_start), reps), dtype=np.uint64).astype(np.uint32)])
+    comp_start, sig_start = comp_start[:n_tx + 1], sig_start[:n_tx + 1]
+    nc, ns = int(comp_start[-1]), int(sig_start[-1])
+    t = TxWorkload(n_tx=n_tx, arena=arena, comp_off=comp_off[:nc].copy(), comp_len=comp_len[:nc].copy(),
+                   comp_start=comp_start, salts=np.tile(w.salts[:32 * w.n_tx], reps)[:32 * n_tx].copy(),
+                   ids=np.tile(w.ids[:32 * w.n_tx], reps)[:32 * n_tx].copy(), sig_start=sig_start,
+                   scheme=np.tile(w.scheme[:n_sig], reps)[:ns].copy(), pk=np.tile(w.pk[:n_sig], (reps, 1))[:ns].copy(),
+                   sig=np.tile(w.sig[:n_sig], (reps, 1))[:ns].copy(), sig_len=np.tile(w.sig_len[:n_sig], reps)[:ns].copy(),
+                   tampered=np.zeros(n_tx, dtype=bool))
+    rng = np.random.default_rng(seed)
+    t.tampered = rng.random(n_tx) < tamper_frac
+    first = t.comp_start[:-1][t.tampered]
+    t.arena[t.comp_off[first] + 8] ^= 1  # first component, past the Kryo header
+    return t
