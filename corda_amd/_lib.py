@@ -46,6 +46,9 @@ PROTOTYPES = {
     "cg_tx_verify_batch": (c_int, [c_void_p, c_int, c_size_t, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p,
                                    c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p, c_size_t, c_void_p,
                                    c_void_p, c_void_p, c_void_p]),
+    "cg_register_host": (c_int, [c_void_p, c_void_p, c_size_t]),
+    "cg_unregister_host": (c_int, [c_void_p, c_void_p]),
+    "cg_release_cached": (c_int, [c_void_p]),
     "cg_set_profiling": (c_int, [c_void_p, c_int]),
     "cg_kernel_stats": (c_int, [c_void_p, c_char_p, POINTER(c_double), POINTER(c_uint64), POINTER(c_uint64)]),
     "cg_reset_stats": (c_int, [c_void_p]),
@@ -145,3 +148,14 @@ class Context:
 
     def reset_stats(self):
         self.check(self.lib.cg_reset_stats(self.h))
+
+    def register_host(self, *arrays):
+        """Page-locks numpy arrays the caller will pass again (cg_register_host)."""
+        for a in arrays:
+            if a is not None and a.nbytes:
+                self.check(self.lib.cg_register_host(self.h, a.ctypes.data, a.nbytes))
+
+    def unregister_host(self, *arrays):
+        for a in arrays:
+            if a is not None and a.nbytes:
+                self.check(self.lib.cg_unregister_host(self.h, a.ctypes.data))

@@ -23,10 +23,11 @@ struct EcdsaBatch {
 
 hipError_t ecdsa_consts_create(EcdsaConsts** out);
 void ecdsa_consts_free(EcdsaConsts* c);
-hipError_t ecdsa_batch_stage(EcdsaBatch& b, int scheme, const uint32_t* host_index, uint32_t n,
-                             const uint8_t* pk_raw_dev, size_t pk_stride, const uint8_t* sig_raw_dev,
-                             size_t sig_stride, const uint32_t* sig_len_dev, const uint64_t* msg_off_all_dev,
-                             const uint32_t* msg_len_all_dev, hipStream_t s);
+// Stages one curve's subset into the SoA buffers of b (allocated by the caller:
+// index[n] already uploaded, q[16n], rs[16n], der/sig_len/msg_len[n], msg_off[n]).
+hipError_t ecdsa_batch_stage(const EcdsaBatch& b, const uint8_t* pk_raw_dev, size_t pk_stride,
+                             const uint8_t* sig_raw_dev, size_t sig_stride, const uint32_t* sig_len_dev,
+                             const uint64_t* msg_off_all_dev, const uint32_t* msg_len_all_dev, hipStream_t s);
 // Scratch is sized for min(n, chunk) elements; a batch is verified chunk by chunk:
 // prep (key check, SHA-256, scalars, k*Q table) then msm (u1 G + u2 Q, x check).
 hipError_t ecdsa_scratch(EcdsaConsts* c, uint32_t n, uint32_t* chunk);
@@ -34,7 +35,6 @@ hipError_t ecdsa_launch_prep(const EcdsaBatch& b, EcdsaConsts* c, uint32_t base,
                              uint32_t mode, hipStream_t s);
 hipError_t ecdsa_launch_msm(const EcdsaBatch& b, EcdsaConsts* c, uint32_t base, uint32_t cnt, uint8_t* verdict,
                             hipStream_t s);
-void ecdsa_batch_free(EcdsaBatch& b);
 // K4 alone: strict DER -> rs [16][cap] LE limbs + status [cap] (0 ok, 1 range, 2 malformed)
 hipError_t launch_der_parse(int scheme, const uint8_t* sig, size_t stride, const uint32_t* sig_len,
                             uint32_t fill_len, const uint32_t* idx, uint32_t n, uint32_t cap, uint32_t* rs,

@@ -1,4 +1,4 @@
-// Host-side interface of the SHA-256 Merkle tx-id kernels (K5 nonce/leaf, K6 tree).
+// Host-side interface of the SHA-256 Merkle tx-id kernels (K5 leaves, K6 tree).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -6,14 +6,19 @@
 namespace cg {
 
 // All pointers are device pointers (layout: merkle_kernels.hip).
-hipError_t launch_merkle_nonce(uint8_t* arena, const uint64_t* slot, const uint32_t* len, const uint32_t* comp_tx,
-                               const uint32_t* comp_idx, const uint32_t* comp_is_salt, const uint32_t* salts,
-                               uint32_t n, hipStream_t s);
-hipError_t launch_merkle_leaf(const uint8_t* arena, const uint64_t* slot, const uint32_t* len,
-                              const uint32_t* comp_is_salt, const uint64_t* leaf_pos, uint32_t n, uint32_t* leaves,
+// comp_tx[c] = owning tx of component c; for every signature s of tx t (sig_start
+// may be null): sig_moff[s] = 32 t, sig_mlen[s] = 32.
+hipError_t launch_tx_index(const uint32_t* comp_start, const uint32_t* sig_start, uint32_t n_tx, uint32_t* comp_tx,
+                           uint64_t* sig_moff, uint32_t* sig_mlen, hipStream_t s);
+// leaves[8c..8c+7] = leaf hash of component c for c in [c_begin, c_end); *err |= 1 when a
+// component lies outside [0, arena_bytes).
+hipError_t launch_merkle_leaf(const uint8_t* arena, uint64_t arena_bytes, const uint64_t* comp_off,
+                              const uint32_t* comp_len, const uint32_t* comp_start, const uint32_t* comp_tx,
+                              const uint32_t* salts, uint32_t c_begin, uint32_t c_end, uint32_t* leaves,
+                              uint32_t* err, hipStream_t s);
+// ids (8 words per tx, digest byte order) = Merkle root over the tx's leaves (in place).
+hipError_t launch_merkle_tree(uint32_t* leaves, const uint32_t* comp_start, uint32_t n_tx, uint32_t* ids,
                               hipStream_t s);
-hipError_t launch_merkle_tree(uint32_t* leaves, const uint64_t* tree_base, const uint32_t* comp_start, uint32_t n_tx,
-                              uint32_t* ids, hipStream_t s);
 // per tx: -1 all signatures ACCEPT, else index of the first non-ACCEPT one; -2 no signatures
 hipError_t launch_first_bad(const uint8_t* verdict, const uint32_t* sig_start, uint32_t n_tx, int32_t* out,
                             hipStream_t s);

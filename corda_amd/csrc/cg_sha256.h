@@ -95,6 +95,52 @@ CG_HD void sha256_mem(uint32_t out[8], const uint8_t* msg, uint32_t n) {
   CG_UNROLL for (int i = 0; i < 8; ++i) out[i] = h[i];
 }
 
+// SHA-256 of msg[0..n) || tail[0..tail_n) (tail_n <= 32): the leaf preimage
+// ser_i || nonce_i of MerkleTransaction.kt:16-30 without first copying ser_i next
+// to its nonce.  The tail sits in a small per-lane buffer read through tb(d)
+// (dwords 0..10, bytes in memory order): bytes 0..3 zero, bytes 4..4+tail_n-1 the
+// tail, byte 4+tail_n = 0x80 (the SHA padding marker), the rest zero.  A message
+// word straddling the end of msg takes its low bytes from memory and the rest from
+// tb at the same byte phase, so both sources are funnel-shifted with
+// v_alignbyte_b32 and OR-ed.  msg may have any alignment; reads never go past
+// the dword holding byte n-1.
+template <typename TB>
+CG_HD void sha256_mem_tail(uint32_t out[8], const uint8_t* msg, uint32_t n, TB&& tb, uint32_t tail_n) {
+  uint32_t h[8], w[16];
+  sha256_init(h);
+  const uintptr_t addr = (uintptr_t)msg;
+  const uint32_t* m4 = (const uint32_t*)(addr & ~(uintptr_t)3);
+  const uint32_t sh = (uint32_t)(addr & 3);
+  const int64_t ndw = ((int64_t)n + sh + 3) >> 2;
+  const uint64_t total = (uint64_t)n + tail_n;
+  const uint32_t nb = (uint32_t)((total + 9 + 63) / 64);
+  CG_NOUNROLL for (uint32_t blk = 0; blk < nb; ++blk) {
+    CG_UNROLL for (int j = 0; j < 16; ++j) {
+      const int64_t q = 64 * (int64_t)blk + 4 * j;
+      const int64_t c = (int64_t)n - q;
+      uint32_t le = 0;
+      if (c > 0) {
+        const int64_t d0 = q >> 2;
+        const uint32_t x0 = m4[d0];
+        const uint32_t x1 = (d0 + 1 < ndw) ? m4[d0 + 1] : 0u;
+        le = alignbyte32(x1, x0, sh);
+        if (c < 4) le &= (1u << (8 * (uint32_t)c)) - 1u;
+      }
+      const int64_t off = 4 - c;  // byte of tb aligned with message byte q
+      if (off >= 1 && off < 40) {
+        const uint32_t d = (uint32_t)off >> 2;
+        le |= alignbyte32(tb(d + 1), tb(d), (uint32_t)off & 3);
+      }
+      uint32_t word = bswap32_(le);
+      if (blk == nb - 1 && j == 14) word = (uint32_t)((total * 8) >> 32);
+      if (blk == nb - 1 && j == 15) word = (uint32_t)(total * 8);
+      w[j] = word;
+    }
+    sha256_block(h, w);
+  }
+  CG_UNROLL for (int i = 0; i < 8; ++i) out[i] = h[i];
+}
+
 // SHA-256 of a short message held in registers as big-endian words (nbytes <= 55
 // gives one block; nbytes = 64 gives two).  Used for nonces (36 B) and nodes (64 B).
 template <int NBYTES>

@@ -10,22 +10,27 @@
 //    each scheme's kernels run on their subset and scatter verdicts back;
 //  * Ed25519 scratch (per-lane tables) is bounded by processing in chunks, so a
 //    100M-signature backlog needs ~3 GB of scratch, not 144 GB;
+//  * device buffers come from a per-context block cache (freed blocks are kept
+//    and reused), so repeated calls do not pay hipMalloc / hipFree;
+//  * the transaction path uploads the caller's component arena as is and derives
+//    all per-component / per-signature metadata on the device;
 //  * no CPU fallback: without a gfx950 device cg_open fails.
 #include "cordagpu.h"
 
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <mutex>
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <mutex>
 #include <new>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
-#include "cg_kernels.h"
 #include "cg_ecdsa_api.h"
+#include "cg_kernels.h"
 #include "cg_merkle_api.h"
 
 namespace {
@@ -50,19 +55,18 @@ struct cg_ctx {
   uint32_t* ed_status = nullptr;
   uint32_t* ed_digits = nullptr;
   int32_t* ed_table = nullptr;
+  uint32_t* err_flag = nullptr;  // device word raised by kernels on malformed layouts
   bool profiling = false;
   std::map<std::string, Stat> stats;
   std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending;
   std::vector<hipEvent_t> event_pool;
   cg::EcdsaConsts* ec = nullptr;
+  // device block cache: size -> free block; live block -> size
+  std::multimap<size_t, void*> free_blocks;
+  std::unordered_map<void*, size_t> live_blocks;
 };
 
 namespace {
-
-struct DevMem {
-  void* p = nullptr;
-  size_t bytes = 0;
-};
 
 cg_status fail(cg_ctx* ctx, cg_status code, const std::string& msg) {
   if (ctx) ctx->err = msg;
@@ -75,9 +79,9 @@ cg_status hip_fail(cg_ctx* ctx, hipError_t e, const char* what) {
   return fail(ctx, e == hipErrorOutOfMemory ? CG_E_OUT_OF_MEMORY : CG_E_DEVICE, m);
 }
 
-#define CG_TRY(ctx, expr, what)                      \
-  do {                                               \
-    hipError_t e_ = (expr);                          \
+#define CG_TRY(ctx, expr, what)                           \
+  do {                                                    \
+    hipError_t e_ = (expr);                               \
     if (e_ != hipSuccess) return hip_fail(ctx, e_, what); \
   } while (0)
 
@@ -129,25 +133,83 @@ void collect_timings(cg_ctx* ctx) {
   ctx->pending.clear();
 }
 
-template <typename T>
-cg_status dalloc(cg_ctx* ctx, T** p, size_t count, const char* what) {
+// ---------------------------------------------------------------- device blocks
+// Requests are rounded to 1/8 of their power-of-two size class so that repeated
+// batches of similar shape hit the cache; a cached block is reused for requests of
+// at least half its size.  All users run on ctx->stream, so reuse is stream-ordered.
+size_t round_block(size_t bytes) {
+  if (bytes <= 4096) return (bytes + 255) & ~(size_t)255;
+  size_t p = 1;
+  while (p * 2 <= bytes) p *= 2;
+  const size_t q = p / 8;
+  return (bytes + q - 1) / q * q;
+}
+
+void release_cached(cg_ctx* ctx) {
+  for (auto& b : ctx->free_blocks) (void)hipFree(b.second);
+  ctx->free_blocks.clear();
+}
+
+cg_status dalloc_bytes(cg_ctx* ctx, void** p, size_t bytes, const char* what) {
   *p = nullptr;
-  if (count == 0) count = 1;
-  hipError_t e = hipMalloc((void**)p, count * sizeof(T));
-  if (e != hipSuccess) return hip_fail(ctx, e, what);
+  const size_t want = round_block(bytes ? bytes : 1);
+  auto it = ctx->free_blocks.lower_bound(want);
+  if (it != ctx->free_blocks.end() && it->first <= 2 * want) {
+    *p = it->second;
+    ctx->live_blocks[it->second] = it->first;
+    ctx->free_blocks.erase(it);
+    return CG_OK;
+  }
+  hipError_t e = hipMalloc(p, want);
+  if (e == hipErrorOutOfMemory && !ctx->free_blocks.empty()) {
+    (void)hipGetLastError();
+    (void)hipStreamSynchronize(ctx->stream);
+    release_cached(ctx);
+    e = hipMalloc(p, want);
+  }
+  if (e != hipSuccess) {
+    *p = nullptr;
+    return hip_fail(ctx, e, what);
+  }
+  ctx->live_blocks[*p] = want;
   return CG_OK;
 }
 
-void dfree(void* p) {
-  if (p) (void)hipFree(p);
+template <typename T>
+cg_status dalloc(cg_ctx* ctx, T** p, size_t count, const char* what) {
+  void* v = nullptr;
+  const cg_status st = dalloc_bytes(ctx, &v, count * sizeof(T), what);
+  *p = (T*)v;
+  return st;
+}
+
+void dfree(cg_ctx* ctx, const void* cp) {
+  void* p = const_cast<void*>(cp);
+  if (!p) return;
+  auto it = ctx->live_blocks.find(p);
+  if (it == ctx->live_blocks.end()) {
+    (void)hipFree(p);
+    return;
+  }
+  ctx->free_blocks.emplace(it->second, p);
+  ctx->live_blocks.erase(it);
+}
+
+template <typename T>
+cg_status upload(cg_ctx* ctx, T** dst, const T* src, size_t count, const char* what) {
+  cg_status st = dalloc(ctx, dst, count, what);
+  if (st != CG_OK) return st;
+  if (count) CG_TRY(ctx, hipMemcpyAsync(*dst, src, count * sizeof(T), hipMemcpyHostToDevice, ctx->stream), what);
+  return CG_OK;
 }
 
 cg_status ensure_ed_scratch(cg_ctx* ctx, uint32_t need) {
   const uint32_t want = std::min(need, kEdChunk);
   if (ctx->ed_scap >= want) return CG_OK;
-  dfree(ctx->ed_status);
-  dfree(ctx->ed_digits);
-  dfree(ctx->ed_table);
+  (void)hipStreamSynchronize(ctx->stream);
+  dfree(ctx, ctx->ed_status);
+  dfree(ctx, ctx->ed_digits);
+  dfree(ctx, ctx->ed_table);
   ctx->ed_status = nullptr;
   ctx->ed_digits = nullptr;
   ctx->ed_table = nullptr;
@@ -172,6 +234,7 @@ struct cg_batch {
   bool arena_owned = true;
   uint64_t* msg_off_all = nullptr;
   uint32_t* msg_len_all = nullptr;
+  bool meta_owned = true;
   // Ed25519 subset
   uint32_t n_ed = 0;
   uint32_t* ed_index = nullptr;  // null when the subset is the whole batch in order
@@ -186,31 +249,49 @@ struct cg_batch {
 
 namespace {
 
-void batch_free(cg_batch* b) {
+void batch_free(cg_ctx* ctx, cg_batch* b) {
   if (!b) return;
-  dfree(b->verdict);
-  dfree(b->bitmap);
-  if (b->arena_owned) dfree(b->arena);
-  dfree(b->msg_off_all);
-  dfree(b->msg_len_all);
-  dfree(b->ed_index);
-  dfree(b->ed_pk);
-  dfree(b->ed_sig);
-  dfree(b->ed_sig_len);
-  dfree(b->ed_msg_off);
-  dfree(b->ed_msg_len);
-  for (auto& e : b->ec) cg::ecdsa_batch_free(e);
+  dfree(ctx, b->verdict);
+  dfree(ctx, b->bitmap);
+  if (b->arena_owned) dfree(ctx, b->arena);
+  if (b->meta_owned) {
+    dfree(ctx, b->msg_off_all);
+    dfree(ctx, b->msg_len_all);
+  }
+  dfree(ctx, b->ed_index);
+  dfree(ctx, b->ed_pk);
+  dfree(ctx, b->ed_sig);
+  dfree(ctx, b->ed_sig_len);
+  dfree(ctx, b->ed_msg_off);
+  dfree(ctx, b->ed_msg_len);
+  for (auto& e : b->ec)
+    for (const void* p : {(const void*)e.index, (const void*)e.q, (const void*)e.rs, (const void*)e.der,
+                          (const void*)e.sig_len, (const void*)e.msg_off, (const void*)e.msg_len})
+      dfree(ctx, p);
   delete b;
 }
 
+// Where a batch's clear data comes from: a host arena with host offsets/lengths
+// (cg_verify_batch / cg_batch_create), or a device arena the library owns with
+// device-side offsets/lengths (the recomputed tx ids of cg_tx_verify_batch).
+struct MsgSrc {
+  const uint8_t* host = nullptr;
+  uint8_t* dev = nullptr;
+  size_t bytes = 0;
+  const uint64_t* off_host = nullptr;
+  const uint32_t* len_host = nullptr;
+  uint64_t* off_dev = nullptr;
+  uint32_t* len_dev = nullptr;
+};
+
 cg_status check_inputs(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const uint8_t* pk, size_t pk_stride,
-                       const uint8_t* sig, size_t sig_stride, const uint32_t* sig_len, const uint8_t* msg,
-                       size_t msg_bytes, const uint64_t* msg_off, const uint32_t* msg_len) {
+                       const uint8_t* sig, size_t sig_stride, const uint32_t* sig_len, const MsgSrc& m) {
   if (!ctx) return CG_E_INVALID_ARGUMENT;
   if (n > 0xFFFFFFF0ull) return fail(ctx, CG_E_INVALID_ARGUMENT, "batch larger than 2^32 - 16 elements");
   if (n == 0) return CG_OK;
-  if (!pk || !sig || !msg_off || !msg_len) return fail(ctx, CG_E_INVALID_ARGUMENT, "null input pointer");
-  if (msg_bytes > 0 && !msg) return fail(ctx, CG_E_INVALID_ARGUMENT, "null message arena");
+  if (!pk || !sig) return fail(ctx, CG_E_INVALID_ARGUMENT, "null input pointer");
+  if (!m.dev && (!m.off_host || !m.len_host)) return fail(ctx, CG_E_INVALID_ARGUMENT, "null input pointer");
+  if (!m.dev && m.bytes > 0 && !m.host) return fail(ctx, CG_E_INVALID_ARGUMENT, "null message arena");
   bool has_ed = false, has_ec = false;
   for (size_t i = 0; i < n; ++i) {
     const uint8_t s = scheme_id ? scheme_id[i] : CG_SCHEME_EDDSA_ED25519_SHA512;
@@ -221,20 +302,12 @@ cg_status check_inputs(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const ui
       if (l > sig_stride)
         return fail(ctx, CG_E_INVALID_ARGUMENT, "ECDSA signature longer than sig_stride at element " + std::to_string(i));
     }
-    if ((uint64_t)msg_off[i] + msg_len[i] > msg_bytes)
+    if (m.off_host && (uint64_t)m.off_host[i] + m.len_host[i] > m.bytes)
       return fail(ctx, CG_E_INVALID_ARGUMENT, "message out of arena bounds at element " + std::to_string(i));
   }
   if (has_ed && (pk_stride < 32 || sig_stride < 64))
     return fail(ctx, CG_E_INVALID_ARGUMENT, "Ed25519 needs pk_stride >= 32 and sig_stride >= 64");
   if (has_ec && pk_stride < 64) return fail(ctx, CG_E_INVALID_ARGUMENT, "ECDSA needs pk_stride >= 64");
-  return CG_OK;
-}
-
-template <typename T>
-cg_status upload(cg_ctx* ctx, T** dst, const T* src, size_t count, const char* what) {
-  cg_status st = dalloc(ctx, dst, count, what);
-  if (st != CG_OK) return st;
-  if (count) CG_TRY(ctx, hipMemcpyAsync(*dst, src, count * sizeof(T), hipMemcpyHostToDevice, ctx->stream), what);
   return CG_OK;
 }
 
@@ -276,7 +349,8 @@ cg_status cg_open(int device, cg_ctx** out) {
   static std::once_flag bt_once;
   std::call_once(bt_once, [] { cg::ed25519_base_table_words(bt); });
   if (dalloc(ctx, &ctx->btab, cg::kEdBaseTableWords, "alloc base table") != CG_OK ||
-      hipMemcpy(ctx->btab, bt, sizeof bt, hipMemcpyHostToDevice) != hipSuccess) {
+      hipMemcpy(ctx->btab, bt, sizeof bt, hipMemcpyHostToDevice) != hipSuccess ||
+      dalloc(ctx, &ctx->err_flag, 1, "alloc error flag") != CG_OK) {
     cg_close(ctx);
     return CG_E_DEVICE;
   }
@@ -293,11 +367,10 @@ void cg_close(cg_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   collect_timings(ctx);
-  dfree(ctx->btab);
-  dfree(ctx->ed_status);
-  dfree(ctx->ed_digits);
-  dfree(ctx->ed_table);
   cg::ecdsa_consts_free(ctx->ec);
+  for (auto& b : ctx->live_blocks) (void)hipFree(b.first);
+  ctx->live_blocks.clear();
+  release_cached(ctx);
   for (hipEvent_t e : ctx->event_pool) (void)hipEventDestroy(e);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
@@ -305,29 +378,55 @@ void cg_close(cg_ctx* ctx) {
 
 const char* cg_last_error(const cg_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
 
+cg_status cg_register_host(cg_ctx* ctx, void* ptr, size_t bytes) {
+  if (!ctx) return CG_E_INVALID_ARGUMENT;
+  if (!ptr || !bytes) return fail(ctx, CG_E_INVALID_ARGUMENT, "null pointer or empty range");
+  if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, CG_E_DEVICE, "hipSetDevice");
+  CG_TRY(ctx, hipHostRegister(ptr, bytes, hipHostRegisterDefault), "hipHostRegister");
+  return CG_OK;
+}
+
+cg_status cg_unregister_host(cg_ctx* ctx, void* ptr) {
+  if (!ctx) return CG_E_INVALID_ARGUMENT;
+  if (!ptr) return fail(ctx, CG_E_INVALID_ARGUMENT, "null pointer");
+  if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, CG_E_DEVICE, "hipSetDevice");
+  CG_TRY(ctx, hipHostUnregister(ptr), "hipHostUnregister");
+  return CG_OK;
+}
+
+cg_status cg_release_cached(cg_ctx* ctx) {
+  if (!ctx) return CG_E_INVALID_ARGUMENT;
+  (void)hipSetDevice(ctx->device);
+  (void)hipStreamSynchronize(ctx->stream);
+  release_cached(ctx);
+  return CG_OK;
+}
+
 }  // extern "C"
 
 namespace {
 
-// Stages a batch; the message arena comes from host memory (msg) or, for the
-// signed-transaction path, from a device buffer the library owns (msg_dev: the
-// recomputed ids), which the batch then references without owning.
+// Stages a batch (see MsgSrc for where its clear data lives).
 cg_status create_batch(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const uint8_t* pk, size_t pk_stride,
-                       const uint8_t* sig, size_t sig_stride, const uint32_t* sig_len, const uint8_t* msg,
-                       uint8_t* msg_dev, size_t msg_bytes, const uint64_t* msg_off, const uint32_t* msg_len,
+                       const uint8_t* sig, size_t sig_stride, const uint32_t* sig_len, const MsgSrc& m,
                        cg_batch** out) {
   if (!out) return fail(ctx, CG_E_INVALID_ARGUMENT, "null out");
   *out = nullptr;
-  cg_status st = check_inputs(ctx, n, scheme_id, pk, pk_stride, sig, sig_stride, sig_len,
-                              msg_dev ? (const uint8_t*)msg_dev : msg, msg_bytes, msg_off, msg_len);
+  cg_status st = check_inputs(ctx, n, scheme_id, pk, pk_stride, sig, sig_stride, sig_len, m);
   if (st != CG_OK) return st;
   if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, CG_E_DEVICE, "hipSetDevice");
   cg_batch* b = new (std::nothrow) cg_batch();
   if (!b) return fail(ctx, CG_E_OUT_OF_MEMORY, "host alloc");
   b->n = n;
+  // raw element-major inputs (temporary)
+  uint8_t *pk_raw = nullptr, *sig_raw = nullptr;
+  uint32_t* sl_raw = nullptr;
   auto bail = [&](cg_status s) {
     (void)hipStreamSynchronize(ctx->stream);
-    batch_free(b);
+    dfree(ctx, pk_raw);
+    dfree(ctx, sig_raw);
+    dfree(ctx, sl_raw);
+    batch_free(ctx, b);
     return s;
   };
   // host-side partition by scheme
@@ -348,54 +447,40 @@ cg_status create_batch(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const ui
   const size_t nwords = (n + 31) / 32;
   if ((st = dalloc(ctx, &b->verdict, n, "alloc verdict")) != CG_OK) return bail(st);
   if ((st = dalloc(ctx, &b->bitmap, nwords, "alloc bitmap")) != CG_OK) return bail(st);
-  // raw element-major inputs (temporary) + arena (kept)
-  uint8_t *pk_raw = nullptr, *sig_raw = nullptr;
-  uint32_t* sl_raw = nullptr;
-  if (msg_dev) {
-    b->arena = msg_dev;  // caller-owned device arena (padded by the caller)
+  if (m.dev) {
+    b->arena = m.dev;  // library-owned device arena (padded by its producer)
     b->arena_owned = false;
+    b->msg_off_all = m.off_dev;
+    b->msg_len_all = m.len_dev;
+    b->meta_owned = false;
   } else {
-    if ((st = dalloc(ctx, &b->arena, msg_bytes + 16, "alloc arena")) != CG_OK) return bail(st);
-    if (msg_bytes)
-      CG_TRY(ctx, hipMemcpyAsync(b->arena, msg, msg_bytes, hipMemcpyHostToDevice, ctx->stream), "upload arena");
-    CG_TRY(ctx, hipMemsetAsync(b->arena + msg_bytes, 0, 16, ctx->stream), "pad arena");
+    if ((st = dalloc(ctx, &b->arena, m.bytes + 16, "alloc arena")) != CG_OK) return bail(st);
+    if (m.bytes) {
+      const hipError_t e = hipMemcpyAsync(b->arena, m.host, m.bytes, hipMemcpyHostToDevice, ctx->stream);
+      if (e != hipSuccess) return bail(hip_fail(ctx, e, "upload arena"));
+    }
+    const hipError_t e = hipMemsetAsync(b->arena + m.bytes, 0, 16, ctx->stream);
+    if (e != hipSuccess) return bail(hip_fail(ctx, e, "pad arena"));
+    if ((st = upload(ctx, &b->msg_off_all, m.off_host, n, "upload msg_off")) != CG_OK) return bail(st);
+    if ((st = upload(ctx, &b->msg_len_all, m.len_host, n, "upload msg_len")) != CG_OK) return bail(st);
   }
-  if ((st = upload(ctx, &b->msg_off_all, msg_off, n, "upload msg_off")) != CG_OK) return bail(st);
-  if ((st = upload(ctx, &b->msg_len_all, msg_len, n, "upload msg_len")) != CG_OK) return bail(st);
   if ((st = upload(ctx, &pk_raw, pk, n * pk_stride, "upload pk")) != CG_OK) return bail(st);
-  if ((st = upload(ctx, &sig_raw, sig, n * sig_stride, "upload sig")) != CG_OK) {
-    dfree(pk_raw);
-    return bail(st);
-  }
-  if (sig_len && (st = upload(ctx, &sl_raw, sig_len, n, "upload sig_len")) != CG_OK) {
-    dfree(pk_raw);
-    dfree(sig_raw);
-    return bail(st);
-  }
-  auto cleanup_raw = [&]() {
-    (void)hipStreamSynchronize(ctx->stream);
-    dfree(pk_raw);
-    dfree(sig_raw);
-    dfree(sl_raw);
-  };
+  if ((st = upload(ctx, &sig_raw, sig, n * sig_stride, "upload sig")) != CG_OK) return bail(st);
+  if (sig_len && (st = upload(ctx, &sl_raw, sig_len, n, "upload sig_len")) != CG_OK) return bail(st);
   {
     Timed t(ctx, "stage", n);
     // Ed25519 subset -> SoA
     const uint32_t ne = (uint32_t)idx[0].size();
     b->n_ed = ne;
     if (ne) {
-      if (!ed_identity && (st = upload(ctx, &b->ed_index, idx[0].data(), ne, "upload ed index")) != CG_OK) {
-        cleanup_raw();
+      if (!ed_identity && (st = upload(ctx, &b->ed_index, idx[0].data(), ne, "upload ed index")) != CG_OK)
         return bail(st);
-      }
       if ((st = dalloc(ctx, &b->ed_pk, (size_t)8 * ne, "alloc ed pk")) != CG_OK ||
           (st = dalloc(ctx, &b->ed_sig, (size_t)16 * ne, "alloc ed sig")) != CG_OK ||
           (st = dalloc(ctx, &b->ed_sig_len, ne, "alloc ed sig_len")) != CG_OK ||
           (st = dalloc(ctx, &b->ed_msg_off, ne, "alloc ed msg_off")) != CG_OK ||
-          (st = dalloc(ctx, &b->ed_msg_len, ne, "alloc ed msg_len")) != CG_OK) {
-        cleanup_raw();
+          (st = dalloc(ctx, &b->ed_msg_len, ne, "alloc ed msg_len")) != CG_OK)
         return bail(st);
-      }
       hipError_t e = cg::launch_gather_words(pk_raw, pk_stride, 0, 8, b->ed_index, ne, ne, b->ed_pk, ctx->stream);
       if (e == hipSuccess)
         e = cg::launch_gather_words(sig_raw, sig_stride, 0, 16, b->ed_index, ne, ne, b->ed_sig, ctx->stream);
@@ -403,50 +488,44 @@ cg_status create_batch(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const ui
         e = cg::launch_gather_u32(sl_raw, b->ed_index, ne, b->ed_sig_len, (uint32_t)sig_stride, ctx->stream);
       if (e == hipSuccess) e = cg::launch_gather_u64(b->msg_off_all, b->ed_index, ne, b->ed_msg_off, ctx->stream);
       if (e == hipSuccess) e = cg::launch_gather_u32(b->msg_len_all, b->ed_index, ne, b->ed_msg_len, 0, ctx->stream);
-      if (e != hipSuccess) {
-        cleanup_raw();
-        return bail(hip_fail(ctx, e, "stage ed25519"));
-      }
+      if (e != hipSuccess) return bail(hip_fail(ctx, e, "stage ed25519"));
     }
     for (int c = 0; c < 2; ++c) {
       const std::vector<uint32_t>& ix = idx[1 + c];
       if (ix.empty()) continue;
-      hipError_t e = cg::ecdsa_batch_stage(b->ec[c], c == 0 ? CG_SCHEME_ECDSA_SECP256K1_SHA256
-                                                           : CG_SCHEME_ECDSA_SECP256R1_SHA256,
-                                           ix.data(), (uint32_t)ix.size(), pk_raw, pk_stride, sig_raw, sig_stride,
-                                           sl_raw, b->msg_off_all, b->msg_len_all, ctx->stream);
-      if (e != hipSuccess) {
-        cleanup_raw();
-        return bail(hip_fail(ctx, e, "stage ecdsa"));
-      }
+      cg::EcdsaBatch& eb = b->ec[c];
+      const size_t ne_c = ix.size();
+      eb.n = (uint32_t)ne_c;
+      eb.scheme = c == 0 ? CG_SCHEME_ECDSA_SECP256K1_SHA256 : CG_SCHEME_ECDSA_SECP256R1_SHA256;
+      if ((st = upload(ctx, &eb.index, ix.data(), ne_c, "upload ecdsa index")) != CG_OK ||
+          (st = dalloc(ctx, &eb.q, 16 * ne_c, "alloc ecdsa q")) != CG_OK ||
+          (st = dalloc(ctx, &eb.rs, 16 * ne_c, "alloc ecdsa rs")) != CG_OK ||
+          (st = dalloc(ctx, &eb.der, ne_c, "alloc ecdsa der")) != CG_OK ||
+          (st = dalloc(ctx, &eb.sig_len, ne_c, "alloc ecdsa sig_len")) != CG_OK ||
+          (st = dalloc(ctx, &eb.msg_off, ne_c, "alloc ecdsa msg_off")) != CG_OK ||
+          (st = dalloc(ctx, &eb.msg_len, ne_c, "alloc ecdsa msg_len")) != CG_OK)
+        return bail(st);
+      const hipError_t e = cg::ecdsa_batch_stage(eb, pk_raw, pk_stride, sig_raw, sig_stride, sl_raw, b->msg_off_all,
+                                                 b->msg_len_all, ctx->stream);
+      if (e != hipSuccess) return bail(hip_fail(ctx, e, "stage ecdsa"));
     }
   }
-  cleanup_raw();
+  // the host index vectors die here: wait for the copies that read them
   hipError_t e = hipStreamSynchronize(ctx->stream);
+  dfree(ctx, pk_raw);
+  dfree(ctx, sig_raw);
+  dfree(ctx, sl_raw);
+  pk_raw = sig_raw = nullptr;
+  sl_raw = nullptr;
   if (e != hipSuccess) return bail(hip_fail(ctx, e, "stage sync"));
   collect_timings(ctx);
   *out = b;
   return CG_OK;
 }
 
-}  // namespace
-
-extern "C" {
-
-cg_status cg_batch_create(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const uint8_t* pk, size_t pk_stride,
-                          const uint8_t* sig, size_t sig_stride, const uint32_t* sig_len, const uint8_t* msg,
-                          size_t msg_bytes, const uint64_t* msg_off, const uint32_t* msg_len, cg_batch** out) {
-  return create_batch(ctx, n, scheme_id, pk, pk_stride, sig, sig_stride, sig_len, msg, nullptr, msg_bytes, msg_off,
-                      msg_len, out);
-}
-
-cg_status cg_batch_verify(cg_ctx* ctx, cg_batch* b, int mode, uint8_t* verdict_out, uint32_t* accept_bitmap_out,
-                          void* device_bitmap_out) {
-  if (!ctx || !b) return fail(ctx, CG_E_INVALID_ARGUMENT, "null context or batch");
-  if (mode != CG_MODE_IS_VALID && mode != CG_MODE_DO_VERIFY) return fail(ctx, CG_E_INVALID_ARGUMENT, "bad mode");
-  if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, CG_E_DEVICE, "hipSetDevice");
+// Launches the verify kernels of a staged batch and the accept bitmap; no sync.
+cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode) {
   const size_t n = b->n;
-  if (n == 0) return CG_OK;
   cg_status st;
   // elements of unsupported schemes keep this value
   CG_TRY(ctx, hipMemsetAsync(b->verdict, CG_UNSUPPORTED, n, ctx->stream), "init verdict");
@@ -501,6 +580,33 @@ cg_status cg_batch_verify(cg_ctx* ctx, cg_batch* b, int mode, uint8_t* verdict_o
     }
   }
   CG_TRY(ctx, cg::launch_verdict_bitmap(b->verdict, (uint32_t)n, b->bitmap, ctx->stream), "launch bitmap");
+  return CG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+cg_status cg_batch_create(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const uint8_t* pk, size_t pk_stride,
+                          const uint8_t* sig, size_t sig_stride, const uint32_t* sig_len, const uint8_t* msg,
+                          size_t msg_bytes, const uint64_t* msg_off, const uint32_t* msg_len, cg_batch** out) {
+  MsgSrc m;
+  m.host = msg;
+  m.bytes = msg_bytes;
+  m.off_host = msg_off;
+  m.len_host = msg_len;
+  return create_batch(ctx, n, scheme_id, pk, pk_stride, sig, sig_stride, sig_len, m, out);
+}
+
+cg_status cg_batch_verify(cg_ctx* ctx, cg_batch* b, int mode, uint8_t* verdict_out, uint32_t* accept_bitmap_out,
+                          void* device_bitmap_out) {
+  if (!ctx || !b) return fail(ctx, CG_E_INVALID_ARGUMENT, "null context or batch");
+  if (mode != CG_MODE_IS_VALID && mode != CG_MODE_DO_VERIFY) return fail(ctx, CG_E_INVALID_ARGUMENT, "bad mode");
+  if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, CG_E_DEVICE, "hipSetDevice");
+  const size_t n = b->n;
+  if (n == 0) return CG_OK;
+  cg_status st = launch_verify(ctx, b, mode);
+  if (st != CG_OK) return st;
   const size_t nwords = (n + 31) / 32;
   if (device_bitmap_out)
     CG_TRY(ctx, hipMemcpyAsync(device_bitmap_out, b->bitmap, nwords * 4, hipMemcpyDeviceToDevice, ctx->stream),
@@ -518,11 +624,10 @@ cg_status cg_batch_verify(cg_ctx* ctx, cg_batch* b, int mode, uint8_t* verdict_o
 size_t cg_batch_size(const cg_batch* b) { return b ? b->n : 0; }
 
 void cg_batch_destroy(cg_ctx* ctx, cg_batch* b) {
-  if (ctx) {
-    (void)hipSetDevice(ctx->device);
-    (void)hipStreamSynchronize(ctx->stream);
-  }
-  batch_free(b);
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  (void)hipStreamSynchronize(ctx->stream);
+  batch_free(ctx, b);
 }
 
 cg_status cg_verify_batch(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme_id, const uint8_t* pk,
@@ -558,7 +663,7 @@ cg_status cg_der_parse_batch(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, co
   cg_status st = CG_OK;
   auto cleanup = [&]() {
     (void)hipStreamSynchronize(ctx->stream);
-    dfree(sig_d); dfree(sl_d); dfree(rs_d); dfree(st_d); dfree(ix_d);
+    dfree(ctx, sig_d); dfree(ctx, sl_d); dfree(ctx, rs_d); dfree(ctx, st_d); dfree(ctx, ix_d);
   };
   if ((st = upload(ctx, &sig_d, sig, n * sig_stride, "upload sig")) != CG_OK ||
       (sig_len && (st = upload(ctx, &sl_d, sig_len, n, "upload sig_len")) != CG_OK) ||
@@ -609,6 +714,7 @@ cg_status cg_der_parse_batch(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, co
 
 cg_status cg_set_profiling(cg_ctx* ctx, int enable) {
   if (!ctx) return CG_E_INVALID_ARGUMENT;
+  collect_timings(ctx);
   ctx->profiling = enable != 0;
   return CG_OK;
 }
@@ -635,88 +741,81 @@ cg_status cg_reset_stats(cg_ctx* ctx) {
 
 namespace {
 
-// Device buffers of one tx-id computation (K5 + K6).
-struct TxIds {
+// Device buffers of one tx-id computation (K5 + K6) and of the signature
+// metadata derived from it.
+struct TxDev {
   uint8_t* arena = nullptr;
-  uint64_t *slot = nullptr, *leaf_pos = nullptr, *tree_base = nullptr;
-  uint32_t *len = nullptr, *comp_tx = nullptr, *comp_idx = nullptr, *is_salt = nullptr, *salts = nullptr,
-           *comp_start = nullptr, *leaves = nullptr;
+  uint64_t* comp_off = nullptr;
+  uint32_t *comp_len = nullptr, *comp_start = nullptr, *comp_tx = nullptr, *salts = nullptr, *leaves = nullptr;
   uint8_t* ids = nullptr;  // 32 B per tx (+16 pad): digest byte order
-  void release() {
-    for (void* p : {(void*)arena, (void*)slot, (void*)leaf_pos, (void*)tree_base, (void*)len, (void*)comp_tx,
-                    (void*)comp_idx, (void*)is_salt, (void*)salts, (void*)comp_start, (void*)leaves, (void*)ids})
-      dfree(p);
-    *this = TxIds();
+  uint32_t* sig_start = nullptr;
+  uint64_t* sig_moff = nullptr;
+  uint32_t* sig_mlen = nullptr;
+  void release(cg_ctx* ctx) {
+    for (const void* p : {(const void*)arena, (const void*)comp_off, (const void*)comp_len, (const void*)comp_start,
+                          (const void*)comp_tx, (const void*)salts, (const void*)leaves, (const void*)ids,
+                          (const void*)sig_start, (const void*)sig_moff, (const void*)sig_mlen})
+      dfree(ctx, p);
+    *this = TxDev();
   }
 };
 
+// Host-side validation is O(n_tx): monotone comp_start / sig_start.  Component
+// bounds are checked by the leaf kernel (error flag, read back by the caller).
 cg_status compute_txids(cg_ctx* ctx, size_t n_tx, const uint8_t* arena, size_t arena_bytes, const uint64_t* comp_off,
-                        const uint32_t* comp_len, const uint32_t* comp_start, const uint8_t* salts, TxIds& d,
-                        bool* any_empty) {
+                        const uint32_t* comp_len, const uint32_t* comp_start, const uint8_t* salts,
+                        const uint32_t* sig_start, TxDev& d, bool* any_empty) {
   if (n_tx > 0xFFFFFFF0ull) return fail(ctx, CG_E_INVALID_ARGUMENT, "too many transactions");
   if (!comp_start || !salts || (comp_start[n_tx] && (!comp_off || !comp_len || !arena)))
     return fail(ctx, CG_E_INVALID_ARGUMENT, "null pointer");
-  const size_t n_comp = comp_start[n_tx];
-  if (n_comp > 0xFFFFFFF0ull) return fail(ctx, CG_E_INVALID_ARGUMENT, "too many components");
-  // host-side layout: aligned slots with 32 spare bytes for the nonce; trees padded to 2^k
-  std::vector<uint64_t> slot(n_comp), leaf_pos(n_comp), tree_base(n_tx + 1);
-  std::vector<uint32_t> comp_tx(n_comp), comp_idx(n_comp), is_salt(n_comp);
-  uint64_t pos = 0, leaves = 0;
   *any_empty = false;
   for (size_t t = 0; t < n_tx; ++t) {
     if (comp_start[t + 1] < comp_start[t]) return fail(ctx, CG_E_INVALID_ARGUMENT, "comp_start not monotone");
-    const uint32_t k = comp_start[t + 1] - comp_start[t];
-    if (k == 0) *any_empty = true;
-    uint32_t kp = 1;
-    while (kp < k) kp <<= 1;
-    tree_base[t] = leaves;
-    leaves += k ? kp : 1;
-    for (uint32_t i = 0; i < k; ++i) {
-      const size_t c = comp_start[t] + i;
-      if (comp_off[c] + comp_len[c] > arena_bytes)
-        return fail(ctx, CG_E_INVALID_ARGUMENT, "component out of arena bounds");
-      slot[c] = pos;
-      pos += ((uint64_t)comp_len[c] + 32 + 3) & ~3ull;
-      comp_tx[c] = (uint32_t)t;
-      comp_idx[c] = i;
-      is_salt[c] = i == k - 1;
-      leaf_pos[c] = tree_base[t] + i;
-    }
+    if (comp_start[t + 1] == comp_start[t]) *any_empty = true;
+    if (sig_start && sig_start[t + 1] < sig_start[t]) return fail(ctx, CG_E_INVALID_ARGUMENT, "sig_start not monotone");
   }
-  std::vector<uint8_t> slotted(pos + 16, 0);
-  for (size_t c = 0; c < n_comp; ++c) std::memcpy(slotted.data() + slot[c], arena + comp_off[c], comp_len[c]);
+  const uint32_t c_begin = comp_start[0], c_end = comp_start[n_tx];
+  const size_t n_comp = c_end;
+  const size_t n_sig = sig_start ? sig_start[n_tx] : 0;
   cg_status st;
-  if ((st = upload(ctx, &d.arena, slotted.data(), slotted.size(), "upload tx arena")) != CG_OK ||
-      (st = upload(ctx, &d.slot, slot.data(), n_comp, "upload slots")) != CG_OK ||
-      (st = upload(ctx, &d.leaf_pos, leaf_pos.data(), n_comp, "upload leaf_pos")) != CG_OK ||
-      (st = upload(ctx, &d.tree_base, tree_base.data(), n_tx, "upload tree_base")) != CG_OK ||
-      (st = upload(ctx, &d.len, comp_len, n_comp, "upload comp_len")) != CG_OK ||
-      (st = upload(ctx, &d.comp_tx, comp_tx.data(), n_comp, "upload comp_tx")) != CG_OK ||
-      (st = upload(ctx, &d.comp_idx, comp_idx.data(), n_comp, "upload comp_idx")) != CG_OK ||
-      (st = upload(ctx, &d.is_salt, is_salt.data(), n_comp, "upload is_salt")) != CG_OK ||
-      (st = upload(ctx, &d.salts, (const uint32_t*)salts, 8 * n_tx, "upload salts")) != CG_OK ||
+  if ((st = dalloc(ctx, &d.arena, arena_bytes + 16, "alloc tx arena")) != CG_OK ||
+      (st = upload(ctx, &d.comp_off, comp_off, n_comp, "upload comp_off")) != CG_OK ||
+      (st = upload(ctx, &d.comp_len, comp_len, n_comp, "upload comp_len")) != CG_OK ||
       (st = upload(ctx, &d.comp_start, comp_start, n_tx + 1, "upload comp_start")) != CG_OK ||
-      (st = dalloc(ctx, &d.leaves, 8 * leaves, "alloc leaves")) != CG_OK ||
-      (st = dalloc(ctx, &d.ids, 32 * n_tx + 16, "alloc ids")) != CG_OK) {
-    (void)hipStreamSynchronize(ctx->stream);
+      (st = upload(ctx, &d.salts, (const uint32_t*)salts, 8 * n_tx, "upload salts")) != CG_OK ||
+      (st = dalloc(ctx, &d.comp_tx, n_comp, "alloc comp_tx")) != CG_OK ||
+      (st = dalloc(ctx, &d.leaves, 8 * n_comp, "alloc leaves")) != CG_OK ||
+      (st = dalloc(ctx, &d.ids, 32 * n_tx + 16, "alloc ids")) != CG_OK)
     return st;
-  }
-  CG_TRY(ctx, hipMemsetAsync(d.leaves, 0, 32 * leaves, ctx->stream), "zero leaves");
+  if (sig_start && ((st = upload(ctx, &d.sig_start, sig_start, n_tx + 1, "upload sig_start")) != CG_OK ||
+                    (st = dalloc(ctx, &d.sig_moff, n_sig, "alloc sig msg_off")) != CG_OK ||
+                    (st = dalloc(ctx, &d.sig_mlen, n_sig, "alloc sig msg_len")) != CG_OK))
+    return st;
+  if (arena_bytes)
+    CG_TRY(ctx, hipMemcpyAsync(d.arena, arena, arena_bytes, hipMemcpyHostToDevice, ctx->stream), "upload tx arena");
+  CG_TRY(ctx, hipMemsetAsync(d.arena + arena_bytes, 0, 16, ctx->stream), "pad tx arena");
   CG_TRY(ctx, hipMemsetAsync(d.ids, 0, 32 * n_tx + 16, ctx->stream), "zero ids");
+  CG_TRY(ctx, hipMemsetAsync(ctx->err_flag, 0, 4, ctx->stream), "zero error flag");
+  CG_TRY(ctx, cg::launch_tx_index(d.comp_start, d.sig_start, (uint32_t)n_tx, d.comp_tx, d.sig_moff, d.sig_mlen,
+                                  ctx->stream), "launch tx_index");
   {
-    Timed t(ctx, "merkle_leaf", n_comp);
-    CG_TRY(ctx, cg::launch_merkle_nonce(d.arena, d.slot, d.len, d.comp_tx, d.comp_idx, d.is_salt, d.salts,
-                                        (uint32_t)n_comp, ctx->stream), "launch merkle_nonce");
-    CG_TRY(ctx, cg::launch_merkle_leaf(d.arena, d.slot, d.len, d.is_salt, d.leaf_pos, (uint32_t)n_comp, d.leaves,
-                                       ctx->stream), "launch merkle_leaf");
+    Timed t(ctx, "merkle_leaf", c_end - c_begin);
+    CG_TRY(ctx, cg::launch_merkle_leaf(d.arena, arena_bytes, d.comp_off, d.comp_len, d.comp_start, d.comp_tx, d.salts,
+                                       c_begin, c_end, d.leaves, ctx->err_flag, ctx->stream), "launch merkle_leaf");
   }
   {
     Timed t(ctx, "merkle_tree", n_tx);
-    CG_TRY(ctx, cg::launch_merkle_tree(d.leaves, d.tree_base, d.comp_start, (uint32_t)n_tx, (uint32_t*)d.ids,
-                                       ctx->stream), "launch merkle_tree");
+    CG_TRY(ctx, cg::launch_merkle_tree(d.leaves, d.comp_start, (uint32_t)n_tx, (uint32_t*)d.ids, ctx->stream),
+           "launch merkle_tree");
   }
-  // the host staging vectors die here: wait for the uploads that read them
-  CG_TRY(ctx, hipStreamSynchronize(ctx->stream), "txid sync");
+  return CG_OK;
+}
+
+cg_status read_err_flag(cg_ctx* ctx) {
+  uint32_t flag = 0;
+  CG_TRY(ctx, hipMemcpyAsync(&flag, ctx->err_flag, 4, hipMemcpyDeviceToHost, ctx->stream), "read error flag");
+  CG_TRY(ctx, hipStreamSynchronize(ctx->stream), "sync error flag");
+  if (flag) return fail(ctx, CG_E_INVALID_ARGUMENT, "component out of arena bounds");
   return CG_OK;
 }
 
@@ -731,15 +830,17 @@ cg_status cg_txid_batch(cg_ctx* ctx, size_t n_tx, const uint8_t* arena, size_t a
   if (n_tx == 0) return CG_OK;
   if (!ids_out) return fail(ctx, CG_E_INVALID_ARGUMENT, "null ids_out");
   if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, CG_E_DEVICE, "hipSetDevice");
-  TxIds d;
+  TxDev d;
   bool any_empty = false;
-  cg_status st = compute_txids(ctx, n_tx, arena, arena_bytes, comp_off, comp_len, comp_start, salts, d, &any_empty);
+  cg_status st = compute_txids(ctx, n_tx, arena, arena_bytes, comp_off, comp_len, comp_start, salts, nullptr, d,
+                               &any_empty);
   if (st == CG_OK) {
     hipError_t e = hipMemcpyAsync(ids_out, d.ids, 32 * n_tx, hipMemcpyDeviceToHost, ctx->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
     if (e != hipSuccess) st = hip_fail(ctx, e, "download ids");
   }
-  d.release();
+  if (st == CG_OK) st = read_err_flag(ctx);
+  (void)hipStreamSynchronize(ctx->stream);
+  d.release(ctx);
   collect_timings(ctx);
   if (st == CG_OK && any_empty)
     return fail(ctx, CG_E_MERKLE_EMPTY, "Cannot calculate Merkle root on empty hash list.");
@@ -757,54 +858,44 @@ cg_status cg_tx_verify_batch(cg_ctx* ctx, int mode, size_t n_tx, const uint8_t* 
   if (!sig_start || !first_bad_out) return fail(ctx, CG_E_INVALID_ARGUMENT, "null pointer");
   if (mode != CG_MODE_IS_VALID && mode != CG_MODE_DO_VERIFY) return fail(ctx, CG_E_INVALID_ARGUMENT, "bad mode");
   if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, CG_E_DEVICE, "hipSetDevice");
-  TxIds d;
+  TxDev d;
   bool any_empty = false;
-  cg_status st = compute_txids(ctx, n_tx, arena, arena_bytes, comp_off, comp_len, comp_start, salts, d, &any_empty);
-  if (st != CG_OK) {
-    d.release();
-    return st;
-  }
+  cg_status st = compute_txids(ctx, n_tx, arena, arena_bytes, comp_off, comp_len, comp_start, salts, sig_start, d,
+                               &any_empty);
   const size_t n_sig = sig_start[n_tx];
-  std::vector<uint64_t> moff(n_sig);
-  std::vector<uint32_t> mlen(n_sig, 32);
-  for (size_t t = 0; t < n_tx; ++t) {
-    if (sig_start[t + 1] < sig_start[t]) {
-      d.release();
-      return fail(ctx, CG_E_INVALID_ARGUMENT, "sig_start not monotone");
-    }
-    for (uint32_t s = sig_start[t]; s < sig_start[t + 1]; ++s) moff[s] = 32 * (uint64_t)t;
-  }
   cg_batch* b = nullptr;
-  if (n_sig) {
-    st = create_batch(ctx, n_sig, scheme_id, pk, pk_stride, sig, sig_stride, sig_len, nullptr, d.ids, 32 * n_tx,
-                      moff.data(), mlen.data(), &b);
-    if (st == CG_OK) st = cg_batch_verify(ctx, b, mode, verdict_out, nullptr, nullptr);
-  }
-  uint32_t* ss_d = nullptr;
   int32_t* fb_d = nullptr;
-  if (st == CG_OK && (st = upload(ctx, &ss_d, sig_start, n_tx + 1, "upload sig_start")) == CG_OK &&
-      (st = dalloc(ctx, &fb_d, n_tx, "alloc first_bad")) == CG_OK) {
-    uint8_t* verdict_dev = b ? b->verdict : nullptr;
-    hipError_t e = cg::launch_first_bad(verdict_dev, ss_d, (uint32_t)n_tx, fb_d, ctx->stream);
+  if (st == CG_OK && n_sig) {
+    MsgSrc m;
+    m.dev = d.ids;
+    m.bytes = 32 * n_tx;
+    m.off_dev = d.sig_moff;
+    m.len_dev = d.sig_mlen;
+    st = create_batch(ctx, n_sig, scheme_id, pk, pk_stride, sig, sig_stride, sig_len, m, &b);
+    if (st == CG_OK) st = launch_verify(ctx, b, mode);
+  }
+  if (st == CG_OK && (st = dalloc(ctx, &fb_d, n_tx, "alloc first_bad")) == CG_OK) {
+    hipError_t e = cg::launch_first_bad(b ? b->verdict : nullptr, d.sig_start, (uint32_t)n_tx, fb_d, ctx->stream);
     if (e == hipSuccess) e = hipMemcpyAsync(first_bad_out, fb_d, 4 * n_tx, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess && verdict_out && b)
+      e = hipMemcpyAsync(verdict_out, b->verdict, n_sig, hipMemcpyDeviceToHost, ctx->stream);
     if (e == hipSuccess && ids_out) e = hipMemcpyAsync(ids_out, d.ids, 32 * n_tx, hipMemcpyDeviceToHost, ctx->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
     if (e != hipSuccess) st = hip_fail(ctx, e, "first_bad");
   }
+  if (st == CG_OK) st = read_err_flag(ctx);
   (void)hipStreamSynchronize(ctx->stream);
-  dfree(ss_d);
-  dfree(fb_d);
-  if (b) cg_batch_destroy(ctx, b);
+  dfree(ctx, fb_d);
+  if (b) batch_free(ctx, b);
+  d.release(ctx);
+  collect_timings(ctx);
+  if (st != CG_OK) return st;
   // a tx with no component has no id: report it as -3 (MerkleTreeException)
-  if (st == CG_OK && any_empty) {
+  if (any_empty) {
     for (size_t t = 0; t < n_tx; ++t)
       if (comp_start[t + 1] == comp_start[t]) first_bad_out[t] = -3;
-  }
-  d.release();
-  collect_timings(ctx);
-  if (st == CG_OK && any_empty)
     return fail(ctx, CG_E_MERKLE_EMPTY, "Cannot calculate Merkle root on empty hash list.");
-  return st;
+  }
+  return CG_OK;
 }
 
 }  // extern "C"

@@ -215,13 +215,6 @@ void ecdsa_consts_free(EcdsaConsts* c) {
   delete c;
 }
 
-void ecdsa_batch_free(EcdsaBatch& b) {
-  for (void* p : {(void*)b.index, (void*)b.q, (void*)b.rs, (void*)b.der, (void*)b.sig_len, (void*)b.msg_off,
-                  (void*)b.msg_len})
-    if (p) (void)hipFree(p);
-  b = EcdsaBatch();
-}
-
 hipError_t launch_der_parse(int scheme, const uint8_t* sig, size_t stride, const uint32_t* sig_len,
                             uint32_t fill_len, const uint32_t* idx, uint32_t n, uint32_t cap, uint32_t* rs,
                             uint32_t* der, hipStream_t s) {
@@ -235,31 +228,17 @@ hipError_t launch_der_parse(int scheme, const uint8_t* sig, size_t stride, const
   return hipGetLastError();
 }
 
-hipError_t ecdsa_batch_stage(EcdsaBatch& b, int scheme, const uint32_t* host_index, uint32_t n,
-                             const uint8_t* pk_raw_dev, size_t pk_stride, const uint8_t* sig_raw_dev,
-                             size_t sig_stride, const uint32_t* sig_len_dev, const uint64_t* msg_off_all_dev,
-                             const uint32_t* msg_len_all_dev, hipStream_t s) {
-  b = EcdsaBatch();
-  b.n = n;
-  b.scheme = scheme;
-  hipError_t e = hipMalloc((void**)&b.index, (size_t)n * 4);
-  if (e == hipSuccess) e = hipMalloc((void**)&b.q, (size_t)16 * n * 4);
-  if (e == hipSuccess) e = hipMalloc((void**)&b.rs, (size_t)16 * n * 4);
-  if (e == hipSuccess) e = hipMalloc((void**)&b.der, (size_t)n * 4);
-  if (e == hipSuccess) e = hipMalloc((void**)&b.sig_len, (size_t)n * 4);
-  if (e == hipSuccess) e = hipMalloc((void**)&b.msg_off, (size_t)n * 8);
-  if (e == hipSuccess) e = hipMalloc((void**)&b.msg_len, (size_t)n * 4);
-  if (e == hipSuccess) e = hipMemcpyAsync(b.index, host_index, (size_t)n * 4, hipMemcpyHostToDevice, s);
-  if (e == hipSuccess) e = launch_gather_words(pk_raw_dev, pk_stride, 0, 16, b.index, n, n, b.q, s);
+hipError_t ecdsa_batch_stage(const EcdsaBatch& b, const uint8_t* pk_raw_dev, size_t pk_stride,
+                             const uint8_t* sig_raw_dev, size_t sig_stride, const uint32_t* sig_len_dev,
+                             const uint64_t* msg_off_all_dev, const uint32_t* msg_len_all_dev, hipStream_t s) {
+  const uint32_t n = b.n;
+  hipError_t e = launch_gather_words(pk_raw_dev, pk_stride, 0, 16, b.index, n, n, b.q, s);
   if (e == hipSuccess)
-    e = launch_der_parse(scheme, sig_raw_dev, sig_stride, sig_len_dev, (uint32_t)sig_stride, b.index, n, n, b.rs,
+    e = launch_der_parse(b.scheme, sig_raw_dev, sig_stride, sig_len_dev, (uint32_t)sig_stride, b.index, n, n, b.rs,
                          b.der, s);
   if (e == hipSuccess) e = launch_gather_u32(sig_len_dev, b.index, n, b.sig_len, (uint32_t)sig_stride, s);
   if (e == hipSuccess) e = launch_gather_u64(msg_off_all_dev, b.index, n, b.msg_off, s);
   if (e == hipSuccess) e = launch_gather_u32(msg_len_all_dev, b.index, n, b.msg_len, 0, s);
-  // host_index must stay valid until the copy completes: callers synchronize before freeing
-  (void)hipStreamSynchronize(s);
-  if (e != hipSuccess) ecdsa_batch_free(b);
   return e;
 }
 

@@ -5,12 +5,15 @@
 // MerkleTransaction.kt:74-93 (component order), MerkleTree.kt:27-66 (zero-hash
 // padding to a power of two, node = SHA256(left || right)), SecureHash.kt:25,37,42.
 //
-// Device layout built by cg_txid stage (cordagpu.cpp): every component is copied
-// into a device arena at a 4-byte aligned offset `slot[c]` followed by 32 bytes
-// reserved for its nonce, so the leaf preimage ser || nonce is contiguous:
-//   cg_merkle_nonce   one lane per component: nonce -> arena[slot + len]
-//   cg_merkle_leaf    one lane per component: leaf hash -> leaves[tree_base[tx] + i]
-//   cg_merkle_tree    one lane per transaction: zero-pad + pairwise reduce in place
+// Device layout: the caller's component arena is uploaded as is (no re-packing);
+// component c of the whole batch lives at arena[comp_off[c] .. + comp_len[c]).
+//   k_tx_index       one lane per tx: comp_tx[c] = t for its components, and the
+//                    message offset / length (its 32-byte id) of each of its signatures
+//   cg_merkle_leaf   one lane per component: nonce computed in registers, staged in
+//                    a per-lane LDS slot and streamed after ser_i -> leaves[c]
+//   cg_merkle_tree   one lane per tx: zero-hash padding done virtually on the first
+//                    level, pairwise reduction in place over the tx's leaves
+//   cg_first_bad     one lane per tx: first non-ACCEPT signature (a7)
 #include "cg_kernels.h"
 #include "cg_merkle_api.h"
 #include "cg_sha256.h"
@@ -19,62 +22,82 @@ using namespace cg;
 
 namespace {
 
-__global__ __launch_bounds__(256) void cg_merkle_nonce(uint8_t* __restrict__ arena, const uint64_t* __restrict__ slot,
-                                                       const uint32_t* __restrict__ len,
-                                                       const uint32_t* __restrict__ comp_tx,
-                                                       const uint32_t* __restrict__ comp_idx,
-                                                       const uint32_t* __restrict__ comp_is_salt,
-                                                       const uint32_t* __restrict__ salts, uint32_t n) {
-  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= n || comp_is_salt[c]) return;
-  const uint32_t t = comp_tx[c];
-  uint32_t m[9];
-  CG_UNROLL for (int w = 0; w < 8; ++w) m[w] = bswap32_(salts[(size_t)t * 8 + w]);
-  m[8] = comp_idx[c];  // ByteBuffer.putInt: big-endian int
-  uint32_t h[8];
-  sha256_words<36>(h, m);
-  uint32_t* dst = (uint32_t*)(arena + slot[c] + len[c]);  // slot is 4-aligned; len may not be
-  const uint32_t l = len[c];
-  if ((l & 3) == 0) {
-    CG_UNROLL for (int w = 0; w < 8; ++w) dst[w] = bswap32_(h[w]);
-  } else {
-    uint8_t* d8 = arena + slot[c] + l;
-    CG_UNROLL for (int w = 0; w < 8; ++w)
-      CG_UNROLL for (int b = 0; b < 4; ++b) d8[4 * w + b] = (uint8_t)(h[w] >> (24 - 8 * b));
+constexpr int kTailWords = 11;  // per-lane LDS tail slot (odd stride: no bank conflicts)
+
+__global__ __launch_bounds__(256) void k_tx_index(const uint32_t* __restrict__ comp_start,
+                                                  const uint32_t* __restrict__ sig_start, uint32_t n_tx,
+                                                  uint32_t* __restrict__ comp_tx, uint64_t* __restrict__ sig_moff,
+                                                  uint32_t* __restrict__ sig_mlen) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n_tx) return;
+  for (uint32_t c = comp_start[t]; c < comp_start[t + 1]; ++c) comp_tx[c] = t;
+  if (sig_start) {
+    for (uint32_t s = sig_start[t]; s < sig_start[t + 1]; ++s) {
+      sig_moff[s] = 32ull * t;  // clear data of every signature = the tx id (TransactionWithSignatures.kt:60)
+      sig_mlen[s] = 32;
+    }
   }
 }
 
-__global__ __launch_bounds__(256) void cg_merkle_leaf(const uint8_t* __restrict__ arena,
-                                                      const uint64_t* __restrict__ slot,
-                                                      const uint32_t* __restrict__ len,
-                                                      const uint32_t* __restrict__ comp_is_salt,
-                                                      const uint64_t* __restrict__ leaf_pos, uint32_t n,
-                                                      uint32_t* __restrict__ leaves) {
-  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= n) return;
-  const uint32_t l = len[c] + (comp_is_salt[c] ? 0u : 32u);
+__global__ __launch_bounds__(256) void cg_merkle_leaf(const uint8_t* __restrict__ arena, uint64_t arena_bytes,
+                                                      const uint64_t* __restrict__ comp_off,
+                                                      const uint32_t* __restrict__ comp_len,
+                                                      const uint32_t* __restrict__ comp_start,
+                                                      const uint32_t* __restrict__ comp_tx,
+                                                      const uint32_t* __restrict__ salts, uint32_t c_begin,
+                                                      uint32_t c_end, uint32_t* __restrict__ leaves,
+                                                      uint32_t* __restrict__ err) {
+  __shared__ uint32_t tails[256 * kTailWords];
+  const uint32_t c = c_begin + blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= c_end) return;
+  const uint32_t t = comp_tx[c];
+  const uint32_t i = c - comp_start[t];
+  const bool salt = c + 1 == comp_start[t + 1];  // the last component is the serialized privacy salt
+  const uint64_t off = comp_off[c];
+  const uint32_t len = comp_len[c];
+  if (off > arena_bytes || len > arena_bytes - off) {
+    atomicOr(err, 1u);
+    return;
+  }
+  uint32_t* tb = tails + threadIdx.x * kTailWords;
+  CG_UNROLL for (int d = 0; d < kTailWords; ++d) tb[d] = 0;
+  if (salt) {
+    tb[1] = 0x80u;  // no tail: padding right after ser_salt
+  } else {
+    uint32_t m[9], h[8];
+    CG_UNROLL for (int w = 0; w < 8; ++w) m[w] = bswap32_(salts[(size_t)t * 8 + w]);
+    m[8] = i;  // ByteBuffer.putInt: big-endian
+    sha256_words<36>(h, m);
+    CG_UNROLL for (int w = 0; w < 8; ++w) tb[1 + w] = bswap32_(h[w]);  // digest bytes in memory order
+    tb[9] = 0x80u;
+  }
   uint32_t h[8];
-  sha256_mem(h, arena + slot[c], l);
-  uint32_t* dst = leaves + leaf_pos[c] * 8;
+  sha256_mem_tail(h, arena + off, len, [&](uint32_t d) { return tb[d]; }, salt ? 0u : 32u);
+  uint32_t* dst = leaves + (size_t)c * 8;
   CG_UNROLL for (int w = 0; w < 8; ++w) dst[w] = h[w];
 }
 
-// leaves: per tx, kp = next power of two >= k slots of 8 big-endian-valued words,
-// starting at tree_base[t]; slots k..kp-1 are zero (zeroHash).  Root -> ids.
+// leaves[c] (8 big-endian-valued words) for every component; the tree of tx t is
+// built in place over leaves[comp_start[t] ..): level-1 positions >= k read the
+// zero hash (padWithZeros), and every later level only reads nodes it wrote.
 __global__ __launch_bounds__(256) void cg_merkle_tree(uint32_t* __restrict__ leaves,
-                                                      const uint64_t* __restrict__ tree_base,
                                                       const uint32_t* __restrict__ comp_start, uint32_t n_tx,
                                                       uint32_t* __restrict__ ids) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n_tx) return;
-  const uint32_t k = comp_start[t + 1] - comp_start[t];
-  uint32_t* nodes = leaves + tree_base[t] * 8;
+  const uint32_t c0 = comp_start[t];
+  const uint32_t k = comp_start[t + 1] - c0;
+  uint32_t* nodes = leaves + (size_t)c0 * 8;
   uint32_t kp = 1;
   while (kp < k) kp <<= 1;
   for (uint32_t w = kp; w > 1; w >>= 1) {
+    const uint32_t valid = w == kp ? k : w;
     for (uint32_t j = 0; j < w / 2; ++j) {
       uint32_t m[16], h[8];
-      CG_UNROLL for (int q = 0; q < 16; ++q) m[q] = nodes[(size_t)16 * j + q];
+      CG_UNROLL for (int q = 0; q < 8; ++q) {
+        m[q] = 2 * j < valid ? nodes[(size_t)16 * j + q] : 0u;
+        m[8 + q] = 2 * j + 1 < valid ? nodes[(size_t)16 * j + 8 + q] : 0u;
+      }
       sha256_words<64>(h, m);
       CG_UNROLL for (int q = 0; q < 8; ++q) nodes[(size_t)8 * j + q] = h[q];
     }
@@ -105,28 +128,28 @@ inline dim3 grid_for(uint32_t n) { return dim3((n + 255) / 256); }
 
 namespace cg {
 
-hipError_t launch_merkle_nonce(uint8_t* arena, const uint64_t* slot, const uint32_t* len, const uint32_t* comp_tx,
-                               const uint32_t* comp_idx, const uint32_t* comp_is_salt, const uint32_t* salts,
-                               uint32_t n, hipStream_t s) {
-  if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(cg_merkle_nonce, grid_for(n), dim3(256), 0, s, arena, slot, len, comp_tx, comp_idx,
-                     comp_is_salt, salts, n);
-  return hipGetLastError();
-}
-
-hipError_t launch_merkle_leaf(const uint8_t* arena, const uint64_t* slot, const uint32_t* len,
-                              const uint32_t* comp_is_salt, const uint64_t* leaf_pos, uint32_t n, uint32_t* leaves,
-                              hipStream_t s) {
-  if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(cg_merkle_leaf, grid_for(n), dim3(256), 0, s, arena, slot, len, comp_is_salt, leaf_pos, n,
-                     leaves);
-  return hipGetLastError();
-}
-
-hipError_t launch_merkle_tree(uint32_t* leaves, const uint64_t* tree_base, const uint32_t* comp_start, uint32_t n_tx,
-                              uint32_t* ids, hipStream_t s) {
+hipError_t launch_tx_index(const uint32_t* comp_start, const uint32_t* sig_start, uint32_t n_tx, uint32_t* comp_tx,
+                           uint64_t* sig_moff, uint32_t* sig_mlen, hipStream_t s) {
   if (n_tx == 0) return hipSuccess;
-  hipLaunchKernelGGL(cg_merkle_tree, grid_for(n_tx), dim3(256), 0, s, leaves, tree_base, comp_start, n_tx, ids);
+  hipLaunchKernelGGL(k_tx_index, grid_for(n_tx), dim3(256), 0, s, comp_start, sig_start, n_tx, comp_tx, sig_moff,
+                     sig_mlen);
+  return hipGetLastError();
+}
+
+hipError_t launch_merkle_leaf(const uint8_t* arena, uint64_t arena_bytes, const uint64_t* comp_off,
+                              const uint32_t* comp_len, const uint32_t* comp_start, const uint32_t* comp_tx,
+                              const uint32_t* salts, uint32_t c_begin, uint32_t c_end, uint32_t* leaves,
+                              uint32_t* err, hipStream_t s) {
+  if (c_end <= c_begin) return hipSuccess;
+  hipLaunchKernelGGL(cg_merkle_leaf, grid_for(c_end - c_begin), dim3(256), 0, s, arena, arena_bytes, comp_off,
+                     comp_len, comp_start, comp_tx, salts, c_begin, c_end, leaves, err);
+  return hipGetLastError();
+}
+
+hipError_t launch_merkle_tree(uint32_t* leaves, const uint32_t* comp_start, uint32_t n_tx, uint32_t* ids,
+                              hipStream_t s) {
+  if (n_tx == 0) return hipSuccess;
+  hipLaunchKernelGGL(cg_merkle_tree, grid_for(n_tx), dim3(256), 0, s, leaves, comp_start, n_tx, ids);
   return hipGetLastError();
 }
 

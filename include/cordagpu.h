@@ -175,9 +175,23 @@ cg_status cg_tx_verify_batch(cg_ctx* ctx, int mode, size_t n_tx, const uint8_t* 
                              uint8_t* ids_out);
 
 /*
+ * Host-memory registration (optional).  Page-locks [ptr, ptr + bytes) for the
+ * device so later uploads from that range run at full PCIe DMA rate instead of
+ * through the runtime's pageable staging copy.  Meant for buffers a caller reuses
+ * across calls (e.g. JVM direct ByteBuffers allocated once per verifier thread);
+ * the library still never retains the pointer itself.  Unregister before freeing.
+ */
+cg_status cg_register_host(cg_ctx* ctx, void* ptr, size_t bytes);
+cg_status cg_unregister_host(cg_ctx* ctx, void* ptr);
+/* Device buffers freed by the library are cached per context for reuse; this
+ * returns the cached (unused) ones to the device allocator. */
+cg_status cg_release_cached(cg_ctx* ctx);
+
+/*
  * Per-kernel device timing (HIP events on the context's stream), accumulated while
- * profiling is enabled.  Names: "ed25519_prep", "ed25519_msm", "ecdsa_verify",
- * "der_parse", "merkle_leaf", "merkle_tree", "stage".
+ * profiling is enabled.  Names: "ed25519_prep", "ed25519_msm", "ecdsa_k1_prep",
+ * "ecdsa_k1_msm", "ecdsa_r1_prep", "ecdsa_r1_msm", "der_parse", "merkle_leaf",
+ * "merkle_tree", "stage".
  */
 cg_status cg_set_profiling(cg_ctx* ctx, int enable);
 cg_status cg_kernel_stats(cg_ctx* ctx, const char* kernel, double* total_ms, uint64_t* launches,

@@ -160,3 +160,17 @@ extern "C" int cgh_ecdsa_joint(int scheme, const uint32_t* u1, const uint32_t* u
                                const uint32_t* qy, uint32_t* out) {
   return scheme == 2 ? joint_host<CurveK1>(u1, u2, qx, qy, out) : joint_host<CurveR1>(u1, u2, qx, qy, out);
 }
+
+// The Merkle leaf preimage streamer: SHA-256(msg[0..n) || tail[0..tail_n)) with the
+// tail staged exactly as cg_merkle_leaf stages it (zero dword, tail, 0x80).
+extern "C" void cgh_sha256_tail(const uint8_t* msg, uint32_t n, const uint8_t* tail, uint32_t tail_n,
+                                uint8_t* out) {
+  uint32_t tb[11] = {0};
+  uint8_t* tb8 = (uint8_t*)tb;
+  memcpy(tb8 + 4, tail, tail_n);
+  tb8[4 + tail_n] = 0x80;
+  uint32_t h[8];
+  sha256_mem_tail(h, msg, n, [&](uint32_t d) { return tb[d]; }, tail_n);
+  for (int i = 0; i < 8; ++i)
+    for (int b = 0; b < 4; ++b) out[4 * i + b] = (uint8_t)(h[i] >> (24 - 8 * b));
+}

@@ -100,3 +100,39 @@ def test_python_mirror_raises_like_check_signatures_are_valid(gpu_ctx):
     stxs[5].sigs = []
     with pytest.raises(T.IllegalArgumentException):
         T.check_signatures_are_valid(gpu_ctx, stxs)
+
+
+def test_component_out_of_arena_is_invalid_argument(gpu_ctx):
+    """Component bounds are validated on the device (leaf kernel error flag)."""
+    from corda_amd._lib import CG_E_INVALID_ARGUMENT
+    arena = np.frombuffer(bytes(range(200)), dtype=np.uint8).copy()
+    comp_off = np.array([0, 150], dtype=np.uint64)
+    comp_len = np.array([100, 60], dtype=np.uint32)  # second component runs past the arena
+    comp_start = np.array([0, 2], dtype=np.uint32)
+    salts = np.zeros(32, dtype=np.uint8)
+    ids = np.zeros(32, dtype=np.uint8)
+    st = gpu_ctx.lib.cg_txid_batch(gpu_ctx.h, 1, ptr(arena), len(arena), ptr(comp_off), ptr(comp_len),
+                                   ptr(comp_start), ptr(salts), ptr(ids))
+    assert st == CG_E_INVALID_ARGUMENT
+    comp_len[1] = 50  # exactly to the end: valid
+    assert gpu_ctx.lib.cg_txid_batch(gpu_ctx.h, 1, ptr(arena), len(arena), ptr(comp_off), ptr(comp_len),
+                                     ptr(comp_start), ptr(salts), ptr(ids)) == 0
+
+
+def test_comp_start_offset_and_registered_buffers(gpu_ctx, oracle):
+    """comp_start need not begin at 0 (components before it are ignored), and
+    page-locked (cg_register_host) caller buffers give the same ids."""
+    w = datagen.make_tx_batch(200, seed=11, tamper_frac=0.0)
+    cs = w.comp_start.copy()
+    # prepend 3 junk components that no tx references
+    comp_off = np.concatenate([np.zeros(3, np.uint64), w.comp_off])
+    comp_len = np.concatenate([np.full(3, 7, np.uint32), w.comp_len])
+    cs = (cs + 3).astype(np.uint32)
+    ids = np.zeros(32 * w.n_tx, dtype=np.uint8)
+    gpu_ctx.register_host(w.arena, comp_off, comp_len, cs, w.salts, ids)
+    try:
+        gpu_ctx.check(gpu_ctx.lib.cg_txid_batch(gpu_ctx.h, w.n_tx, ptr(w.arena), len(w.arena), ptr(comp_off),
+                                                ptr(comp_len), ptr(cs), ptr(w.salts), ptr(ids)))
+    finally:
+        gpu_ctx.unregister_host(w.arena, comp_off, comp_len, cs, w.salts, ids)
+    assert np.array_equal(ids, oracle_ids(oracle, w))

@@ -93,6 +93,22 @@ def test_sha512_alignment(host):
         assert bytes(o16) == hashlib.sha512(r + ab + buf[off:off + n]).digest()
 
 
+def test_sha256_leaf_tail_alignment(host):
+    """Merkle leaf = SHA-256(ser_i || nonce_i) streamed from the arena plus a staged
+    32-byte tail (MerkleTransaction.kt:16-30), and the salt leaf (no tail), at
+    every alignment and around every block boundary."""
+    rnd = random.Random(5)
+    buf = rnd.randbytes(1500)
+    mb = (ctypes.c_uint8 * (len(buf) + 16)).from_buffer_copy(buf + bytes(16))
+    out = (ctypes.c_uint8 * 32)()
+    cases = [(n, off) for n in range(0, 140) for off in range(4)] + \
+            [(rnd.randint(0, 1400), rnd.randint(0, 60)) for _ in range(300)]
+    for n, off in cases:
+        tail = rnd.randbytes(32) if (n + off) % 3 else b""
+        host.cgh_sha256_tail(ctypes.byref(mb, off), n, tail, len(tail), out)
+        assert bytes(out) == hashlib.sha256(buf[off:off + n] + tail).digest(), (n, off, len(tail))
+
+
 def test_verify_golden(host, golden_ed25519):
     for e in golden_ed25519:
         pk, sig, msg = (bytes.fromhex(e[k]) for k in ("pk", "sig", "msg"))
