@@ -1,24 +1,29 @@
 // Per-signature Ed25519 verification pipeline with i2p eddsa 0.2.0 semantics
-// (SURVEY Appendix A), split in the two phases the HIP kernels run:
+// (SURVEY Appendix A), split in the three phases the HIP kernels run:
 //
-//   phase 1 (prep):  decode A (A.2), canonical Abyte (A.4), h = SHA-512(R||Abyte||M)
-//                    mod L (A.5), S_eff = slide-effective S mod L (A.6/A.7),
-//                    signed radix-32 digits of h, signed radix-256 digits of
-//                    S_eff, table k*(-A), k = 0..16.
-//   phase 2 (msm):   R' = [S_eff]B + [h](-A) by fixed windows (5 bits for A, 8 bits
-//                    for B) shared by all lanes of a wave (no divergence),
-//                    canonical encoding, byte compare with R (A.8/A.9).
+//   hash    (no curve arithmetic) length / empty-argument checks (A.1, Crypto.kt:
+//           474-476), canonical Abyte straight from the key bytes (A.4),
+//           h = SHA-512(R || Abyte || M) mod L (A.5), S_eff = slide-effective S
+//           mod L (A.6/A.7), the half-size scalars (c0, c1) of cg_halfscalar.h and
+//           b = c1 S_eff mod L, recoded to signed digits.
+//   points  decode A (A.2: no root -> KEY_INVALID, which takes precedence over the
+//           hash phase's verdicts), decode R strictly (a non-canonical or off-curve
+//           R can never equal a canonical encoding: REJECT, A.9), tables k*(-A)
+//           and k*R, k = 0..8.
+//   msm     P = [b]B + [c0](-A) + [c1](-R) with ~130 shared doublings, fixed 4-bit
+//           windows for A and R (one lane per signature, every lane of the wave
+//           on the same bit position) and 8-bit windows over two shared tables
+//           B and 2^128 B; accept iff P is the identity.
 //
 // Reference call path: Crypto.isValid -> EdDSAEngine.engineVerify
 // (/root/reference/core/src/main/kotlin/net/corda/core/crypto/Crypto.kt:534-541).
-// The kernels are not a transliteration of i2p's slide()/sliding-window loop:
-// that loop adds at data-dependent positions, which on a 64-wide wave makes
-// every position pay for an addition.  Instead the same group element is
-// computed with a regular window; equality of the results follows from exact
-// group arithmetic and from using i2p's own effective scalars.
+// i2p computes R' = [S]B + [h](-A) with a sliding window and compares enc(R') with
+// R; the identity test above is the same predicate (cg_halfscalar.h), computed
+// with exact, complete group arithmetic, so torsion components, S >= L and the
+// slide carry loss give i2p's verdicts bit for bit.
 #pragma once
 #include "cg_ge25519.h"
-#include "cg_sc25519.h"
+#include "cg_halfscalar.h"
 #include "cg_sha512.h"
 
 namespace cg {
@@ -26,26 +31,113 @@ namespace cg {
 enum : uint32_t { V_ACCEPT = 0, V_REJECT = 1, V_SIG_MALFORMED = 2, V_KEY_INVALID = 3, V_ARG_EMPTY = 4, V_COMPUTE = 0xff };
 enum : uint32_t { MODE_IS_VALID = 0, MODE_DO_VERIFY = 1 };
 
-constexpr int kATabEntries = 17;   // A side, w = 5 signed digits: k*(-A), |d| <= 16
-constexpr int kBTabEntries = 129;  // B side, w = 8 signed digits: k*B, |d| <= 128
+constexpr int kATabEntries = 9;    // per-lane tables, 4-bit signed digits: k*P, |d| <= 8
+constexpr int kBTabEntries = 129;  // shared tables, 8-bit signed digits: k*B, k*2^128 B, |d| <= 128
+constexpr int kDigitWords = 24;    // A nibbles (8) | R nibbles (8) | B bytes (8)
+constexpr int kMinDigits = 32;     // the loop always covers bit positions 0..127 (B tables)
 
-// Verdict precedence before any curve arithmetic (mirrors the JVM order: the
-// PublicKey object exists before doVerify runs, then Crypto.kt:474-476, then the
-// engine's length check).
-CG_HD uint32_t ed25519_precheck(uint32_t key_ok, uint32_t sig_len, uint32_t msg_len, uint32_t mode) {
-  if (!key_ok) return V_KEY_INVALID;
+// Status word of the hash/points phases: verdict (bits 0-7; V_COMPUTE while the
+// MSM must decide), radix-16 digit count (bits 8-15), R sign flag (bit 16).
+CG_HD uint32_t ed_status_verdict(uint32_t st) { return st & 0xff; }
+CG_HD uint32_t ed_status_ndig(uint32_t st) { return (st >> 8) & 0xff; }
+CG_HD uint32_t ed_status_rneg(uint32_t st) { return (st >> 16) & 1; }
+
+// Verdicts that do not need the key (JVM order: the key object exists first, then
+// Crypto.kt:474-476, then the engine's length check); the points phase lets
+// KEY_INVALID override these.
+CG_HD uint32_t ed25519_precheck_sig(uint32_t sig_len, uint32_t msg_len, uint32_t mode) {
   if (mode == MODE_DO_VERIFY && (sig_len == 0 || msg_len == 0)) return V_ARG_EMPTY;
   if (sig_len != 64) return V_SIG_MALFORMED;
   return V_COMPUTE;
 }
 
-// Abyte of a decoded point with Z = 1: canonical y, sign of x in bit 255.
-CG_HD void ed25519_abyte(uint32_t ab[8], const ge_p3& A) {
-  fe_tobytes(ab, A.Y);
-  ab[7] |= fe_isnegative(A.X) << 31;
+// Abyte = enc(decode(A)) without decoding (A.4): i2p re-encodes y mod p, and the
+// sign of the decoded x, which equals the key's bit 255 unless x = 0 (y = +-1).
+CG_HD void ed25519_abyte(uint32_t ab[8], const uint32_t pk[8]) {
+  fe y;
+  fe_frombytes(y, pk);
+  fe_tobytes(ab, y);
+  uint32_t rest = ab[1] | ab[2] | ab[3] | ab[4] | ab[5] | ab[6];
+  const uint32_t one = (ab[0] == 1u) & (rest == 0) & (ab[7] == 0);
+  rest = ~(ab[1] & ab[2] & ab[3] & ab[4] & ab[5] & ab[6]);
+  const uint32_t minus_one = (ab[0] == 0xffffffecu) & (rest == 0) & (ab[7] == 0x7fffffffu);
+  if (!(one | minus_one)) ab[7] |= pk[7] & 0x80000000u;
 }
 
-// Table entry k*P (k = 0..16) in cached form, P given as p3; writes via `put`.
+// Hash phase for one signature.  Returns the pre-verdict and fills dig / the
+// digit count and R sign (packed into the status word by the caller).
+// FULL_LENGTH (tests only) forces the (h, 1) fallback of the half-size reduction.
+template <bool FULL_LENGTH = false>
+CG_HD uint32_t ed25519_hash_stage(const uint32_t pk[8], const uint32_t sig[16], uint32_t sig_len, const uint8_t* msg,
+                                  uint32_t msg_len, uint32_t mode, uint32_t dig[kDigitWords], uint32_t& ndig,
+                                  uint32_t& rneg) {
+  ndig = kMinDigits;
+  rneg = 0;
+  const uint32_t pre = ed25519_precheck_sig(sig_len, msg_len, mode);
+  if (pre != V_COMPUTE) return pre;
+  uint32_t ab[8], hd[16], h[8], s[8], c0[8], c1[8], b[8];
+  ed25519_abyte(ab, pk);
+  sha512_ed25519(hd, sig, ab, msg, msg_len);
+  sc_reduce512(h, hd);
+  sc_effective_s(s, sig + 8);
+  uint32_t c1neg = 0;
+  if (FULL_LENGTH) {
+    CG_UNROLL for (int w = 0; w < 8; ++w) {
+      c0[w] = h[w];
+      c1[w] = w == 0;
+    }
+  } else {
+    ed25519_half_scalars(h, c0, c1, c1neg);
+  }
+  // [c1 S mod L] B + [c0](-A) + [c1](-R) = 0, with c1 = (-1)^c1neg |c1|
+  sc_mul_mod(b, c1, s);
+  if (c1neg) {
+    const uint32_t zero[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    sc_sub_mod(b, zero, b);
+  }
+  rneg = c1neg ^ 1u;  // the R term is [|c1|](-R) when c1 > 0, [|c1|]R when c1 < 0
+  sc_recode16(dig, c0);
+  sc_recode16(dig + 8, c1);
+  sc_recode8(dig + 16, b);
+  uint32_t x0[9], x1[9];
+  CG_UNROLL for (int w = 0; w < 9; ++w) {
+    x0[w] = w < 8 ? c0[w] : 0u;
+    x1[w] = w < 8 ? c1[w] : 0u;
+  }
+  const uint32_t bl = mp9_bitlen(x0) > mp9_bitlen(x1) ? mp9_bitlen(x0) : mp9_bitlen(x1);
+  // digits in [-8, 7]: the carry out of the top nonzero nibble needs one more digit
+  const uint32_t nd = (bl + 7) / 4;
+  ndig = nd > (uint32_t)kMinDigits ? nd : (uint32_t)kMinDigits;
+  return V_COMPUTE;
+}
+
+// Strict decode of R: canonical y (< p), a square root exists, and not (x = 0
+// with the sign bit set) — exactly the byte strings enc() can produce.
+CG_HD uint32_t ge_frombytes_strict(ge_p3& h, const uint32_t w[8]) {
+  if (!ge_frombytes_i2p(h, w)) return 0;
+  uint32_t yc[8];
+  fe_tobytes(yc, h.Y);
+  uint32_t diff = yc[7] ^ (w[7] & 0x7fffffffu);
+  CG_UNROLL for (int i = 0; i < 7; ++i) diff |= yc[i] ^ w[i];
+  if (diff) return 0;
+  if ((w[7] >> 31) && fe_iszero(h.X)) return 0;
+  return 1;
+}
+
+// Points phase: final pre-verdict and the decoded -A and R.
+CG_HD uint32_t ed25519_points_stage(const uint32_t pk[8], const uint32_t r[8], uint32_t pre, ge_p3& negA,
+                                    ge_p3& R) {
+  ge_p3 A;
+  if (!ge_frombytes_i2p(A, pk)) return V_KEY_INVALID;
+  if (pre != V_COMPUTE) return pre;
+  if (!ge_frombytes_strict(R, r)) return V_REJECT;
+  negA = A;
+  fe_neg(negA.X, A.X);
+  fe_neg(negA.T, A.T);
+  return V_COMPUTE;
+}
+
+// Table entry k*P (k = 0..8) in cached form, P given as p3; writes via `put`.
 template <typename Put>
 CG_HD void ed25519_build_table(const ge_p3& P, Put&& put) {
   ge_cached c;
@@ -67,20 +159,26 @@ CG_HD void ed25519_build_table(const ge_p3& P, Put&& put) {
   }
 }
 
-// Shared table k*B (k = 0..NB-1) in affine precomputed form; computed once on the
-// host at context creation and uploaded (the MSM kernel stages it in LDS).
-CG_HD void ed25519_base_table(ge_precomp tab[kBTabEntries]) {
+// Shared table k*P (k = 0..128) in affine precomputed form, for P = B (shift 0)
+// or P = 2^128 B (shift 128); computed once on the host per context and
+// uploaded (the MSM kernel stages both in LDS).
+CG_HD void ed25519_base_table(ge_precomp tab[kBTabEntries], int shift) {
   const uint32_t benc[8] = {0x66666658u, 0x66666666u, 0x66666666u, 0x66666666u,
                             0x66666666u, 0x66666666u, 0x66666666u, 0x66666666u};
   const fe d2 = CG_FE_D2;
-  ge_p3 B, cur;
-  ge_frombytes_i2p(B, benc);
-  ge_cached bc;
-  ge_p3_to_cached(bc, B);
+  ge_p3 P, cur;
+  ge_frombytes_i2p(P, benc);
+  for (int i = 0; i < shift; ++i) {
+    ge_p1p1 t;
+    ge_p3_dbl(t, P);
+    ge_p1p1_to_p3(P, t);
+  }
+  ge_cached pc;
+  ge_p3_to_cached(pc, P);
   fe_1(tab[0].yplusx);
   fe_1(tab[0].yminusx);
   fe_0(tab[0].xy2d);
-  cur = B;
+  cur = P;
   for (int k = 1; k < kBTabEntries; ++k) {
     fe recip, x, y;
     fe_invert(recip, cur.Z);
@@ -93,73 +191,95 @@ CG_HD void ed25519_base_table(ge_precomp tab[kBTabEntries]) {
     fe_reduce(tab[k].yplusx);
     fe_reduce(tab[k].yminusx);
     ge_p1p1 t;
-    ge_add_cached(t, cur, bc, 0);
+    ge_add_cached(t, cur, pc, 0);
     ge_p1p1_to_p3(cur, t);
   }
 }
 
-// Phase 1 for one signature, everything but the table write.  Returns the
-// pre-verdict (V_COMPUTE when the curve arithmetic must decide).
-CG_HD uint32_t ed25519_prep(const uint32_t pk[8], const uint32_t sig[16], uint32_t sig_len, const uint8_t* msg,
-                            uint32_t msg_len, uint32_t mode, ge_p3& negA, uint32_t hd[13], uint32_t sd[8]) {
-  ge_p3 A;
-  const uint32_t key_ok = ge_frombytes_i2p(A, pk);
-  const uint32_t pre = ed25519_precheck(key_ok, sig_len, msg_len, mode);
-  if (pre != V_COMPUTE) return pre;
-  uint32_t ab[8], dig[16], h[8], s[8];
-  ed25519_abyte(ab, A);
-  sha512_ed25519(dig, sig, ab, msg, msg_len);
-  sc_reduce512(h, dig);
-  sc_effective_s(s, sig + 8);
-  sc_recode5(hd, h);
-  sc_recode8(sd, s);
-  negA = A;
-  fe_neg(negA.X, A.X);
-  fe_neg(negA.T, A.T);
-  return V_COMPUTE;
+// x <<= 4 * n (nibbles) for a 256-bit value; n uniform across the wave.
+CG_HD void shl_nibbles(uint32_t x[8], uint32_t n) {
+  const uint32_t ws = n >> 3, bs = 4 * (n & 7);
+  CG_UNROLL for (int k = 4; k >= 1; k >>= 1) {
+    if (ws & k) {
+      CG_UNROLL for (int w = 7; w >= 0; --w) x[w] = w >= k ? x[w - k] : 0u;
+    }
+  }
+  if (bs) {
+    CG_UNROLL for (int w = 7; w >= 1; --w) x[w] = (x[w] << bs) | (x[w - 1] >> (32 - bs));
+    x[0] <<= bs;
+  }
 }
 
-// Phase 2: R' = [S_eff]B + [h](-A) by a bit-position loop shared by every lane
-// of the wave: double at every position, add the A-table entry of the next
-// 5-bit digit at positions = 0 mod 5 and the B-table entry of the next 8-bit digit
-// at positions = 0 mod 8 (both uniform, scalar branches).  hd (13 words) / sd (8)
-// are the MSB-first digit bytes from sc_recode5 / sc_recode8 (consumed).
-// getA(idx, cached&) loads k*(-A) (k = 0..16); getB(idx, precomp&) loads k*B
-// (k = 0..128).  Returns the canonical encoding of R'.
-template <typename GetA, typename GetB>
-CG_HD void ed25519_msm(uint32_t out[8], uint32_t hd[13], uint32_t sd[8], GetA&& getA, GetB&& getB) {
+// MSM phase: P = [b]B + [c0](-A) + [c1](+-R) over ndig radix-16 positions (ndig
+// uniform across the wave, >= 32).  getA(k, cached&) loads k*(-A), getR(k,
+// cached&) loads k*R, getB(t, k, precomp&) loads k*B (t = 0) or k*2^128 B (t = 1).
+// Returns 1 iff P is the identity.
+template <typename GetA, typename GetR, typename GetB>
+CG_HD uint32_t ed25519_msm(uint32_t ndig, const uint32_t dig[kDigitWords], uint32_t rneg, GetA&& getA, GetR&& getR,
+                           GetB&& getB) {
+  uint32_t da[8], dr[8], bh[4], bl[4];
+  CG_UNROLL for (int w = 0; w < 8; ++w) {
+    da[w] = dig[w];
+    dr[w] = dig[8 + w];
+  }
+  CG_UNROLL for (int w = 0; w < 4; ++w) {
+    bh[w] = dig[16 + w];  // B digits 31..16 (the 2^128 B table), most significant first
+    bl[w] = dig[20 + w];  // B digits 15..0 (the B table)
+  }
+  shl_nibbles(da, 64 - ndig);  // top digit to the top nibble
+  shl_nibbles(dr, 64 - ndig);
   ge_p2 r2;
   ge_p3 r3;
-  ge_p1p1 t;  // starts as the identity: x = X/Z = 0, y = Y/T = 1
+  ge_p1p1 t;  // identity: x = X/Z = 0, y = Y/T = 1
   ge_cached ca;
   ge_precomp pb;
   fe_0(t.X);
   fe_1(t.Y);
   fe_1(t.Z);
   fe_1(t.T);
-  CG_NOUNROLL for (int pos = 250; pos >= 0; --pos) {
-    if (pos != 250) ge_p2_dbl(t, r2);
-    if (pos % 5 == 0) {
-      const uint32_t e = hd[0] & 0xff;
-      CG_UNROLL for (int w = 0; w < 12; ++w) hd[w] = hd[w] >> 8 | hd[w + 1] << 24;
-      hd[12] >>= 8;
-      const uint32_t neg = e < 16, a = neg ? 16 - e : e - 16;
-      getA(a, ca);
-      ge_p1p1_to_p3(r3, t);
-      ge_add_cached(t, r3, ca, neg);
+  const int top = 4 * ((int)ndig - 1);  // the first digit is added to the identity, no doubling
+  CG_NOUNROLL for (int pos = top; pos >= 0; --pos) {
+    if (pos != top) {
+      ge_p1p1_to_p2(r2, t);
+      ge_p2_dbl(t, r2);
     }
-    if (pos % 8 == 0) {
-      const uint32_t e = sd[0] & 0xff;
-      CG_UNROLL for (int w = 0; w < 7; ++w) sd[w] = sd[w] >> 8 | sd[w + 1] << 24;
-      sd[7] >>= 8;
-      const uint32_t neg = e < 128, a = neg ? 128 - e : e - 128;
-      getB(a, pb);
+    if ((pos & 3) == 0) {
+      const uint32_t ea = da[7] >> 28, er = dr[7] >> 28;
+      CG_UNROLL for (int w = 7; w >= 1; --w) {
+        da[w] = (da[w] << 4) | (da[w - 1] >> 28);
+        dr[w] = (dr[w] << 4) | (dr[w - 1] >> 28);
+      }
+      da[0] <<= 4;
+      dr[0] <<= 4;
+      const uint32_t na = ea < 8, nr = er < 8;
+      getA(na ? 8 - ea : ea - 8, ca);
       ge_p1p1_to_p3(r3, t);
-      ge_madd(t, r3, pb, neg);
+      ge_add_cached(t, r3, ca, na);
+      getR(nr ? 8 - er : er - 8, ca);
+      ge_p1p1_to_p3(r3, t);
+      ge_add_cached(t, r3, ca, nr ^ rneg);
     }
-    ge_p1p1_to_p2(r2, t);
+    if ((pos & 7) == 0 && pos < 128) {
+      const uint32_t el = bl[0] & 0xff, eh = bh[0] & 0xff;
+      CG_UNROLL for (int w = 0; w < 3; ++w) {
+        bl[w] = bl[w] >> 8 | bl[w + 1] << 24;
+        bh[w] = bh[w] >> 8 | bh[w + 1] << 24;
+      }
+      bl[3] >>= 8;
+      bh[3] >>= 8;
+      const uint32_t nl = el < 128, nh = eh < 128;
+      getB(0, nl ? 128 - el : el - 128, pb);
+      ge_p1p1_to_p3(r3, t);
+      ge_madd(t, r3, pb, nl);
+      getB(1, nh ? 128 - eh : eh - 128, pb);
+      ge_p1p1_to_p3(r3, t);
+      ge_madd(t, r3, pb, nh);
+    }
   }
-  ge_tobytes(out, r2.X, r2.Y, r2.Z);
+  // identity <=> x = X/Z = 0 and y = Y/T = 1
+  fe d;
+  fe_sub(d, t.Y, t.T);
+  return fe_iszero(t.X) & fe_iszero(d);
 }
 
 }  // namespace cg

@@ -547,8 +547,12 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode) {
       d.table = ctx->ed_table;
       d.btab = ctx->btab;
       {
-        Timed t(ctx, "ed25519_prep", cnt);
-        CG_TRY(ctx, cg::launch_ed25519_prep(d, cnt, (uint32_t)mode, ctx->stream), "launch ed25519_prep");
+        Timed t(ctx, "ed25519_hash", cnt);
+        CG_TRY(ctx, cg::launch_ed25519_hash(d, cnt, (uint32_t)mode, ctx->stream), "launch ed25519_hash");
+      }
+      {
+        Timed t(ctx, "ed25519_points", cnt);
+        CG_TRY(ctx, cg::launch_ed25519_points(d, cnt, ctx->stream), "launch ed25519_points");
       }
       {
         Timed t(ctx, "ed25519_msm", cnt);

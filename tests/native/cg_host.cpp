@@ -41,7 +41,6 @@ uint32_t cgh_slide_drop(const uint32_t* s) { return slide_drops_carry(s); }
 void cgh_effective_s(const uint32_t* s, uint32_t* out) { sc_effective_s(out, s); }
 
 void cgh_recode16(const uint32_t* k, uint32_t* out) { sc_recode16(out, k); }
-void cgh_recode5(const uint32_t* k, uint32_t* out) { sc_recode5(out, k); }
 void cgh_recode8(const uint32_t* k, uint32_t* out) { sc_recode8(out, k); }
 
 void cgh_sha512_ed25519(const uint32_t* r, const uint32_t* ab, const uint8_t* msg, uint32_t n, uint32_t* out) {
@@ -51,32 +50,51 @@ void cgh_sha512_ed25519(const uint32_t* r, const uint32_t* ab, const uint8_t* ms
 int cgh_abyte(const uint32_t* pk, uint32_t* out) {
   ge_p3 A;
   if (!ge_frombytes_i2p(A, pk)) return -1;
-  ed25519_abyte(out, A);
+  ed25519_abyte(out, pk);
   return 0;
 }
 
-static ge_precomp g_btab[kBTabEntries];
+// The half-size scalar reduction: c0 = c1 h mod 8L, c1 odd; returns 1, or 0 when
+// the fallback (h, 1) was taken.
+int cgh_half_scalars(const uint32_t* h, uint32_t* c0, uint32_t* c1, uint32_t* c1neg) {
+  return (int)ed25519_half_scalars(h, c0, c1, *c1neg);
+}
+
+static ge_precomp g_btab[2][kBTabEntries];
 static int g_init;
 
-int cgh_ed25519_verify(const uint8_t* pk_bytes, const uint8_t* sig_bytes, uint32_t sig_len, const uint8_t* msg,
-                       uint32_t msg_len, uint32_t mode) {
+// The three device phases in sequence (hash -> points -> msm) for one signature;
+// the digit count is the lane's own (on the device it is the wave maximum, which
+// only adds leading zero digits).  force_ndig > 0 overrides it.
+int cgh_ed25519_verify_nd(const uint8_t* pk_bytes, const uint8_t* sig_bytes, uint32_t sig_len, const uint8_t* msg,
+                          uint32_t msg_len, uint32_t mode, uint32_t force_ndig, uint32_t full_length) {
   if (!g_init) {
-    ed25519_base_table(g_btab);
+    ed25519_base_table(g_btab[0], 0);
+    ed25519_base_table(g_btab[1], 128);
     g_init = 1;
   }
   uint32_t pk[8], sig[16] = {0};
   memcpy(pk, pk_bytes, 32);
   memcpy(sig, sig_bytes, sig_len < 64 ? sig_len : 64);
-  ge_p3 negA;
-  uint32_t hd[13], sd[8];
-  const uint32_t pre = ed25519_prep(pk, sig, sig_len, msg, msg_len, mode, negA, hd, sd);
+  uint32_t dig[kDigitWords], ndig, rneg;
+  uint32_t pre = full_length ? ed25519_hash_stage<true>(pk, sig, sig_len, msg, msg_len, mode, dig, ndig, rneg)
+                             : ed25519_hash_stage(pk, sig, sig_len, msg, msg_len, mode, dig, ndig, rneg);
+  ge_p3 negA, R;
+  pre = ed25519_points_stage(pk, sig, pre, negA, R);
   if (pre != V_COMPUTE) return (int)pre;
-  ge_cached tab[kATabEntries];
-  ed25519_build_table(negA, [&](int k, const ge_cached& c) { tab[k] = c; });
-  uint32_t rc[8];
-  ed25519_msm(
-      rc, hd, sd, [&](uint32_t k, ge_cached& c) { c = tab[k]; }, [&](uint32_t k, ge_precomp& p) { p = g_btab[k]; });
-  return memcmp(rc, sig, 32) == 0 ? (int)V_ACCEPT : (int)V_REJECT;
+  ge_cached ta[kATabEntries], tr[kATabEntries];
+  ed25519_build_table(negA, [&](int k, const ge_cached& c) { ta[k] = c; });
+  ed25519_build_table(R, [&](int k, const ge_cached& c) { tr[k] = c; });
+  if (force_ndig > ndig) ndig = force_ndig;
+  const uint32_t ok = ed25519_msm(
+      ndig, dig, rneg, [&](uint32_t k, ge_cached& c) { c = ta[k]; }, [&](uint32_t k, ge_cached& c) { c = tr[k]; },
+      [&](uint32_t t, uint32_t k, ge_precomp& p) { p = g_btab[t][k]; });
+  return ok ? (int)V_ACCEPT : (int)V_REJECT;
+}
+
+int cgh_ed25519_verify(const uint8_t* pk_bytes, const uint8_t* sig_bytes, uint32_t sig_len, const uint8_t* msg,
+                       uint32_t msg_len, uint32_t mode) {
+  return cgh_ed25519_verify_nd(pk_bytes, sig_bytes, sig_len, msg, msg_len, mode, 0, 0);
 }
 }
 

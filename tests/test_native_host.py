@@ -30,6 +30,8 @@ def host():
     lib = ctypes.CDLL(SO)
     lib.cgh_ed25519_verify.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p,
                                        ctypes.c_uint32, ctypes.c_uint32]
+    lib.cgh_ed25519_verify_nd.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p,
+                                          ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]
     return lib
 
 
@@ -130,3 +132,49 @@ def test_verify_random_vs_oracle(host, oracle):
             for mode in (0, 1):
                 assert host.cgh_ed25519_verify(p, sg, len(sg), msg, len(msg), mode) == \
                     oracle.oracle_ed25519_verify(p, sg, len(sg), msg, len(msg), mode)
+
+
+def test_verify_golden_full_length_and_padded_digits(host, golden_ed25519):
+    """The (h, 1) fallback of the half-size reduction, and a lane whose digit
+    count is raised by a longer scalar elsewhere in its wave (leading zero
+    digits), give the same verdicts."""
+    for e in golden_ed25519:
+        pk, sig, msg = (bytes.fromhex(e[k]) for k in ("pk", "sig", "msg"))
+        for nd, full in ((0, 1), (40, 0), (64, 0)):
+            assert host.cgh_ed25519_verify_nd(pk, sig, len(sig), msg, len(msg), 0, nd, full) == e["is_valid"], \
+                (e["cls"], nd, full)
+
+
+def test_half_scalars_property(host):
+    """c0 = c1 h (mod 8L), c1 odd, both ~128 bits, for random and edge h."""
+    N = 8 * L
+    rnd = random.Random(6)
+    edge = [0, 1, 2, L - 1, 2**128 - 1, 2**128, 2**252, N // 3 % L]
+    for h in edge + [rnd.randrange(L) for _ in range(3000)]:
+        c0, c1, neg = (ctypes.c_uint32 * 8)(), (ctypes.c_uint32 * 8)(), ctypes.c_uint32()
+        ok = host.cgh_half_scalars(w8(h), c0, c1, ctypes.byref(neg))
+        C0, C1 = val(c0), val(c1) * (-1 if neg.value else 1)
+        assert C1 % 2 == 1 and (C0 - C1 * h) % N == 0 and C0 >= 0, hex(h)
+        if ok:  # correct but long for a few edge values (a huge partial quotient); short for hashes
+            assert max(C0.bit_length(), abs(C1).bit_length()) <= (252 if h in edge else 136), hex(h)
+        else:
+            assert (C0, C1) == (h, 1)
+
+
+def test_verify_random_mutations_vs_oracle(host, oracle):
+    """Valid signatures and single-bit mutations of R, S, M and A, plus S + kL,
+    across lengths, against the C oracle."""
+    rnd = random.Random(7)
+    for _ in range(400):
+        seed, msg = rnd.randbytes(32), rnd.randbytes(rnd.randint(1, 300))
+        pk, sig = ED.sign(seed, msg)
+        cases = [(pk, sig, msg)]
+        for part in range(4):
+            b = bytearray(pk if part == 3 else sig if part < 2 else msg)
+            i = rnd.randrange(len(b)) if part >= 2 else (rnd.randrange(32) + 32 * part)
+            b[i] ^= 1 << rnd.randrange(8)
+            cases.append((bytes(b), sig, msg) if part == 3 else (pk, bytes(b), msg) if part < 2 else (pk, sig, bytes(b)))
+        for p, sg, m in cases:
+            nd = rnd.choice([0, 0, 34, 64])
+            assert host.cgh_ed25519_verify_nd(p, sg, len(sg), m, len(m), 0, nd, 0) == \
+                oracle.oracle_ed25519_verify(p, sg, len(sg), m, len(m), 0)

@@ -107,13 +107,14 @@ def main():
     with open(os.path.join(prof, f"{tag}_pmc_summary.json"), "w") as f:
         json.dump(summary, f, indent=1)
     msm = kernels.get("cg_ed25519_msm", {})
-    prep = kernels.get("cg_ed25519_prep", {})
     traffic = {"source": f"profiles/{tag}_pmc_summary.json",
                "ed25519_msm_bytes_per_launch": msm.get("hbm_bytes_per_launch"),
-               "ed25519_prep_bytes_per_launch": prep.get("hbm_bytes_per_launch"),
                "ed25519_msm_valu_instr_per_verify": msm.get("valu_instr_per_verify"),
-               "ed25519_msm_effective_clock_GHz": msm.get("effective_clock_GHz"),
-               "ed25519_prep_valu_instr_per_verify": prep.get("valu_instr_per_verify")}
+               "ed25519_msm_effective_clock_GHz": msm.get("effective_clock_GHz")}
+    for k in ("hash", "points"):
+        e = kernels.get(f"cg_ed25519_{k}", {})
+        traffic[f"ed25519_{k}_bytes_per_launch"] = e.get("hbm_bytes_per_launch")
+        traffic[f"ed25519_{k}_valu_instr_per_verify"] = e.get("valu_instr_per_verify")
     with open(os.path.join(prof, "pmc_traffic.json"), "w") as f:
         json.dump(traffic, f, indent=1)
     print(json.dumps({k: {kk: vv for kk, vv in v.items() if kk != "counters"} for k, v in kernels.items()},
