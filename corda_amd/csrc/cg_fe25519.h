@@ -42,6 +42,17 @@ CG_HD void fe_select(fe& h, const fe& f, const fe& g, uint32_t c) {
   CG_UNROLL for (int i = 0; i < 10; ++i) h.v[i] = f.v[i] ^ ((f.v[i] ^ g.v[i]) & m);
 }
 
+// Pins a scaled limb (19 g_j, 2 f_i, ...) as a 32-bit value.  Without it LLVM
+// rewrites sext(2 x) as 2 sext(x) (the product cannot overflow, so the rewrite is
+// legal) and the limb product becomes a 64 x 64 multiply: v_mad_u64_u32 + two
+// v_mul_lo_u32 + v_add3_u32 instead of one v_mad_i64_i32.
+CG_HD int32_t fe_pin(int32_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm("" : "+v"(x));
+#endif
+  return x;
+}
+
 // Signed carry chain (round-to-nearest) on 64-bit column sums -> reduced limbs.
 // With rounding carries c = (t + 2^(w-1)) >> w, the residue t - c*2^w is exactly
 // the sign-extended low w bits of t, so it costs one v_bfe_i32 instead of a
@@ -74,7 +85,7 @@ CG_HD void fe_carry_wide(fe& h, int64_t t[10]) {
   CG_C26(0)
 #undef CG_C26
 #undef CG_C25
-  CG_UNROLL for (int i = 0; i < 10; ++i) h.v[i] = (int32_t)t[i];
+  CG_UNROLL for (int i = 0; i < 10; ++i) h.v[i] = fe_pin((int32_t)t[i]);
 }
 
 // Same chain on 32-bit limbs (for values already within ~2^29 per limb).
@@ -106,8 +117,8 @@ CG_HD void fe_reduce(fe& h) {
 // odd limbs are 25 bits wide.
 CG_HD void fe_mul(fe& h, const fe& f, const fe& g) {
   int32_t g19[10], f2[10];
-  CG_UNROLL for (int j = 0; j < 10; ++j) g19[j] = 19 * g.v[j];
-  CG_UNROLL for (int i = 0; i < 10; ++i) f2[i] = (i & 1) ? 2 * f.v[i] : f.v[i];
+  CG_UNROLL for (int j = 0; j < 10; ++j) g19[j] = fe_pin(19 * g.v[j]);
+  CG_UNROLL for (int i = 0; i < 10; ++i) f2[i] = (i & 1) ? fe_pin(2 * f.v[i]) : f.v[i];
   int64_t t[10];
   CG_UNROLL for (int k = 0; k < 10; ++k) t[k] = 0;
   CG_UNROLL for (int i = 0; i < 10; ++i) {
@@ -124,15 +135,19 @@ CG_HD void fe_mul(fe& h, const fe& f, const fe& g) {
 // h = f^2 (DOUBLE ? 2 f^2 : f^2): 55 products using the symmetry f_i f_j = f_j f_i.
 template <bool DOUBLE>
 CG_HD void fe_sq_t(fe& h, const fe& f) {
-  int32_t f19[10];
-  CG_UNROLL for (int j = 0; j < 10; ++j) f19[j] = 19 * f.v[j];
+  int32_t f19[10], f2[10], f4[10];
+  CG_UNROLL for (int j = 0; j < 10; ++j) {
+    f19[j] = fe_pin(19 * f.v[j]);
+    f2[j] = fe_pin(2 * f.v[j]);
+    f4[j] = fe_pin(4 * f.v[j]);
+  }
   int64_t t[10];
   CG_UNROLL for (int k = 0; k < 10; ++k) t[k] = 0;
   CG_UNROLL for (int i = 0; i < 10; ++i) {
     CG_UNROLL for (int j = i; j < 10; ++j) {
       const int k = i + j;
       const int m = ((i == j) ? 1 : 2) * (((i & 1) && (j & 1)) ? 2 : 1);
-      const int32_t a = m * f.v[i];
+      const int32_t a = m == 1 ? f.v[i] : m == 2 ? f2[i] : f4[i];
       const int32_t b = (k >= 10) ? f19[j] : f.v[j];
       t[k >= 10 ? k - 10 : k] += (int64_t)a * b;
     }
