@@ -32,7 +32,42 @@ static const uint64_t kSha512K[80] = {
     0x28db77f523047d84ULL, 0x32caab7b40c72493ULL, 0x3c9ebe0a15c9bebcULL, 0x431d67c49c100d4cULL,
     0x4cc5d4becb3e42b6ULL, 0x597f299cfc657e2aULL, 0x5fcb6fab3ad6faecULL, 0x6c44198c4a475817ULL};
 
-CG_HD uint64_t rotr64(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+// 64-bit words live in VGPR pairs; a rotate is two v_alignbit_b32 and the
+// three-input boolean functions are one v_bitop3_b32 per half (gfx950).
+CG_HD uint32_t lo32(uint64_t x) { return (uint32_t)x; }
+CG_HD uint32_t hi32(uint64_t x) { return (uint32_t)(x >> 32); }
+#if defined(__HIP_DEVICE_COMPILE__)
+typedef uint32_t cg_u32x2 __attribute__((ext_vector_type(2)));
+// a bit cast of the register pair: LLVM keeps it whole instead of splitting
+// later 64-bit adds into a zero-extended low half and a 32-bit high half
+CG_HD uint64_t mk64(uint32_t hi, uint32_t lo) { return __builtin_bit_cast(uint64_t, cg_u32x2{lo, hi}); }
+#else
+CG_HD uint64_t mk64(uint32_t hi, uint32_t lo) { return (uint64_t)hi << 32 | lo; }
+#endif
+
+CG_HD uint64_t rotr64(uint64_t x, int n) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t l = lo32(x), h = hi32(x);
+  if (n < 32) return mk64(__builtin_amdgcn_alignbit(l, h, n), __builtin_amdgcn_alignbit(h, l, n));
+  return mk64(__builtin_amdgcn_alignbit(h, l, n - 32), __builtin_amdgcn_alignbit(l, h, n - 32));
+#else
+  return (x >> n) | (x << (64 - n));
+#endif
+}
+
+#if defined(__HIP_DEVICE_COMPILE__)
+#define CG_BITOP3_64(a, b, c, imm)                                                  \
+  mk64(__builtin_amdgcn_bitop3_b32(hi32(a), hi32(b), hi32(c), imm),                 \
+       __builtin_amdgcn_bitop3_b32(lo32(a), lo32(b), lo32(c), imm))
+CG_HD uint64_t xor3_64(uint64_t a, uint64_t b, uint64_t c) { return CG_BITOP3_64(a, b, c, 0x96); }
+CG_HD uint64_t ch64(uint64_t e, uint64_t f, uint64_t g) { return CG_BITOP3_64(e, f, g, 0xca); }
+CG_HD uint64_t maj64(uint64_t a, uint64_t b, uint64_t c) { return CG_BITOP3_64(a, b, c, 0xe8); }
+#undef CG_BITOP3_64
+#else
+CG_HD uint64_t xor3_64(uint64_t a, uint64_t b, uint64_t c) { return a ^ b ^ c; }
+CG_HD uint64_t ch64(uint64_t e, uint64_t f, uint64_t g) { return (e & f) ^ (~e & g); }
+CG_HD uint64_t maj64(uint64_t a, uint64_t b, uint64_t c) { return (a & b) ^ (a & c) ^ (b & c); }
+#endif
 
 CG_HD uint32_t bswap32(uint32_t x) {
   return (x >> 24) | ((x >> 8) & 0xff00u) | ((x << 8) & 0xff0000u) | (x << 24);
@@ -50,26 +85,44 @@ CG_HD void sha512_init(uint64_t h[8]) {
   h[6] = 0x1f83d9abfb41bd6bULL; h[7] = 0x5be0cd19137e2179ULL;
 }
 
-// One compression.  The schedule is kept as a 16-word ring; rounds run in an
-// outer loop of 5 x 16 so the code stays small (I-cache is shared per CU pair).
+CG_HD void sha512_round(uint64_t a, uint64_t b, uint64_t c, uint64_t& d, uint64_t e, uint64_t f, uint64_t g,
+                        uint64_t& h, uint64_t kw) {
+  const uint64_t t1 = h + xor3_64(rotr64(e, 14), rotr64(e, 18), rotr64(e, 41)) + ch64(e, f, g) + kw;
+  d += t1;
+  h = t1 + xor3_64(rotr64(a, 28), rotr64(a, 34), rotr64(a, 39)) + maj64(a, b, c);
+}
+
+// Eight rounds with the working variables renamed in place (no register moves).
+#define CG_SHA512_8(K, W, base)                                             \
+  sha512_round(a, b, c, d, e, f, g, hh, (K)[(base) + 0] + (W)[0]);         \
+  sha512_round(hh, a, b, c, d, e, f, g, (K)[(base) + 1] + (W)[1]);         \
+  sha512_round(g, hh, a, b, c, d, e, f, (K)[(base) + 2] + (W)[2]);         \
+  sha512_round(f, g, hh, a, b, c, d, e, (K)[(base) + 3] + (W)[3]);         \
+  sha512_round(e, f, g, hh, a, b, c, d, (K)[(base) + 4] + (W)[4]);         \
+  sha512_round(d, e, f, g, hh, a, b, c, (K)[(base) + 5] + (W)[5]);         \
+  sha512_round(c, d, e, f, g, hh, a, b, (K)[(base) + 6] + (W)[6]);         \
+  sha512_round(b, c, d, e, f, g, hh, a, (K)[(base) + 7] + (W)[7]);
+
+// One compression: rounds 0-15 on the message words, then four 16-round
+// passes that extend the schedule in its 16-word ring (an outer loop, so the
+// code stays small; 16 rounds close the variable renaming).
 CG_HD void sha512_block(uint64_t h[8], uint64_t w[16]) {
   uint64_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
-  CG_NOUNROLL for (int r = 0; r < 80; r += 16) {
+  CG_SHA512_8(kSha512K, w, 0)
+  CG_SHA512_8(kSha512K, w + 8, 8)
+  CG_NOUNROLL for (int r = 16; r < 80; r += 16) {
     CG_UNROLL for (int j = 0; j < 16; ++j) {
-      if (r > 0) {
-        const uint64_t w15 = w[(j + 1) & 15], w2 = w[(j + 14) & 15];
-        const uint64_t s0 = rotr64(w15, 1) ^ rotr64(w15, 8) ^ (w15 >> 7);
-        const uint64_t s1 = rotr64(w2, 19) ^ rotr64(w2, 61) ^ (w2 >> 6);
-        w[j] += s0 + w[(j + 9) & 15] + s1;
-      }
-      const uint64_t t1 = hh + (rotr64(e, 14) ^ rotr64(e, 18) ^ rotr64(e, 41)) + ((e & f) ^ (~e & g)) +
-                          kSha512K[r + j] + w[j];
-      const uint64_t t2 = (rotr64(a, 28) ^ rotr64(a, 34) ^ rotr64(a, 39)) + ((a & b) ^ (a & c) ^ (b & c));
-      hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+      const uint64_t w15 = w[(j + 1) & 15], w2 = w[(j + 14) & 15];
+      const uint64_t s0 = xor3_64(rotr64(w15, 1), rotr64(w15, 8), w15 >> 7);
+      const uint64_t s1 = xor3_64(rotr64(w2, 19), rotr64(w2, 61), w2 >> 6);
+      w[j] += s0 + w[(j + 9) & 15] + s1;
     }
+    CG_SHA512_8(kSha512K, w, r)
+    CG_SHA512_8(kSha512K, w + 8, r + 8)
   }
   h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
 }
+#undef CG_SHA512_8
 
 // Loads dword i of a message whose bytes start at `m` (any alignment handled
 // by the caller through `sh`); `m4` is the 4-byte-aligned base.
