@@ -106,6 +106,119 @@ CG_HD uint32_t mp9_abs(uint32_t out[9], const uint32_t t[9]) {
 }
 
 // ---------------------------------------------------------------- reduction
+// One exact Euclid step (a, b, ta, tb) -> (b, a mod b, tb, ta - q tb) with the
+// quotient estimated in fp64 and corrected exactly.  Returns 0 when q >= 2^31
+// (the caller falls back).
+CG_HD uint32_t hs_exact_step(uint32_t a[9], uint32_t b[9], uint32_t ta[9], uint32_t tb[9]) {
+  const double qd = mp9_to_double(a) / mp9_to_double(b);
+  if (!(qd < 2147483648.0)) return 0;
+  const uint32_t q = (uint32_t)qd;
+  uint32_t r[9], tn[9];
+  uint32_t neg = mp9_submul(r, a, b, q);
+  mp9_submul(tn, ta, tb, q);
+  // the fp64 estimate is within +-1 of floor(a/b) here; correct it exactly
+  CG_NOUNROLL for (int k = 0; k < 2 && neg; ++k) {
+    neg = mp9_add(r, b) ? 0u : 1u;
+    mp9_add(tn, tb);
+  }
+  CG_NOUNROLL for (int k = 0; k < 2 && !neg && mp9_ge(r, b); ++k) {
+    mp9_sub(r, b);
+    mp9_sub(tn, tb);
+  }
+  if (neg || mp9_ge(r, b)) return 0;
+  CG_UNROLL for (int w = 0; w < 9; ++w) {
+    a[w] = b[w];
+    b[w] = r[w];
+    ta[w] = tb[w];
+    tb[w] = tn[w];
+  }
+  return 1;
+}
+
+// floor(x / 2^s) & (2^64 - 1) for a 9-word x; s is per lane (select chain, no
+// dynamically indexed registers).
+CG_HD uint64_t mp9_shr64(const uint32_t x[9], uint32_t s) {
+  const uint32_t ws = s >> 5, bs = s & 31;
+  uint32_t w0 = 0, w1 = 0, w2 = 0;
+  CG_UNROLL for (int w = 0; w < 9; ++w) {
+    w0 = (uint32_t)w == ws ? x[w] : w0;
+    w1 = (uint32_t)w == ws + 1 ? x[w] : w1;
+    w2 = (uint32_t)w == ws + 2 ? x[w] : w2;
+  }
+  const uint64_t lo = bs ? ((uint64_t)w0 >> bs | (uint64_t)w1 << (32 - bs)) : w0;
+  const uint64_t hi = bs ? ((uint64_t)w1 >> bs | (uint64_t)w2 << (32 - bs)) : w1;
+  return (lo & 0xffffffffull) | hi << 32;
+}
+
+// out = (A x + B y) mod 2^288 for signed 32-bit A, B (two's complement words).
+CG_HD void mp9_lincomb(uint32_t out[9], const uint32_t x[9], const uint32_t y[9], int64_t A, int64_t B) {
+  const uint32_t ma = (uint32_t)(A < 0 ? -A : A), mb = (uint32_t)(B < 0 ? -B : B);
+  const uint32_t na = A < 0 ? 0xffffffffu : 0u, nb = B < 0 ? 0xffffffffu : 0u;
+  // (+-ma x) = (ma x) ^ na + (na & 1), likewise for y; both folded into one carry chain
+  uint64_t cx = 0, cy = 0, c = (uint64_t)(na & 1u) + (nb & 1u);
+  CG_UNROLL for (int w = 0; w < 9; ++w) {
+    const uint64_t px = (uint64_t)ma * x[w] + cx, py = (uint64_t)mb * y[w] + cy;
+    cx = px >> 32;
+    cy = py >> 32;
+    c += (uint64_t)((uint32_t)px ^ na) + ((uint32_t)py ^ nb);
+    out[w] = (uint32_t)c;
+    c >>= 32;
+  }
+}
+
+// Lehmer's algorithm (Knuth TAOCP 4.5.2, Algorithm L) on 52-bit leading digits:
+// up to ~20 Euclid quotients emulated in 64-bit arithmetic (each verified by
+// Knuth's two-sided test, so the quotient sequence is exactly Euclid's), then
+// applied to (a, b, ta, tb) at once.  The emulation stops before a remainder
+// can get close to 2^128, so the exact single steps find the first remainder
+// below 2^128 — the same (a, b, ta, tb) the plain step-by-step loop reaches.
+// Returns 0 when no quotient was emulated (the caller takes an exact step).
+CG_HD uint32_t hs_lehmer(uint32_t a[9], uint32_t b[9], uint32_t ta[9], uint32_t tb[9]) {
+  const uint32_t s = mp9_bitlen(a) - 52;  // caller guarantees bitlen(a) > 132
+  int64_t uh = (int64_t)mp9_shr64(a, s), vh = (int64_t)mp9_shr64(b, s);
+  // An emulated remainder T stands for a true one in (T - |C| - |D|, T + |C| + |D|)
+  // * 2^s with |C|, |D| < 2^31: T >= 2^(129-s) + 2^33 keeps every emulated
+  // remainder above 2^128 (s ranges over 81..204).
+  const int64_t thr = (s < 129 ? (int64_t)1 << (129 - s) : (int64_t)0) + ((int64_t)1 << 33);
+  int64_t A = 1, B = 0, C = 0, D = 1;
+  CG_NOUNROLL for (int it = 0; it < 48; ++it) {
+    const int64_t y1 = vh + C, y2 = vh + D, x1 = uh + A, x2 = uh + B;
+    if (y1 <= 0 || y2 <= 0 || x1 < 0 || x2 < 0) break;
+    // q = floor(x1 / y1): operands < 2^53 are exact doubles, the rounded quotient
+    // is within 1 of the floor
+    int64_t q = (int64_t)((double)x1 / (double)y1);
+    const int64_t r1 = x1 - q * y1;
+    q = r1 < 0 ? q - 1 : (r1 >= y1 ? q + 1 : q);
+    if (q < 1 || q >= ((int64_t)1 << 31)) break;
+    // Knuth's test: the other bound gives the same quotient (q y2 <= x2 < 2^53)
+    if ((double)q * (double)y2 > 9.0e15) break;
+    const int64_t r2 = x2 - q * y2;
+    if (r2 < 0 || r2 >= y2) break;
+    const int64_t T = uh - q * vh, nC = A - q * C, nD = B - q * D;
+    const int64_t lim = ((int64_t)1 << 31) - 1;
+    if (T < thr || nC > lim || nC < -lim || nD > lim || nD < -lim) break;
+    A = C;
+    C = nC;
+    B = D;
+    D = nD;
+    uh = vh;
+    vh = T;
+  }
+  if (B == 0) return 0;
+  uint32_t na[9], nb[9], nta[9], ntb[9];
+  mp9_lincomb(na, a, b, A, B);
+  mp9_lincomb(nb, a, b, C, D);
+  mp9_lincomb(nta, ta, tb, A, B);
+  mp9_lincomb(ntb, ta, tb, C, D);
+  CG_UNROLL for (int w = 0; w < 9; ++w) {
+    a[w] = na[w];
+    b[w] = nb[w];
+    ta[w] = nta[w];
+    tb[w] = ntb[w];
+  }
+  return 1;
+}
+
 // c0 = c1 h mod 8L with c1 odd; c0 >= 0 and |c1| returned with its sign.  Both
 // are < 2^253 on success (typically ~2^128).  Returns 0 when the caller must
 // fall back to (h, 1).
@@ -118,33 +231,14 @@ CG_HD uint32_t ed25519_half_scalars(const uint32_t h[8], uint32_t c0[8], uint32_
   }
   uint32_t ok = 1, steps = 0;
   CG_NOUNROLL while ((b[4] | b[5] | b[6] | b[7] | b[8]) != 0) {  // b >= 2^128
-    const double qd = mp9_to_double(a) / mp9_to_double(b);
-    if (!(qd < 2147483648.0) || ++steps > 200) {
+    if (++steps > 160) {
       ok = 0;
       break;
     }
-    uint32_t q = (uint32_t)qd;
-    uint32_t r[9], tn[9];
-    uint32_t neg = mp9_submul(r, a, b, q);
-    mp9_submul(tn, ta, tb, q);
-    // the fp64 estimate is within +-1 of floor(a/b) here; correct it exactly
-    CG_NOUNROLL for (int k = 0; k < 2 && neg; ++k) {
-      neg = mp9_add(r, b) ? 0u : 1u;
-      mp9_add(tn, tb);
-    }
-    CG_NOUNROLL for (int k = 0; k < 2 && !neg && mp9_ge(r, b); ++k) {
-      mp9_sub(r, b);
-      mp9_sub(tn, tb);
-    }
-    if (neg || mp9_ge(r, b)) {
+    if (mp9_bitlen(a) > 132 && hs_lehmer(a, b, ta, tb)) continue;
+    if (!hs_exact_step(a, b, ta, tb)) {
       ok = 0;
       break;
-    }
-    CG_UNROLL for (int w = 0; w < 9; ++w) {
-      a[w] = b[w];
-      b[w] = r[w];
-      ta[w] = tb[w];
-      tb[w] = tn[w];
     }
   }
   // candidates: (b, tb) when tb is odd; else (a, ta) and one more step (both odd,

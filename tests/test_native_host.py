@@ -161,6 +161,48 @@ def test_half_scalars_property(host):
             assert (C0, C1) == (h, 1)
 
 
+def _half_scalars_euclid(h):
+    """Plain step-by-step Euclid on (8L, h) to the first remainder below 2^128 and
+    the candidate choice of cg_halfscalar.h: the device's Lehmer version must land
+    on exactly these (c0, |c1|, sign), or return None for the (h, 1) fallback."""
+    a, b, ta, tb = 8 * L, h, 0, 1
+    while b >= 1 << 128:
+        q = a // b
+        if q >= 1 << 31:
+            return None
+        a, b, ta, tb = b, a - q * b, tb, ta - q * tb
+    x0, x1 = b, tb
+    if tb % 2 == 0:
+        x0, x1 = a, ta
+        best = max(a.bit_length(), abs(ta).bit_length())
+        if b:
+            q = a // b
+            if q < 1 << 31:
+                r, tn = a - q * b, ta - q * tb
+                if max(r.bit_length(), abs(tn).bit_length()) < best:
+                    x0, x1 = r, tn
+    if x1 % 2 == 0 or x0.bit_length() > 252 or abs(x1).bit_length() > 252:
+        return None
+    return x0, abs(x1), int(x1 < 0)
+
+
+def test_half_scalars_lehmer_equals_euclid(host):
+    """The Lehmer-accelerated reduction reproduces plain Euclid's result exactly."""
+    rnd = random.Random(11)
+    hs = [0, 1, 2, 3, L - 1, L - 2, 2**128 - 1, 2**128, 2**128 + 1, 2**133, 2**200 + 5, 2**252, (8 * L) // 3 % L,
+          (8 * L) // 5 % L]
+    hs += [rnd.randrange(L) for _ in range(4000)]
+    hs += [rnd.randrange(1 << rnd.randrange(120, 253)) for _ in range(2000)]
+    for h in hs:
+        c0, c1, neg = (ctypes.c_uint32 * 8)(), (ctypes.c_uint32 * 8)(), ctypes.c_uint32()
+        ok = host.cgh_half_scalars(w8(h), c0, c1, ctypes.byref(neg))
+        exp = _half_scalars_euclid(h)
+        if exp is None:
+            assert ok == 0 and (val(c0), val(c1), neg.value) == (h, 1, 0), hex(h)
+        else:
+            assert ok == 1 and (val(c0), val(c1), neg.value) == exp, hex(h)
+
+
 def test_verify_random_mutations_vs_oracle(host, oracle):
     """Valid signatures and single-bit mutations of R, S, M and A, plus S + kL,
     across lengths, against the C oracle."""
