@@ -22,6 +22,8 @@ own JSON line; they are evidence for DESIGN.md, not the driver's line):
     backlog  config 5: 100M Ed25519 signatures over 32 B tx ids, split by index
              over the ranks (strong scaling), staged in 2^24 chunks, verdict-
              bitmap all-gather over RCCL
+    ftx      SURVEY 8(f) row 1: 1M FilteredTransaction.verify (non-validating
+             notary: filtered-leaf hashes + partial Merkle tree + multiset check)
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload ed25519|ecdsa|tx|backlog]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
@@ -58,7 +60,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--workload", choices=["ed25519", "ecdsa", "tx", "backlog"], default="ed25519")
+    p.add_argument("--workload", choices=["ed25519", "ecdsa", "tx", "backlog", "ftx"], default="ed25519")
     p.add_argument("--batch", type=int, default=None,
                    help="per-GPU units (default: 1M signatures / 1M per curve / 1M txs; backlog: 100M total)")
     p.add_argument("--pool", type=int, default=131072,
@@ -514,6 +516,68 @@ def run_tx(args, dist):
     return line
 
 
+# ------------------------------------------------------------------ §8(f) row 1
+def run_ftx(args, dist):
+    """Non-validating notary: FilteredTransaction.verify over a batch (SURVEY §8f
+    rank 1; NonValidatingNotaryFlow.kt:25-27 -> MerkleTransaction.kt:173-178 ->
+    PartialMerkleTree.kt:130-155)."""
+    import datagen
+    from corda_amd import Context
+    from corda_amd._lib import ptr
+
+    n = args.batch or (1 << 20)
+    rank, world = dist.rank, dist.world
+    t_gen = time.perf_counter()
+    pool = datagen.make_ftx_batch(min(args.pool, n), seed=11 + rank)
+    w = datagen.tile_ftx_batch(pool, n, adversarial=args.adversarial, seed=12 + rank)
+    t_gen = time.perf_counter() - t_gen
+    ctx = Context(dist.local_rank)
+    out = np.zeros(n, dtype=np.uint8)
+    arrs = (w.arena, w.comp_off, w.comp_len, w.comp_start, w.nonces, w.node_start, w.node_kind, w.node_hash, w.roots)
+    ctx.register_host(*arrs, out)
+
+    def step():
+        ctx.check(ctx.lib.cg_ftx_verify_batch(ctx.h, n, ptr(w.arena), len(w.arena), *(ptr(x) for x in arrs[1:]),
+                                              ptr(out)))
+
+    elapsed = timed(dist, ctx, step, args.steps, args.warmup)
+    ctx.unregister_host(*arrs, out)
+    ks = kstats(ctx, ["merkle_leaf", "pmt_eval"])
+    blocks = int(((w.comp_len.astype(np.int64) + 32 + 9 + 63) // 64).sum() + 2 * int((w.node_kind == 2).sum()))
+    ops = blocks * OP_MODEL["primitives"]["sha256_block"]
+    kms = sum(ks.get(k, {}).get("avg_launch_ms", 0) for k in ("merkle_leaf", "pmt_eval"))
+    ach = ops / (kms / 1e3) / 1e12 if kms else 0.0
+    value = n * world * args.steps / elapsed
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        m = min(args.cpu_sample or 262144, n)
+        lib = oracle_lib()
+        lib.oracle_ftx_verify_batch.argtypes = [ctypes.c_void_p] * 9 + [ctypes.c_size_t, ctypes.c_void_p]
+        cres = np.zeros(m, dtype=np.uint8)
+        t0 = time.perf_counter()
+        lib.oracle_ftx_verify_batch(*(x.ctypes.data for x in arrs), m, cres.ctypes.data)
+        dt = time.perf_counter() - t0
+        cpu = {"value": round(m / dt, 1), "unit": "ftx/s", "cores": 1, "kind": "port",
+               "sample": f"first {m} filtered txs of the same workload, C restatement (oracle/liboracle.so "
+                         f"oracle_ftx_verify_batch, single thread of '{host_cpu_model()}'), {dt:.1f} s wall",
+               "results_match_gpu": bool(np.array_equal(cres, out[:m]))}
+    line = base_line(args, dist, "FilteredTransaction verifies/sec", "ftx/s", value, elapsed * 1e3 / args.steps, {
+        "workload": f"SURVEY 8(f) row 1 (non-validating notary): {n} FilteredTransactions per GPU = config-4 "
+                    "transactions filtered to inputs + time window (NotaryFlow.kt:72), partial Merkle tree over "
+                    f"the full tx, {args.adversarial:.0%} adversarial (component / root / tree-hash byte flips); "
+                    "host buffers (page-locked once) in, results out",
+        "batch_per_gpu": n, "global_batch": n * world, "parallelism": f"dp{world} (ftx-index shards)"})
+    line.update({
+        "roofline": {"bound": "valu_int32", "kernel": "merkle_leaf+pmt_eval", "achieved": round(ach, 3),
+                     "peak": PEAK, "unit": "TOPS", "frac": round(ach / PEAK, 4), "traffic": None,
+                     "ops_per_launch": ops, "sha256_blocks": blocks},
+        "kernels": ks, "cpu_baseline": cpu,
+        "checks": {"results_match_generator": bool(np.array_equal(out, w.expected)), "false": int(out.sum()),
+                   "components": int(w.comp_start[-1]), "nodes": int(w.node_start[-1]), "datagen_s": round(t_gen, 1)}})
+    ctx.close()
+    return line
+
+
 # ------------------------------------------------------------------ config 5
 def run_backlog(args, dist):
     import datagen
@@ -596,7 +660,8 @@ def run_backlog(args, dist):
 def main():
     args = parse()
     dist = Dist()
-    run = {"ed25519": run_ed25519, "ecdsa": run_ecdsa, "tx": run_tx, "backlog": run_backlog}[args.workload]
+    run = {"ed25519": run_ed25519, "ecdsa": run_ecdsa, "tx": run_tx, "backlog": run_backlog,
+           "ftx": run_ftx}[args.workload]
     line = run(args, dist)
     if dist.rank == 0:
         print(json.dumps(line), flush=True)

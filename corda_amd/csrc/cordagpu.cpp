@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -805,7 +806,8 @@ cg_status compute_txids(cg_ctx* ctx, size_t n_tx, const uint8_t* arena, size_t a
   {
     Timed t(ctx, "merkle_leaf", c_end - c_begin);
     CG_TRY(ctx, cg::launch_merkle_leaf(d.arena, arena_bytes, d.comp_off, d.comp_len, d.comp_start, d.comp_tx, d.salts,
-                                       c_begin, c_end, d.leaves, ctx->err_flag, ctx->stream), "launch merkle_leaf");
+                                       nullptr, c_begin, c_end, d.leaves, ctx->err_flag, ctx->stream),
+           "launch merkle_leaf");
   }
   {
     Timed t(ctx, "merkle_tree", n_tx);
@@ -900,6 +902,136 @@ cg_status cg_tx_verify_batch(cg_ctx* ctx, int mode, size_t n_tx, const uint8_t* 
     return fail(ctx, CG_E_MERKLE_EMPTY, "Cannot calculate Merkle root on empty hash list.");
   }
   return CG_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+// Host pass over the post-order node programs: each must be exactly one tree
+// (kinds 0..2, a Node never underflows, one value left).  Returns the deepest
+// stack any tx needs; malformed txs get kPmtMalformed in status.
+uint32_t pmt_scan(size_t n_ftx, const uint32_t* node_start, const uint8_t* node_kind, uint8_t* status) {
+  uint32_t max_depth = 1;
+  for (size_t t = 0; t < n_ftx; ++t) {
+    uint64_t sp = 0, deepest = 0;
+    bool bad = node_start[t + 1] == node_start[t];
+    for (uint32_t j = node_start[t]; j < node_start[t + 1] && !bad; ++j) {
+      const uint8_t k = node_kind[j];
+      if (k == cg::kPmtIncluded || k == cg::kPmtLeaf) {
+        deepest = ++sp > deepest ? sp : deepest;
+      } else if (k == cg::kPmtNode && sp >= 2) {
+        --sp;
+      } else {
+        bad = true;
+      }
+    }
+    bad = bad || sp != 1;
+    status[t] = bad ? cg::kPmtMalformed : cg::kPmtTrue;
+    if (!bad && deepest > max_depth) max_depth = (uint32_t)deepest;
+  }
+  return max_depth;
+}
+
+bool hash_less(const std::array<uint8_t, 32>& a, const std::array<uint8_t, 32>& b) { return a < b; }
+
+}  // namespace
+
+extern "C" {
+
+cg_status cg_ftx_verify_batch(cg_ctx* ctx, size_t n_ftx, const uint8_t* arena, size_t arena_bytes,
+                              const uint64_t* comp_off, const uint32_t* comp_len, const uint32_t* comp_start,
+                              const uint8_t* nonces, const uint32_t* node_start, const uint8_t* node_kind,
+                              const uint8_t* node_hash, const uint8_t* root_hashes, uint8_t* result_out) {
+  if (!ctx) return CG_E_INVALID_ARGUMENT;
+  if (n_ftx == 0) return CG_OK;
+  if (n_ftx > 0xFFFFFFF0ull) return fail(ctx, CG_E_INVALID_ARGUMENT, "too many transactions");
+  if (!comp_start || !node_start || !root_hashes || !result_out || (node_start[n_ftx] && (!node_kind || !node_hash)) ||
+      (comp_start[n_ftx] && (!comp_off || !comp_len || !arena || !nonces)))
+    return fail(ctx, CG_E_INVALID_ARGUMENT, "null pointer");
+  for (size_t t = 0; t < n_ftx; ++t)
+    if (comp_start[t + 1] < comp_start[t] || node_start[t + 1] < node_start[t])
+      return fail(ctx, CG_E_INVALID_ARGUMENT, "comp_start / node_start not monotone");
+  if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, CG_E_DEVICE, "hipSetDevice");
+  std::vector<uint8_t> status(n_ftx);
+  const uint32_t depth = pmt_scan(n_ftx, node_start, node_kind, status.data());
+  const size_t n_comp = comp_start[n_ftx], n_node = node_start[n_ftx];
+  TxDev d;
+  uint32_t *nonces_d = nullptr, *node_start_d = nullptr, *node_hash_d = nullptr, *roots_d = nullptr,
+           *stack_d = nullptr;
+  uint8_t *kind_d = nullptr, *status_d = nullptr;
+  cg_status st;
+  if ((st = dalloc(ctx, &d.arena, arena_bytes + 16, "alloc ftx arena")) == CG_OK &&
+      (st = upload(ctx, &d.comp_off, comp_off, n_comp, "upload comp_off")) == CG_OK &&
+      (st = upload(ctx, &d.comp_len, comp_len, n_comp, "upload comp_len")) == CG_OK &&
+      (st = upload(ctx, &d.comp_start, comp_start, n_ftx + 1, "upload comp_start")) == CG_OK &&
+      (st = upload(ctx, &nonces_d, (const uint32_t*)nonces, 8 * n_comp, "upload nonces")) == CG_OK &&
+      (st = dalloc(ctx, &d.comp_tx, n_comp, "alloc comp_tx")) == CG_OK &&
+      (st = dalloc(ctx, &d.leaves, 8 * n_comp, "alloc leaves")) == CG_OK &&
+      (st = upload(ctx, &node_start_d, node_start, n_ftx + 1, "upload node_start")) == CG_OK &&
+      (st = upload(ctx, &kind_d, node_kind, n_node, "upload node_kind")) == CG_OK &&
+      (st = upload(ctx, &node_hash_d, (const uint32_t*)node_hash, 8 * n_node, "upload node_hash")) == CG_OK &&
+      (st = upload(ctx, &roots_d, (const uint32_t*)root_hashes, 8 * n_ftx, "upload roots")) == CG_OK &&
+      (st = upload(ctx, &status_d, status.data(), n_ftx, "upload status")) == CG_OK &&
+      (st = dalloc(ctx, &stack_d, (size_t)8 * depth * n_ftx, "alloc pmt stack")) == CG_OK) {
+    hipError_t e = arena_bytes ? hipMemcpyAsync(d.arena, arena, arena_bytes, hipMemcpyHostToDevice, ctx->stream)
+                               : hipSuccess;
+    if (e == hipSuccess) e = hipMemsetAsync(d.arena + arena_bytes, 0, 16, ctx->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(ctx->err_flag, 0, 4, ctx->stream);
+    if (e == hipSuccess)
+      e = cg::launch_tx_index(d.comp_start, nullptr, (uint32_t)n_ftx, d.comp_tx, nullptr, nullptr, ctx->stream);
+    if (e == hipSuccess) {
+      Timed tm(ctx, "merkle_leaf", n_comp);
+      e = cg::launch_merkle_leaf(d.arena, arena_bytes, d.comp_off, d.comp_len, d.comp_start, d.comp_tx, nullptr,
+                                 nonces_d, 0, (uint32_t)n_comp, d.leaves, ctx->err_flag, ctx->stream);
+    }
+    if (e == hipSuccess) {
+      Timed tm(ctx, "pmt_eval", n_ftx);
+      e = cg::launch_pmt_eval(node_start_d, kind_d, node_hash_d, d.comp_start, d.leaves, roots_d, (uint32_t)n_ftx,
+                              stack_d, status_d, ctx->stream);
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(result_out, status_d, n_ftx, hipMemcpyDeviceToHost, ctx->stream);
+    if (e != hipSuccess) st = hip_fail(ctx, e, "ftx verify");
+  }
+  if (st == CG_OK) st = read_err_flag(ctx);
+  // txs whose root matched but whose included-leaf multiset is too large for one lane:
+  // compare sorted hash lists here (the hashes were computed on the device)
+  std::vector<uint32_t> big;
+  if (st == CG_OK)
+    for (size_t t = 0; t < n_ftx; ++t)
+      if (result_out[t] == cg::kPmtHostCheck) big.push_back((uint32_t)t);
+  for (uint32_t t : big) {
+    const uint32_t c0 = comp_start[t], k = comp_start[t + 1] - c0;
+    std::vector<uint32_t> lv(8 * (size_t)k);
+    hipError_t e = hipMemcpy(lv.data(), d.leaves + (size_t)8 * c0, 32 * (size_t)k, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) {
+      st = hip_fail(ctx, e, "download leaves");
+      break;
+    }
+    std::vector<std::array<uint8_t, 32>> a, b;
+    for (uint32_t c = 0; c < k; ++c) {
+      std::array<uint8_t, 32> h;
+      for (int q = 0; q < 8; ++q)
+        for (int y = 0; y < 4; ++y) h[4 * q + y] = (uint8_t)(lv[8 * (size_t)c + q] >> (24 - 8 * y));  // big-endian words
+      a.push_back(h);
+    }
+    for (uint32_t j = node_start[t]; j < node_start[t + 1]; ++j)
+      if (node_kind[j] == cg::kPmtIncluded) {
+        std::array<uint8_t, 32> h;
+        memcpy(h.data(), node_hash + 32 * (size_t)j, 32);
+        b.push_back(h);
+      }
+    std::sort(a.begin(), a.end(), hash_less);
+    std::sort(b.begin(), b.end(), hash_less);
+    result_out[t] = a == b ? cg::kPmtTrue : cg::kPmtFalse;
+  }
+  (void)hipStreamSynchronize(ctx->stream);
+  for (const void* p : {(const void*)nonces_d, (const void*)node_start_d, (const void*)node_hash_d,
+                        (const void*)roots_d, (const void*)stack_d, (const void*)kind_d, (const void*)status_d})
+    dfree(ctx, p);
+  d.release(ctx);
+  collect_timings(ctx);
+  return st;
 }
 
 }  // extern "C"

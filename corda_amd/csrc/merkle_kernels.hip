@@ -14,6 +14,11 @@
 //   cg_merkle_tree   one lane per tx: zero-hash padding done virtually on the first
 //                    level, pairwise reduction in place over the tx's leaves
 //   cg_first_bad     one lane per tx: first non-ACCEPT signature (a7)
+//   cg_pmt_eval      one lane per FilteredTransaction: the partial Merkle tree
+//                    (post-order node program) evaluated over a per-lane stack in
+//                    HBM scratch, root compare, multiset check of the included
+//                    leaves against the filtered components' hashes
+//                    (PartialMerkleTree.kt:130-155, MerkleTransaction.kt:173-178)
 #include "cg_kernels.h"
 #include "cg_merkle_api.h"
 #include "cg_sha256.h"
@@ -44,7 +49,8 @@ __global__ __launch_bounds__(256) void cg_merkle_leaf(const uint8_t* __restrict_
                                                       const uint32_t* __restrict__ comp_len,
                                                       const uint32_t* __restrict__ comp_start,
                                                       const uint32_t* __restrict__ comp_tx,
-                                                      const uint32_t* __restrict__ salts, uint32_t c_begin,
+                                                      const uint32_t* __restrict__ salts,
+                                                      const uint32_t* __restrict__ nonces, uint32_t c_begin,
                                                       uint32_t c_end, uint32_t* __restrict__ leaves,
                                                       uint32_t* __restrict__ err) {
   __shared__ uint32_t tails[256 * kTailWords];
@@ -52,7 +58,9 @@ __global__ __launch_bounds__(256) void cg_merkle_leaf(const uint8_t* __restrict_
   if (c >= c_end) return;
   const uint32_t t = comp_tx[c];
   const uint32_t i = c - comp_start[t];
-  const bool salt = c + 1 == comp_start[t + 1];  // the last component is the serialized privacy salt
+  // WireTransaction: the last component is the serialized privacy salt.  FilteredLeaves
+  // (nonces given): no salt, every component carries its nonce (MerkleTransaction.kt:23-27).
+  const bool salt = !nonces && c + 1 == comp_start[t + 1];
   const uint64_t off = comp_off[c];
   const uint32_t len = comp_len[c];
   if (off > arena_bytes || len > arena_bytes - off) {
@@ -63,6 +71,9 @@ __global__ __launch_bounds__(256) void cg_merkle_leaf(const uint8_t* __restrict_
   CG_UNROLL for (int d = 0; d < kTailWords; ++d) tb[d] = 0;
   if (salt) {
     tb[1] = 0x80u;  // no tail: padding right after ser_salt
+  } else if (nonces) {
+    CG_UNROLL for (int w = 0; w < 8; ++w) tb[1 + w] = nonces[(size_t)c * 8 + w];  // bytes in memory order
+    tb[9] = 0x80u;
   } else {
     uint32_t m[9], h[8];
     CG_UNROLL for (int w = 0; w < 8; ++w) m[w] = bswap32_(salts[(size_t)t * 8 + w]);
@@ -122,6 +133,84 @@ __global__ __launch_bounds__(256) void cg_first_bad(const uint8_t* __restrict__ 
   out[t] = r;
 }
 
+
+// Partial Merkle tree of FilteredTransaction t: nodes node_start[t] .. node_start[t+1]-1
+// in post-order, kind 0 IncludedLeaf / 1 Leaf (hash given) / 2 Node (hash of the two
+// subtrees just below it on the stack).  status[t] arrives as 0, or kPmtMalformed when
+// the host found the program is not one tree.  Result: kPmtTrue / kPmtFalse,
+// kPmtNoLeaves (MerkleTreeException), or kPmtHostCheck when the root matches but the
+// multiset comparison is too large for one lane (> kPmtMaxLane included leaves).
+__global__ __launch_bounds__(256) void cg_pmt_eval(const uint32_t* __restrict__ node_start,
+                                                   const uint8_t* __restrict__ node_kind,
+                                                   const uint32_t* __restrict__ node_hash,
+                                                   const uint32_t* __restrict__ comp_start,
+                                                   const uint32_t* __restrict__ leaves,
+                                                   const uint32_t* __restrict__ roots, uint32_t n,
+                                                   uint32_t* __restrict__ stack, uint8_t* __restrict__ status) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const uint32_t c0 = comp_start[t], k = comp_start[t + 1] - c0;
+  if (k == 0) {  // FilteredTransaction.verify checks this before touching the tree
+    status[t] = kPmtNoLeaves;
+    return;
+  }
+  if (status[t] == kPmtMalformed) return;
+  // stack slot d, word q of lane t at stack[(8 d + q) n + t]: coalesced across the wave
+  auto slot = [&](uint32_t d, int q) -> uint32_t& { return stack[((size_t)8 * d + q) * n + t]; };
+  const uint32_t j0 = node_start[t], j1 = node_start[t + 1];
+  uint32_t sp = 0, m = 0;
+  for (uint32_t j = j0; j < j1; ++j) {
+    if (node_kind[j] != kPmtNode) {
+      CG_UNROLL for (int q = 0; q < 8; ++q) slot(sp, q) = bswap32_(node_hash[(size_t)j * 8 + q]);
+      ++sp;
+      m += node_kind[j] == kPmtIncluded;
+    } else {
+      uint32_t msg[16], h[8];
+      CG_UNROLL for (int q = 0; q < 8; ++q) {
+        msg[q] = slot(sp - 2, q);
+        msg[8 + q] = slot(sp - 1, q);
+      }
+      sha256_words<64>(h, msg);  // SecureHash.hashConcat (SecureHash.kt:25)
+      CG_UNROLL for (int q = 0; q < 8; ++q) slot(sp - 2, q) = h[q];
+      --sp;
+    }
+  }
+  uint32_t diff = 0;
+  CG_UNROLL for (int q = 0; q < 8; ++q) diff |= slot(0, q) ^ bswap32_(roots[(size_t)t * 8 + q]);
+  // hashesToCheck.groupBy == usedHashes.groupBy, then verifyRoot == merkleRootHash: either
+  // failing gives false, so the root test can go first
+  if (diff || m != k) {
+    status[t] = kPmtFalse;
+    return;
+  }
+  if (m > kPmtMaxLane) {
+    status[t] = kPmtHostCheck;
+    return;
+  }
+  // multiset equality: |included| == |components| and every included hash occurs as
+  // often among the included leaves as among the component hashes
+  uint32_t ok = 1;
+  for (uint32_t j = j0; j < j1 && ok; ++j) {
+    if (node_kind[j] != kPmtIncluded) continue;
+    uint32_t x[8];
+    CG_UNROLL for (int q = 0; q < 8; ++q) x[q] = node_hash[(size_t)j * 8 + q];
+    uint32_t ni = 0, nc = 0;
+    for (uint32_t i = j0; i < j1; ++i) {
+      if (node_kind[i] != kPmtIncluded) continue;
+      uint32_t d = 0;
+      CG_UNROLL for (int q = 0; q < 8; ++q) d |= node_hash[(size_t)i * 8 + q] ^ x[q];
+      ni += d == 0;
+    }
+    for (uint32_t c = 0; c < k; ++c) {
+      uint32_t d = 0;
+      CG_UNROLL for (int q = 0; q < 8; ++q) d |= bswap32_(leaves[(size_t)(c0 + c) * 8 + q]) ^ x[q];
+      nc += d == 0;
+    }
+    ok = ni == nc;
+  }
+  status[t] = ok ? kPmtTrue : kPmtFalse;
+}
+
 inline dim3 grid_for(uint32_t n) { return dim3((n + 255) / 256); }
 
 }  // namespace
@@ -138,11 +227,11 @@ hipError_t launch_tx_index(const uint32_t* comp_start, const uint32_t* sig_start
 
 hipError_t launch_merkle_leaf(const uint8_t* arena, uint64_t arena_bytes, const uint64_t* comp_off,
                               const uint32_t* comp_len, const uint32_t* comp_start, const uint32_t* comp_tx,
-                              const uint32_t* salts, uint32_t c_begin, uint32_t c_end, uint32_t* leaves,
-                              uint32_t* err, hipStream_t s) {
+                              const uint32_t* salts, const uint32_t* nonces, uint32_t c_begin, uint32_t c_end,
+                              uint32_t* leaves, uint32_t* err, hipStream_t s) {
   if (c_end <= c_begin) return hipSuccess;
   hipLaunchKernelGGL(cg_merkle_leaf, grid_for(c_end - c_begin), dim3(256), 0, s, arena, arena_bytes, comp_off,
-                     comp_len, comp_start, comp_tx, salts, c_begin, c_end, leaves, err);
+                     comp_len, comp_start, comp_tx, salts, nonces, c_begin, c_end, leaves, err);
   return hipGetLastError();
 }
 
@@ -157,6 +246,15 @@ hipError_t launch_first_bad(const uint8_t* verdict, const uint32_t* sig_start, u
                             hipStream_t s) {
   if (n_tx == 0) return hipSuccess;
   hipLaunchKernelGGL(cg_first_bad, grid_for(n_tx), dim3(256), 0, s, verdict, sig_start, n_tx, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_pmt_eval(const uint32_t* node_start, const uint8_t* node_kind, const uint32_t* node_hash,
+                           const uint32_t* comp_start, const uint32_t* leaves, const uint32_t* roots, uint32_t n,
+                           uint32_t* stack, uint8_t* status, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(cg_pmt_eval, grid_for(n), dim3(256), 0, s, node_start, node_kind, node_hash, comp_start, leaves,
+                     roots, n, stack, status);
   return hipGetLastError();
 }
 

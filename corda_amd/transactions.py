@@ -4,6 +4,9 @@ mirroring Corda's transaction layer (Kerwong/corda @ 0.14):
 * ``WireTransaction.id`` = Merkle root of ``availableComponentHashes``
   (core/src/main/kotlin/net/corda/core/transactions/WireTransaction.kt:39,104;
   MerkleTransaction.kt:16-33,74-93; crypto/MerkleTree.kt:27-66)
+* ``FilteredTransaction.verify`` / ``PartialMerkleTree.verify`` — the non-validating
+  notary's check (transactions/MerkleTransaction.kt:140-178,
+  crypto/PartialMerkleTree.kt:44-156, NonValidatingNotaryFlow.kt:25-27)
 * ``TransactionWithSignatures.checkSignaturesAreValid`` — every signature over
   ``id.bytes``, in order, the first failure throws
   (transactions/TransactionWithSignatures.kt:58-62; DigitalSignature.kt:25 ->
@@ -118,3 +121,184 @@ def check_signatures_are_valid(ctx: _lib.Context, stxs: Sequence[SignedTx]) -> N
                 e.tx_index, e.sig_index = t, fb
                 raise
         base += len(s.sigs)
+
+
+# ---------------------------------------------------------------- filtered transactions
+ZERO_HASH = bytes(32)
+
+
+@dataclass(frozen=True)
+class IncludedLeaf:
+    """PartialMerkleTree.PartialTree.IncludedLeaf (PartialMerkleTree.kt:55)."""
+    hash: bytes
+
+
+@dataclass(frozen=True)
+class Leaf:
+    """PartialMerkleTree.PartialTree.Leaf (PartialMerkleTree.kt:56)."""
+    hash: bytes
+
+
+@dataclass(frozen=True)
+class Node:
+    """PartialMerkleTree.PartialTree.Node (PartialMerkleTree.kt:57)."""
+    left: object
+    right: object
+
+
+class PartialMerkleTree:
+    """net.corda.core.crypto.PartialMerkleTree (PartialMerkleTree.kt:44-157).  ``build``
+    is the sender side (structural: it only reads the hashes the full MerkleTree already
+    carries); verification of filtered transactions runs on the device
+    (``verify_filtered_batch``)."""
+
+    def __init__(self, root):
+        self.root = root
+
+    @staticmethod
+    def build(merkle_root, include_hashes: Sequence[bytes]) -> "PartialMerkleTree":
+        """PartialMerkleTree.build (PartialMerkleTree.kt:66-76).  ``merkle_root`` is a
+        full MerkleTree: objects with ``hash`` and, for nodes, ``left``/``right``."""
+        include = list(include_hashes)
+        if ZERO_HASH in include:
+            raise IllegalArgumentException("Zero hashes shouldn't be included in partial tree.")
+        PartialMerkleTree._check_full(merkle_root)
+        used: list[bytes] = []
+        tree = PartialMerkleTree._build(merkle_root, include, used)[1]
+        if len(include) != len(used):
+            raise MerkleTreeException("Some of the provided hashes are not in the tree.")
+        return PartialMerkleTree(tree)
+
+    @staticmethod
+    def _is_leaf(t) -> bool:
+        return getattr(t, "left", None) is None
+
+    @staticmethod
+    def _check_full(tree, level: int = 0) -> int:  # PartialMerkleTree.kt:79-89
+        if PartialMerkleTree._is_leaf(tree):
+            return level
+        l1 = PartialMerkleTree._check_full(tree.left, level + 1)
+        l2 = PartialMerkleTree._check_full(tree.right, level + 1)
+        if l1 != l2:
+            raise MerkleTreeException("Got not full binary tree.")
+        return l1
+
+    @staticmethod
+    def _build(root, include: list, used: list):  # PartialMerkleTree.kt:98-123
+        if PartialMerkleTree._is_leaf(root):
+            if root.hash in include:
+                used.append(root.hash)
+                return True, IncludedLeaf(root.hash)
+            return False, Leaf(root.hash)
+        lf, ln = PartialMerkleTree._build(root.left, include, used)
+        rf, rn = PartialMerkleTree._build(root.right, include, used)
+        if lf or rf:
+            return True, Node(ln, rn)
+        return False, Leaf(root.hash)
+
+    @staticmethod
+    def from_postorder(prog: Sequence[tuple[int, bytes]]) -> "PartialMerkleTree":
+        """Inverse of ``postorder`` (e.g. for a tree received as a node program)."""
+        st: list = []
+        for kind, h in prog:
+            if kind == 0:
+                st.append(IncludedLeaf(bytes(h)))
+            elif kind == 1:
+                st.append(Leaf(bytes(h)))
+            elif kind == 2 and len(st) >= 2:
+                r = st.pop()
+                st.append(Node(st.pop(), r))
+            else:
+                raise IllegalArgumentException("not a post-order partial tree program")
+        if len(st) != 1:
+            raise IllegalArgumentException("not a post-order partial tree program")
+        return PartialMerkleTree(st[0])
+
+    def postorder(self) -> list[tuple[int, bytes]]:
+        """The node program cg_ftx_verify_batch takes: (kind, hash) in post-order, kind 0
+        IncludedLeaf / 1 Leaf / 2 Node.  Iterative, so adversarially deep trees encode."""
+        out, stack = [], [(self.root, False)]
+        while stack:
+            node, seen = stack.pop()
+            if isinstance(node, IncludedLeaf):
+                out.append((0, node.hash))
+            elif isinstance(node, Leaf):
+                out.append((1, node.hash))
+            elif seen:
+                out.append((2, ZERO_HASH))
+            else:
+                stack += [(node, True), (node.right, False), (node.left, False)]
+        return out
+
+
+@dataclass
+class FilteredLeaves:
+    """FilteredLeaves (MerkleTransaction.kt:140-170): the visible components, serialized
+    (Kryo P2P no-refs bytes, availableComponents order), each with its nonce."""
+    components: list[bytes]
+    nonces: list[bytes]
+
+    def __post_init__(self):
+        if len(self.components) != len(self.nonces):  # MerkleTransaction.kt:153
+            raise IllegalArgumentException("Each visible component should be accompanied by a nonce.")
+        if any(len(n) != 32 for n in self.nonces):
+            raise IllegalArgumentException("nonces are 32-byte SecureHashes")
+
+
+@dataclass
+class FilteredTransaction:
+    """FilteredTransaction (MerkleTransaction.kt:179-209)."""
+    root_hash: bytes
+    filtered_leaves: FilteredLeaves
+    partial_merkle_tree: PartialMerkleTree
+
+    def verify(self, ctx: _lib.Context) -> bool:
+        """FilteredTransaction.verify (MerkleTransaction.kt:173-178) on the device."""
+        return verify_filtered(ctx, [self])[0]
+
+
+def _pack_ftxs(ftxs: Sequence[FilteredTransaction]):
+    comps = [c for f in ftxs for c in f.filtered_leaves.components]
+    comp_len = np.array([len(c) for c in comps] or [0], dtype=np.uint32)
+    comp_off = np.zeros(max(len(comps), 1), dtype=np.uint64)
+    if len(comps) > 1:
+        comp_off[1:len(comps)] = np.cumsum(comp_len[:len(comps) - 1], dtype=np.uint64)
+    comp_start = np.zeros(len(ftxs) + 1, dtype=np.uint32)
+    comp_start[1:] = np.cumsum([len(f.filtered_leaves.components) for f in ftxs])
+    arena = np.frombuffer(b"".join(comps) or b"\0", dtype=np.uint8).copy()
+    nonces = np.frombuffer(b"".join(n for f in ftxs for n in f.filtered_leaves.nonces) or bytes(32),
+                           dtype=np.uint8).copy()
+    progs = [f.partial_merkle_tree.postorder() for f in ftxs]
+    node_start = np.zeros(len(ftxs) + 1, dtype=np.uint32)
+    node_start[1:] = np.cumsum([len(p) for p in progs])
+    node_kind = np.array([k for p in progs for k, _ in p] or [0], dtype=np.uint8)
+    node_hash = np.frombuffer(b"".join(h for p in progs for _, h in p) or bytes(32), dtype=np.uint8).copy()
+    if any(len(f.root_hash) != 32 for f in ftxs):
+        raise IllegalArgumentException("rootHash must be a 32-byte SecureHash")
+    roots = np.frombuffer(b"".join(f.root_hash for f in ftxs), dtype=np.uint8).copy()
+    return arena, comp_off, comp_len, comp_start, nonces, node_start, node_kind, node_hash, roots
+
+
+def verify_filtered_batch(ctx: _lib.Context, ftxs: Sequence[FilteredTransaction]) -> np.ndarray:
+    """FilteredTransaction.verify for every tx in one device batch; per tx one of
+    FTX_TRUE / FTX_FALSE / FTX_NO_LEAVES (verify() would throw MerkleTreeException) /
+    FTX_MALFORMED."""
+    if not ftxs:
+        return np.zeros(0, dtype=np.uint8)
+    a = _pack_ftxs(ftxs)
+    out = np.zeros(len(ftxs), dtype=np.uint8)
+    ctx.check(ctx.lib.cg_ftx_verify_batch(ctx.h, len(ftxs), _lib.ptr(a[0]), len(a[0]), *(_lib.ptr(x) for x in a[1:]),
+                                          _lib.ptr(out)))
+    return out
+
+
+def verify_filtered(ctx: _lib.Context, ftxs: Sequence[FilteredTransaction]) -> list[bool]:
+    """A loop of ``ftx.verify()``: raises MerkleTreeException where the first such tx
+    would, returns the Boolean results otherwise."""
+    res = verify_filtered_batch(ctx, ftxs)
+    for t, r in enumerate(res):
+        if r == _lib.FTX_NO_LEAVES:
+            raise MerkleTreeException("Transaction without included leaves.")
+        if r == _lib.FTX_MALFORMED:
+            raise IllegalArgumentException(f"filtered transaction {t}: partial tree is not a single tree")
+    return [bool(r == _lib.FTX_TRUE) for r in res]

@@ -33,6 +33,13 @@
  *       SignedTransaction signature loop: TransactionWithSignatures.checkSignaturesAreValid
  *       core/.../transactions/TransactionWithSignatures.kt:58-62 (in order, first
  *       failure wins), over ids recomputed as cg_txid_batch does.
+ *   cg_ftx_verify_batch
+ *       a loop of FilteredTransaction.verify() — the non-validating notary's check
+ *       (node/.../transactions/NonValidatingNotaryFlow.kt:25-27):
+ *       core/.../transactions/MerkleTransaction.kt:173-178 (FilteredLeaves hashes with
+ *       the given nonces, MerkleTransaction.kt:23-27,153) and
+ *       core/.../crypto/PartialMerkleTree.kt:130-155 (root of the partial tree, multiset
+ *       of included leaves == filtered component hashes).
  *
  * Verdict codes (one byte per element) map to the JVM outcomes:
  *   CG_ACCEPT          isValid -> true / doVerify returns true
@@ -175,6 +182,24 @@ cg_status cg_tx_verify_batch(cg_ctx* ctx, int mode, size_t n_tx, const uint8_t* 
                              uint8_t* ids_out);
 
 /*
+ * FilteredTransaction batch (non-validating notary).  n_ftx filtered transactions.
+ * Filtered leaves of tx t: components comp_start[t] .. comp_start[t+1]-1 (n_ftx + 1
+ * entries), serialized bytes at arena[comp_off[c] .. + comp_len[c]) in availableComponents
+ * order, each with its 32-byte nonce at nonces[32 c] (FilteredLeaves.nonces).
+ * Partial Merkle tree of tx t: nodes node_start[t] .. node_start[t+1]-1 (n_ftx + 1 entries)
+ * in post-order (left subtree, right subtree, then the node): node_kind[j] = 0 IncludedLeaf,
+ * 1 Leaf, 2 Node; node_hash[32 j] is the leaf's SecureHash (ignored for a Node).
+ * root_hashes: FilteredTransaction.rootHash, 32 bytes per tx.
+ * result_out (n_ftx bytes): CG_FTX_TRUE / CG_FTX_FALSE = what verify() returns;
+ * CG_FTX_NO_LEAVES = it throws MerkleTreeException("Transaction without included leaves.");
+ * CG_FTX_MALFORMED = the node program is not a single tree (no such PartialTree object exists).
+ */
+enum { CG_FTX_TRUE = 0, CG_FTX_FALSE = 1, CG_FTX_NO_LEAVES = 2, CG_FTX_MALFORMED = 3 };
+cg_status cg_ftx_verify_batch(cg_ctx* ctx, size_t n_ftx, const uint8_t* arena, size_t arena_bytes,
+                              const uint64_t* comp_off, const uint32_t* comp_len, const uint32_t* comp_start,
+                              const uint8_t* nonces, const uint32_t* node_start, const uint8_t* node_kind,
+                              const uint8_t* node_hash, const uint8_t* root_hashes, uint8_t* result_out);
+/*
  * Host-memory registration (optional).  Page-locks [ptr, ptr + bytes) for the
  * device so later uploads from that range run at full PCIe DMA rate instead of
  * through the runtime's pageable staging copy.  Meant for buffers a caller reuses
@@ -189,9 +214,9 @@ cg_status cg_release_cached(cg_ctx* ctx);
 
 /*
  * Per-kernel device timing (HIP events on the context's stream), accumulated while
- * profiling is enabled.  Names: "ed25519_prep", "ed25519_msm", "ecdsa_k1_prep",
- * "ecdsa_k1_msm", "ecdsa_r1_prep", "ecdsa_r1_msm", "der_parse", "merkle_leaf",
- * "merkle_tree", "stage".
+ * profiling is enabled.  Names: "ed25519_hash", "ed25519_points", "ed25519_msm",
+ * "ecdsa_k1_prep", "ecdsa_k1_msm", "ecdsa_r1_prep", "ecdsa_r1_msm", "der_parse",
+ * "merkle_leaf", "merkle_tree", "pmt_eval", "stage".
  */
 cg_status cg_set_profiling(cg_ctx* ctx, int enable);
 cg_status cg_kernel_stats(cg_ctx* ctx, const char* kernel, double* total_ms, uint64_t* launches,

@@ -25,6 +25,63 @@ void oracle_sha512(const uint8_t* p, size_t n, uint8_t out[64]) {
 
 static int is_pow2(uint32_t n) { return (n & (n - 1)) == 0; }
 
+static int cmp_hash(const void* a, const void* b) { return memcmp(a, b, 32); }
+
+/* FilteredTransaction.verify for a batch, same flat layout as cg_ftx_verify_batch:
+ * MerkleTransaction.kt:173-178 (no hashes -> MerkleTreeException = 2; leaf hashes
+ * SHA256(ser || nonce), MerkleTransaction.kt:23-27,153) and PartialMerkleTree.kt:130-155
+ * (the post-order program evaluated with an explicit stack; multiset equality by
+ * sorting; root compare).  3 = the program is not one tree. */
+int oracle_ftx_verify_batch(const uint8_t* arena, const uint64_t* comp_off, const uint32_t* comp_len,
+                            const uint32_t* comp_start, const uint8_t* nonces, const uint32_t* node_start,
+                            const uint8_t* node_kind, const uint8_t* node_hash, const uint8_t* roots, size_t n_ftx,
+                            uint8_t* result) {
+  for (size_t t = 0; t < n_ftx; ++t) {
+    const uint32_t c0 = comp_start[t], k = comp_start[t + 1] - c0;
+    const uint32_t j0 = node_start[t], nn = node_start[t + 1] - j0;
+    if (k == 0) { result[t] = 2; continue; }
+    uint8_t* stack = (uint8_t*)malloc(32 * (size_t)(nn + 1));
+    uint8_t* used = (uint8_t*)malloc(32 * (size_t)(nn + 1));
+    uint8_t* hashes = (uint8_t*)malloc(32 * (size_t)k);
+    size_t sp = 0, nu = 0;
+    int bad = nn == 0;
+    for (uint32_t j = j0; j < j0 + nn && !bad; ++j) {
+      const uint8_t kind = node_kind[j];
+      if (kind == 0 || kind == 1) {
+        memcpy(stack + 32 * sp++, node_hash + 32 * (size_t)j, 32);
+        if (kind == 0) memcpy(used + 32 * nu++, node_hash + 32 * (size_t)j, 32);
+      } else if (kind == 2 && sp >= 2) {
+        or_sha256(stack + 32 * (sp - 2), 64, stack + 32 * (sp - 2));
+        --sp;
+      } else {
+        bad = 1;
+      }
+    }
+    if (bad || sp != 1) {
+      result[t] = 3;
+    } else {
+      for (uint32_t i = 0; i < k; ++i) {
+        or_sha256_ctx c;
+        or_sha256_init(&c);
+        or_sha256_update(&c, arena + comp_off[c0 + i], comp_len[c0 + i]);
+        or_sha256_update(&c, nonces + 32 * (size_t)(c0 + i), 32);
+        or_sha256_final(&c, hashes + 32 * (size_t)i);
+      }
+      int same = nu == k;
+      if (same) {
+        qsort(hashes, k, 32, cmp_hash);
+        qsort(used, nu, 32, cmp_hash);
+        same = memcmp(hashes, used, 32 * (size_t)k) == 0;
+      }
+      result[t] = (same && memcmp(stack, roots + 32 * t, 32) == 0) ? 0 : 1;
+    }
+    free(stack);
+    free(used);
+    free(hashes);
+  }
+  return 0;
+}
+
 int oracle_txid_batch(const uint8_t* arena, const uint64_t* comp_off, const uint32_t* comp_len,
                       const uint32_t* comp_start, const uint8_t* salts, size_t n_tx, uint8_t* ids_out) {
   int rc = 0;

@@ -36,6 +36,10 @@ void oracle_sha512(const uint8_t* p, size_t n, uint8_t out[64]);
  * [comp_start[t], comp_start[t+1]) into (arena, comp_off, comp_len); the last
  * component of each tx is the serialized privacy salt; salts are 32 B each.
  * Returns 0, or -1 if some tx has no component (MerkleTreeException). */
+int oracle_ftx_verify_batch(const uint8_t* arena, const uint64_t* comp_off, const uint32_t* comp_len,
+                            const uint32_t* comp_start, const uint8_t* nonces, const uint32_t* node_start,
+                            const uint8_t* node_kind, const uint8_t* node_hash, const uint8_t* roots, size_t n_ftx,
+                            uint8_t* result);
 int oracle_txid_batch(const uint8_t* arena, const uint64_t* comp_off, const uint32_t* comp_len,
                       const uint32_t* comp_start, const uint8_t* salts, size_t n_tx, uint8_t* ids_out);
 

@@ -37,6 +37,7 @@ def oracle():
     lib.oracle_ecdsa_verify.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p, sz, ctypes.c_char_p, sz,
                                         ctypes.c_int]
     lib.oracle_txid_batch.argtypes = [vp, vp, vp, vp, vp, sz, vp]
+    lib.oracle_ftx_verify_batch.argtypes = [vp] * 9 + [sz, vp]
     return lib
 
 
@@ -58,6 +59,11 @@ def golden_ecdsa():
 @pytest.fixture(scope="session")
 def golden_merkle():
     return load_golden("merkle_golden.json")
+
+
+@pytest.fixture(scope="session")
+def golden_ftx():
+    return load_golden("ftx_golden.json")
 
 
 @pytest.fixture(scope="session")

@@ -30,6 +30,7 @@ import merkle_tx as MK  # noqa: E402
 import openssl_xcheck as OSSL  # noqa: E402
 
 ORACLE = ctypes.CDLL(os.path.join(ROOT, "oracle", "liboracle.so"))
+ORACLE.oracle_ftx_verify_batch.argtypes = [ctypes.c_void_p] * 9 + [ctypes.c_size_t, ctypes.c_void_p]
 
 RFC8032 = [  # (secret, public, message, signature) — RFC 8032 §7.1 TEST 1..3
     ("9d61b19deffd5a60ba844af492ec2cc44449c5697b326919703bac031cae7f60",
@@ -315,7 +316,115 @@ def merkle_cases():
     return {"txs": txs, "roots": roots}
 
 
+# ------------------------------------------------------- FilteredTransaction
+def _ftx_row(cls, comps, nonces, prog, root, result):
+    return {"cls": cls, "components": [c.hex() for c in comps], "nonces": [n.hex() for n in nonces],
+            "program": [[k, h.hex()] for k, h in prog], "root": root.hex(), "result": result}
+
+
+def _ftx_expected(comps, nonces, prog, root):
+    tree = MK.pmt_from_postorder(prog)
+    if not comps:
+        return 2
+    if tree is None:
+        return 3
+    return 0 if MK.ftx_verify(comps, nonces, tree, root) else 1
+
+
+def ftx_cases():
+    """FilteredTransaction.verify fixtures: the PartialMerkleTreeTest.kt:159-230 cases
+    recast as filtered transactions (components + nonces whose leaf hashes are the
+    test's `hashed`), plus adversarial node programs."""
+    rnd = random.Random(77)
+    header = b"corda\x00\x00\x01"
+    salt = rnd.randbytes(32)
+    comps = [header + bytes([ord(ch)]) + rnd.randbytes(rnd.randint(20, 300)) for ch in "abcdef"]
+    nonces = [MK.compute_nonce(salt, i) for i in range(6)]
+    hashed = [MK.filtered_leaf_hash(c, n) for c, n in zip(comps, nonces)]
+    mt = MK.get_merkle_tree(hashed)
+    rows = []
+
+    def add(cls, idx, tree, root, comp_override=None):
+        cs = comp_override if comp_override is not None else [comps[i] for i in idx]
+        ns = [nonces[i] for i in idx]
+        prog = MK.pmt_postorder(tree) if not isinstance(tree, list) else tree
+        rows.append(_ftx_row(cls, cs, ns, prog, root, _ftx_expected(cs, ns, prog, root)))
+
+    t35 = MK.pmt_build(mt, [hashed[3], hashed[5]])
+    add("only_left_branch", [3, 5], t35, mt.hash)
+    add("order_swapped", [5, 3], t35, mt.hash)
+    add("include_zero_leaves", [], MK.pmt_build(mt, []), mt.hash)
+    add("include_all", range(6), MK.pmt_build(mt, hashed), mt.hash)
+    add("too_many_leaves", [3, 5, 0], t35, mt.hash)
+    add("too_little_leaves", [3, 5], MK.pmt_build(mt, [hashed[3], hashed[5], hashed[0]]), mt.hash)
+    mt5 = MK.get_merkle_tree(hashed[:5])
+    add("duplicate_leaves", [3, 4, 4], MK.pmt_build(mt5, [hashed[3], hashed[4]]), mt5.hash)
+    add("different_leaves", [2, 4], t35, mt.hash)
+    add("wrong_root", [3, 5], t35, MK.sha256(hashed[3] + hashed[5]))
+    add("same_count_other_multiset", [3, 3], t35, mt.hash)
+    tampered = bytearray(comps[5]); tampered[9] ^= 1
+    add("tampered_component", [3, 5], t35, mt.hash, [comps[3], bytes(tampered)])
+    add("single_leaf_tree", [2], MK.PTIncluded(hashed[2]), hashed[2])
+    add("malformed_node_only", [3], [(2, MK.ZERO_HASH)], mt.hash)
+    add("malformed_two_roots", [3], [(0, hashed[3]), (1, hashed[4])], mt.hash)
+    add("malformed_empty", [3], [], mt.hash)
+    add("malformed_bad_kind", [3], [(7, hashed[3])], mt.hash)
+    add("no_leaves_beats_malformed", [], [(2, MK.ZERO_HASH)], mt.hash)
+    # identical leaves (PartialMerkleTreeTest.kt:185-190 "aaa")
+    same = [comps[0]] * 3
+    hs = [MK.filtered_leaf_hash(c, nonces[0]) for c in same]
+    mta = MK.get_merkle_tree(hs)
+    ta = MK.pmt_build(mta, hs)
+    rows.append(_ftx_row("identical_leaves_all", same, [nonces[0]] * 3, MK.pmt_postorder(ta), mta.hash,
+                         _ftx_expected(same, [nonces[0]] * 3, MK.pmt_postorder(ta), mta.hash)))
+    rows.append(_ftx_row("identical_leaves_fewer", same[:2], [nonces[0]] * 2, MK.pmt_postorder(ta), mta.hash,
+                         _ftx_expected(same[:2], [nonces[0]] * 2, MK.pmt_postorder(ta), mta.hash)))
+    # a deep chain (adversarial shape, depth 40): root computed along the chain
+    tree, root = MK.PTIncluded(hashed[1]), hashed[1]
+    for d in range(40):
+        sib = rnd.randbytes(32)
+        tree, root = (MK.PTNode(tree, MK.PTLeaf(sib)), MK.sha256(root + sib)) if d % 2 else \
+            (MK.PTNode(MK.PTLeaf(sib), tree), MK.sha256(sib + root))
+    add("deep_chain_40", [1], tree, root)
+    # more included leaves than one lane compares (the library's host multiset path)
+    big_c = [header + rnd.randbytes(40) for _ in range(300)]
+    big_n = [MK.compute_nonce(salt, i) for i in range(300)]
+    big_h = [MK.filtered_leaf_hash(c, n) for c, n in zip(big_c, big_n)]
+    mtb = MK.get_merkle_tree(big_h)
+    pb = MK.pmt_postorder(MK.pmt_build(mtb, big_h))
+    rows.append(_ftx_row("many_leaves_300", big_c, big_n, pb, mtb.hash, _ftx_expected(big_c, big_n, pb, mtb.hash)))
+    swap_c = list(big_c); swap_c[7] = big_c[8]
+    swap_n = list(big_n); swap_n[7] = big_n[8]
+    rows.append(_ftx_row("many_leaves_300_other_multiset", swap_c, swap_n, pb, mtb.hash,
+                         _ftx_expected(swap_c, swap_n, pb, mtb.hash)))
+    # cross-check with the C oracle
+    for r in rows:
+        cs = [bytes.fromhex(c) for c in r["components"]]
+        arena = b"".join(cs) or b"\0"
+        offs, o = [], 0
+        for c in cs:
+            offs.append(o); o += len(c)
+        prog = r["program"]
+        out = ctypes.create_string_buffer(1)
+        ORACLE.oracle_ftx_verify_batch(arena, (ctypes.c_uint64 * max(1, len(cs)))(*offs),
+                                       (ctypes.c_uint32 * max(1, len(cs)))(*[len(c) for c in cs]),
+                                       (ctypes.c_uint32 * 2)(0, len(cs)),
+                                       b"".join(bytes.fromhex(n) for n in r["nonces"]) or bytes(32),
+                                       (ctypes.c_uint32 * 2)(0, len(prog)), bytes([k for k, _ in prog]) or b"\0",
+                                       b"".join(bytes.fromhex(h) for _, h in prog) or bytes(32),
+                                       bytes.fromhex(r["root"]), 1, out)
+        assert out.raw[0] == r["result"], r["cls"]
+    return rows
+
+
 def main():
+    if "--only-ftx" in sys.argv:
+        fx = ftx_cases()
+        with open(os.path.join(HERE, "ftx_golden.json"), "w") as f:
+            json.dump(fx, f, indent=0)
+        from collections import Counter
+        print("ftx", len(fx), Counter(r["result"] for r in fx))
+        return
     ed = ed25519_cases()
     with open(os.path.join(HERE, "ed25519_golden.json"), "w") as f:
         json.dump(ed, f, indent=0)
@@ -329,6 +438,9 @@ def main():
     print("ed25519", len(ed), Counter(c["is_valid"] for c in ed))
     print("ecdsa", len(ec), Counter(c["is_valid"] for c in ec))
     print("merkle", len(mk["txs"]))
+    fx = ftx_cases()
+    with open(os.path.join(HERE, "ftx_golden.json"), "w") as f:
+        json.dump(fx, f, indent=0)
 
 
 if __name__ == "__main__":

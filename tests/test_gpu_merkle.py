@@ -136,3 +136,59 @@ def test_comp_start_offset_and_registered_buffers(gpu_ctx, oracle):
     finally:
         gpu_ctx.unregister_host(w.arena, comp_off, comp_len, cs, w.salts, ids)
     assert np.array_equal(ids, oracle_ids(oracle, w))
+
+
+# ------------------------------------------------------------------ FilteredTransaction.verify
+def _ftx_call(ctx, a, n):
+    out = np.full(n, 0xEE, dtype=np.uint8)
+    ctx.check(ctx.lib.cg_ftx_verify_batch(ctx.h, n, ptr(a[0]), len(a[0]), *(ptr(x) for x in a[1:]), ptr(out)))
+    return out
+
+
+@pytest.mark.gpu
+def test_ftx_golden(gpu_ctx, golden_ftx):
+    """Every FilteredTransaction fixture (PartialMerkleTreeTest.kt cases recast, deep
+    chain, > 256 included leaves, malformed programs) in one device batch, then each
+    row alone (no cross-row state)."""
+    from test_oracle import _ftx_flat
+    exp = [r["result"] for r in golden_ftx]
+    assert _ftx_call(gpu_ctx, _ftx_flat(golden_ftx), len(golden_ftx)).tolist() == exp
+    for r in golden_ftx:
+        assert _ftx_call(gpu_ctx, _ftx_flat([r]), 1).tolist() == [r["result"]], r["cls"]
+
+
+@pytest.mark.gpu
+def test_ftx_python_mirror(gpu_ctx, golden_ftx):
+    """FilteredTransaction.verify through the Python mirror: True/False, and
+    MerkleTreeException for a tx without included leaves."""
+    from corda_amd.crypto import IllegalArgumentException
+    ftxs = []
+    for r in golden_ftx:
+        try:
+            pmt = T.PartialMerkleTree.from_postorder([(k, bytes.fromhex(h)) for k, h in r["program"]])
+        except IllegalArgumentException:  # no PartialMerkleTree object exists for this program
+            assert r["result"] in (2, 3)
+            continue
+        ftxs.append((r, T.FilteredTransaction(bytes.fromhex(r["root"]), T.FilteredLeaves(
+            [bytes.fromhex(c) for c in r["components"]], [bytes.fromhex(n) for n in r["nonces"]]), pmt)))
+    for r, f in ftxs:
+        if r["result"] == 2:
+            with pytest.raises(T.MerkleTreeException):
+                f.verify(gpu_ctx)
+        else:
+            assert f.verify(gpu_ctx) == (r["result"] == 0), r["cls"]
+    res = T.verify_filtered_batch(gpu_ctx, [f for _, f in ftxs])
+    assert res.tolist() == [r["result"] for r, _ in ftxs]
+
+
+@pytest.mark.gpu
+def test_ftx_notary_shapes_vs_oracle(gpu_ctx, oracle):
+    """Config-4 transactions filtered as NotaryFlow.kt:72 does (inputs + time window),
+    tiled with 5 % adversarial copies, against the C oracle and the generator's truth."""
+    w = datagen.tile_ftx_batch(datagen.make_ftx_batch(3000, seed=21), 20000, adversarial=0.05, seed=3)
+    a = (w.arena, w.comp_off, w.comp_len, w.comp_start, w.nonces, w.node_start, w.node_kind, w.node_hash, w.roots)
+    got = _ftx_call(gpu_ctx, a, w.n)
+    exp = np.zeros(w.n, dtype=np.uint8)
+    oracle.oracle_ftx_verify_batch(*(x.ctypes.data for x in a), w.n, exp.ctypes.data)
+    assert np.array_equal(exp, w.expected)
+    assert np.array_equal(got, exp)

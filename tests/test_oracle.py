@@ -153,3 +153,72 @@ def test_merkle_structure_like_reference():
 def test_merkle_nonce_is_big_endian_index():
     salt = bytes(range(32))
     assert MK.compute_nonce(salt, 1) == hashlib.sha256(salt + b"\0\0\0\1").digest()
+
+
+def _ftx_flat(rows):
+    """Flat cg_ftx_verify_batch / oracle_ftx_verify_batch arrays for fixture rows."""
+    comps = [bytes.fromhex(c) for r in rows for c in r["components"]]
+    arena = np.frombuffer(b"".join(comps) + b"\0", dtype=np.uint8).copy()
+    offs = np.cumsum([0] + [len(c) for c in comps]).astype(np.uint64)
+    lens = np.array([len(c) for c in comps] or [0], dtype=np.uint32)
+    cstart = np.cumsum([0] + [len(r["components"]) for r in rows]).astype(np.uint32)
+    nonces = np.frombuffer(b"".join(bytes.fromhex(n) for r in rows for n in r["nonces"]) + bytes(32),
+                           dtype=np.uint8).copy()
+    nstart = np.cumsum([0] + [len(r["program"]) for r in rows]).astype(np.uint32)
+    kinds = np.array([k for r in rows for k, _ in r["program"]] + [0], dtype=np.uint8)
+    hashes = np.frombuffer(b"".join(bytes.fromhex(h) for r in rows for _, h in r["program"]) + bytes(32),
+                           dtype=np.uint8).copy()
+    roots = np.frombuffer(b"".join(bytes.fromhex(r["root"]) for r in rows), dtype=np.uint8).copy()
+    return arena, offs, lens, cstart, nonces, nstart, kinds, hashes, roots
+
+
+def test_ftx_golden_c_oracle(oracle, golden_ftx):
+    """FilteredTransaction.verify fixtures (PartialMerkleTreeTest.kt:159-230 recast +
+    adversarial programs): the C restatement, all rows in one batch."""
+    a = _ftx_flat(golden_ftx)
+    out = np.zeros(len(golden_ftx), dtype=np.uint8)
+    oracle.oracle_ftx_verify_batch(*(x.ctypes.data for x in a), len(golden_ftx), out.ctypes.data)
+    assert out.tolist() == [r["result"] for r in golden_ftx]
+
+
+def test_ftx_golden_python_twin(golden_ftx):
+    for r in golden_ftx:
+        comps = [bytes.fromhex(c) for c in r["components"]]
+        nonces = [bytes.fromhex(n) for n in r["nonces"]]
+        tree = MK.pmt_from_postorder([(k, bytes.fromhex(h)) for k, h in r["program"]])
+        if not comps:
+            with pytest.raises(MK.MerkleTreeException):
+                MK.ftx_verify(comps, nonces, tree, bytes.fromhex(r["root"]))
+            assert r["result"] == 2
+        elif tree is None:
+            assert r["result"] == 3
+        else:
+            assert MK.ftx_verify(comps, nonces, tree, bytes.fromhex(r["root"])) == (r["result"] == 0), r["cls"]
+
+
+def test_partial_merkle_build_like_reference():
+    """PartialMerkleTreeTest.kt:86-96,159-190 through the product's (structural)
+    PartialMerkleTree.build, against the oracle's restatement."""
+    from corda_amd.crypto import IllegalArgumentException
+    from corda_amd.transactions import MerkleTreeException, PartialMerkleTree
+    hashed = [MK.sha256(bytes([c])) for c in b"abcdef"]
+    mt = MK.get_merkle_tree(hashed)
+    for incl in ([hashed[3], hashed[5]], [], hashed, [hashed[0]]):
+        assert PartialMerkleTree.build(mt, incl).postorder() == MK.pmt_postorder(MK.pmt_build(mt, incl))
+    with pytest.raises(MerkleTreeException):  # duplicate leaves failure
+        PartialMerkleTree.build(mt, [hashed[3], hashed[5], hashed[3], hashed[5]])
+    aaa = [MK.sha256(b"a")] * 3
+    with pytest.raises(MerkleTreeException):  # only duplicate leaves, less included
+        PartialMerkleTree.build(MK.get_merkle_tree(aaa), aaa[:1])
+    with pytest.raises(IllegalArgumentException):
+        PartialMerkleTree.build(mt, [MK.ZERO_HASH])
+    h = hashed[0]
+    right = MK.MTNode(h, MK.MTLeaf(h), MK.MTLeaf(h))
+    left = MK.MTNode(h, MK.MTNode(h, MK.MTLeaf(h), MK.MTLeaf(h)), MK.MTNode(h, MK.MTLeaf(h), MK.MTLeaf(h)))
+    with pytest.raises(MerkleTreeException):  # check full tree
+        PartialMerkleTree.build(MK.MTNode(h, left, right), [h])
+    PartialMerkleTree.build(right, [h, h])
+    PartialMerkleTree.build(MK.MTLeaf(h), [h])
+    # the post-order program round-trips through the oracle's decoder
+    t = MK.pmt_build(mt, [hashed[1], hashed[4]])
+    assert MK.pmt_postorder(MK.pmt_from_postorder(MK.pmt_postorder(t))) == MK.pmt_postorder(t)

@@ -239,15 +239,9 @@ class TxWorkload:
         self.__dict__.update(kw)
 
 
-def make_tx_batch(n_tx: int, seed: int = 4, key_base: int = 9_000_000, threads: int | None = None,
-                  tamper_frac: float = 0.01) -> TxWorkload:
-    """Trader-demo / loadtest shapes (SURVEY §8d config 4): inputs U{0..3},
-    attachments U{0..1}, outputs U{1..3}, commands U{1..2}, notary 1,
-    timeWindow p=0.3, salt 1; estimated Kryo sizes; signers = distinct command
-    signers (+ notary when inputs > 0 or a time window); schemes 70/15/15 %
-    Ed25519/R1/K1; signatures over the tx id; tamper_frac of txs get one leaf byte
-    flipped after signing (their id changes, so every signature rejects)."""
-    rng = np.random.default_rng(seed)
+def _tx_components(n_tx: int, rng, seed: int):
+    """Component layout of config-4 transactions (shared by the SignedTransaction and
+    the FilteredTransaction workloads)."""
     c = lib()
     n_in = rng.integers(0, 4, n_tx); n_att = rng.integers(0, 2, n_tx); n_out = rng.integers(1, 4, n_tx)
     n_cmd = rng.integers(1, 3, n_tx); has_tw = rng.random(n_tx) < 0.3
@@ -275,6 +269,21 @@ def make_tx_batch(n_tx: int, seed: int = 4, key_base: int = 9_000_000, threads: 
         np.frombuffer(HEADER, dtype=np.uint8), len(comp_off))
     salts = np.empty(32 * n_tx, dtype=np.uint8)
     c.dg_fill_bytes(salts.ctypes.data, len(salts), seed * 1000 + 2)
+    return n_in, n_att, n_out, n_cmd, has_tw, arena, comp_off, comp_len, comp_start, salts
+
+
+def make_tx_batch(n_tx: int, seed: int = 4, key_base: int = 9_000_000, threads: int | None = None,
+                  tamper_frac: float = 0.01) -> TxWorkload:
+    """Trader-demo / loadtest shapes (SURVEY §8d config 4): inputs U{0..3},
+    attachments U{0..1}, outputs U{1..3}, commands U{1..2}, notary 1,
+    timeWindow p=0.3, salt 1; estimated Kryo sizes; signers = distinct command
+    signers (+ notary when inputs > 0 or a time window); schemes 70/15/15 %
+    Ed25519/R1/K1; signatures over the tx id; tamper_frac of txs get one leaf byte
+    flipped after signing (their id changes, so every signature rejects)."""
+    rng = np.random.default_rng(seed)
+    c = lib()
+    (n_in, n_att, n_out, n_cmd, has_tw, arena, comp_off, comp_len, comp_start,
+     salts) = _tx_components(n_tx, rng, seed)
     ids = np.zeros(32 * n_tx, dtype=np.uint8)
     assert c.dg_txid_batch(arena.ctypes.data, comp_off.ctypes.data, comp_len.ctypes.data, comp_start.ctypes.data,
                            salts.ctypes.data, n_tx, ids.ctypes.data) == 0
@@ -327,4 +336,110 @@ def tile_tx_batch(w: TxWorkload, n_tx: int, tamper_frac: float = 0.01, seed: int
     t.tampered = rng.random(n_tx) < tamper_frac
     first = t.comp_start[:-1][t.tampered]
     t.arena[t.comp_off[first] + 8] ^= 1  # first component, past the Kryo header
+    return t
+
+
+# ------------------------------------------------------------ FilteredTransactions
+class FtxWorkload:
+    """FilteredTransaction batch in the cg_ftx_verify_batch layout."""
+
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+
+def _sha256(b: bytes) -> bytes:
+    import hashlib
+    return hashlib.sha256(b).digest()
+
+
+def _partial_postorder(leaves: list, include: set) -> list:
+    """PartialMerkleTree.build over the full tree of `leaves` (zero-hash padded),
+    emitted as the (kind, hash) post-order program; returns (root, program)."""
+    level = list(leaves)
+    while len(level) & (len(level) - 1):
+        level.append(bytes(32))
+    # each entry: (hash, has_included, program)
+    nodes = [(h, h in include, [(0 if h in include else 1, h)]) for h in level]
+    while len(nodes) > 1:
+        nxt = []
+        for i in range(0, len(nodes), 2):
+            (hl, fl, pl), (hr, fr, pr) = nodes[i], nodes[i + 1]
+            h = _sha256(hl + hr)
+            nxt.append((h, fl or fr, pl + pr + [(2, bytes(32))] if (fl or fr) else [(1, h)]))
+        nodes = nxt
+    return nodes[0][0], nodes[0][2]
+
+
+def make_ftx_batch(n_pool: int, seed: int = 11) -> FtxWorkload:
+    """What the non-validating notary receives (NotaryFlow.kt:72): each config-4
+    transaction filtered to its inputs and time window (transactions with neither
+    are not notarised and are skipped), with the nonces of those components and the
+    partial Merkle tree over the full tx (PartialMerkleTree.build).  All valid."""
+    rng = np.random.default_rng(seed)
+    (n_in, n_att, n_out, n_cmd, has_tw, arena, comp_off, comp_len, comp_start,
+     salts) = _tx_components(n_pool, rng, seed)
+    f_comps, f_nonces, progs, roots = [], [], [], []
+    for t in range(n_pool):
+        if n_in[t] == 0 and not has_tw[t]:
+            continue
+        c0, c1 = int(comp_start[t]), int(comp_start[t + 1])
+        salt = salts[32 * t:32 * t + 32].tobytes()
+        sers = [arena[int(comp_off[c]):int(comp_off[c]) + int(comp_len[c])].tobytes() for c in range(c0, c1)]
+        nonces = [_sha256(salt + i.to_bytes(4, "big")) for i in range(len(sers) - 1)]
+        leaves = [_sha256(x + n) for x, n in zip(sers, nonces)] + [_sha256(sers[-1])]
+        vis = list(range(int(n_in[t])))
+        if has_tw[t]:
+            vis.append(len(sers) - 2)  # the time window sits just before the salt
+        root, prog = _partial_postorder(leaves, {leaves[i] for i in vis})
+        f_comps.append([sers[i] for i in vis])
+        f_nonces.append([nonces[i] for i in vis])
+        progs.append(prog)
+        roots.append(root)
+    n = len(roots)
+    flat = [x for cs in f_comps for x in cs]
+    fcl = np.array([len(x) for x in flat], dtype=np.uint32)
+    fco = np.zeros(len(flat), dtype=np.uint64)
+    fco[1:] = np.cumsum(fcl[:-1], dtype=np.uint64)
+    fcs = np.zeros(n + 1, dtype=np.uint32)
+    fcs[1:] = np.cumsum([len(cs) for cs in f_comps])
+    nst = np.zeros(n + 1, dtype=np.uint32)
+    nst[1:] = np.cumsum([len(p) for p in progs])
+    return FtxWorkload(
+        n=n, arena=np.frombuffer(b"".join(flat) + b"\0", dtype=np.uint8).copy(), comp_off=fco, comp_len=fcl,
+        comp_start=fcs, nonces=np.frombuffer(b"".join(x for ns in f_nonces for x in ns), dtype=np.uint8).copy(),
+        node_start=nst, node_kind=np.array([k for p in progs for k, _ in p], dtype=np.uint8),
+        node_hash=np.frombuffer(b"".join(h for p in progs for _, h in p), dtype=np.uint8).copy(),
+        roots=np.frombuffer(b"".join(roots), dtype=np.uint8).copy(), expected=np.zeros(n, dtype=np.uint8))
+
+
+def tile_ftx_batch(w: FtxWorkload, n: int, adversarial: float = 0.01, seed: int = 12) -> FtxWorkload:
+    """The pool repeated to n filtered transactions (each copy owns its bytes), then
+    `adversarial` of them broken, split over: a flipped component byte, a flipped
+    root byte, a flipped Leaf/IncludedLeaf hash byte in the tree (expected FALSE)."""
+    reps = -(-n // w.n)
+    a_len = int(w.comp_off[-1]) + int(w.comp_len[-1])
+    nc, nn = int(w.comp_start[-1]), int(w.node_start[-1])
+    comp_start = np.concatenate([[0], np.cumsum(np.tile(np.diff(w.comp_start), reps), dtype=np.uint64)])
+    node_start = np.concatenate([[0], np.cumsum(np.tile(np.diff(w.node_start), reps), dtype=np.uint64)])
+    comp_start, node_start = comp_start[:n + 1].astype(np.uint32), node_start[:n + 1].astype(np.uint32)
+    tc, tn = int(comp_start[-1]), int(node_start[-1])
+    t = FtxWorkload(
+        n=n, arena=np.concatenate([np.tile(w.arena[:a_len], reps), np.zeros(1, np.uint8)]),
+        comp_off=(w.comp_off[None, :nc] + np.arange(reps, dtype=np.uint64)[:, None] * np.uint64(a_len)).ravel()[:tc],
+        comp_len=np.tile(w.comp_len[:nc], reps)[:tc].copy(), comp_start=comp_start,
+        nonces=np.tile(w.nonces[:32 * nc], reps)[:32 * tc].copy(), node_start=node_start,
+        node_kind=np.tile(w.node_kind[:nn], reps)[:tn].copy(), node_hash=np.tile(w.node_hash[:32 * nn], reps)[:32 * tn].copy(),
+        roots=np.tile(w.roots[:32 * w.n], reps)[:32 * n].copy(), expected=np.zeros(n, dtype=np.uint8))
+    rng = np.random.default_rng(seed)
+    bad = np.flatnonzero(rng.random(n) < adversarial)
+    cls = rng.integers(0, 3, len(bad))
+    for b, k in zip(bad, cls):
+        if k == 0:
+            t.arena[int(t.comp_off[t.comp_start[b]]) + 8] ^= 1
+        elif k == 1:
+            t.roots[32 * b + 5] ^= 1
+        else:
+            j = next(j for j in range(int(t.node_start[b]), int(t.node_start[b + 1])) if t.node_kind[j] != 2)
+            t.node_hash[32 * j + 3] ^= 1
+        t.expected[b] = 1
     return t
