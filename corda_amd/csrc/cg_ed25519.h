@@ -12,8 +12,8 @@
 //           and k*R, k = 0..8.
 //   msm     P = [b]B + [c0](-A) + [c1](-R) with ~130 shared doublings, fixed 4-bit
 //           windows for A and R (one lane per signature, every lane of the wave
-//           on the same bit position) and 8-bit windows over two shared tables
-//           B and 2^128 B; accept iff P is the identity.
+//           on the same bit position) and kBWin-bit windows over two shared
+//           tables B and 2^128 B; accept iff P is the identity.
 //
 // Reference call path: Crypto.isValid -> EdDSAEngine.engineVerify
 // (/root/reference/core/src/main/kotlin/net/corda/core/crypto/Crypto.kt:534-541).
@@ -31,9 +31,16 @@ namespace cg {
 enum : uint32_t { V_ACCEPT = 0, V_REJECT = 1, V_SIG_MALFORMED = 2, V_KEY_INVALID = 3, V_ARG_EMPTY = 4, V_COMPUTE = 0xff };
 enum : uint32_t { MODE_IS_VALID = 0, MODE_DO_VERIFY = 1 };
 
-constexpr int kATabEntries = 9;    // per-lane tables, 4-bit signed digits: k*P, |d| <= 8
-constexpr int kBTabEntries = 129;  // shared tables, 8-bit signed digits: k*B, k*2^128 B, |d| <= 128
-constexpr int kDigitWords = 24;    // A nibbles (8) | R nibbles (8) | B bytes (8)
+// Width of the B windows (bits).  16: two shared tables of 2^15 + 1 affine points
+// (k*B and k*2^128 B, 3.9 MB each, read from L2 / MALL) and 16 mixed additions per
+// verify; 8: two 129-entry tables and 32 mixed additions.
+#ifndef CG_ED_BWIN
+#define CG_ED_BWIN 16
+#endif
+constexpr int kBWin = CG_ED_BWIN;
+constexpr int kATabEntries = 9;                          // per-lane tables, 4-bit signed digits: k*P, |d| <= 8
+constexpr int kBTabEntries = (1 << (kBWin - 1)) + 1;     // shared tables, |d| <= 2^(kBWin-1)
+constexpr int kDigitWords = 24;    // A nibbles (8) | R nibbles (8) | B digits (8 words, 256 bits)
 constexpr int kMinDigits = 32;     // the loop always covers bit positions 0..127 (B tables)
 
 // Status word of the hash/points phases: verdict (bits 0-7; V_COMPUTE while the
@@ -98,7 +105,7 @@ CG_HD uint32_t ed25519_hash_stage(const uint32_t pk[8], const uint32_t sig[16], 
   rneg = c1neg ^ 1u;  // the R term is [|c1|](-R) when c1 > 0, [|c1|]R when c1 < 0
   sc_recode16(dig, c0);
   sc_recode16(dig + 8, c1);
-  sc_recode8(dig + 16, b);
+  sc_recode_b<kBWin>(dig + 16, b);
   uint32_t x0[9], x1[9];
   CG_UNROLL for (int w = 0; w < 9; ++w) {
     x0[w] = w < 8 ? c0[w] : 0u;
@@ -159,41 +166,44 @@ CG_HD void ed25519_build_table(const ge_p3& P, Put&& put) {
   }
 }
 
-// Shared table k*P (k = 0..128) in affine precomputed form, for P = B (shift 0)
-// or P = 2^128 B (shift 128); computed once on the host per context and
-// uploaded (the MSM kernel stages both in LDS).
-CG_HD void ed25519_base_table(ge_precomp tab[kBTabEntries], int shift) {
+// Entry k (0 <= k <= 2^(kBWin-1)) of shared table t in affine precomputed form:
+// k*B (t = 0) or k*2^128 B (t = 1).  One call per lane of the table-building
+// kernel at context creation (and on the host for the tests).
+CG_HD void ed25519_btab_entry(ge_precomp& out, uint32_t t, uint32_t k) {
   const uint32_t benc[8] = {0x66666658u, 0x66666666u, 0x66666666u, 0x66666666u,
                             0x66666666u, 0x66666666u, 0x66666666u, 0x66666666u};
   const fe d2 = CG_FE_D2;
-  ge_p3 P, cur;
+  ge_p3 P, R;
+  ge_p1p1 x;
   ge_frombytes_i2p(P, benc);
-  for (int i = 0; i < shift; ++i) {
-    ge_p1p1 t;
-    ge_p3_dbl(t, P);
-    ge_p1p1_to_p3(P, t);
+  CG_NOUNROLL for (uint32_t i = 0; i < 128 * t; ++i) {
+    ge_p3_dbl(x, P);
+    ge_p1p1_to_p3(P, x);
   }
   ge_cached pc;
   ge_p3_to_cached(pc, P);
-  fe_1(tab[0].yplusx);
-  fe_1(tab[0].yminusx);
-  fe_0(tab[0].xy2d);
-  cur = P;
-  for (int k = 1; k < kBTabEntries; ++k) {
-    fe recip, x, y;
-    fe_invert(recip, cur.Z);
-    fe_mul(x, cur.X, recip);
-    fe_mul(y, cur.Y, recip);
-    fe_add(tab[k].yplusx, y, x);
-    fe_sub(tab[k].yminusx, y, x);
-    fe_mul(tab[k].xy2d, x, y);
-    fe_mul(tab[k].xy2d, tab[k].xy2d, d2);
-    fe_reduce(tab[k].yplusx);
-    fe_reduce(tab[k].yminusx);
-    ge_p1p1 t;
-    ge_add_cached(t, cur, pc, 0);
-    ge_p1p1_to_p3(cur, t);
+  fe_0(R.X);
+  fe_1(R.Y);
+  fe_1(R.Z);
+  fe_0(R.T);
+  CG_NOUNROLL for (int b = 16; b >= 0; --b) {  // left to right over k (< 2^17), complete formulas
+    ge_p3_dbl(x, R);
+    ge_p1p1_to_p3(R, x);
+    if ((k >> b) & 1) {
+      ge_add_cached(x, R, pc, 0);
+      ge_p1p1_to_p3(R, x);
+    }
   }
+  fe recip, ax, ay;
+  fe_invert(recip, R.Z);
+  fe_mul(ax, R.X, recip);
+  fe_mul(ay, R.Y, recip);
+  fe_add(out.yplusx, ay, ax);
+  fe_sub(out.yminusx, ay, ax);
+  fe_mul(out.xy2d, ax, ay);
+  fe_mul(out.xy2d, out.xy2d, d2);
+  fe_reduce(out.yplusx);
+  fe_reduce(out.yminusx);
 }
 
 // x <<= 4 * n (nibbles) for a 256-bit value; n uniform across the wave.
@@ -212,7 +222,8 @@ CG_HD void shl_nibbles(uint32_t x[8], uint32_t n) {
 
 // MSM phase: P = [b]B + [c0](-A) + [c1](+-R) over ndig radix-16 positions (ndig
 // uniform across the wave, >= 32).  getA(k, cached&) loads k*(-A), getR(k,
-// cached&) loads k*R, getB(t, k, precomp&) loads k*B (t = 0) or k*2^128 B (t = 1).
+// cached&) loads k*R, getB(t, k, precomp&) loads k*B (t = 0) or k*2^128 B (t = 1),
+// k <= 2^(kBWin-1).
 // Returns 1 iff P is the identity.
 template <typename GetA, typename GetR, typename GetB>
 CG_HD uint32_t ed25519_msm(uint32_t ndig, const uint32_t dig[kDigitWords], uint32_t rneg, GetA&& getA, GetR&& getR,
@@ -259,19 +270,20 @@ CG_HD uint32_t ed25519_msm(uint32_t ndig, const uint32_t dig[kDigitWords], uint3
       ge_p1p1_to_p3(r3, t);
       ge_add_cached(t, r3, ca, nr ^ rneg);
     }
-    if ((pos & 7) == 0 && pos < 128) {
-      const uint32_t el = bl[0] & 0xff, eh = bh[0] & 0xff;
+    if ((pos & (kBWin - 1)) == 0 && pos < 128) {
+      constexpr uint32_t kMask = (1u << kBWin) - 1, kHalf = 1u << (kBWin - 1);
+      const uint32_t el = bl[0] & kMask, eh = bh[0] & kMask;
       CG_UNROLL for (int w = 0; w < 3; ++w) {
-        bl[w] = bl[w] >> 8 | bl[w + 1] << 24;
-        bh[w] = bh[w] >> 8 | bh[w + 1] << 24;
+        bl[w] = bl[w] >> kBWin | bl[w + 1] << (32 - kBWin);
+        bh[w] = bh[w] >> kBWin | bh[w + 1] << (32 - kBWin);
       }
-      bl[3] >>= 8;
-      bh[3] >>= 8;
-      const uint32_t nl = el < 128, nh = eh < 128;
-      getB(0, nl ? 128 - el : el - 128, pb);
+      bl[3] >>= kBWin;
+      bh[3] >>= kBWin;
+      const uint32_t nl = el < kHalf, nh = eh < kHalf;
+      getB(0, nl ? kHalf - el : el - kHalf, pb);
       ge_p1p1_to_p3(r3, t);
       ge_madd(t, r3, pb, nl);
-      getB(1, nh ? 128 - eh : eh - 128, pb);
+      getB(1, nh ? kHalf - eh : eh - kHalf, pb);
       ge_p1p1_to_p3(r3, t);
       ge_madd(t, r3, pb, nh);
     }

@@ -20,13 +20,13 @@ struct Ed25519Dev {
   uint32_t* status = nullptr;    // [scap]
   uint32_t* digits = nullptr;    // [24][scap]
   int32_t* table = nullptr;      // [scap][18][40] lane-contiguous k*(-A), k*R
-  const int32_t* btab = nullptr; // [2][129][30] shared k*B, k*2^128 B tables
+  const int32_t* btab = nullptr; // [2][kBTabEntries][30] shared k*B, k*2^128 B tables
 };
 
-constexpr int kEdBaseTableWords = 2 * 129 * 30;
+size_t ed25519_btab_words();
 size_t ed25519_table_bytes(uint32_t cap);
 size_t ed25519_digit_words();
-void ed25519_base_table_words(int32_t out[kEdBaseTableWords]);
+hipError_t launch_ed25519_btab_build(int32_t* btab, hipStream_t s);
 hipError_t launch_ed25519_hash(const Ed25519Dev& d, uint32_t n, uint32_t mode, hipStream_t s);
 hipError_t launch_ed25519_points(const Ed25519Dev& d, uint32_t n, hipStream_t s);
 hipError_t launch_ed25519_msm(const Ed25519Dev& d, uint32_t n, const uint32_t* out_index, uint8_t* verdict,

@@ -180,6 +180,26 @@ CG_HD void sc_recode_msb(uint32_t out[NWORDS], const uint32_t k[8]) {
 CG_HD void sc_recode5(uint32_t out[13], const uint32_t k[8]) { sc_recode_msb<5, 51, 13>(out, k); }
 CG_HD void sc_recode8(uint32_t out[8], const uint32_t k[8]) { sc_recode_msb<8, 32, 8>(out, k); }
 
+// B-side digits for W-bit windows (W = 8 or 16) of k < 2^253: 256/W signed digits
+// d in [-2^(W-1), 2^(W-1)), stored as e = d + 2^(W-1) in W-bit fields, most
+// significant first (consumed from the low field of word 0 onward).  Words 0..3
+// hold the digits of bits 255..128 (the 2^128 B table), words 4..7 those of bits
+// 127..0 (the B table).
+template <int W>
+CG_HD void sc_recode_b(uint32_t out[8], const uint32_t k[8]) {
+  constexpr int NDIG = 256 / W, PER = 32 / W;
+  uint32_t dig[NDIG];
+  uint32_t carry = 0;
+  CG_UNROLL for (int i = 0; i < NDIG; ++i) {
+    const uint32_t chunk = W == 32 ? k[i] : (k[(W * i) >> 5] >> ((W * i) & 31)) & ((1u << W) - 1);
+    const uint32_t v = chunk + carry;
+    carry = v >= (1u << (W - 1));
+    dig[i] = v + (1u << (W - 1)) - (carry << W);
+  }
+  CG_UNROLL for (int w = 0; w < 8; ++w) out[w] = 0;
+  CG_UNROLL for (int j = 0; j < NDIG; ++j) out[j / PER] |= dig[NDIG - 1 - j] << (W * (j % PER));
+}
+
 // S_eff mod L for i2p's slide semantics.
 CG_HD void sc_effective_s(uint32_t out[8], const uint32_t s[8]) {
   uint32_t x[16];

@@ -346,11 +346,10 @@ cg_status cg_open(int device, cg_ctx** out) {
     delete ctx;
     return CG_E_DEVICE;
   }
-  static int32_t bt[cg::kEdBaseTableWords];
-  static std::once_flag bt_once;
-  std::call_once(bt_once, [] { cg::ed25519_base_table_words(bt); });
-  if (dalloc(ctx, &ctx->btab, cg::kEdBaseTableWords, "alloc base table") != CG_OK ||
-      hipMemcpy(ctx->btab, bt, sizeof bt, hipMemcpyHostToDevice) != hipSuccess ||
+  // the shared Ed25519 base tables (k*B, k*2^128 B) are built on the device, once per context
+  if (dalloc(ctx, &ctx->btab, cg::ed25519_btab_words(), "alloc base table") != CG_OK ||
+      cg::launch_ed25519_btab_build(ctx->btab, ctx->stream) != hipSuccess ||
+      hipStreamSynchronize(ctx->stream) != hipSuccess ||
       dalloc(ctx, &ctx->err_flag, 1, "alloc error flag") != CG_OK) {
     cg_close(ctx);
     return CG_E_DEVICE;

@@ -6,8 +6,9 @@
 //   cg_ed25519_points   decode A and R (two square roots), tables k*(-A) and k*R
 //                       (k = 0..8) written to HBM scratch
 //   cg_ed25519_msm      [b]B + [c0](-A) + [c1](+-R) over ~132 shared bit positions
-//                       (4-bit windows for A/R, 8-bit windows over B and 2^128 B
-//                       staged in LDS), identity test -> verdict
+//                       (4-bit windows for A/R, kBWin-bit windows over the shared
+//                       tables B and 2^128 B in HBM), identity test -> verdict
+//   cg_ed25519_btab_build  the shared tables (context creation)
 //
 // Integer VALU work only (no MFMA): field products are v_mad_i64_i32.
 // Device layout (SoA, word-major, `cap` = batch capacity, i = element):
@@ -31,7 +32,7 @@ namespace {
 
 constexpr int kTabLimbs = 40;  // cached point: 4 fe x 10 limbs
 constexpr int kLaneEntries = 2 * kATabEntries;
-constexpr int kBLimbs = 30;    // precomputed point: 3 fe x 10 limbs
+constexpr int kBStride = 32;   // shared-table entry (precomputed point, 3 fe x 10 limbs) padded to one 128-byte line
 
 CG_DEV int4* lane_table(int32_t* table, uint32_t i) {
   return reinterpret_cast<int4*>(table + (size_t)i * (kLaneEntries * kTabLimbs));
@@ -106,6 +107,22 @@ __global__ __launch_bounds__(256) void cg_ed25519_points(const uint32_t* __restr
   });
 }
 
+// The shared B tables: entry k of table t = k * 2^(128 t) B in affine form,
+// one lane per entry (2 * (2^(kBWin-1) + 1) lanes), at context creation.
+__global__ __launch_bounds__(256) void cg_ed25519_btab_build(int32_t* __restrict__ btab) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 2 * (uint32_t)kBTabEntries) return;
+  ge_precomp e;
+  ed25519_btab_entry(e, i / kBTabEntries, i % kBTabEntries);
+  int32_t* o = btab + (size_t)i * kBStride;
+  CG_UNROLL for (int l = 0; l < 10; ++l) {
+    o[l] = e.yplusx.v[l];
+    o[10 + l] = e.yminusx.v[l];
+    o[20 + l] = e.xy2d.v[l];
+  }
+  o[30] = o[31] = 0;
+}
+
 CG_DEV uint32_t wave_max(uint32_t v) {
   CG_UNROLL for (int o = 32; o >= 1; o >>= 1) {
     const uint32_t u = (uint32_t)__shfl_xor((int)v, o, 64);
@@ -118,9 +135,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_MSM_WAVE
     const uint32_t* __restrict__ sig, const uint32_t* __restrict__ status, const uint32_t* __restrict__ digits,
     const int32_t* __restrict__ table, const int32_t* __restrict__ btab_g, uint32_t n, uint32_t cap, uint32_t scap,
     const uint32_t* __restrict__ out_index, uint8_t* __restrict__ verdict) {
-  __shared__ int32_t btab[2 * kBTabEntries * kBLimbs];
-  for (int t = threadIdx.x; t < 2 * kBTabEntries * kBLimbs; t += blockDim.x) btab[t] = btab_g[t];
-  __syncthreads();
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t st = i < n ? status[i] : 0u;
   const bool live = i < n && ed_status_verdict(st) == V_COMPUTE;
@@ -140,11 +154,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_MSM_WAVE
       [&](uint32_t k, ge_cached& c) { load_cached(lt + k * (kTabLimbs / 4), c); },
       [&](uint32_t k, ge_cached& c) { load_cached(lt + (kATabEntries + k) * (kTabLimbs / 4), c); },
       [&](uint32_t t, uint32_t k, ge_precomp& p) {
-        const int32_t* b = btab + (t * kBTabEntries + k) * kBLimbs;
+        // one 128-byte line per entry: eight 16-byte loads (L2 / MALL resident table)
+        const int4* b = reinterpret_cast<const int4*>(btab_g + ((size_t)t * kBTabEntries + k) * kBStride);
+        int32_t v[kBStride];
+        CG_UNROLL for (int q = 0; q < kBStride / 4; ++q) {
+          const int4 x = b[q];
+          v[4 * q] = x.x;
+          v[4 * q + 1] = x.y;
+          v[4 * q + 2] = x.z;
+          v[4 * q + 3] = x.w;
+        }
         CG_UNROLL for (int l = 0; l < 10; ++l) {
-          p.yplusx.v[l] = b[l];
-          p.yminusx.v[l] = b[10 + l];
-          p.xy2d.v[l] = b[20 + l];
+          p.yplusx.v[l] = v[l];
+          p.yminusx.v[l] = v[10 + l];
+          p.xy2d.v[l] = v[20 + l];
         }
       });
   verdict[dst] = ok ? (uint8_t)V_ACCEPT : (uint8_t)V_REJECT;
@@ -156,20 +179,12 @@ namespace cg {
 
 size_t ed25519_table_bytes(uint32_t scap) { return (size_t)kLaneEntries * kTabLimbs * scap * sizeof(int32_t); }
 size_t ed25519_digit_words() { return kDigitWords; }
+size_t ed25519_btab_words() { return (size_t)2 * kBTabEntries * kBStride; }
 
-void ed25519_base_table_words(int32_t out[kEdBaseTableWords]) {
-  static_assert(kEdBaseTableWords == 2 * kBTabEntries * kBLimbs, "base table size");
-  for (int t = 0; t < 2; ++t) {
-    ge_precomp tab[kBTabEntries];
-    ed25519_base_table(tab, 128 * t);
-    for (int k = 0; k < kBTabEntries; ++k)
-      for (int l = 0; l < 10; ++l) {
-        int32_t* o = out + (t * kBTabEntries + k) * kBLimbs;
-        o[l] = tab[k].yplusx.v[l];
-        o[10 + l] = tab[k].yminusx.v[l];
-        o[20 + l] = tab[k].xy2d.v[l];
-      }
-  }
+hipError_t launch_ed25519_btab_build(int32_t* btab, hipStream_t s) {
+  const uint32_t n = 2 * kBTabEntries;
+  hipLaunchKernelGGL(cg_ed25519_btab_build, dim3((n + 255) / 256), dim3(256), 0, s, btab);
+  return hipGetLastError();
 }
 
 hipError_t launch_ed25519_hash(const Ed25519Dev& d, uint32_t n, uint32_t mode, hipStream_t s) {

@@ -60,7 +60,7 @@ int cgh_half_scalars(const uint32_t* h, uint32_t* c0, uint32_t* c1, uint32_t* c1
   return (int)ed25519_half_scalars(h, c0, c1, *c1neg);
 }
 
-static ge_precomp g_btab[2][kBTabEntries];
+static ge_precomp g_btab[2][kBTabEntries];  // the device's shared tables, built with the same code
 static int g_init;
 
 // The three device phases in sequence (hash -> points -> msm) for one signature;
@@ -69,8 +69,8 @@ static int g_init;
 int cgh_ed25519_verify_nd(const uint8_t* pk_bytes, const uint8_t* sig_bytes, uint32_t sig_len, const uint8_t* msg,
                           uint32_t msg_len, uint32_t mode, uint32_t force_ndig, uint32_t full_length) {
   if (!g_init) {
-    ed25519_base_table(g_btab[0], 0);
-    ed25519_base_table(g_btab[1], 128);
+    for (uint32_t t = 0; t < 2; ++t)
+      for (uint32_t k = 0; k < (uint32_t)kBTabEntries; ++k) ed25519_btab_entry(g_btab[t][k], t, k);
     g_init = 1;
   }
   uint32_t pk[8], sig[16] = {0};
