@@ -20,6 +20,53 @@ struct fe {
   int32_t v[10];
 };
 
+// Host-only bound checking (tests/native, -DCG_CHECK_BOUNDS): recomputes every
+// column sum of a mul/sq in 128 bits, traps on int64 overflow and records the
+// largest input limb and column sum seen (cg_bounds_report).
+#if defined(CG_CHECK_BOUNDS) && !defined(__HIP_DEVICE_COMPILE__)
+struct CgBounds {
+  int64_t max_limb = 0;
+  __int128 max_col = 0;
+};
+inline CgBounds& cg_bounds() {
+  static CgBounds b;
+  return b;
+}
+template <typename F, typename G>
+inline void cg_bounds_mul(const F& f, const G& g, const int64_t t[10], int dbl) {
+  CgBounds& b = cg_bounds();
+  __int128 col[10] = {0};
+  for (int i = 0; i < 10; ++i) {
+    const int64_t af = f.v[i] < 0 ? -(int64_t)f.v[i] : f.v[i], ag = g.v[i] < 0 ? -(int64_t)g.v[i] : g.v[i];
+    if (af > b.max_limb) b.max_limb = af;
+    if (ag > b.max_limb) b.max_limb = ag;
+    for (int j = 0; j < 10; ++j) {
+      const int k = i + j;
+      __int128 p = (__int128)f.v[i] * g.v[j] * (((i & 1) && (j & 1)) ? 2 : 1) * (k >= 10 ? 19 : 1);
+      col[k >= 10 ? k - 10 : k] += p;
+    }
+  }
+  for (int k = 0; k < 10; ++k) {
+    const __int128 c = col[k] * (dbl ? 2 : 1);
+    const __int128 a = c < 0 ? -c : c;
+    if (a > b.max_col) b.max_col = a;
+    const int64_t tk = t[k];
+    if (a >= ((__int128)1 << 62) || (int64_t)c != tk) {
+      fprintf(stderr, "cg bounds: column %d = 2^%.2f (int64 %s)\n  f:", k, __builtin_log2((double)a),
+              (int64_t)c != tk ? "wrapped" : "ok");
+      for (int i = 0; i < 10; ++i) fprintf(stderr, " %d", f.v[i]);
+      fprintf(stderr, "\n  g:");
+      for (int i = 0; i < 10; ++i) fprintf(stderr, " %d", g.v[i]);
+      fprintf(stderr, "\n");
+      __builtin_trap();
+    }
+  }
+}
+#define CG_BOUNDS_MUL(f, g, t, dbl) cg_bounds_mul(f, g, t, dbl)
+#else
+#define CG_BOUNDS_MUL(f, g, t, dbl) ((void)0)
+#endif
+
 CG_HD void fe_0(fe& h) {
   CG_UNROLL for (int i = 0; i < 10; ++i) h.v[i] = 0;
 }
@@ -129,6 +176,7 @@ CG_HD void fe_mul(fe& h, const fe& f, const fe& g) {
       t[k >= 10 ? k - 10 : k] += (int64_t)a * b;
     }
   }
+  CG_BOUNDS_MUL(f, g, t, 0);
   fe_carry_wide(h, t);
 }
 
@@ -155,6 +203,7 @@ CG_HD void fe_sq_t(fe& h, const fe& f) {
   if (DOUBLE) {
     CG_UNROLL for (int k = 0; k < 10; ++k) t[k] *= 2;
   }
+  CG_BOUNDS_MUL(f, f, t, DOUBLE);
   fe_carry_wide(h, t);
 }
 CG_HD void fe_sq(fe& h, const fe& f) { fe_sq_t<false>(h, f); }

@@ -3,6 +3,7 @@
 // algorithm — limb bounds, carries, scalar recodings, window arithmetic — against
 // the CPU oracle on millions of cases without a GPU.  Not part of the product.
 #include <stdint.h>
+#include <stdio.h>
 #include <string.h>
 
 #include "cg_ed25519.h"
@@ -192,3 +193,10 @@ extern "C" void cgh_sha256_tail(const uint8_t* msg, uint32_t n, const uint8_t* t
   for (int i = 0; i < 8; ++i)
     for (int b = 0; b < 4; ++b) out[4 * i + b] = (uint8_t)(h[i] >> (24 - 8 * b));
 }
+
+#if defined(CG_CHECK_BOUNDS)
+extern "C" void cgh_bounds_report(int64_t* max_limb, double* log2_max_col) {
+  *max_limb = cg_bounds().max_limb;
+  *log2_max_col = __builtin_log2((double)cg_bounds().max_col);
+}
+#endif

@@ -220,3 +220,36 @@ def test_verify_random_mutations_vs_oracle(host, oracle):
             nd = rnd.choice([0, 0, 34, 64])
             assert host.cgh_ed25519_verify_nd(p, sg, len(sg), m, len(m), 0, nd, 0) == \
                 oracle.oracle_ed25519_verify(p, sg, len(sg), m, len(m), 0)
+
+
+def test_field_bounds_whole_pipeline(golden_ed25519, oracle):
+    """The limb-bound argument of cg_fe25519.h (signed reduced limbs, int32
+    prescaling of 19 g_j), checked on the real operation sequences: a
+    host build with 128-bit shadow column sums (-DCG_CHECK_BOUNDS traps when a
+    column leaves +-2^62 or differs from the device formulation) runs the golden fixtures (incl.
+    small-order / non-canonical points) and random + mutated signatures through all
+    three phases, forcing the full-length and padded-digit variants too."""
+    so = os.path.join(ROOT, "tests", "native", "libcg_host_bounds.so")
+    src = os.path.join(ROOT, "tests", "native", "cg_host.cpp")
+    subprocess.check_call(["g++", "-O1", "-std=c++17", "-shared", "-fPIC", "-DCG_CHECK_BOUNDS", "-I",
+                           os.path.join(ROOT, "corda_amd", "csrc"), src, "-o", so])
+    lib = ctypes.CDLL(so)
+    lib.cgh_ed25519_verify_nd.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p,
+                                          ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]
+    cases = [(bytes.fromhex(e["pk"]), bytes.fromhex(e["sig"]), bytes.fromhex(e["msg"]), e["is_valid"])
+             for e in golden_ed25519]
+    rnd = random.Random(9)
+    for _ in range(150):
+        seed, msg = rnd.randbytes(32), rnd.randbytes(rnd.randint(0, 200))
+        pk, sig = ED.sign(seed, msg)
+        bad = bytearray(sig)
+        bad[rnd.randrange(64)] ^= 1 << rnd.randrange(8)
+        for s in (sig, bytes(bad)):
+            cases.append((pk, s, msg, oracle.oracle_ed25519_verify(pk, s, len(s), msg, len(msg), 0)))
+    for i, (pk, sig, msg, exp) in enumerate(cases):
+        nd, full = ((0, 0), (0, 1), (64, 0))[i % 3]
+        assert lib.cgh_ed25519_verify_nd(pk, sig, len(sig), msg, len(msg), 0, nd, full) == exp
+    ml, lc = ctypes.c_int64(), ctypes.c_double()
+    lib.cgh_bounds_report(ctypes.byref(ml), ctypes.byref(lc))
+    # inputs stay below 1.69 * 2^26 (19 * limb fits int32), column sums far inside int64
+    assert ml.value < 1.69 * 2**26 and lc.value < 61, (ml.value / 2**26, lc.value)
