@@ -228,10 +228,11 @@ def test_field_bounds_whole_pipeline(golden_ed25519, oracle):
     host build with 128-bit shadow column sums (-DCG_CHECK_BOUNDS traps when a
     column leaves +-2^62 or differs from the device formulation) runs the golden fixtures (incl.
     small-order / non-canonical points) and random + mutated signatures through all
-    three phases, forcing the full-length and padded-digit variants too."""
+    three phases, forcing the full-length and padded-digit variants too (8-bit B
+    windows here: the same formulas, a 258-entry table instead of 65,538)."""
     so = os.path.join(ROOT, "tests", "native", "libcg_host_bounds.so")
     src = os.path.join(ROOT, "tests", "native", "cg_host.cpp")
-    subprocess.check_call(["g++", "-O1", "-std=c++17", "-shared", "-fPIC", "-DCG_CHECK_BOUNDS", "-I",
+    subprocess.check_call(["g++", "-O1", "-std=c++17", "-shared", "-fPIC", "-DCG_CHECK_BOUNDS", "-DCG_ED_BWIN=8", "-I",
                            os.path.join(ROOT, "corda_amd", "csrc"), src, "-o", so])
     lib = ctypes.CDLL(so)
     lib.cgh_ed25519_verify_nd.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p,
