@@ -26,6 +26,8 @@ ACCEPT, REJECT, SIG_MALFORMED, KEY_INVALID, ARG_EMPTY, UNSUPPORTED = 0, 1, 2, 3,
 MODE_IS_VALID, MODE_DO_VERIFY = 0, 1
 # FilteredTransaction.verify outcomes (cg_ftx_verify_batch)
 FTX_TRUE, FTX_FALSE, FTX_NO_LEAVES, FTX_MALFORMED = 0, 1, 2, 3
+# CompositeKey fulfilment (cg_composite_eval_batch)
+COMPOSITE_LEAF, COMPOSITE_NODE, COMPOSITE_INVALID = 0, 1, 0x80
 
 # exported symbols and their prototypes: (restype, argtypes)
 _u8p, _u32p, _u64p, _i32p = POINTER(c_uint8), POINTER(c_uint32), POINTER(c_uint64), POINTER(ctypes.c_int32)
@@ -50,6 +52,8 @@ PROTOTYPES = {
                                    c_void_p, c_void_p, c_void_p]),
     "cg_ftx_verify_batch": (c_int, [c_void_p, c_size_t, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_void_p,
                                     c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "cg_composite_eval_batch": (c_int, [c_void_p, c_size_t, c_void_p, c_void_p, c_size_t, c_void_p, c_void_p,
+                                        c_void_p]),
     "cg_register_host": (c_int, [c_void_p, c_void_p, c_size_t]),
     "cg_unregister_host": (c_int, [c_void_p, c_void_p]),
     "cg_release_cached": (c_int, [c_void_p]),

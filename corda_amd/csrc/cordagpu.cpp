@@ -30,6 +30,7 @@
 #include <unordered_map>
 #include <vector>
 
+#include "cg_composite_api.h"
 #include "cg_ecdsa_api.h"
 #include "cg_kernels.h"
 #include "cg_merkle_api.h"
@@ -1029,6 +1030,90 @@ cg_status cg_ftx_verify_batch(cg_ctx* ctx, size_t n_ftx, const uint8_t* arena, s
                         (const void*)roots_d, (const void*)stack_d, (const void*)kind_d, (const void*)status_d})
     dfree(ctx, p);
   d.release(ctx);
+  collect_timings(ctx);
+  return st;
+}
+
+}  // extern "C"
+
+namespace {
+
+// Host pass over the composite-key programs: the construction-time constraints of
+// CompositeKey (CompositeKey.kt:73-85, 139-144: arity >= 2, weights > 0, threshold
+// > 0 and <= the children's total weight, totals that fit an Int) and the stack
+// discipline of a single tree.  Returns the deepest stack; bad programs get
+// kCompositeInvalid.
+uint32_t composite_scan(size_t n, const uint32_t* prog_start, const int32_t* prog, size_t n_sig, uint8_t* out) {
+  uint32_t max_depth = 1;
+  std::vector<int64_t> st;
+  for (size_t q = 0; q < n; ++q) {
+    st.clear();
+    bool bad = prog_start[q + 1] == prog_start[q];
+    for (uint32_t o = prog_start[q]; o < prog_start[q + 1] && !bad; ++o) {
+      const int32_t* op = prog + 4 * (size_t)o;
+      if (op[2] <= 0) {
+        bad = true;
+      } else if (op[0] == cg::kCompositeLeaf) {
+        bad = op[1] < -1 || (op[1] >= 0 && (size_t)op[1] >= n_sig);
+        st.push_back(op[2]);
+      } else if (op[0] == cg::kCompositeNode && op[1] >= 2 && (size_t)op[1] <= st.size()) {
+        int64_t total = 0;
+        for (int32_t c = 0; c < op[1]; ++c) {
+          total += st.back();
+          st.pop_back();
+        }
+        bad = total > INT32_MAX || op[3] <= 0 || op[3] > total;
+        st.push_back(op[2]);
+      } else {
+        bad = true;
+      }
+      if (st.size() > max_depth) max_depth = (uint32_t)st.size();
+    }
+    out[q] = (bad || st.size() != 1) ? cg::kCompositeInvalid : 0;
+  }
+  return max_depth;
+}
+
+}  // namespace
+
+extern "C" {
+
+cg_status cg_composite_eval_batch(cg_ctx* ctx, size_t n_q, const uint32_t* prog_start, const int32_t* prog,
+                                  size_t n_sig, const uint32_t* sig_start, const uint8_t* verdicts, uint8_t* out) {
+  if (!ctx) return CG_E_INVALID_ARGUMENT;
+  if (n_q == 0) return CG_OK;
+  if (n_q > 0xFFFFFFF0ull) return fail(ctx, CG_E_INVALID_ARGUMENT, "too many queries");
+  if (!prog_start || !sig_start || !out || (prog_start[n_q] && !prog) || false)
+    return fail(ctx, CG_E_INVALID_ARGUMENT, "null pointer");
+  for (size_t q = 0; q < n_q; ++q)
+    if (prog_start[q + 1] < prog_start[q] || sig_start[q + 1] < sig_start[q] || sig_start[q + 1] > n_sig)
+      return fail(ctx, CG_E_INVALID_ARGUMENT, "prog_start / sig_start not monotone or out of range");
+  if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, CG_E_DEVICE, "hipSetDevice");
+  const uint32_t depth = composite_scan(n_q, prog_start, prog, n_sig, out);
+  const size_t n_ops = prog_start[n_q];
+  uint32_t *ps_d = nullptr, *ss_d = nullptr, *stack_d = nullptr;
+  int32_t* prog_d = nullptr;
+  uint8_t *ver_d = nullptr, *out_d = nullptr;
+  cg_status st;
+  if ((st = upload(ctx, &ps_d, prog_start, n_q + 1, "upload prog_start")) == CG_OK &&
+      (st = upload(ctx, &prog_d, prog, 4 * n_ops, "upload prog")) == CG_OK &&
+      (st = upload(ctx, &ss_d, sig_start, n_q + 1, "upload sig_start")) == CG_OK &&
+      (!verdicts || !n_sig || (st = upload(ctx, &ver_d, verdicts, n_sig, "upload verdicts")) == CG_OK) &&
+      (st = upload(ctx, &out_d, out, n_q, "upload status")) == CG_OK &&
+      (st = dalloc(ctx, &stack_d, (size_t)depth * n_q, "alloc composite stack")) == CG_OK) {
+    hipError_t e;
+    {
+      Timed tm(ctx, "composite_eval", n_q);
+      e = cg::launch_composite_eval(ps_d, prog_d, ss_d, ver_d, (uint32_t)n_q, stack_d, out_d, ctx->stream);
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(out, out_d, n_q, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) st = hip_fail(ctx, e, "composite eval");
+  }
+  (void)hipStreamSynchronize(ctx->stream);
+  for (const void* p : {(const void*)ps_d, (const void*)prog_d, (const void*)ss_d, (const void*)ver_d,
+                        (const void*)out_d, (const void*)stack_d})
+    dfree(ctx, p);
   collect_timings(ctx);
   return st;
 }

@@ -40,6 +40,12 @@
  *       the given nonces, MerkleTransaction.kt:23-27,153) and
  *       core/.../crypto/PartialMerkleTree.kt:130-155 (root of the partial tree, multiset
  *       of included leaves == filtered component hashes).
+ *   cg_composite_eval_batch
+ *       PublicKey.isFulfilledBy / CompositeKey.isFulfilledBy over the signers of a
+ *       batch (core/.../crypto/CryptoUtils.kt:78-82, composite/CompositeKey.kt:186-209),
+ *       as used by TransactionWithSignatures.getMissingSignatures
+ *       (TransactionWithSignatures.kt:72-77) and the composite signature engine
+ *       (composite/CompositeSignature.kt:77-85).
  *
  * Verdict codes (one byte per element) map to the JVM outcomes:
  *   CG_ACCEPT          isValid -> true / doVerify returns true
@@ -200,6 +206,24 @@ cg_status cg_ftx_verify_batch(cg_ctx* ctx, size_t n_ftx, const uint8_t* arena, s
                               const uint8_t* nonces, const uint32_t* node_start, const uint8_t* node_kind,
                               const uint8_t* node_hash, const uint8_t* root_hashes, uint8_t* result_out);
 /*
+ * CompositeKey fulfilment over verification verdicts.  n_q queries; query q is a key
+ * (plain or composite) as a post-order op program ops[prog_start[q] .. prog_start[q+1])
+ * of 4 int32 each: {CG_COMPOSITE_LEAF, sig, weight, 0} — sig = index (0 .. n_sig-1) of
+ * a signature by that key among the query's signers, or -1 when the key did not sign;
+ * {CG_COMPOSITE_NODE, n_children, weight, threshold} — the children are the n_children
+ * subtrees just before it.  weight is the NodeAndWeight weight in the parent (1 for the
+ * root).  The signers of query q are signatures sig_start[q] .. sig_start[q+1]-1 (n_q + 1
+ * entries), verdicts[n_sig] their cg_verify_batch codes (NULL: all valid).
+ * out[q]: bit 0 = isFulfilledBy(the signers' keys); bit 1 = every signature of the
+ * query is CG_ACCEPT (the composite signature engine verifies iff both bits are set);
+ * CG_COMPOSITE_INVALID = the tree violates CompositeKey's construction constraints
+ * (IllegalArgumentException): arity < 2, weight <= 0, threshold <= 0 or > total
+ * weight, Int overflow of a total, or not a single tree.
+ */
+enum { CG_COMPOSITE_LEAF = 0, CG_COMPOSITE_NODE = 1, CG_COMPOSITE_INVALID = 0x80 };
+cg_status cg_composite_eval_batch(cg_ctx* ctx, size_t n_q, const uint32_t* prog_start, const int32_t* prog,
+                                  size_t n_sig, const uint32_t* sig_start, const uint8_t* verdicts, uint8_t* out);
+/*
  * Host-memory registration (optional).  Page-locks [ptr, ptr + bytes) for the
  * device so later uploads from that range run at full PCIe DMA rate instead of
  * through the runtime's pageable staging copy.  Meant for buffers a caller reuses
@@ -216,7 +240,7 @@ cg_status cg_release_cached(cg_ctx* ctx);
  * Per-kernel device timing (HIP events on the context's stream), accumulated while
  * profiling is enabled.  Names: "ed25519_hash", "ed25519_points", "ed25519_msm",
  * "ecdsa_k1_prep", "ecdsa_k1_msm", "ecdsa_r1_prep", "ecdsa_r1_msm", "der_parse",
- * "merkle_leaf", "merkle_tree", "pmt_eval", "stage".
+ * "merkle_leaf", "merkle_tree", "pmt_eval", "composite_eval", "stage".
  */
 cg_status cg_set_profiling(cg_ctx* ctx, int enable);
 cg_status cg_kernel_stats(cg_ctx* ctx, const char* kernel, double* total_ms, uint64_t* launches,

@@ -67,6 +67,11 @@ def golden_ftx():
 
 
 @pytest.fixture(scope="session")
+def golden_composite():
+    return load_golden("composite_golden.json")
+
+
+@pytest.fixture(scope="session")
 def gpu_ctx():
     from corda_amd import Context
     ctx = Context(int(os.environ.get("LOCAL_RANK", "0")))

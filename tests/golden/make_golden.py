@@ -417,7 +417,91 @@ def ftx_cases():
     return rows
 
 
+# ------------------------------------------------------- CompositeKey fulfilment
+def composite_cases():
+    """CompositeKey fulfilment fixtures: the CompositeKeyTests.kt:45-82,126-174,284-305
+    cases plus random trees and signer subsets, each as the flat op program of
+    cg_composite_eval_batch with its expected out byte (oracle/py/composite.py)."""
+    import composite as CK
+    rnd = random.Random(99)
+    alice, bob, charlie, dave, eve = (bytes([0x30 + i]) * 32 for i in range(5))
+    rows = []
+
+    def add(cls, key, signers, verdicts=None):
+        idx = {}
+        for i, k in enumerate(signers):
+            idx.setdefault(k, i)
+        prog = CK.program(key, idx)
+        vs = verdicts if verdicts is not None else [0] * len(signers)
+        exp = int(CK.is_fulfilled_by(key, signers)) | (int(all(v == 0 for v in vs)) << 1)
+        rows.append({"cls": cls, "prog": [list(o) for o in prog], "n_sig": len(signers), "verdicts": vs,
+                     "out": exp})
+
+    B = CK.Builder
+    add("alice_by_alice", alice, [alice])
+    add("alice_by_charlie", alice, [charlie])
+    a_or_b = B().add_keys(alice, bob).build(1)
+    for sg in ([alice], [bob], [alice, bob], [charlie], []):
+        add("alice_or_bob", a_or_b, sg)
+    a_and_b = B().add_keys(alice, bob).build()
+    for sg in ([alice], [bob], [alice, bob], [bob, alice, charlie]):
+        add("alice_and_bob", a_and_b, sg)
+    ab_or_c = B().add_keys(a_and_b, charlie).build(1)
+    for sg in ([alice, bob], [charlie], [alice], [bob, charlie]):
+        add("alice_and_bob_or_charlie", ab_or_c, sg)
+    node2 = B().add_keys(alice, bob).build(2)
+    add("node2_by_alice", node2, [alice])
+    two_of_three = B().add_keys(alice, bob, charlie).build(2)
+    for sg, vs in (([alice], [0]), ([alice, bob], [0, 0]), ([alice, charlie], [0, 0]),
+                   ([alice, bob, charlie], [0, 0, 0]), ([alice, bob], [0, 1]), ([alice, bob, charlie], [0, 0, 2])):
+        add("two_of_three_composite_signature", two_of_three, sg, vs)
+    weighted = B().add_key(B().add_keys(alice, bob).build(), 3).add_key(charlie, 2).add_key(dave, 1).build(3)
+    for sg in ([alice, bob], [charlie], [charlie, dave], [alice, dave], [eve]):
+        add("weighted_tree", weighted, sg)
+    five = B().add_keys(alice, bob, charlie, dave, eve).build()
+    add("all_five", five, [eve, dave, charlie, bob, alice])
+    add("all_five_minus_one", five, [eve, dave, charlie, bob])
+    # random trees
+    keys = [bytes([i]) * 31 + b"k" for i in range(24)]
+
+    def rand_tree(depth):
+        n = rnd.randint(2, 4)
+        kids = rnd.sample(keys, n)
+        b = B()
+        for k in kids:
+            if depth > 0 and rnd.random() < 0.3:
+                b.add_key(rand_tree(depth - 1), rnd.randint(1, 4))
+            else:
+                b.add_key(k, rnd.randint(1, 4))
+        tot = sum(w for _, w in b.children)
+        return b.build(rnd.randint(1, tot))
+    for t in range(300):
+        key = rand_tree(3)
+        leaves = sorted(key.leaf_keys)
+        sg = rnd.sample(leaves, rnd.randint(0, len(leaves))) + ([keys[-1]] if t % 7 == 0 else [])
+        vs = [0 if rnd.random() < 0.9 else 1 for _ in sg]
+        add("random_tree", key, sg, vs)
+    # programs violating CompositeKey's constraints (IllegalArgumentException)
+    bad = [[[0, -1, 1, 0], [1, 1, 1, 1]],                       # arity 1
+           [[0, -1, 1, 0], [0, -1, 0, 0], [1, 2, 1, 1]],         # zero weight
+           [[0, -1, 2, 0], [0, -1, 2, 0], [1, 2, 1, 5]],         # threshold > total weight
+           [[0, -1, 1, 0], [0, -1, 1, 0], [1, 2, 1, 0]],         # threshold 0
+           [[0, -1, 2**31 - 1, 0], [0, -1, 2**31 - 1, 0], [1, 2, 1, 1]],  # Int overflow of the total
+           [[0, -1, 1, 0], [0, -1, 1, 0]],                       # two roots
+           [[1, 2, 1, 1]],                                       # node without children
+           []]                                                   # empty
+    for i, prog in enumerate(bad):
+        rows.append({"cls": f"invalid_{i}", "prog": prog, "n_sig": 0, "verdicts": [], "out": 0x80})
+    return rows
+
+
 def main():
+    if "--only-composite" in sys.argv:
+        rows = composite_cases()
+        with open(os.path.join(HERE, "composite_golden.json"), "w") as f:
+            json.dump(rows, f, indent=0)
+        print("composite", len(rows))
+        return
     if "--only-ftx" in sys.argv:
         fx = ftx_cases()
         with open(os.path.join(HERE, "ftx_golden.json"), "w") as f:
@@ -441,6 +525,9 @@ def main():
     fx = ftx_cases()
     with open(os.path.join(HERE, "ftx_golden.json"), "w") as f:
         json.dump(fx, f, indent=0)
+    rows = composite_cases()
+    with open(os.path.join(HERE, "composite_golden.json"), "w") as f:
+        json.dump(rows, f, indent=0)
 
 
 if __name__ == "__main__":
