@@ -259,6 +259,36 @@ CG_HD void recode16_65(uint32_t packed[9], const uint32_t k[8]) {
   packed[8] = carry + 8;
 }
 
+// Width of the fixed-base windows over G (bits).  16: one shared table of 2^15 + 1
+// affine points k*G per curve (2.1 MB, built on the device, read from L2) and 17
+// mixed additions per verify; 4: eight points in LDS and 65 mixed additions.
+#ifndef CG_EC_GWIN
+#define CG_EC_GWIN 16
+#endif
+constexpr int kGWin = CG_EC_GWIN;
+constexpr uint32_t kGTabEntries = (1u << (kGWin - 1)) + 1;  // k*G, k = 0 .. 2^(kGWin-1)
+
+// Digits of u1 for the G table: kGWin = 4 -> recode16_65; kGWin = 16 -> 16 signed
+// radix-2^16 digits d in [-2^15, 2^15) stored as e = d + 2^15, two per word (digit
+// 2w in the low half of word w), and the top digit (0 or 1) in word 8.
+CG_HD void recode_g(uint32_t out[9], const uint32_t k[8]) {
+  if (kGWin == 4) {
+    recode16_65(out, k);
+    return;
+  }
+  uint32_t carry = 0;
+  CG_UNROLL for (int w = 0; w < 8; ++w) {
+    const uint32_t lo = (k[w] & 0xffffu) + carry;
+    carry = lo >= 0x8000u;
+    const uint32_t e0 = lo + 0x8000u - (carry << 16);
+    const uint32_t hi = (k[w] >> 16) + carry;
+    carry = hi >= 0x8000u;
+    const uint32_t e1 = hi + 0x8000u - (carry << 16);
+    out[w] = e0 | e1 << 16;
+  }
+  out[8] = carry + 0x8000u;
+}
+
 // Phase 1: everything up to the scalars; returns the pre-verdict
 // (V_* codes of cg_ed25519.h: 0 accept .. 4 arg-empty, 0xff compute).
 template <class C>
@@ -278,13 +308,13 @@ CG_HD uint32_t ecdsa_prep(const uint32_t qx[8], const uint32_t qy[8], uint32_t d
   mn_inv<C>(w, s);
   mn_mulmod<C>(u1, e, w);
   mn_mulmod<C>(u2, r, w);
-  recode16_65(d1, u1);
+  recode_g(d1, u1);
   recode16_65(d2, u2);
   return 0xff;
 }
 
 // P = u1 G + u2 Q from the packed digits; getQ(k, jpt&) loads k*Q (k = 1..8),
-// getG(k, jpt&) loads affine k*G.
+// getG(k, jpt&) loads affine k*G (k = 1 .. 2^(kGWin-1)).
 template <class C, typename GetQ, typename GetG>
 CG_HD void ecdsa_joint(jpt& acc, uint32_t d1[9], uint32_t d2[9], GetQ&& getQ, GetG&& getG) {
   jpt t;
@@ -294,15 +324,24 @@ CG_HD void ecdsa_joint(jpt& acc, uint32_t d1[9], uint32_t d2[9], GetQ&& getQ, Ge
     if (i != 64) {
       CG_NOUNROLL for (int k = 0; k < 4; ++k) ec_dbl<C>(acc, acc);
     }
-    const uint32_t eg = i == 64 ? (d1[8] & 15) : (d1[7] >> 28);  // digit of u1 (G)
     const uint32_t eq = i == 64 ? (d2[8] & 15) : (d2[7] >> 28);  // digit of u2 (Q)
+    uint32_t eg = 0, has_g = 1;                                   // digit of u1 (G)
+    if (kGWin == 4) {
+      eg = i == 64 ? (d1[8] & 15) : (d1[7] >> 28);
+    } else {
+      has_g = (i & 3) == 0;  // one 16-bit digit every fourth position
+      eg = i == 64 ? d1[8] : d1[7] >> 16;
+    }
     if (i != 64) {
-      CG_UNROLL for (int w = 7; w > 0; --w) {
-        d1[w] = d1[w] << 4 | d1[w - 1] >> 28;
-        d2[w] = d2[w] << 4 | d2[w - 1] >> 28;
-      }
-      d1[0] <<= 4;
+      CG_UNROLL for (int w = 7; w > 0; --w) d2[w] = d2[w] << 4 | d2[w - 1] >> 28;
       d2[0] <<= 4;
+      if (kGWin == 4) {
+        CG_UNROLL for (int w = 7; w > 0; --w) d1[w] = d1[w] << 4 | d1[w - 1] >> 28;
+        d1[0] <<= 4;
+      } else if (has_g) {
+        CG_UNROLL for (int w = 7; w > 0; --w) d1[w] = d1[w] << 16 | d1[w - 1] >> 16;
+        d1[0] <<= 16;
+      }
     }
     // Q part
     {
@@ -315,8 +354,9 @@ CG_HD void ecdsa_joint(jpt& acc, uint32_t d1[9], uint32_t d2[9], GetQ&& getQ, Ge
       ec_add<C, false>(acc, acc, t, a == 0);
     }
     // G part (affine)
-    {
-      const uint32_t neg = eg < 8, a = neg ? 8 - eg : eg - 8;
+    if (has_g) {
+      constexpr uint32_t kHalf = 1u << (kGWin - 1);
+      const uint32_t neg = eg < kHalf, a = neg ? kHalf - eg : eg - kHalf;
       getG(a == 0 ? 1u : a, t);
       uint32_t ny[8];
       fp_neg<C>(ny, t.Y);
@@ -364,28 +404,34 @@ CG_HD void ecdsa_q_table(const uint32_t qx[8], const uint32_t qy[8], Put&& put) 
   }
 }
 
-// Affine k*G (k = 1..8) for the shared generator table (host-side setup).
+// Affine k*G (1 <= k < 2^17) for the shared generator table: left-to-right binary
+// with the exact formulas, then one inversion.  One lane per entry at context
+// creation (and on the host for the tests).
 template <class C>
-CG_HD void ecdsa_g_table(jpt tab[9]) {
+CG_HD void ecdsa_g_entry(uint32_t k, uint32_t x[8], uint32_t y[8]) {
   const uint32_t k1x[8] = {0x16F81798u, 0x59F2815Bu, 0x2DCE28D9u, 0x029BFCDBu, 0xCE870B07u, 0x55A06295u, 0xF9DCBBACu, 0x79BE667Eu};
   const uint32_t k1y[8] = {0xFB10D4B8u, 0x9C47D08Fu, 0xA6855419u, 0xFD17B448u, 0x0E1108A8u, 0x5DA4FBFCu, 0x26A3C465u, 0x483ADA77u};
   const uint32_t r1x[8] = {0xD898C296u, 0xF4A13945u, 0x2DEB33A0u, 0x77037D81u, 0x63A440F2u, 0xF8BCE6E5u, 0xE12C4247u, 0x6B17D1F2u};
   const uint32_t r1y[8] = {0x37BF51F5u, 0xCBB64068u, 0x6B315ECEu, 0x2BCE3357u, 0x7C0F9E16u, 0x8EE7EB4Au, 0xFE1A7F9Bu, 0x4FE342E2u};
-  uint32_t gx[8], gy[8];
-  for (int i = 0; i < 8; ++i) {
-    gx[i] = C::kScheme == 2 ? k1x[i] : r1x[i];
-    gy[i] = C::kScheme == 2 ? k1y[i] : r1y[i];
+  jpt g, acc;
+  CG_UNROLL for (int i = 0; i < 8; ++i) {
+    g.X[i] = C::kScheme == 2 ? k1x[i] : r1x[i];
+    g.Y[i] = C::kScheme == 2 ? k1y[i] : r1y[i];
+    g.Z[i] = i == 0;
+    acc.X[i] = acc.Y[i] = acc.Z[i] = 0;
   }
-  ecdsa_q_table<C>(gx, gy, [&](int k, const jpt& p) {
-    uint32_t zi[8], zi2[8], zi3[8];
-    fp_inv<C>(zi, p.Z);
-    fp_sqr<C>(zi2, zi);
-    fp_mul<C>(zi3, zi2, zi);
-    fp_mul<C>(tab[k].X, p.X, zi2);
-    fp_mul<C>(tab[k].Y, p.Y, zi3);
-    for (int i = 0; i < 8; ++i) tab[k].Z[i] = i == 0;
-    tab[k].inf = 0;
-  });
+  g.inf = 0;
+  acc.inf = 1;
+  CG_NOUNROLL for (int b = 16; b >= 0; --b) {
+    ec_dbl<C>(acc, acc);
+    if ((k >> b) & 1) ec_add<C, true>(acc, acc, g, 0);
+  }
+  uint32_t zi[8], zi2[8], zi3[8];
+  fp_inv<C>(zi, acc.Z);
+  fp_sqr<C>(zi2, zi);
+  fp_mul<C>(zi3, zi2, zi);
+  fp_mul<C>(x, acc.X, zi2);
+  fp_mul<C>(y, acc.Y, zi3);
 }
 
 }  // namespace cg

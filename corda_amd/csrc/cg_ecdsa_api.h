@@ -21,7 +21,7 @@ struct EcdsaBatch {
   uint32_t* msg_len = nullptr;  // [n]
 };
 
-hipError_t ecdsa_consts_create(EcdsaConsts** out);
+hipError_t ecdsa_consts_create(EcdsaConsts** out, hipStream_t s);
 void ecdsa_consts_free(EcdsaConsts* c);
 // Stages one curve's subset into the SoA buffers of b (allocated by the caller:
 // index[n] already uploaded, q[16n], rs[16n], der/sig_len/msg_len[n], msg_off[n]).

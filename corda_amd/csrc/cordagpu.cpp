@@ -355,7 +355,7 @@ cg_status cg_open(int device, cg_ctx** out) {
     cg_close(ctx);
     return CG_E_DEVICE;
   }
-  if (cg::ecdsa_consts_create(&ctx->ec) != hipSuccess) {
+  if (cg::ecdsa_consts_create(&ctx->ec, ctx->stream) != hipSuccess) {
     cg_close(ctx);
     return CG_E_DEVICE;
   }

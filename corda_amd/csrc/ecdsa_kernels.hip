@@ -101,9 +101,6 @@ __global__ __launch_bounds__(256) void cg_ecdsa_msm(const uint32_t* __restrict__
                                                     const uint32_t* __restrict__ gtab_g, uint32_t n, uint32_t cap,
                                                     uint32_t scap, const uint32_t* __restrict__ out_index,
                                                     uint8_t* __restrict__ verdict) {
-  __shared__ uint32_t gtab[8 * 16];
-  for (int t = threadIdx.x; t < 8 * 16; t += blockDim.x) gtab[t] = gtab_g[t];
-  __syncthreads();
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint32_t dst = out_index[i];
@@ -130,12 +127,17 @@ __global__ __launch_bounds__(256) void cg_ecdsa_msm(const uint32_t* __restrict__
         p.inf = 0;
       },
       [&](uint32_t k, jpt& p) {
-        const uint32_t* g = gtab + (k - 1) * 16;
-        CG_UNROLL for (int w = 0; w < 8; ++w) {
-          p.X[w] = g[w];
-          p.Y[w] = g[8 + w];
-          p.Z[w] = w == 0;
+        // affine k*G: 64 bytes, four 16-byte loads from the L2-resident shared table
+        const uint4* g = reinterpret_cast<const uint4*>(gtab_g + (size_t)k * 16);
+        CG_UNROLL for (int q = 0; q < 4; ++q) {
+          const uint4 v = g[q];
+          uint32_t* dst = q < 2 ? p.X + 4 * q : p.Y + 4 * (q - 2);
+          dst[0] = v.x;
+          dst[1] = v.y;
+          dst[2] = v.z;
+          dst[3] = v.w;
         }
+        CG_UNROLL for (int w = 0; w < 8; ++w) p.Z[w] = w == 0;
         p.inf = 0;
       });
   verdict[dst] = (uint8_t)v;
@@ -143,15 +145,18 @@ __global__ __launch_bounds__(256) void cg_ecdsa_msm(const uint32_t* __restrict__
 
 inline dim3 grid_for(uint32_t n) { return dim3((n + 255) / 256); }
 
+// The shared generator table of curve C: entry k = affine k*G (16 words: x then y,
+// LE limbs), k = 1 .. kGTabEntries - 1; entry 0 unused (zero).  One lane per entry.
 template <class C>
-void g_table_words(uint32_t out[128]) {
-  jpt tab[9];
-  ecdsa_g_table<C>(tab);
-  for (int k = 1; k <= 8; ++k)
-    for (int w = 0; w < 8; ++w) {
-      out[(k - 1) * 16 + w] = tab[k].X[w];
-      out[(k - 1) * 16 + 8 + w] = tab[k].Y[w];
-    }
+__global__ __launch_bounds__(256) void cg_ecdsa_gtab_build(uint32_t* __restrict__ out) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= kGTabEntries) return;
+  uint32_t x[8] = {0, 0, 0, 0, 0, 0, 0, 0}, y[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (k) ecdsa_g_entry<C>(k, x, y);
+  CG_UNROLL for (int w = 0; w < 8; ++w) {
+    out[(size_t)k * 16 + w] = x[w];
+    out[(size_t)k * 16 + 8 + w] = y[w];
+  }
 }
 
 hipError_t ensure_scratch(EcdsaConsts* c, uint32_t need) {
@@ -191,18 +196,24 @@ hipError_t launch_msm(const EcdsaBatch& b, EcdsaConsts* c, uint32_t base, uint32
 
 namespace cg {
 
-hipError_t ecdsa_consts_create(EcdsaConsts** out) {
+hipError_t ecdsa_consts_create(EcdsaConsts** out, hipStream_t s) {
   EcdsaConsts* c = new EcdsaConsts();
-  uint32_t w[2][128];
-  g_table_words<CurveK1>(w[0]);
-  g_table_words<CurveR1>(w[1]);
-  for (int k = 0; k < 2; ++k) {
-    hipError_t e = hipMalloc((void**)&c->gtab[k], sizeof w[k]);
-    if (e == hipSuccess) e = hipMemcpy(c->gtab[k], w[k], sizeof w[k], hipMemcpyHostToDevice);
-    if (e != hipSuccess) {
-      ecdsa_consts_free(c);
-      return e;
-    }
+  const size_t bytes = (size_t)kGTabEntries * 16 * sizeof(uint32_t);
+  hipError_t e = hipSuccess;
+  for (int k = 0; k < 2 && e == hipSuccess; ++k) e = hipMalloc((void**)&c->gtab[k], bytes);
+  const dim3 grid((kGTabEntries + 255) / 256);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(cg_ecdsa_gtab_build<CurveK1>, grid, dim3(256), 0, s, c->gtab[0]);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(cg_ecdsa_gtab_build<CurveR1>, grid, dim3(256), 0, s, c->gtab[1]);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) {
+    ecdsa_consts_free(c);
+    return e;
   }
   *out = c;
   return hipSuccess;

@@ -102,18 +102,26 @@ int cgh_ed25519_verify(const uint8_t* pk_bytes, const uint8_t* sig_bytes, uint32
 // ------------------------------------------------------------------ ECDSA
 #include "cg_ecdsa.h"
 
+// the device's shared generator table (kGTabEntries affine points), built on the host
+// with the same code
 template <class C>
-static void g_table(jpt tab[9]) { ecdsa_g_table<C>(tab); }
+static const jpt* g_table() {
+  static jpt* tab = nullptr;
+  if (!tab) {
+    tab = new jpt[kGTabEntries];
+    for (uint32_t k = 1; k < kGTabEntries; ++k) {
+      ecdsa_g_entry<C>(k, tab[k].X, tab[k].Y);
+      for (int i = 0; i < 8; ++i) tab[k].Z[i] = i == 0;
+      tab[k].inf = 0;
+    }
+  }
+  return tab;
+}
 
 template <class C>
 static int ecdsa_verify_host(const uint8_t* q_be, const uint8_t* sig, uint32_t sig_len, const uint8_t* msg,
                              uint32_t msg_len, uint32_t mode) {
-  static jpt gtab[9];
-  static int init = 0;
-  if (!init) {
-    g_table<C>(gtab);
-    init = 1;
-  }
+  const jpt* gtab = g_table<C>();
   uint32_t qw[16], qx[8], qy[8], r[8], s[8], nn[8], d1[9], d2[9];
   memcpy(qw, q_be, 64);
   be_words_to_limbs(qx, qw);
@@ -158,11 +166,11 @@ uint32_t cgh_der_parse(int scheme, const uint8_t* sig, uint32_t n, uint32_t* r, 
 // x||y (LE limbs), or 1 when the result is the point at infinity.
 template <class C>
 static int joint_host(const uint32_t* u1, const uint32_t* u2, const uint32_t* qx, const uint32_t* qy, uint32_t* out) {
-  jpt gtab[9], qtab[9], acc;
-  g_table<C>(gtab);
+  jpt qtab[9], acc;
+  const jpt* gtab = g_table<C>();
   ecdsa_q_table<C>(qx, qy, [&](int k, const jpt& p) { qtab[k] = p; });
   uint32_t d1[9], d2[9];
-  recode16_65(d1, u1);
+  recode_g(d1, u1);
   recode16_65(d2, u2);
   ecdsa_joint<C>(acc, d1, d2, [&](uint32_t k, jpt& p) { p = qtab[k]; }, [&](uint32_t k, jpt& p) { p = gtab[k]; });
   if (acc.inf) return 1;
