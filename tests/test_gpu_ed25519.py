@@ -141,3 +141,48 @@ def test_config2_scale_properties(gpu_ctx, oracle):
     sub = w.subset(np.flatnonzero(adv))
     exp = oracle_verdicts(oracle, sub, MODE_IS_VALID)
     assert np.array_equal(got[adv], exp)
+
+
+def test_reference_message_shapes_all_schemes(gpu_ctx, oracle):
+    """CryptoUtilsTest.kt:123-286 shapes for all three schemes in one ragged batch:
+    a 1 MB message, 100 zero bytes, a 1-byte message, a 1 KB message; each signed
+    (valid), with sig[0] incremented (reject / malformed DER), an empty signature and
+    empty clear data (doVerify: IllegalArgumentException; isValid: engine outcome)."""
+    rng = np.random.default_rng(17)
+    msgs = [rng.integers(0, 256, 1 << 20, dtype=np.uint8).tobytes(), bytes(100), b"\x07",
+            rng.integers(0, 256, 1024, dtype=np.uint8).tobytes()]
+    schemes = [4, 3, 2]
+    rows = [(s, m) for s in schemes for m in msgs]
+    n = len(rows)
+    arena = np.frombuffer(b"".join(m for _, m in rows) + bytes(8), dtype=np.uint8).copy()
+    msg_len = np.array([len(m) for _, m in rows], dtype=np.uint32)
+    msg_off = np.concatenate([[0], np.cumsum(msg_len[:-1])]).astype(np.uint64)
+    sch = np.array([s for s, _ in rows], dtype=np.uint8)
+    pk = np.zeros((n, 64), np.uint8)
+    sig = np.zeros((n, 72), np.uint8)
+    sl = np.zeros(n, np.uint32)
+    assert datagen.lib().dg_sign_batch(n, sch.ctypes.data, 4242, pk.ctypes.data, 64, sig.ctypes.data, 72,
+                                       sl.ctypes.data, arena.ctypes.data, msg_off.ctypes.data, msg_len.ctypes.data,
+                                       8) == 0
+    # variants: valid, sig[0]++, empty signature, empty message
+    reps = 4
+    sch4, pk4, sig4 = np.tile(sch, reps), np.tile(pk, (reps, 1)), np.tile(sig, (reps, 1))
+    sl4, off4, len4 = np.tile(sl, reps), np.tile(msg_off, reps), np.tile(msg_len, reps)
+    sig4[n:2 * n, 0] += 1
+    sl4[2 * n:3 * n] = 0
+    len4[3 * n:] = 0
+    w = datagen.Workload(4 * n, sch4, pk4, 64, sig4, 72, sl4, arena, off4, len4)
+    for mode in (MODE_IS_VALID, MODE_DO_VERIFY):
+        exp = oracle_verdicts(oracle, w, mode)
+        got = gpu_verdicts(gpu_ctx, w, mode)
+        assert np.array_equal(got, exp), (mode, got.tolist(), exp.tolist())
+        assert (got[:n] == ACCEPT).all() and (got[n:2 * n] != ACCEPT).all()
+        if mode == MODE_DO_VERIFY:
+            assert (got[2 * n:] == 4).all()  # ARG_EMPTY for empty signature / clear data
+
+
+def test_empty_batch_is_ok(gpu_ctx):
+    v = np.zeros(1, np.uint8)
+    st = gpu_ctx.lib.cg_verify_batch(gpu_ctx.h, 0, MODE_IS_VALID, None, None, 64, None, 64, None, None, 0, None, None,
+                                     ptr(v), None)
+    assert st == 0

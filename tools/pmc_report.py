@@ -115,8 +115,9 @@ def main():
         e = kernels.get(f"cg_ed25519_{k}", {})
         traffic[f"ed25519_{k}_bytes_per_launch"] = e.get("hbm_bytes_per_launch")
         traffic[f"ed25519_{k}_valu_instr_per_verify"] = e.get("valu_instr_per_verify")
-    with open(os.path.join(prof, "pmc_traffic.json"), "w") as f:
-        json.dump(traffic, f, indent=1)
+    if "--no-traffic" not in sys.argv:  # pmc_traffic.json feeds bench.py's default (Ed25519) line
+        with open(os.path.join(prof, "pmc_traffic.json"), "w") as f:
+            json.dump(traffic, f, indent=1)
     print(json.dumps({k: {kk: vv for kk, vv in v.items() if kk != "counters"} for k, v in kernels.items()},
                      indent=1))
 
