@@ -12,7 +12,11 @@
 #define CG_HDM __host__ __device__ __forceinline__
 #define CG_UNROLL _Pragma("unroll")
 #define CG_NOUNROLL _Pragma("unroll 1")
+// lambdas called more than once must still inline: an outlined call passes the
+// point arrays by pointer, i.e. through scratch memory
+#define CG_LINLINE __attribute__((always_inline))
 #else
+#define CG_LINLINE
 #define CG_HD static inline
 #define CG_DEV static inline
 #define CG_HDM inline

@@ -292,14 +292,14 @@ CG_HD void recode_g(uint32_t out[9], const uint32_t k[8]) {
 // Phase 1: everything up to the scalars; returns the pre-verdict
 // (V_* codes of cg_ed25519.h: 0 accept .. 4 arg-empty, 0xff compute).
 template <class C>
-CG_HD uint32_t ecdsa_prep(const uint32_t qx[8], const uint32_t qy[8], uint32_t der_status, const uint32_t r[8],
-                          const uint32_t s[8], uint32_t sig_len, const uint8_t* msg, uint32_t msg_len, uint32_t mode,
-                          uint32_t d1[9], uint32_t d2[9]) {
+CG_HD uint32_t ecdsa_prep_scalars(const uint32_t qx[8], const uint32_t qy[8], uint32_t der_status,
+                                  const uint32_t r[8], const uint32_t s[8], uint32_t sig_len, const uint8_t* msg,
+                                  uint32_t msg_len, uint32_t mode, uint32_t u1[8], uint32_t u2[8]) {
   if (!ec_on_curve<C>(qx, qy)) return 3;                        // KEY_INVALID
   if (mode == 1 && (sig_len == 0 || msg_len == 0)) return 4;      // ARG_EMPTY (doVerify)
   if (der_status == DER_MALFORMED) return 2;                      // SIG_MALFORMED
   if (der_status == DER_RANGE) return 1;                          // REJECT
-  uint32_t hbe[8], e[8], nn[8], t[8], w[8], u1[8], u2[8];
+  uint32_t hbe[8], e[8], nn[8], t[8], w[8];
   sha256_mem(hbe, msg, msg_len);
   CG_UNROLL for (int i = 0; i < 8; ++i) e[i] = hbe[7 - i];
   C::n(nn);
@@ -308,6 +308,16 @@ CG_HD uint32_t ecdsa_prep(const uint32_t qx[8], const uint32_t qy[8], uint32_t d
   mn_inv<C>(w, s);
   mn_mulmod<C>(u1, e, w);
   mn_mulmod<C>(u2, r, w);
+  return 0xff;
+}
+
+template <class C>
+CG_HD uint32_t ecdsa_prep(const uint32_t qx[8], const uint32_t qy[8], uint32_t der_status, const uint32_t r[8],
+                          const uint32_t s[8], uint32_t sig_len, const uint8_t* msg, uint32_t msg_len, uint32_t mode,
+                          uint32_t d1[9], uint32_t d2[9]) {
+  uint32_t u1[8], u2[8];
+  const uint32_t pre = ecdsa_prep_scalars<C>(qx, qy, der_status, r, s, sig_len, msg, msg_len, mode, u1, u2);
+  if (pre != 0xff) return pre;
   recode_g(d1, u1);
   recode16_65(d2, u2);
   return 0xff;
@@ -367,11 +377,237 @@ CG_HD void ecdsa_joint(jpt& acc, uint32_t d1[9], uint32_t d2[9], GetQ&& getQ, Ge
   }
 }
 
-// Phase 2: joint multiplication + the projective x check.  Returns ACCEPT (0) / REJECT (1).
-template <class C, typename GetQ, typename GetG>
-CG_HD uint32_t ecdsa_msm_check(uint32_t d1[9], uint32_t d2[9], const uint32_t r[8], GetQ&& getQ, GetG&& getG) {
-  jpt acc;
-  ecdsa_joint<C>(acc, d1, d2, getQ, getG);
+// ------------------------------------------------------------ secp256k1 GLV
+// secp256k1 has an efficient endomorphism phi(x, y) = (beta x, y) = [lambda](x, y)
+// on every point (cofactor 1).  u2 Q = k1 Q + k2 phi(Q) with |k1|, |k2| < 2^128
+// (Gallant-Lambert-Vanstone; the lattice constants and the rounding by
+// g = round(2^384 b / n) are those of libsecp256k1's scalar_split_lambda), so the
+// variable-base part needs 128 doublings instead of 256 and u1 G is taken from two
+// fixed tables (G and 2^128 G).  The split is exact: k1 = u2 - k2 lambda mod n is
+// computed from k2, so k1 + k2 lambda == u2 whatever the rounding, and the group
+// element (hence the verdict) is the same; a split whose halves exceed 129 bits
+// (never seen; guarded anyway) falls back to (|u2|, 0) on a full-length loop.
+struct GlvK1 {
+  CG_HDM static void lambda(uint32_t r[8]) {
+    const uint32_t v[8] = {0x1B23BD72u, 0xDF02967Cu, 0x20816678u, 0x122E22EAu,
+                           0x8812645Au, 0xA5261C02u, 0xC05C30E0u, 0x5363AD4Cu};
+    CG_UNROLL for (int i = 0; i < 8; ++i) r[i] = v[i];
+  }
+  CG_HDM static void beta(uint32_t r[8]) {
+    const uint32_t v[8] = {0x719501EEu, 0xC1396C28u, 0x12F58995u, 0x9CF04975u,
+                           0xAC3434E9u, 0x6E64479Eu, 0x657C0710u, 0x7AE96A2Bu};
+    CG_UNROLL for (int i = 0; i < 8; ++i) r[i] = v[i];
+  }
+  CG_HDM static void g1(uint32_t r[8]) {  // round(2^384 b2 / n)
+    const uint32_t v[8] = {0x45DBB031u, 0xE893209Au, 0x71E8CA7Fu, 0x3DAA8A14u,
+                           0x9284EB15u, 0xE86C90E4u, 0xA7D46BCDu, 0x3086D221u};
+    CG_UNROLL for (int i = 0; i < 8; ++i) r[i] = v[i];
+  }
+  CG_HDM static void g2(uint32_t r[8]) {  // round(2^384 (-b1) / n)
+    const uint32_t v[8] = {0x8AC47F71u, 0x1571B4AEu, 0x9DF506C6u, 0x221208ACu,
+                           0x0ABFE4C4u, 0x6F547FA9u, 0x010E8828u, 0xE4437ED6u};
+    CG_UNROLL for (int i = 0; i < 8; ++i) r[i] = v[i];
+  }
+  CG_HDM static void minus_b1(uint32_t r[8]) {  // -b1 (128 bits)
+    const uint32_t v[8] = {0x0ABFE4C3u, 0x6F547FA9u, 0x010E8828u, 0xE4437ED6u, 0, 0, 0, 0};
+    CG_UNROLL for (int i = 0; i < 8; ++i) r[i] = v[i];
+  }
+  CG_HDM static void minus_b2(uint32_t r[8]) {  // n - b2
+    const uint32_t v[8] = {0x3DB1562Cu, 0xD765CDA8u, 0x0774346Du, 0x8A280AC5u,
+                           0xFFFFFFFEu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+    CG_UNROLL for (int i = 0; i < 8; ++i) r[i] = v[i];
+  }
+};
+
+// (k g) >> 384, rounded (k, g < 2^256).
+CG_HD void glv_round_mul(uint32_t c[8], const uint32_t k[8], const uint32_t g[8]) {
+  uint32_t t[16];
+  mp_mul256(t, k, g);
+  const uint32_t round = t[11] >> 31;
+  uint64_t acc = round;
+  CG_UNROLL for (int i = 0; i < 4; ++i) {
+    acc += t[12 + i];
+    c[i] = (uint32_t)acc;
+    acc >>= 32;
+  }
+  CG_UNROLL for (int i = 4; i < 8; ++i) c[i] = 0;
+}
+
+CG_HD void mn_sub_mod(uint32_t r[8], const uint32_t a[8], const uint32_t b[8], const uint32_t nn[8]) {
+  uint32_t t[8];
+  const uint32_t bw = mp_sub(r, a, b);
+  mp_add(t, r, nn);
+  mp_select(r, r, t, bw);
+}
+
+// |r| as a signed residue mod n (r or n - r, whichever is <= n/2) and its sign.
+CG_HD uint32_t glv_abs(uint32_t out[8], const uint32_t r[8], const uint32_t nn[8]) {
+  uint32_t half[8], t[8];
+  CG_UNROLL for (int i = 0; i < 8; ++i) half[i] = nn[i] >> 1 | (i < 7 ? nn[i + 1] << 31 : 0u);
+  const uint32_t neg = mp_lt(half, r);
+  mp_sub(t, nn, r);
+  mp_select(out, r, t, neg);
+  return neg;
+}
+
+CG_HD uint32_t mp_bitlen256(const uint32_t a[8]) {
+  uint32_t bl = 0;
+  CG_UNROLL for (int w = 0; w < 8; ++w) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const uint32_t lz = __clz((int)a[w]);
+#else
+    const uint32_t lz = a[w] ? (uint32_t)__builtin_clz(a[w]) : 32u;
+#endif
+    bl = a[w] ? 32u * (w + 1) - lz : bl;
+  }
+  return bl;
+}
+
+// u2 -> (|k1|, |k2|, signs) with u2 == k1 + k2 lambda (mod n); returns the number of
+// signed radix-16 digits the joint loop needs (>= 33: the 2^128 G table's top digit
+// sits at bit 128).
+CG_HD uint32_t glv_split(const uint32_t u2[8], uint32_t k1[8], uint32_t k2[8], uint32_t& neg1, uint32_t& neg2) {
+  uint32_t nn[8], g[8], c1[8], c2[8], t1[8], t2[8], r1[8], r2[8], lam[8];
+  CurveK1::n(nn);
+  GlvK1::g1(g);
+  glv_round_mul(c1, u2, g);
+  GlvK1::g2(g);
+  glv_round_mul(c2, u2, g);
+  GlvK1::minus_b1(g);
+  mn_mulmod<CurveK1>(t1, c1, g);
+  GlvK1::minus_b2(g);
+  mn_mulmod<CurveK1>(t2, c2, g);
+  const uint32_t carry = mp_add(r2, t1, t2);  // t1 + t2 < 2n: one conditional subtraction
+  mp_sub(t1, r2, nn);
+  mp_select(r2, r2, t1, carry | !mp_lt(r2, nn));
+  GlvK1::lambda(lam);
+  mn_mulmod<CurveK1>(t1, r2, lam);
+  mn_sub_mod(r1, u2, t1, nn);
+  neg1 = glv_abs(k1, r1, nn);
+  neg2 = glv_abs(k2, r2, nn);
+  uint32_t bl = mp_bitlen256(k1);
+  const uint32_t b2 = mp_bitlen256(k2);
+  bl = b2 > bl ? b2 : bl;
+  if (bl > 129) {  // fallback: u2 Q on its own, full length
+    neg1 = glv_abs(k1, u2, nn);
+    neg2 = 0;
+    CG_UNROLL for (int i = 0; i < 8; ++i) k2[i] = 0;
+    bl = mp_bitlen256(k1);
+  }
+  const uint32_t nd = (bl + 3) / 4 + 1;  // nibbles plus the signed-recoding carry
+  return nd < 33 ? 33u : nd;
+}
+
+// secp256k1 phase 1 with the GLV split: dg = recode_g(u1), dk1/dk2 = recode16_65 of
+// |k1|, |k2|; nd / signs returned through `aux` (nd | neg1 << 8 | neg2 << 9).
+CG_HD uint32_t ecdsa_prep_k1glv(const uint32_t qx[8], const uint32_t qy[8], uint32_t der_status, const uint32_t r[8],
+                                const uint32_t s[8], uint32_t sig_len, const uint8_t* msg, uint32_t msg_len,
+                                uint32_t mode, uint32_t dg[9], uint32_t dk1[9], uint32_t dk2[9], uint32_t& aux) {
+  uint32_t u1[8], u2[8], k1[8], k2[8], neg1, neg2;
+  aux = 33;
+  const uint32_t pre =
+      ecdsa_prep_scalars<CurveK1>(qx, qy, der_status, r, s, sig_len, msg, msg_len, mode, u1, u2);
+  if (pre != 0xff) return pre;
+  const uint32_t nd = glv_split(u2, k1, k2, neg1, neg2);
+  recode_g(dg, u1);
+  recode16_65(dk1, k1);
+  recode16_65(dk2, k2);
+  aux = nd | neg1 << 8 | neg2 << 9;
+  return 0xff;
+}
+
+// x <<= 4 s (s uniform across the wave) on a 9-word (72-nibble) value.
+CG_HD void shl_nibbles9(uint32_t x[9], uint32_t s) {
+  const uint32_t ws = s >> 3, bs = 4 * (s & 7);
+  CG_UNROLL for (int k = 8; k >= 1; k >>= 1) {
+    if (ws & k) {
+      CG_UNROLL for (int w = 8; w >= 0; --w) x[w] = w >= k ? x[w - k] : 0u;
+    }
+  }
+  if (bs) {
+    CG_UNROLL for (int w = 8; w >= 1; --w) x[w] = (x[w] << bs) | (x[w - 1] >> (32 - bs));
+    x[0] <<= bs;
+  }
+}
+
+// P = u1 G + k1 Q + k2 phi(Q) over nd nibble positions (nd uniform, >= 33).
+// dk1/dk2: recode16_65 digits of |k1|, |k2| (signs neg1/neg2); dg: recode_g digits of
+// u1.  getQ(k, jpt&) loads k*Q (k = 1..8); getG(t, k, jpt&) loads affine k*G (t = 0)
+// or k*2^128 G (t = 1).
+template <typename GetQ, typename GetG>
+CG_HD void ecdsa_joint_glv(jpt& acc, uint32_t nd, uint32_t dk1[9], uint32_t dk2[9], uint32_t neg1, uint32_t neg2,
+                           const uint32_t dg[9], GetQ&& getQ, GetG&& getG) {
+  using C = CurveK1;
+  uint32_t glo[4], ghi[4];
+  CG_UNROLL for (int w = 0; w < 4; ++w) {
+    glo[w] = dg[w];      // digits 0..7 (G table)
+    ghi[w] = dg[4 + w];  // digits 8..15 (2^128 G table)
+  }
+  const uint32_t gtop = dg[8];  // top carry digit of u1
+  shl_nibbles9(dk1, 72 - nd);  // digit nd-1 to the top nibble
+  shl_nibbles9(dk2, 72 - nd);
+  jpt t;
+  CG_UNROLL for (int i = 0; i < 8; ++i) { acc.X[i] = 0; acc.Y[i] = 0; acc.Z[i] = 0; }
+  acc.inf = 1;
+  CG_NOUNROLL for (int i = (int)nd - 1; i >= 0; --i) {
+    if (i != (int)nd - 1) {
+      CG_NOUNROLL for (int k = 0; k < 4; ++k) ec_dbl<C>(acc, acc);
+    }
+    const uint32_t e1 = dk1[8] >> 28, e2 = dk2[8] >> 28;
+    CG_UNROLL for (int w = 8; w > 0; --w) {
+      dk1[w] = dk1[w] << 4 | dk1[w - 1] >> 28;
+      dk2[w] = dk2[w] << 4 | dk2[w - 1] >> 28;
+    }
+    dk1[0] <<= 4;
+    dk2[0] <<= 4;
+    // +-|digit| * Q, then +-|digit| * phi(Q): one add site in a rolled loop keeps
+    // the register footprint of a single Jacobian addition
+    CG_NOUNROLL for (uint32_t slot = 0; slot < 2; ++slot) {
+      const uint32_t e = slot ? e2 : e1;
+      const uint32_t neg = (e < 8) ^ (slot ? neg2 : neg1), a = e < 8 ? 8 - e : e - 8;
+      getQ(a == 0 ? 1u : a, t);
+      if (slot) {
+        uint32_t beta[8], bx[8];
+        GlvK1::beta(beta);
+        fp_mul<C>(bx, t.X, beta);  // phi(X:Y:Z) = (beta X : Y : Z)
+        CG_UNROLL for (int w = 0; w < 8; ++w) t.X[w] = bx[w];
+      }
+      uint32_t ny[8];
+      fp_neg<C>(ny, t.Y);
+      mp_select(t.Y, t.Y, ny, neg);
+      t.inf = 0;
+      ec_add<C, false>(acc, acc, t, a == 0);
+    }
+    // +-|digit| * (k G or k 2^128 G) from the shared tables: 16-bit windows at bits 16 j
+    if ((i & 3) == 0 && i <= 32) {
+      uint32_t eg = 0, eh = gtop;  // at bit 128 only the top carry digit of u1 (2^128 * 2^128)
+      if (i != 32) {
+        eg = glo[3] >> 16;  // digit j (G table)
+        eh = ghi[3] >> 16;  // digit j + 8 (2^128 G table)
+        CG_UNROLL for (int w = 3; w > 0; --w) {
+          glo[w] = glo[w] << 16 | glo[w - 1] >> 16;
+          ghi[w] = ghi[w] << 16 | ghi[w - 1] >> 16;
+        }
+        glo[0] <<= 16;
+        ghi[0] <<= 16;
+      }
+      CG_NOUNROLL for (uint32_t tb = i == 32 ? 1u : 0u; tb < 2; ++tb) {
+        const uint32_t e = tb ? eh : eg;
+        const uint32_t neg = e < 0x8000u, a = neg ? 0x8000u - e : e - 0x8000u;
+        getG(tb, a == 0 ? 1u : a, t);
+        uint32_t ny[8];
+        fp_neg<C>(ny, t.Y);
+        mp_select(t.Y, t.Y, ny, neg);
+        t.inf = 0;
+        ec_add<C, true>(acc, acc, t, a == 0);
+      }
+    }
+  }
+}
+
+// The projective x check of B.4/B.5 on the joint result.
+template <class C>
+CG_HD uint32_t ecdsa_x_check(const jpt& acc, const uint32_t r[8]) {
   if (acc.inf) return 1;
   // x(P) mod n == r  <=>  X == r Z^2  or  (r + n < p and X == (r + n) Z^2)
   uint32_t z2[8], rz[8], nn[8], pp[8], rn[8];
@@ -386,6 +622,14 @@ CG_HD uint32_t ecdsa_msm_check(uint32_t d1[9], uint32_t d2[9], const uint32_t r[
     if (mp_eq(rz, acc.X)) return 0;
   }
   return 1;
+}
+
+// Phase 2: joint multiplication + the projective x check.  Returns ACCEPT (0) / REJECT (1).
+template <class C, typename GetQ, typename GetG>
+CG_HD uint32_t ecdsa_msm_check(uint32_t d1[9], uint32_t d2[9], const uint32_t r[8], GetQ&& getQ, GetG&& getG) {
+  jpt acc;
+  ecdsa_joint<C>(acc, d1, d2, getQ, getG);
+  return ecdsa_x_check<C>(acc, r);
 }
 
 // k*Q, k = 1..8, Jacobian (Q affine, on the curve, prime order: no exceptions).
@@ -404,11 +648,12 @@ CG_HD void ecdsa_q_table(const uint32_t qx[8], const uint32_t qy[8], Put&& put) 
   }
 }
 
-// Affine k*G (1 <= k < 2^17) for the shared generator table: left-to-right binary
+// Affine k*G (or k*2^128 G, shift128 = 1; 1 <= k < 2^17) for the shared generator
+// tables: left-to-right binary
 // with the exact formulas, then one inversion.  One lane per entry at context
 // creation (and on the host for the tests).
 template <class C>
-CG_HD void ecdsa_g_entry(uint32_t k, uint32_t x[8], uint32_t y[8]) {
+CG_HD void ecdsa_g_entry(uint32_t k, uint32_t x[8], uint32_t y[8], uint32_t shift128 = 0) {
   const uint32_t k1x[8] = {0x16F81798u, 0x59F2815Bu, 0x2DCE28D9u, 0x029BFCDBu, 0xCE870B07u, 0x55A06295u, 0xF9DCBBACu, 0x79BE667Eu};
   const uint32_t k1y[8] = {0xFB10D4B8u, 0x9C47D08Fu, 0xA6855419u, 0xFD17B448u, 0x0E1108A8u, 0x5DA4FBFCu, 0x26A3C465u, 0x483ADA77u};
   const uint32_t r1x[8] = {0xD898C296u, 0xF4A13945u, 0x2DEB33A0u, 0x77037D81u, 0x63A440F2u, 0xF8BCE6E5u, 0xE12C4247u, 0x6B17D1F2u};
@@ -422,6 +667,20 @@ CG_HD void ecdsa_g_entry(uint32_t k, uint32_t x[8], uint32_t y[8]) {
   }
   g.inf = 0;
   acc.inf = 1;
+  CG_NOUNROLL for (uint32_t i = 0; i < 128 * shift128; ++i) ec_dbl<C>(g, g);  // 2^128 G (its own table)
+  if (shift128) {  // back to affine: the table loop adds g with the mixed formula
+    uint32_t zi[8], zi2[8], zi3[8], gx[8], gy[8];
+    fp_inv<C>(zi, g.Z);
+    fp_sqr<C>(zi2, zi);
+    fp_mul<C>(zi3, zi2, zi);
+    fp_mul<C>(gx, g.X, zi2);
+    fp_mul<C>(gy, g.Y, zi3);
+    CG_UNROLL for (int i = 0; i < 8; ++i) {
+      g.X[i] = gx[i];
+      g.Y[i] = gy[i];
+      g.Z[i] = i == 0;
+    }
+  }
   CG_NOUNROLL for (int b = 16; b >= 0; --b) {
     ec_dbl<C>(acc, acc);
     if ((k >> b) & 1) ec_add<C, true>(acc, acc, g, 0);

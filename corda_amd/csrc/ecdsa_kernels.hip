@@ -2,14 +2,19 @@
 // for gfx950, BouncyCastle 1.57 semantics (cg_ecdsa.h).
 //
 //   cg_der_parse<C>   staging-time pre-pass: strict DER -> r, s limbs + status
-//   cg_ecdsa_prep<C>  key check, SHA-256(M), s^-1 / u1 / u2 mod n, digits, k*Q table
-//   cg_ecdsa_msm<C>   u1 G + u2 Q (fixed 4-bit window, G table in LDS), x check
+//   cg_ecdsa_prep<C>  key check, SHA-256(M), s^-1 / u1 / u2 mod n, digits, k*Q table;
+//                     secp256k1 also splits u2 = k1 + k2 lambda (GLV, cg_ecdsa.h)
+//   cg_ecdsa_msm<C>   P-256: u1 G + u2 Q over 256 bits (4-bit Q windows, 16-bit G
+//                     windows); secp256k1: u1 G + k1 Q + k2 phi(Q) over ~129 bits
+//                     (G and 2^128 G tables); then the projective x check
+//   cg_ecdsa_gtab_build<C>  the shared generator tables (context creation)
 //
 // Device layout (cap = subset size, scap = scratch chunk):
 //   q[w*cap+i] (16 words: the 64-byte big-endian X||Y as staged little-endian
 //   words), rs[w*cap+i] (16 LE limbs: r then s), der[i], sig_len[i], msg_off[i],
-//   msg_len[i]; scratch status[i], digits[w*scap+i] (18 words), qtab[(e*24+w)*scap+i]
-//   (e = k-1 for k*Q, k = 1..8, X|Y|Z).
+//   msg_len[i]; scratch status[i] (verdict | digit count << 8 | signs << 16 for
+//   secp256k1), digits[w*scap+i] (27 words: u1 G digits, then k1 / k2 or u2
+//   nibbles), qtab[(e*24+w)*scap+i] (e = k-1 for k*Q, k = 1..8, X|Y|Z).
 #include <vector>
 
 #include "cg_ecdsa.h"
@@ -21,7 +26,7 @@ using namespace cg;
 namespace cg {
 
 struct EcdsaConsts {
-  uint32_t* gtab[2] = {nullptr, nullptr};  // [8][16] affine k*G, K1 then R1
+  uint32_t* gtab[2] = {nullptr, nullptr};  // affine k*G [kGTabEntries][16]; K1 also k*2^128 G after it
   uint32_t scap = 0;
   uint32_t* status = nullptr;
   uint32_t* digits = nullptr;
@@ -34,6 +39,15 @@ namespace {
 
 constexpr uint32_t kEcChunk = 1u << 20;
 constexpr int kQWords = 24;
+constexpr int kDigitWordsEc = 27;
+
+CG_DEV uint32_t wave_max_u32(uint32_t v) {
+  CG_UNROLL for (int o = 32; o >= 1; o >>= 1) {
+    const uint32_t u = (uint32_t)__shfl_xor((int)v, o, 64);
+    v = u > v ? u : v;
+  }
+  return v;
+}
 
 template <class C>
 __global__ __launch_bounds__(256) void cg_der_parse(const uint8_t* __restrict__ sig, size_t stride,
@@ -75,13 +89,18 @@ __global__ __launch_bounds__(256) void cg_ecdsa_prep(const uint32_t* __restrict_
     r[w] = rs[(size_t)w * cap + i];
     s[w] = rs[(size_t)(8 + w) * cap + i];
   }
-  const uint32_t pre =
-      ecdsa_prep<C>(qx, qy, der[i], r, s, sig_len[i], arena + msg_off[i], msg_len[i], mode, d1, d2);
-  status[i] = pre;
+  uint32_t pre, aux = 0, d3[9];
+  if constexpr (C::kScheme == 2) {
+    pre = ecdsa_prep_k1glv(qx, qy, der[i], r, s, sig_len[i], arena + msg_off[i], msg_len[i], mode, d1, d2, d3, aux);
+  } else {
+    pre = ecdsa_prep<C>(qx, qy, der[i], r, s, sig_len[i], arena + msg_off[i], msg_len[i], mode, d1, d2);
+  }
+  status[i] = pre | aux << 8;
   if (pre != 0xff) return;
   CG_UNROLL for (int w = 0; w < 9; ++w) {
     digits[(size_t)w * scap + i] = d1[w];
     digits[(size_t)(9 + w) * scap + i] = d2[w];
+    if constexpr (C::kScheme == 2) digits[(size_t)(18 + w) * scap + i] = d3[w];
   }
   ecdsa_q_table<C>(qx, qy, [&](int k, const jpt& p) {
     uint32_t* base = qtab + (size_t)(k - 1) * kQWords * scap + i;
@@ -93,8 +112,16 @@ __global__ __launch_bounds__(256) void cg_ecdsa_prep(const uint32_t* __restrict_
   });
 }
 
+// Two waves per SIMD (<= 256 VGPRs); the GLV loop keeps one add site per formula
+// (rolled slot loops) so it fits without scratch spills.
 template <class C>
-__global__ __launch_bounds__(256) void cg_ecdsa_msm(const uint32_t* __restrict__ rs,
+constexpr int ecdsa_msm_waves_min() { return 2; }
+template <class C>
+constexpr int ecdsa_msm_waves_max() { return 8; }
+
+template <class C>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ecdsa_msm_waves_min<C>(), ecdsa_msm_waves_max<C>())))
+void cg_ecdsa_msm(const uint32_t* __restrict__ rs,
                                                     const uint32_t* __restrict__ status,
                                                     const uint32_t* __restrict__ digits,
                                                     const uint32_t* __restrict__ qtab,
@@ -102,22 +129,24 @@ __global__ __launch_bounds__(256) void cg_ecdsa_msm(const uint32_t* __restrict__
                                                     uint32_t scap, const uint32_t* __restrict__ out_index,
                                                     uint8_t* __restrict__ verdict) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t st = i < n ? status[i] : 0u;
+  const bool live = i < n && (st & 0xff) == 0xff;
+  // secp256k1: every lane of the wave walks the longest split scalar's digits
+  const uint32_t nd = C::kScheme == 2 ? wave_max_u32(live ? (st >> 8) & 0xff : 0u) : 0u;
   if (i >= n) return;
   const uint32_t dst = out_index[i];
-  const uint32_t st = status[i];
-  if (st != 0xff) {
+  if (!live) {
     verdict[dst] = (uint8_t)st;
     return;
   }
-  uint32_t d1[9], d2[9], r[8];
+  uint32_t d1[9], d2[9], d3[9], r[8];
   CG_UNROLL for (int w = 0; w < 9; ++w) {
     d1[w] = digits[(size_t)w * scap + i];
     d2[w] = digits[(size_t)(9 + w) * scap + i];
+    d3[w] = C::kScheme == 2 ? digits[(size_t)(18 + w) * scap + i] : 0u;
   }
   CG_UNROLL for (int w = 0; w < 8; ++w) r[w] = rs[(size_t)w * cap + i];
-  const uint32_t v = ecdsa_msm_check<C>(
-      d1, d2, r,
-      [&](uint32_t k, jpt& p) {
+  auto getQ = [&](uint32_t k, jpt& p) CG_LINLINE {
         const uint32_t* base = qtab + (size_t)(k - 1) * kQWords * scap + i;
         CG_UNROLL for (int w = 0; w < 8; ++w) {
           p.X[w] = base[(size_t)w * scap];
@@ -125,10 +154,11 @@ __global__ __launch_bounds__(256) void cg_ecdsa_msm(const uint32_t* __restrict__
           p.Z[w] = base[(size_t)(16 + w) * scap];
         }
         p.inf = 0;
-      },
-      [&](uint32_t k, jpt& p) {
-        // affine k*G: 64 bytes, four 16-byte loads from the L2-resident shared table
-        const uint4* g = reinterpret_cast<const uint4*>(gtab_g + (size_t)k * 16);
+      };
+  auto getG = [&](uint32_t t, uint32_t k, jpt& p) CG_LINLINE {
+        // affine k*G (t = 0) or k*2^128 G (t = 1): 64 bytes, four 16-byte loads from the
+        // L2-resident shared table
+        const uint4* g = reinterpret_cast<const uint4*>(gtab_g + ((size_t)t * kGTabEntries + k) * 16);
         CG_UNROLL for (int q = 0; q < 4; ++q) {
           const uint4 v = g[q];
           uint32_t* dst = q < 2 ? p.X + 4 * q : p.Y + 4 * (q - 2);
@@ -139,7 +169,15 @@ __global__ __launch_bounds__(256) void cg_ecdsa_msm(const uint32_t* __restrict__
         }
         CG_UNROLL for (int w = 0; w < 8; ++w) p.Z[w] = w == 0;
         p.inf = 0;
-      });
+      };
+  uint32_t v;
+  if constexpr (C::kScheme == 2) {
+    jpt acc;
+    ecdsa_joint_glv(acc, nd, d2, d3, (st >> 16) & 1, (st >> 17) & 1, d1, getQ, getG);
+    v = ecdsa_x_check<C>(acc, r);
+  } else {
+    v = ecdsa_msm_check<C>(d1, d2, r, getQ, [&](uint32_t k, jpt& p) CG_LINLINE { getG(0, k, p); });
+  }
   verdict[dst] = (uint8_t)v;
 }
 
@@ -148,14 +186,15 @@ inline dim3 grid_for(uint32_t n) { return dim3((n + 255) / 256); }
 // The shared generator table of curve C: entry k = affine k*G (16 words: x then y,
 // LE limbs), k = 1 .. kGTabEntries - 1; entry 0 unused (zero).  One lane per entry.
 template <class C>
-__global__ __launch_bounds__(256) void cg_ecdsa_gtab_build(uint32_t* __restrict__ out) {
-  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= kGTabEntries) return;
+__global__ __launch_bounds__(256) void cg_ecdsa_gtab_build(uint32_t* __restrict__ out, uint32_t tables) {
+  const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= tables * kGTabEntries) return;
+  const uint32_t t = e / kGTabEntries, k = e % kGTabEntries;
   uint32_t x[8] = {0, 0, 0, 0, 0, 0, 0, 0}, y[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (k) ecdsa_g_entry<C>(k, x, y);
+  if (k) ecdsa_g_entry<C>(k, x, y, t);
   CG_UNROLL for (int w = 0; w < 8; ++w) {
-    out[(size_t)k * 16 + w] = x[w];
-    out[(size_t)k * 16 + 8 + w] = y[w];
+    out[(size_t)e * 16 + w] = x[w];
+    out[(size_t)e * 16 + 8 + w] = y[w];
   }
 }
 
@@ -168,7 +207,7 @@ hipError_t ensure_scratch(EcdsaConsts* c, uint32_t need) {
   c->status = c->digits = c->qtab = nullptr;
   c->scap = 0;
   hipError_t e = hipMalloc((void**)&c->status, (size_t)want * 4);
-  if (e == hipSuccess) e = hipMalloc((void**)&c->digits, (size_t)18 * want * 4);
+  if (e == hipSuccess) e = hipMalloc((void**)&c->digits, (size_t)kDigitWordsEc * want * 4);
   if (e == hipSuccess) e = hipMalloc((void**)&c->qtab, (size_t)8 * kQWords * want * 4);
   if (e == hipSuccess) c->scap = want;
   return e;
@@ -198,16 +237,19 @@ namespace cg {
 
 hipError_t ecdsa_consts_create(EcdsaConsts** out, hipStream_t s) {
   EcdsaConsts* c = new EcdsaConsts();
-  const size_t bytes = (size_t)kGTabEntries * 16 * sizeof(uint32_t);
+  // secp256k1 (GLV, ~129-bit loop): k*G and k*2^128 G; P-256 (256-bit loop): k*G
+  const uint32_t tables[2] = {2, 1};
   hipError_t e = hipSuccess;
-  for (int k = 0; k < 2 && e == hipSuccess; ++k) e = hipMalloc((void**)&c->gtab[k], bytes);
-  const dim3 grid((kGTabEntries + 255) / 256);
+  for (int k = 0; k < 2 && e == hipSuccess; ++k)
+    e = hipMalloc((void**)&c->gtab[k], (size_t)tables[k] * kGTabEntries * 16 * sizeof(uint32_t));
   if (e == hipSuccess) {
-    hipLaunchKernelGGL(cg_ecdsa_gtab_build<CurveK1>, grid, dim3(256), 0, s, c->gtab[0]);
+    hipLaunchKernelGGL(cg_ecdsa_gtab_build<CurveK1>, dim3((2 * kGTabEntries + 255) / 256), dim3(256), 0, s,
+                       c->gtab[0], tables[0]);
     e = hipGetLastError();
   }
   if (e == hipSuccess) {
-    hipLaunchKernelGGL(cg_ecdsa_gtab_build<CurveR1>, grid, dim3(256), 0, s, c->gtab[1]);
+    hipLaunchKernelGGL(cg_ecdsa_gtab_build<CurveR1>, dim3((kGTabEntries + 255) / 256), dim3(256), 0, s,
+                       c->gtab[1], tables[1]);
     e = hipGetLastError();
   }
   if (e == hipSuccess) e = hipStreamSynchronize(s);

@@ -102,36 +102,59 @@ int cgh_ed25519_verify(const uint8_t* pk_bytes, const uint8_t* sig_bytes, uint32
 // ------------------------------------------------------------------ ECDSA
 #include "cg_ecdsa.h"
 
-// the device's shared generator table (kGTabEntries affine points), built on the host
-// with the same code
+// the device's shared generator tables (kGTabEntries affine points: k*G, and for
+// secp256k1 also k*2^128 G), built on the host with the same code
 template <class C>
-static const jpt* g_table() {
-  static jpt* tab = nullptr;
-  if (!tab) {
-    tab = new jpt[kGTabEntries];
+static const jpt* g_table(uint32_t t = 0) {
+  static jpt* tab[2] = {nullptr, nullptr};
+  if (!tab[t]) {
+    tab[t] = new jpt[kGTabEntries];
     for (uint32_t k = 1; k < kGTabEntries; ++k) {
-      ecdsa_g_entry<C>(k, tab[k].X, tab[k].Y);
-      for (int i = 0; i < 8; ++i) tab[k].Z[i] = i == 0;
-      tab[k].inf = 0;
+      ecdsa_g_entry<C>(k, tab[t][k].X, tab[t][k].Y, t);
+      for (int i = 0; i < 8; ++i) tab[t][k].Z[i] = i == 0;
+      tab[t][k].inf = 0;
     }
   }
-  return tab;
+  return tab[t];
+}
+
+// secp256k1 joint multiplication exactly as cg_ecdsa_msm runs it (GLV split, the
+// lane's own digit count raised to force_nd like a longer scalar elsewhere in the wave).
+static void joint_k1glv(jpt& acc, const uint32_t u1[8], const uint32_t u2[8], const jpt qtab[9], uint32_t force_nd) {
+  uint32_t k1[8], k2[8], neg1, neg2, dg[9], dk1[9], dk2[9];
+  uint32_t nd = glv_split(u2, k1, k2, neg1, neg2);
+  if (force_nd > nd) nd = force_nd;
+  recode_g(dg, u1);
+  recode16_65(dk1, k1);
+  recode16_65(dk2, k2);
+  const jpt* g0 = g_table<CurveK1>(0);
+  const jpt* g1 = g_table<CurveK1>(1);
+  ecdsa_joint_glv(acc, nd, dk1, dk2, neg1, neg2, dg, [&](uint32_t k, jpt& p) { p = qtab[k]; },
+                  [&](uint32_t t, uint32_t k, jpt& p) { p = t ? g1[k] : g0[k]; });
 }
 
 template <class C>
 static int ecdsa_verify_host(const uint8_t* q_be, const uint8_t* sig, uint32_t sig_len, const uint8_t* msg,
                              uint32_t msg_len, uint32_t mode) {
   const jpt* gtab = g_table<C>();
-  uint32_t qw[16], qx[8], qy[8], r[8], s[8], nn[8], d1[9], d2[9];
+  uint32_t qw[16], qx[8], qy[8], r[8], s[8], nn[8], u1[8], u2[8];
   memcpy(qw, q_be, 64);
   be_words_to_limbs(qx, qw);
   be_words_to_limbs(qy, qw + 8);
   C::n(nn);
   const uint32_t ds = der_parse([&](uint32_t i) { return (uint32_t)sig[i]; }, sig_len, nn, r, s);
-  const uint32_t pre = ecdsa_prep<C>(qx, qy, ds, r, s, sig_len, msg, msg_len, mode, d1, d2);
+  const uint32_t pre = ecdsa_prep_scalars<C>(qx, qy, ds, r, s, sig_len, msg, msg_len, mode, u1, u2);
   if (pre != 0xff) return (int)pre;
   jpt qtab[9];
   ecdsa_q_table<C>(qx, qy, [&](int k, const jpt& p) { qtab[k] = p; });
+  if (C::kScheme == 2) {
+    jpt acc;
+    joint_k1glv(acc, u1, u2, qtab, 0);
+    return (int)ecdsa_x_check<C>(acc, r);
+  }
+  uint32_t d1[9], d2[9];
+  recode_g(d1, u1);
+  recode16_65(d2, u2);
   return (int)ecdsa_msm_check<C>(d1, d2, r, [&](uint32_t k, jpt& p) { p = qtab[k]; },
                                  [&](uint32_t k, jpt& p) { p = gtab[k]; });
 }
@@ -163,16 +186,22 @@ uint32_t cgh_der_parse(int scheme, const uint8_t* sig, uint32_t n, uint32_t* r, 
 }
 
 // u1*G + u2*Q through the device's joint multiplication; returns 0 and affine
-// x||y (LE limbs), or 1 when the result is the point at infinity.
+// x||y (LE limbs), or 1 when the result is the point at infinity.  secp256k1 goes
+// through the GLV path with the digit count raised to force_nd.
 template <class C>
-static int joint_host(const uint32_t* u1, const uint32_t* u2, const uint32_t* qx, const uint32_t* qy, uint32_t* out) {
+static int joint_host(const uint32_t* u1, const uint32_t* u2, const uint32_t* qx, const uint32_t* qy, uint32_t* out,
+                      uint32_t force_nd) {
   jpt qtab[9], acc;
   const jpt* gtab = g_table<C>();
   ecdsa_q_table<C>(qx, qy, [&](int k, const jpt& p) { qtab[k] = p; });
-  uint32_t d1[9], d2[9];
-  recode_g(d1, u1);
-  recode16_65(d2, u2);
-  ecdsa_joint<C>(acc, d1, d2, [&](uint32_t k, jpt& p) { p = qtab[k]; }, [&](uint32_t k, jpt& p) { p = gtab[k]; });
+  if (C::kScheme == 2) {
+    joint_k1glv(acc, u1, u2, qtab, force_nd);
+  } else {
+    uint32_t d1[9], d2[9];
+    recode_g(d1, u1);
+    recode16_65(d2, u2);
+    ecdsa_joint<C>(acc, d1, d2, [&](uint32_t k, jpt& p) { p = qtab[k]; }, [&](uint32_t k, jpt& p) { p = gtab[k]; });
+  }
   if (acc.inf) return 1;
   uint32_t zi[8], zi2[8], zi3[8];
   fp_inv<C>(zi, acc.Z);
@@ -184,8 +213,14 @@ static int joint_host(const uint32_t* u1, const uint32_t* u2, const uint32_t* qx
 }
 
 extern "C" int cgh_ecdsa_joint(int scheme, const uint32_t* u1, const uint32_t* u2, const uint32_t* qx,
-                               const uint32_t* qy, uint32_t* out) {
-  return scheme == 2 ? joint_host<CurveK1>(u1, u2, qx, qy, out) : joint_host<CurveR1>(u1, u2, qx, qy, out);
+                               const uint32_t* qy, uint32_t* out, uint32_t force_nd) {
+  return scheme == 2 ? joint_host<CurveK1>(u1, u2, qx, qy, out, force_nd)
+                     : joint_host<CurveR1>(u1, u2, qx, qy, out, force_nd);
+}
+
+// The GLV split itself: k1, k2 (LE limbs), signs; returns the digit count.
+extern "C" uint32_t cgh_glv_split(const uint32_t* u2, uint32_t* k1, uint32_t* k2, uint32_t* neg1, uint32_t* neg2) {
+  return glv_split(u2, k1, k2, *neg1, *neg2);
 }
 
 // The Merkle leaf preimage streamer: SHA-256(msg[0..n) || tail[0..tail_n)) with the

@@ -288,10 +288,29 @@ def test_ecdsa_joint_vs_python(host):
             qpt = EC._mul(c, d, c.g)
             u1 = [0, 1, c.n - 1, 2**255 - 1 if 2**255 - 1 < c.n else c.n - 2, 0x8000 << 240][t] if t < 5 \
                 else rnd.randrange(c.n)
-            u2 = rnd.randrange(1, c.n)
+            u2 = [1, c.n - 1, 2**128, (c.n + 1) // 2, (c.n - 1) // 2][t] if t < 5 else rnd.randrange(1, c.n)
             exp = EC._add(c, EC._mul(c, u1, c.g), EC._mul(c, u2, qpt))
-            inf = host.cgh_ecdsa_joint(scheme, w8(u1), w8(u2), w8(qpt[0]), w8(qpt[1]), out)
+            force = (0, 0, 40, 65)[t % 4]  # the wave-maximum digit count may exceed the lane's own
+            inf = host.cgh_ecdsa_joint(scheme, w8(u1), w8(u2), w8(qpt[0]), w8(qpt[1]), out, force)
             if exp is None:
                 assert inf == 1
             else:
                 assert inf == 0 and val(out) == exp[0] and val(out[8:], 8) == exp[1], (scheme, t)
+
+
+def test_glv_split_properties(host):
+    """secp256k1 GLV split: k1 + k2 lambda == u2 (mod n) with signs, both halves at
+    most 129 bits for random and edge scalars (else the full-length fallback)."""
+    import ecdsa_bc as EC
+    n = EC.SECP256K1.n
+    lam = 0x5363AD4CC05C30E0A5261C028812645A122E22EA20816678DF02967C1B23BD72
+    rnd = random.Random(21)
+    vals = [0, 1, 2, n - 1, n - 2, 2**128, 2**128 - 1, (n - 1) // 2, (n + 1) // 2, lam, n - lam]
+    vals += [rnd.randrange(n) for _ in range(3000)]
+    k1, k2, n1, n2 = (ctypes.c_uint32 * 8)(), (ctypes.c_uint32 * 8)(), ctypes.c_uint32(), ctypes.c_uint32()
+    host.cgh_glv_split.restype = ctypes.c_uint32
+    for u in vals:
+        nd = host.cgh_glv_split(w8(u), k1, k2, ctypes.byref(n1), ctypes.byref(n2))
+        a, b = val(k1) * (-1 if n1.value else 1), val(k2) * (-1 if n2.value else 1)
+        assert (a + b * lam - u) % n == 0, hex(u)
+        assert max(val(k1).bit_length(), val(k2).bit_length()) <= 129 and nd == 33 or nd == 34, (hex(u), nd)
