@@ -3,8 +3,9 @@ Corda's verification hot path.
 
 The compute lives in libcordagpu.so (HIP kernels for gfx950, C ABI in
 include/cordagpu.h).  This package is the host-side mirror of the reference's
-``Crypto`` batch surface (crypto.py), transaction helpers (transactions.py),
-key decoding (keys.py) and the multi-GPU sharding driver (dist.py).
+``Crypto`` batch surface (crypto.py), transaction helpers incl. filtered
+transactions (transactions.py), CompositeKey fulfilment (composite.py) and the
+multi-GPU sharding driver (dist.py).
 """
 from ._lib import Context, CordaGpuError, load  # noqa: F401
 
