@@ -118,7 +118,7 @@ const char* cg_last_error(const cg_ctx* ctx);
  *   pk         n * pk_stride bytes.  Ed25519: the 32-byte key A as carried on the wire
  *              (Kryo Ed25519PublicKeySerializer, Kryo.kt:330-340).  ECDSA: 64 bytes X||Y,
  *              big-endian affine coordinates decoded from the X.509 SubjectPublicKeyInfo by the
- *              caller (Kryo.kt:388-398; corda_amd.keys has a host helper).
+ *              caller (Kryo.kt:388-398; corda_amd.keys.decode_spki is the host helper).
  *   sig        n * sig_stride bytes; element i uses sig_len[i] bytes (sig_len NULL: sig_stride).
  *              Ed25519: R||S; ECDSA: the DER SEQUENCE{r, s} exactly as produced by the signer.
  *   msg        the clear-data arena (msg_bytes long); element i's data is
