@@ -118,10 +118,10 @@ CG_HD uint32_t ed25519_hash_stage(const uint32_t pk[8], const uint32_t sig[16], 
   return V_COMPUTE;
 }
 
-// Strict decode of R: canonical y (< p), a square root exists, and not (x = 0
-// with the sign bit set) — exactly the byte strings enc() can produce.
-CG_HD uint32_t ge_frombytes_strict(ge_p3& h, const uint32_t w[8]) {
-  if (!ge_frombytes_i2p(h, w)) return 0;
+// Strict decode of R on top of the i2p decode: canonical y (< p), a square root
+// exists, and not (x = 0 with the sign bit set) — exactly the byte strings enc()
+// can produce.
+CG_HD uint32_t ge_strict_check(const ge_p3& h, const uint32_t w[8]) {
   uint32_t yc[8];
   fe_tobytes(yc, h.Y);
   uint32_t diff = yc[7] ^ (w[7] & 0x7fffffffu);
@@ -130,17 +130,33 @@ CG_HD uint32_t ge_frombytes_strict(ge_p3& h, const uint32_t w[8]) {
   if ((w[7] >> 31) && fe_iszero(h.X)) return 0;
   return 1;
 }
+CG_HD uint32_t ge_frombytes_strict(ge_p3& h, const uint32_t w[8]) {
+  return ge_frombytes_i2p(h, w) && ge_strict_check(h, w);
+}
 
-// Points phase: final pre-verdict and the decoded -A and R.
+// Points phase: final pre-verdict and the decoded -A and R (both decodes run
+// together, their square roots interleaved).
 CG_HD uint32_t ed25519_points_stage(const uint32_t pk[8], const uint32_t r[8], uint32_t pre, ge_p3& negA,
                                     ge_p3& R) {
-  ge_p3 A;
-  if (!ge_frombytes_i2p(A, pk)) return V_KEY_INVALID;
+  ge_p3 P[2];
+  uint32_t ok[2];
+#ifndef CG_ED_PAIR_DECODE
+#define CG_ED_PAIR_DECODE 1
+#endif
+#if CG_ED_PAIR_DECODE
+  const uint32_t* const w[2] = {pk, r};
+  ge_frombytes_i2p_pair(P, w, ok);
+#else
+  ok[0] = ge_frombytes_i2p(P[0], pk);
+  ok[1] = ge_frombytes_i2p(P[1], r);
+#endif
+  if (!ok[0]) return V_KEY_INVALID;
   if (pre != V_COMPUTE) return pre;
-  if (!ge_frombytes_strict(R, r)) return V_REJECT;
-  negA = A;
-  fe_neg(negA.X, A.X);
-  fe_neg(negA.T, A.T);
+  if (!ok[1] || !ge_strict_check(P[1], r)) return V_REJECT;
+  R = P[1];
+  negA = P[0];
+  fe_neg(negA.X, P[0].X);
+  fe_neg(negA.T, P[0].T);
   return V_COMPUTE;
 }
 
@@ -153,15 +169,12 @@ CG_HD void ed25519_build_table(const ge_p3& P, Put&& put) {
   fe_1(c.Z);
   fe_0(c.T2d);
   put(0, c);
-  ge_cached p1;
-  ge_p3_to_cached(p1, P);
-  put(1, p1);
-  ge_p3 cur = P;
+  ge_p3_to_cached(c, P);
+  put(1, c);
   ge_p1p1 t;
-  CG_NOUNROLL for (int k = 2; k < kATabEntries; ++k) {
-    ge_add_cached(t, cur, p1, 0);
-    ge_p1p1_to_p3(cur, t);
-    ge_p3_to_cached(c, cur);
+  CG_NOUNROLL for (int k = 2; k < kATabEntries; ++k) {  // (k-1)P + P, kept in cached form only
+    ge_add_cached(t, P, c, 0);
+    ge_p1p1_to_cached(c, t);
     put(k, c);
   }
 }

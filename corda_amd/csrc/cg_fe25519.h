@@ -159,10 +159,126 @@ CG_HD void fe_reduce(fe& h) {
 #undef CG_C25
 }
 
+// 64-bit column accumulator barrier: an empty asm so LLVM cannot reassociate a
+// column's mad chain (it would move the incoming carry to the end of the chain,
+// costing one 64-bit add per column).
+CG_HD int64_t fe_pin64(int64_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm("" : "+v"(x));
+#endif
+  return x;
+}
+
+#ifndef CG_FE_FOLD
+#define CG_FE_FOLD 1
+#endif
+
+// Product sources for the column chains: op(k, i, acc) returns acc + the i-th
+// product of column k (acc unchanged if column k has no i-th product).
+struct FeMulOp {
+  int32_t f[10], f2[10], g[10], g19[10];
+  CG_HDM FeMulOp(const fe& F, const fe& G) {
+    CG_UNROLL for (int j = 0; j < 10; ++j) {
+      f[j] = F.v[j];
+      g[j] = G.v[j];
+      g19[j] = fe_pin(19 * G.v[j]);
+      f2[j] = (j & 1) ? fe_pin(2 * F.v[j]) : F.v[j];
+    }
+  }
+  CG_HDM int64_t operator()(int k, int i, int64_t acc) const {
+    const int j = (k - i + 10) % 10;
+    const int32_t a = (j & 1) ? f2[i] : f[i];
+    const int32_t b = (i + j >= 10) ? g19[j] : g[j];
+    return fe_pin64(acc + (int64_t)a * b);
+  }
+};
+// f^2 (DOUBLE: 2 f^2, by doubling the limb multipliers: 8 f_i <= 2^30.7 for the
+// odd limbs, within int32 like 19 f_j).
+template <bool DOUBLE>
+struct FeSqOp {
+  int32_t f[10], f2[10], f4[10], f8[10], f19[10];
+  CG_HDM explicit FeSqOp(const fe& F) {
+    CG_UNROLL for (int j = 0; j < 10; ++j) {
+      f[j] = F.v[j];
+      f19[j] = fe_pin(19 * F.v[j]);
+      f2[j] = fe_pin(2 * F.v[j]);
+      f4[j] = fe_pin(4 * F.v[j]);
+      f8[j] = fe_pin(8 * F.v[j]);
+    }
+  }
+  // column k: products i <= j, i + j = k (mod 10), by rank n: i = n for
+  // n <= k/2 (j = k - i), then i = k + 1 ... (k + 10)/2 (j = k + 10 - i)
+  CG_HDM int64_t operator()(int k, int n, int64_t acc) const {
+    const int i = n <= k / 2 ? n : k + n - k / 2;
+    if (i > (k + 10) / 2) return acc;
+    const int j = (k - i + 10) % 10;
+    const int m = ((i == j) ? 1 : 2) * (((i & 1) && (j & 1)) ? 2 : 1) * (DOUBLE ? 2 : 1);
+    const int32_t a = m == 1 ? f[i] : m == 2 ? f2[i] : m == 4 ? f4[i] : f8[i];
+    const int32_t b = (i + j >= 10) ? f19[j] : f[j];
+    return fe_pin64(acc + (int64_t)a * b);
+  }
+};
+
+// Column-serial carry chain: column k's mad chain starts from column k-1's
+// carry (the mad's 64-bit addend, so the carry costs no add), then carry out
+// with round-to-nearest.  Columns 0..9 in order, the wrap 19*c9 into limb 0 and
+// one more carry 0 -> 1: 11 carries of 3 instructions instead of the 12 of 4 of
+// fe_carry_wide.  Output limb bounds match fe_carry_wide's (|h_k| <= 2^25 /
+// 2^24, limb 1 a few units more).  fe_fold_pair runs two independent chains in
+// lockstep so consecutive mads never depend on each other (a dependent
+// v_mad_i64_i32 needs a wait state).
+struct FeFoldState {
+  int64_t acc, c;
+  int32_t r[10];
+};
+CG_HD void fe_fold_carry(FeFoldState& s, int k) {
+  const int w = (k & 1) ? 25 : 26;
+  s.c = (s.acc + (1LL << (w - 1))) >> w;
+  s.r[k] = (int32_t)sext_low64(s.acc, w);
+}
+CG_HD void fe_fold_finish(fe& h, FeFoldState& s) {
+  const int64_t t0 = (int64_t)s.r[0] + s.c * 19;
+  const int64_t c = (t0 + (1LL << 25)) >> 26;
+  s.r[0] = (int32_t)sext_low64(t0, 26);
+  s.r[1] += (int32_t)c;
+  CG_UNROLL for (int i = 0; i < 10; ++i) h.v[i] = fe_pin(s.r[i]);
+}
+template <typename Op>
+CG_HD void fe_fold_chain(fe& h, const Op& op) {
+  FeFoldState s;
+  s.c = 0;
+  CG_UNROLL for (int k = 0; k < 10; ++k) {
+    s.acc = s.c;
+    CG_UNROLL for (int i = 0; i < 10; ++i) s.acc = op(k, i, s.acc);
+    fe_fold_carry(s, k);
+  }
+  fe_fold_finish(h, s);
+}
+template <typename Op0, typename Op1>
+CG_HD void fe_fold_pair(fe& h0, const Op0& op0, fe& h1, const Op1& op1) {
+  FeFoldState s0, s1;
+  s0.c = s1.c = 0;
+  CG_UNROLL for (int k = 0; k < 10; ++k) {
+    s0.acc = s0.c;
+    s1.acc = s1.c;
+    CG_UNROLL for (int i = 0; i < 10; ++i) {
+      s0.acc = op0(k, i, s0.acc);
+      s1.acc = op1(k, i, s1.acc);
+    }
+    fe_fold_carry(s0, k);
+    fe_fold_carry(s1, k);
+  }
+  fe_fold_finish(h0, s0);
+  fe_fold_finish(h1, s1);
+}
+
 // h = f * g.  Column k collects f_i g_j for i+j = k (and 19 f_i g_j for
 // i+j = k+10); products of two odd limbs carry an extra factor 2 because the
 // odd limbs are 25 bits wide.
 CG_HD void fe_mul(fe& h, const fe& f, const fe& g) {
+#if CG_FE_FOLD && !defined(CG_CHECK_BOUNDS)
+  fe_fold_chain(h, FeMulOp(f, g));
+#else
   int32_t g19[10], f2[10];
   CG_UNROLL for (int j = 0; j < 10; ++j) g19[j] = fe_pin(19 * g.v[j]);
   CG_UNROLL for (int i = 0; i < 10; ++i) f2[i] = (i & 1) ? fe_pin(2 * f.v[i]) : f.v[i];
@@ -178,11 +294,15 @@ CG_HD void fe_mul(fe& h, const fe& f, const fe& g) {
   }
   CG_BOUNDS_MUL(f, g, t, 0);
   fe_carry_wide(h, t);
+#endif
 }
 
 // h = f^2 (DOUBLE ? 2 f^2 : f^2): 55 products using the symmetry f_i f_j = f_j f_i.
 template <bool DOUBLE>
 CG_HD void fe_sq_t(fe& h, const fe& f) {
+#if CG_FE_FOLD && !defined(CG_CHECK_BOUNDS)
+  fe_fold_chain(h, FeSqOp<DOUBLE>(f));
+#else
   int32_t f19[10], f2[10], f4[10];
   CG_UNROLL for (int j = 0; j < 10; ++j) {
     f19[j] = fe_pin(19 * f.v[j]);
@@ -205,9 +325,76 @@ CG_HD void fe_sq_t(fe& h, const fe& f) {
   }
   CG_BOUNDS_MUL(f, f, t, DOUBLE);
   fe_carry_wide(h, t);
+#endif
 }
 CG_HD void fe_sq(fe& h, const fe& f) { fe_sq_t<false>(h, f); }
 CG_HD void fe_sq2(fe& h, const fe& f) { fe_sq_t<true>(h, f); }
+
+template <typename Op0, typename Op1, typename Op2>
+CG_HD void fe_fold_triple(fe& h0, const Op0& op0, fe& h1, const Op1& op1, fe& h2, const Op2& op2) {
+  FeFoldState s0, s1, s2;
+  s0.c = s1.c = s2.c = 0;
+  CG_UNROLL for (int k = 0; k < 10; ++k) {
+    s0.acc = s0.c;
+    s1.acc = s1.c;
+    s2.acc = s2.c;
+    CG_UNROLL for (int i = 0; i < 10; ++i) {
+      s0.acc = op0(k, i, s0.acc);
+      s1.acc = op1(k, i, s1.acc);
+      s2.acc = op2(k, i, s2.acc);
+    }
+    fe_fold_carry(s0, k);
+    fe_fold_carry(s1, k);
+    fe_fold_carry(s2, k);
+  }
+  fe_fold_finish(h0, s0);
+  fe_fold_finish(h1, s1);
+  fe_fold_finish(h2, s2);
+}
+
+// Two independent products interleaved (h0 = op0, h1 = op1); the ops copy their
+// inputs, so h0 / h1 may alias any source.
+struct FeMul {
+  const fe& f;
+  const fe& g;
+};
+struct FeSq {
+  const fe& f;
+};
+struct FeSq2 {
+  const fe& f;
+};
+CG_HD void fe_single(fe& h, const FeMul& o) { fe_mul(h, o.f, o.g); }
+CG_HD void fe_single(fe& h, const FeSq& o) { fe_sq(h, o.f); }
+CG_HD void fe_single(fe& h, const FeSq2& o) { fe_sq2(h, o.f); }
+CG_HD FeMulOp fe_op(const FeMul& o) { return FeMulOp(o.f, o.g); }
+CG_HD FeSqOp<false> fe_op(const FeSq& o) { return FeSqOp<false>(o.f); }
+CG_HD FeSqOp<true> fe_op(const FeSq2& o) { return FeSqOp<true>(o.f); }
+template <typename A, typename B>
+CG_HD void fe_pair(fe& h0, const A& a, fe& h1, const B& b) {
+#if CG_FE_FOLD && !defined(CG_CHECK_BOUNDS)
+  fe_fold_pair(h0, fe_op(a), h1, fe_op(b));
+#else
+  fe t;
+  fe_single(t, a);
+  fe_single(h1, b);
+  h0 = t;
+#endif
+}
+
+template <typename A, typename B, typename C>
+CG_HD void fe_triple(fe& h0, const A& a, fe& h1, const B& b, fe& h2, const C& c) {
+#if CG_FE_FOLD && !defined(CG_CHECK_BOUNDS)
+  fe_fold_triple(h0, fe_op(a), h1, fe_op(b), h2, fe_op(c));
+#else
+  fe t0, t1;
+  fe_single(t0, a);
+  fe_single(t1, b);
+  fe_single(h2, c);
+  h0 = t0;
+  h1 = t1;
+#endif
+}
 
 CG_HD void fe_sqn(fe& h, const fe& f, int n) {
   fe_sq(h, f);
@@ -305,6 +492,42 @@ CG_HD void fe_pow22523(fe& out, const fe& z) {
   fe_pow2_250_1(t, z11, z);
   fe_sqn(t, t, 2);
   fe_mul(out, t, z);    // z^(2^252 - 3)
+}
+
+// The same chains on two independent inputs in lockstep (the key and R decodes
+// of the points kernel): every step is an fe_pair, so the dependent squarings of
+// one chain interleave with the other's.
+CG_HD void fe_sqn_pair(fe& h0, const fe& f0, fe& h1, const fe& f1, int n) {
+  fe_pair(h0, FeSq{f0}, h1, FeSq{f1});
+  CG_NOUNROLL for (int i = 1; i < n; ++i) fe_pair(h0, FeSq{h0}, h1, FeSq{h1});
+}
+CG_HD void fe_mul_pair(fe& h0, const fe& f0, const fe& g0, fe& h1, const fe& f1, const fe& g1) {
+  fe_pair(h0, FeMul{f0, g0}, h1, FeMul{f1, g1});
+}
+CG_HD void fe_pow22523_pair(fe& out0, const fe& z0, fe& out1, const fe& z1) {
+  fe z2[2], z9[2], z11[2], t[2], a[2], b[2];
+  fe_sqn_pair(z2[0], z0, z2[1], z1, 1);
+  fe_sqn_pair(t[0], z2[0], t[1], z2[1], 2);
+  fe_mul_pair(z9[0], t[0], z0, z9[1], t[1], z1);
+  fe_mul_pair(z11[0], z9[0], z2[0], z11[1], z9[1], z2[1]);
+  fe_sqn_pair(t[0], z11[0], t[1], z11[1], 1);
+  fe_mul_pair(a[0], t[0], z9[0], a[1], t[1], z9[1]);      // 2^5 - 1
+  fe_sqn_pair(t[0], a[0], t[1], a[1], 5);
+  fe_mul_pair(a[0], t[0], a[0], a[1], t[1], a[1]);        // 2^10 - 1
+  fe_sqn_pair(t[0], a[0], t[1], a[1], 10);
+  fe_mul_pair(b[0], t[0], a[0], b[1], t[1], a[1]);        // 2^20 - 1
+  fe_sqn_pair(t[0], b[0], t[1], b[1], 20);
+  fe_mul_pair(t[0], t[0], b[0], t[1], t[1], b[1]);        // 2^40 - 1
+  fe_sqn_pair(t[0], t[0], t[1], t[1], 10);
+  fe_mul_pair(a[0], t[0], a[0], a[1], t[1], a[1]);        // 2^50 - 1
+  fe_sqn_pair(t[0], a[0], t[1], a[1], 50);
+  fe_mul_pair(b[0], t[0], a[0], b[1], t[1], a[1]);        // 2^100 - 1
+  fe_sqn_pair(t[0], b[0], t[1], b[1], 100);
+  fe_mul_pair(t[0], t[0], b[0], t[1], t[1], b[1]);        // 2^200 - 1
+  fe_sqn_pair(t[0], t[0], t[1], t[1], 50);
+  fe_mul_pair(t[0], t[0], a[0], t[1], t[1], a[1]);        // 2^250 - 1
+  fe_sqn_pair(t[0], t[0], t[1], t[1], 2);
+  fe_mul_pair(out0, t[0], z0, out1, t[1], z1);            // z^(2^252 - 3)
 }
 
 // Constants (limbs of the canonical values).

@@ -23,16 +23,12 @@ struct ge_cached { fe YplusX, YminusX, Z, T2d; };
 struct ge_precomp { fe yplusx, yminusx, xy2d; };
 
 CG_HD void ge_p1p1_to_p2(ge_p2& r, const ge_p1p1& p) {
-  fe_mul(r.X, p.X, p.T);
-  fe_mul(r.Y, p.Y, p.Z);
-  fe_mul(r.Z, p.Z, p.T);
+  fe_triple(r.X, FeMul{p.X, p.T}, r.Y, FeMul{p.Y, p.Z}, r.Z, FeMul{p.Z, p.T});
 }
 
 CG_HD void ge_p1p1_to_p3(ge_p3& r, const ge_p1p1& p) {
-  fe_mul(r.X, p.X, p.T);
-  fe_mul(r.Y, p.Y, p.Z);
-  fe_mul(r.Z, p.Z, p.T);
-  fe_mul(r.T, p.X, p.Y);
+  fe_pair(r.X, FeMul{p.X, p.T}, r.Y, FeMul{p.Y, p.Z});
+  fe_pair(r.Z, FeMul{p.Z, p.T}, r.T, FeMul{p.X, p.Y});
 }
 
 CG_HD void ge_p3_to_cached(ge_cached& r, const ge_p3& p) {
@@ -43,15 +39,24 @@ CG_HD void ge_p3_to_cached(ge_cached& r, const ge_p3& p) {
   fe_mul(r.T2d, p.T, d2);
 }
 
+// p1p1 straight to cached: (Y3+X3, Y3-X3, Z3, 2d T3) with X3 = XT, Y3 = YZ,
+// Z3 = ZT, 2d T3 = (2d X) Y — five products in a triple and a pair.
+CG_HD void ge_p1p1_to_cached(ge_cached& r, const ge_p1p1& p) {
+  const fe d2 = CG_FE_D2;
+  fe x3, y3, dx;
+  fe_triple(x3, FeMul{p.X, p.T}, y3, FeMul{p.Y, p.Z}, dx, FeMul{p.X, d2});
+  fe_pair(r.Z, FeMul{p.Z, p.T}, r.T2d, FeMul{dx, p.Y});
+  fe_add(r.YplusX, y3, x3);
+  fe_sub(r.YminusX, y3, x3);
+}
+
 // 2P: x = E/G, y = H/F with E = (X+Y)^2 - X^2 - Y^2, G = Y^2 - X^2,
 // H = -(X^2 + Y^2), F = G - 2Z^2  (stored as p1p1 with the signs folded).
 CG_HD void ge_p2_dbl(ge_p1p1& r, const ge_p2& p) {
   fe t0;
-  fe_sq(r.X, p.X);
-  fe_sq(r.Z, p.Y);
-  fe_sq2(r.T, p.Z);
+  fe_pair(r.X, FeSq{p.X}, r.Z, FeSq{p.Y});
   fe_add(r.Y, p.X, p.Y);
-  fe_sq(t0, r.Y);
+  fe_pair(r.T, FeSq2{p.Z}, t0, FeSq{r.Y});
   fe_add(r.Y, r.Z, r.X);  // YY + XX
   fe_sub(r.Z, r.Z, r.X);  // YY - XX
   fe_sub(r.X, t0, r.Y);   // (X+Y)^2 - YY - XX
@@ -71,10 +76,8 @@ CG_HD void ge_add_cached(ge_p1p1& r, const ge_p3& p, const ge_cached& q, uint32_
   fe_select(qb, q.YminusX, q.YplusX, neg);
   fe_add(a, p.Y, p.X);
   fe_sub(b, p.Y, p.X);
-  fe_mul(a, a, qa);
-  fe_mul(b, b, qb);
-  fe_mul(c, q.T2d, p.T);
-  fe_mul(d, p.Z, q.Z);
+  fe_pair(a, FeMul{a, qa}, b, FeMul{b, qb});
+  fe_pair(c, FeMul{q.T2d, p.T}, d, FeMul{p.Z, q.Z});
   fe_add(d, d, d);
   fe_sub(r.X, a, b);
   fe_add(r.Y, a, b);
@@ -93,9 +96,7 @@ CG_HD void ge_madd(ge_p1p1& r, const ge_p3& p, const ge_precomp& q, uint32_t neg
   fe_select(qb, q.yminusx, q.yplusx, neg);
   fe_add(a, p.Y, p.X);
   fe_sub(b, p.Y, p.X);
-  fe_mul(a, a, qa);
-  fe_mul(b, b, qb);
-  fe_mul(c, q.xy2d, p.T);
+  fe_triple(a, FeMul{a, qa}, b, FeMul{b, qb}, c, FeMul{q.xy2d, p.T});
   fe_add(d, p.Z, p.Z);
   fe_sub(r.X, a, b);
   fe_add(r.Y, a, b);
@@ -152,6 +153,49 @@ CG_HD uint32_t ge_frombytes_i2p(ge_p3& h, const uint32_t w[8]) {
   fe_select(h.X, h.X, negx, fe_isnegative(h.X) ^ (w[7] >> 31));
   fe_mul(h.T, h.X, h.Y);
   return ok;
+}
+
+// ge_frombytes_i2p on two encodings at once (ok[i] as its return value), with
+// the two square-root exponentiations interleaved; branch-free.
+CG_HD void ge_frombytes_i2p_pair(ge_p3 h[2], const uint32_t* const w[2], uint32_t ok[2]) {
+  const fe d = CG_FE_D, sqrtm1 = CG_FE_SQRTM1;
+  fe u[2], v[2], v3[2], x[2], vxx[2], one;
+  fe_1(one);
+  CG_UNROLL for (int i = 0; i < 2; ++i) {
+    fe_frombytes(h[i].Y, w[i]);
+    fe_reduce(h[i].Y);
+    fe_1(h[i].Z);
+  }
+  fe_sqn_pair(u[0], h[0].Y, u[1], h[1].Y, 1);
+  fe_mul_pair(v[0], u[0], d, v[1], u[1], d);
+  CG_UNROLL for (int i = 0; i < 2; ++i) {
+    fe_sub(u[i], u[i], one);  // y^2 - 1
+    fe_add(v[i], v[i], one);  // d y^2 + 1
+  }
+  fe_sqn_pair(v3[0], v[0], v3[1], v[1], 1);
+  fe_mul_pair(v3[0], v3[0], v[0], v3[1], v3[1], v[1]);  // v^3
+  fe_sqn_pair(x[0], v3[0], x[1], v3[1], 1);
+  fe_mul_pair(x[0], x[0], v[0], x[1], x[1], v[1]);
+  fe_mul_pair(x[0], x[0], u[0], x[1], x[1], u[1]);      // u v^7
+  fe_pow22523_pair(x[0], x[0], x[1], x[1]);
+  fe_mul_pair(x[0], x[0], v3[0], x[1], x[1], v3[1]);
+  fe_mul_pair(x[0], x[0], u[0], x[1], x[1], u[1]);      // u v^3 (u v^7)^((p-5)/8)
+  fe_sqn_pair(vxx[0], x[0], vxx[1], x[1], 1);
+  fe_mul_pair(vxx[0], vxx[0], v[0], vxx[1], vxx[1], v[1]);
+  fe xi[2];
+  fe_mul_pair(xi[0], x[0], sqrtm1, xi[1], x[1], sqrtm1);
+  CG_UNROLL for (int i = 0; i < 2; ++i) {
+    fe check;
+    fe_sub(check, vxx[i], u[i]);
+    const uint32_t direct = fe_iszero(check);
+    fe_add(check, vxx[i], u[i]);
+    ok[i] = direct | fe_iszero(check);
+    fe_select(h[i].X, xi[i], x[i], direct);
+    fe negx;
+    fe_neg(negx, h[i].X);
+    fe_select(h[i].X, h[i].X, negx, fe_isnegative(h[i].X) ^ (w[i][7] >> 31));
+  }
+  fe_mul_pair(h[0].T, h[0].X, h[0].Y, h[1].T, h[1].X, h[1].Y);
 }
 
 }  // namespace cg

@@ -85,7 +85,10 @@ CG_DEV void load_cached(const int4* src, ge_cached& c) {
   }
 }
 
-__global__ __launch_bounds__(256) void cg_ed25519_points(const uint32_t* __restrict__ pk,
+#ifndef CG_POINTS_WAVES
+#define CG_POINTS_WAVES 2
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_POINTS_WAVES, 8))) void cg_ed25519_points(const uint32_t* __restrict__ pk,
                                                          const uint32_t* __restrict__ sig, uint32_t n, uint32_t cap,
                                                          uint32_t* __restrict__ status, int32_t* __restrict__ table) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
