@@ -4,8 +4,8 @@
 // ceil(25.5 i); widths 26,25,26,...).  Products are accumulated in 64 bits, which
 // gfx950 issues as one full-rate v_mad_i64_i32 per limb product (measured
 // profiles/r01_isa_rates.json: mad_u64_u32 at the same rate as any VOP3 integer
-// op), so a multiply is 100 mads + ~55 carry ops and fe_add / fe_sub need no
-// carry at all.  Bounds follow the classic 25.5-bit analysis: reduced limbs are
+// op), so a multiply is 100 mads + ~35 carry ops (fe_fold_chain) and fe_add / fe_sub
+// need no carry at all.  Bounds follow the classic 25.5-bit analysis: reduced limbs are
 // |h| <= 1.01*2^25 (even) / 2^24 (odd); mul/sq inputs may be up to 1.65x the
 // 2^26 / 2^25 limb widths, i.e. any sum/difference of <= 3 reduced values.
 //
@@ -276,9 +276,7 @@ CG_HD void fe_fold_pair(fe& h0, const Op0& op0, fe& h1, const Op1& op1) {
 // i+j = k+10); products of two odd limbs carry an extra factor 2 because the
 // odd limbs are 25 bits wide.
 CG_HD void fe_mul(fe& h, const fe& f, const fe& g) {
-#if CG_FE_FOLD && !defined(CG_CHECK_BOUNDS)
-  fe_fold_chain(h, FeMulOp(f, g));
-#else
+#if !CG_FE_FOLD || defined(CG_CHECK_BOUNDS)
   int32_t g19[10], f2[10];
   CG_UNROLL for (int j = 0; j < 10; ++j) g19[j] = fe_pin(19 * g.v[j]);
   CG_UNROLL for (int i = 0; i < 10; ++i) f2[i] = (i & 1) ? fe_pin(2 * f.v[i]) : f.v[i];
@@ -293,6 +291,10 @@ CG_HD void fe_mul(fe& h, const fe& f, const fe& g) {
     }
   }
   CG_BOUNDS_MUL(f, g, t, 0);
+#endif
+#if CG_FE_FOLD
+  fe_fold_chain(h, FeMulOp(f, g));
+#else
   fe_carry_wide(h, t);
 #endif
 }
@@ -300,9 +302,7 @@ CG_HD void fe_mul(fe& h, const fe& f, const fe& g) {
 // h = f^2 (DOUBLE ? 2 f^2 : f^2): 55 products using the symmetry f_i f_j = f_j f_i.
 template <bool DOUBLE>
 CG_HD void fe_sq_t(fe& h, const fe& f) {
-#if CG_FE_FOLD && !defined(CG_CHECK_BOUNDS)
-  fe_fold_chain(h, FeSqOp<DOUBLE>(f));
-#else
+#if !CG_FE_FOLD || defined(CG_CHECK_BOUNDS)
   int32_t f19[10], f2[10], f4[10];
   CG_UNROLL for (int j = 0; j < 10; ++j) {
     f19[j] = fe_pin(19 * f.v[j]);
@@ -324,6 +324,10 @@ CG_HD void fe_sq_t(fe& h, const fe& f) {
     CG_UNROLL for (int k = 0; k < 10; ++k) t[k] *= 2;
   }
   CG_BOUNDS_MUL(f, f, t, DOUBLE);
+#endif
+#if CG_FE_FOLD
+  fe_fold_chain(h, FeSqOp<DOUBLE>(f));
+#else
   fe_carry_wide(h, t);
 #endif
 }
