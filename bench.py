@@ -274,7 +274,7 @@ def run_ed25519(args, dist):
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = cpu_threads()
-        sample = w.subset(np.arange(min(args.cpu_sample or 131072, n)))
+        sample = w.subset(np.arange(min(args.cpu_sample or 524288, n)))
         cv, dt = oracle_verify(sample, threads)
         cpu = {"value": round(sample.n / dt, 1), "unit": "verifies/s", "cores": threads, "kind": "port",
                "sample": f"first {sample.n} signatures of the same workload ({msg_bytes} B msgs, incl. its "
@@ -377,7 +377,7 @@ def run_ecdsa(args, dist):
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = cpu_threads()
-        m = min(args.cpu_sample or 32768, n)
+        m = min(args.cpu_sample or 131072, n)
         idx = np.concatenate([np.arange(m // 2), n + np.arange(m // 2)])
         sample = w.subset(idx)
         cv, dt = oracle_verify(sample, threads)
@@ -471,7 +471,7 @@ def run_tx(args, dist):
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from concurrent.futures import ThreadPoolExecutor
         threads = cpu_threads()
-        m = min(args.cpu_sample or 16384, n_tx)
+        m = min(args.cpu_sample or 65536, n_tx)
         lib = oracle_lib()
         t0 = time.perf_counter()
         cids = np.zeros(32 * m, dtype=np.uint8)
@@ -550,7 +550,7 @@ def run_ftx(args, dist):
     value = n * world * args.steps / elapsed
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        m = min(args.cpu_sample or 262144, n)
+        m = min(args.cpu_sample or 2097152, n)
         lib = oracle_lib()
         lib.oracle_ftx_verify_batch.argtypes = [ctypes.c_void_p] * 9 + [ctypes.c_size_t, ctypes.c_void_p]
         cres = np.zeros(m, dtype=np.uint8)
