@@ -11,6 +11,7 @@
 // Jacobian arithmetic with explicit infinity flags and exception handling (H == 0),
 // so P = +-T inside the double-scalar loop (reachable with crafted keys) is exact.
 #pragma once
+#include "cg_fp26.h"
 #include "cg_mp256.h"
 #include "cg_sha256.h"
 
@@ -88,67 +89,78 @@ CG_HD uint32_t der_parse(Byte&& b, uint32_t n, const uint32_t order[8], uint32_t
 }
 
 // ------------------------------------------------------------ points
+// Jacobian (X : Y : Z) over the Montgomery field of cg_fp26.h; every coordinate is a
+// "unit" value (a multiplication output or f26_norm'ed).  The comment next to each
+// product gives c_a x c_b of its inputs (<= 150 allowed), next to each f26_norm the
+// c of its input (<= 16 allowed).
 struct jpt {
-  uint32_t X[8], Y[8], Z[8];
+  f26 X, Y, Z;
   uint32_t inf;
 };
 
 template <class C>
 CG_HD void ec_dbl(jpt& r, const jpt& p) {
-  uint32_t t0[8], t1[8], t2[8], t3[8], x3[8], y3[8], z3[8];
+  f26 t0, t1, t2, t3, x3, y3, z3;
   if (C::kAMinus3) {
     // dbl-2001-b: delta = Z^2, gamma = Y^2, beta = X gamma, alpha = 3 (X - delta)(X + delta)
-    uint32_t delta[8], gamma[8], beta[8], alpha[8];
-    fp_sqr<C>(delta, p.Z);
-    fp_sqr<C>(gamma, p.Y);
-    fp_mul<C>(beta, p.X, gamma);
-    fp_sub<C>(t0, p.X, delta);
-    fp_add<C>(t1, p.X, delta);
-    fp_mul<C>(t2, t0, t1);
-    fp_add<C>(alpha, t2, t2);
-    fp_add<C>(alpha, alpha, t2);
-    fp_sqr<C>(x3, alpha);
-    fp_add<C>(t0, beta, beta);   // 2 beta
-    fp_add<C>(t0, t0, t0);       // 4 beta
-    fp_add<C>(t1, t0, t0);       // 8 beta
-    fp_sub<C>(x3, x3, t1);
-    fp_add<C>(t2, p.Y, p.Z);
-    fp_sqr<C>(z3, t2);
-    fp_sub<C>(z3, z3, gamma);
-    fp_sub<C>(z3, z3, delta);
-    fp_sub<C>(t0, t0, x3);       // 4 beta - X3
-    fp_mul<C>(y3, alpha, t0);
-    fp_sqr<C>(t3, gamma);
-    fp_add<C>(t3, t3, t3);
-    fp_add<C>(t3, t3, t3);
-    fp_add<C>(t3, t3, t3);       // 8 gamma^2
-    fp_sub<C>(y3, y3, t3);
+    f26 delta, gamma, beta, alpha;
+    f26_sqr<C>(delta, p.Z);
+    f26_sqr<C>(gamma, p.Y);
+    f26_mul<C>(beta, p.X, gamma);
+    f26_sub(t0, p.X, delta);
+    f26_add(t1, p.X, delta);
+    f26_mul<C>(t2, t0, t1);  // 2 x 2
+    f26_add(alpha, t2, t2);
+    f26_add(alpha, alpha, t2);  // c 3
+    f26_sqr<C>(x3, alpha);      // 3 x 3
+    f26_add(t0, beta, beta);
+    f26_add(t0, t0, t0);  // 4 beta
+    f26_add(t1, t0, t0);  // 8 beta
+    f26_sub(x3, x3, t1);
+    f26_norm<C>(x3);  // c 9
+    f26_add(t2, p.Y, p.Z);
+    f26_sqr<C>(z3, t2);  // 2 x 2
+    f26_sub(z3, z3, gamma);
+    f26_sub(z3, z3, delta);
+    f26_norm<C>(z3);      // c 3
+    f26_sub(t0, t0, x3);  // 4 beta - X3: c 5
+    f26_mul<C>(y3, alpha, t0);  // 3 x 5
+    f26_sqr<C>(t3, gamma);
+    f26_add(t3, t3, t3);
+    f26_add(t3, t3, t3);
+    f26_add(t3, t3, t3);  // 8 gamma^2
+    f26_sub(y3, y3, t3);
+    f26_norm<C>(y3);  // c 9
   } else {
     // dbl-2009-l (a = 0)
-    uint32_t A[8], B[8], Cc[8], D[8], E[8], F[8];
-    fp_sqr<C>(A, p.X);
-    fp_sqr<C>(B, p.Y);
-    fp_sqr<C>(Cc, B);
-    fp_add<C>(t0, p.X, B);
-    fp_sqr<C>(t1, t0);
-    fp_sub<C>(t1, t1, A);
-    fp_sub<C>(t1, t1, Cc);
-    fp_add<C>(D, t1, t1);
-    fp_add<C>(E, A, A);
-    fp_add<C>(E, E, A);
-    fp_sqr<C>(F, E);
-    fp_add<C>(t2, D, D);
-    fp_sub<C>(x3, F, t2);
-    fp_sub<C>(t2, D, x3);
-    fp_mul<C>(y3, E, t2);
-    fp_add<C>(t3, Cc, Cc);
-    fp_add<C>(t3, t3, t3);
-    fp_add<C>(t3, t3, t3);
-    fp_sub<C>(y3, y3, t3);
-    fp_mul<C>(z3, p.Y, p.Z);
-    fp_add<C>(z3, z3, z3);
+    f26 A, B, Cc, D, E, F;
+    f26_sqr<C>(A, p.X);
+    f26_sqr<C>(B, p.Y);
+    f26_sqr<C>(Cc, B);
+    f26_add(t0, p.X, B);
+    f26_sqr<C>(t1, t0);  // 2 x 2
+    f26_sub(t1, t1, A);
+    f26_sub(t1, t1, Cc);
+    f26_add(D, t1, t1);  // c 6
+    f26_add(E, A, A);
+    f26_add(E, E, A);    // c 3
+    f26_sqr<C>(F, E);    // 3 x 3
+    f26_add(t2, D, D);
+    f26_sub(x3, F, t2);
+    f26_norm<C>(x3);      // c 13
+    f26_sub(t2, D, x3);   // c 7
+    f26_mul<C>(y3, E, t2);  // 3 x 7
+    f26_add(t3, Cc, Cc);
+    f26_add(t3, t3, t3);
+    f26_add(t3, t3, t3);
+    f26_sub(y3, y3, t3);
+    f26_norm<C>(y3);  // c 9
+    f26_add(t0, p.Y, p.Y);
+    f26_mul<C>(z3, t0, p.Z);  // 2 x 1
   }
-  CG_UNROLL for (int i = 0; i < 8; ++i) { r.X[i] = x3[i]; r.Y[i] = y3[i]; r.Z[i] = z3[i]; }
+  r.X = x3;
+  r.Y = y3;
+  r.Z = z3;
   r.inf = p.inf;
 }
 
@@ -156,42 +168,47 @@ CG_HD void ec_dbl(jpt& r, const jpt& p) {
 // q_skip: q is the identity (digit 0).  Exact in every case.
 template <class C, bool AFFINE>
 CG_HD void ec_add(jpt& r, const jpt& p, const jpt& q, uint32_t q_skip) {
-  uint32_t z1z1[8], u1[8], u2[8], s1[8], s2[8], t[8], h[8], rr[8], hh[8], hhh[8], v[8], x3[8], y3[8], z3[8];
-  fp_sqr<C>(z1z1, p.Z);
+  f26 z1z1, u1, u2, s1, s2, t, h, rr, hh, hhh, v, x3, y3, z3;
+  f26_sqr<C>(z1z1, p.Z);
   if (AFFINE) {
-    CG_UNROLL for (int i = 0; i < 8; ++i) { u1[i] = p.X[i]; s1[i] = p.Y[i]; }
+    u1 = p.X;
+    s1 = p.Y;
   } else {
-    uint32_t z2z2[8];
-    fp_sqr<C>(z2z2, q.Z);
-    fp_mul<C>(u1, p.X, z2z2);
-    fp_mul<C>(t, q.Z, z2z2);
-    fp_mul<C>(s1, p.Y, t);
+    f26 z2z2;
+    f26_sqr<C>(z2z2, q.Z);
+    f26_mul<C>(u1, p.X, z2z2);
+    f26_mul<C>(t, q.Z, z2z2);
+    f26_mul<C>(s1, p.Y, t);
   }
-  fp_mul<C>(u2, q.X, z1z1);
-  fp_mul<C>(t, p.Z, z1z1);
-  fp_mul<C>(s2, q.Y, t);
-  fp_sub<C>(h, u2, u1);
-  fp_sub<C>(rr, s2, s1);
-  fp_sqr<C>(hh, h);
-  fp_mul<C>(hhh, h, hh);
-  fp_mul<C>(v, u1, hh);
-  fp_sqr<C>(x3, rr);
-  fp_sub<C>(x3, x3, hhh);
-  fp_sub<C>(x3, x3, v);
-  fp_sub<C>(x3, x3, v);
-  fp_sub<C>(t, v, x3);
-  fp_mul<C>(y3, rr, t);
-  fp_mul<C>(t, s1, hhh);
-  fp_sub<C>(y3, y3, t);
+  f26_mul<C>(u2, q.X, z1z1);
+  f26_mul<C>(t, p.Z, z1z1);
+  f26_mul<C>(s2, q.Y, t);
+  f26_sub(h, u2, u1);    // c 2
+  f26_sub(rr, s2, s1);   // c 2
+  f26_sqr<C>(hh, h);     // 2 x 2
+  f26_mul<C>(hhh, h, hh);  // 2 x 1
+  f26_mul<C>(v, u1, hh);
+  f26_sqr<C>(x3, rr);    // 2 x 2
+  f26_sub(x3, x3, hhh);
+  f26_sub(x3, x3, v);
+  f26_sub(x3, x3, v);
+  f26_norm<C>(x3);       // c 4
+  f26_sub(t, v, x3);     // c 2
+  f26_mul<C>(y3, rr, t);   // 2 x 2
+  f26_mul<C>(t, s1, hhh);
+  f26_sub(y3, y3, t);
+  f26_norm<C>(y3);       // c 2
   if (AFFINE) {
-    fp_mul<C>(z3, p.Z, h);
+    f26_mul<C>(z3, p.Z, h);  // 1 x 2
   } else {
-    fp_mul<C>(t, p.Z, q.Z);
-    fp_mul<C>(z3, t, h);
+    f26_mul<C>(t, p.Z, q.Z);
+    f26_mul<C>(z3, t, h);    // 1 x 2
   }
-  const uint32_t hz = mp_iszero(h), rz = mp_iszero(rr);
+  const uint32_t hz = f26_iszero<C>(h), rz = f26_iszero<C>(rr);
   jpt out;
-  CG_UNROLL for (int i = 0; i < 8; ++i) { out.X[i] = x3[i]; out.Y[i] = y3[i]; out.Z[i] = z3[i]; }
+  out.X = x3;
+  out.Y = y3;
+  out.Z = z3;
   out.inf = 0;
   const uint32_t live = !p.inf & !q_skip;
   if (live & hz) {  // P == +-Q: rare (crafted keys only); divergent branch, exact result
@@ -205,37 +222,41 @@ CG_HD void ec_add(jpt& r, const jpt& p, const jpt& q, uint32_t q_skip) {
   const uint32_t take_q = p.inf & !q_skip, take_p = q_skip;
   jpt qq = q;
   if (AFFINE) {
-    CG_UNROLL for (int i = 0; i < 8; ++i) qq.Z[i] = 0;
-    qq.Z[0] = 1;
+    F26<C>::one(qq.Z);
     qq.inf = 0;
   }
-  mp_select(out.X, out.X, qq.X, take_q);
-  mp_select(out.Y, out.Y, qq.Y, take_q);
-  mp_select(out.Z, out.Z, qq.Z, take_q);
+  f26_select(out.X, out.X, qq.X, take_q);
+  f26_select(out.Y, out.Y, qq.Y, take_q);
+  f26_select(out.Z, out.Z, qq.Z, take_q);
   out.inf = take_q ? qq.inf : out.inf;
-  mp_select(out.X, out.X, p.X, take_p);
-  mp_select(out.Y, out.Y, p.Y, take_p);
-  mp_select(out.Z, out.Z, p.Z, take_p);
+  f26_select(out.X, out.X, p.X, take_p);
+  f26_select(out.Y, out.Y, p.Y, take_p);
+  f26_select(out.Z, out.Z, p.Z, take_p);
   out.inf = take_p ? p.inf : out.inf;
   r = out;
 }
 
+// B.6: x, y < p and y^2 == x^3 + a x + b; returns the point in Montgomery form.
 template <class C>
-CG_HD uint32_t ec_on_curve(const uint32_t x[8], const uint32_t y[8]) {
-  uint32_t pp[8], lhs[8], rhs[8], t[8], b[8];
+CG_HD uint32_t ec_on_curve(const uint32_t x[8], const uint32_t y[8], f26& xm, f26& ym) {
+  uint32_t pp[8];
   C::p(pp);
+  f26_from_u256<C>(xm, x);
+  f26_from_u256<C>(ym, y);
   if (!mp_lt(x, pp) || !mp_lt(y, pp)) return 0;
-  fp_sqr<C>(lhs, y);
-  fp_sqr<C>(rhs, x);
-  fp_mul<C>(rhs, rhs, x);
+  f26 lhs, rhs, t, b;
+  f26_sqr<C>(lhs, ym);
+  f26_sqr<C>(rhs, xm);
+  f26_mul<C>(rhs, rhs, xm);
   if (C::kAMinus3) {
-    fp_add<C>(t, x, x);
-    fp_add<C>(t, t, x);
-    fp_sub<C>(rhs, rhs, t);
+    f26_add(t, xm, xm);
+    f26_add(t, t, xm);
+    f26_sub(rhs, rhs, t);
   }
-  C::b(b);
-  fp_add<C>(rhs, rhs, b);
-  return mp_eq(lhs, rhs);
+  F26<C>::b(b);
+  f26_add(rhs, rhs, b);
+  f26_sub(t, lhs, rhs);  // c 6
+  return f26_iszero<C>(t);
 }
 
 // 8 big-endian bytes-as-LE-words (staged layout) -> LE limbs of a 256-bit BE number
@@ -289,22 +310,35 @@ CG_HD void recode_g(uint32_t out[9], const uint32_t k[8]) {
   out[8] = carry + 0x8000u;
 }
 
-// Phase 1: everything up to the scalars; returns the pre-verdict
-// (V_* codes of cg_ed25519.h: 0 accept .. 4 arg-empty, 0xff compute).
+// Phase 1a: key check, verdict precedence, e = SHA-256(M) mod n; returns the
+// pre-verdict (V_* codes of cg_ed25519.h: 0 accept .. 4 arg-empty, 0xff compute).
 template <class C>
-CG_HD uint32_t ecdsa_prep_scalars(const uint32_t qx[8], const uint32_t qy[8], uint32_t der_status,
-                                  const uint32_t r[8], const uint32_t s[8], uint32_t sig_len, const uint8_t* msg,
-                                  uint32_t msg_len, uint32_t mode, uint32_t u1[8], uint32_t u2[8]) {
-  if (!ec_on_curve<C>(qx, qy)) return 3;                        // KEY_INVALID
+CG_HD uint32_t ecdsa_prep_front(const uint32_t qx[8], const uint32_t qy[8], uint32_t der_status, uint32_t sig_len,
+                                const uint8_t* msg, uint32_t msg_len, uint32_t mode, uint32_t e[8]) {
+  f26 xm, ym;
+  if (!ec_on_curve<C>(qx, qy, xm, ym)) return 3;                // KEY_INVALID
   if (mode == 1 && (sig_len == 0 || msg_len == 0)) return 4;      // ARG_EMPTY (doVerify)
   if (der_status == DER_MALFORMED) return 2;                      // SIG_MALFORMED
   if (der_status == DER_RANGE) return 1;                          // REJECT
-  uint32_t hbe[8], e[8], nn[8], t[8], w[8];
+  uint32_t hbe[8], nn[8], t[8];
   sha256_mem(hbe, msg, msg_len);
   CG_UNROLL for (int i = 0; i < 8; ++i) e[i] = hbe[7 - i];
   C::n(nn);
   const uint32_t bw = mp_sub(t, e, nn);
   mp_select(e, t, e, bw);  // e mod n (e < 2^256 < 2n)
+  return 0xff;
+}
+
+// Phase 1: everything up to the scalars, one lane on its own (host tests; the
+// kernels replace mn_inv by a batched inversion over the whole chunk and take
+// u1 = e w, u2 = r w from w in Montgomery form, ecdsa_kernels.hip).
+template <class C>
+CG_HD uint32_t ecdsa_prep_scalars(const uint32_t qx[8], const uint32_t qy[8], uint32_t der_status,
+                                  const uint32_t r[8], const uint32_t s[8], uint32_t sig_len, const uint8_t* msg,
+                                  uint32_t msg_len, uint32_t mode, uint32_t u1[8], uint32_t u2[8]) {
+  uint32_t e[8], w[8];
+  const uint32_t pre = ecdsa_prep_front<C>(qx, qy, der_status, sig_len, msg, msg_len, mode, e);
+  if (pre != 0xff) return pre;
   mn_inv<C>(w, s);
   mn_mulmod<C>(u1, e, w);
   mn_mulmod<C>(u2, r, w);
@@ -328,7 +362,7 @@ CG_HD uint32_t ecdsa_prep(const uint32_t qx[8], const uint32_t qy[8], uint32_t d
 template <class C, typename GetQ, typename GetG>
 CG_HD void ecdsa_joint(jpt& acc, uint32_t d1[9], uint32_t d2[9], GetQ&& getQ, GetG&& getG) {
   jpt t;
-  CG_UNROLL for (int i = 0; i < 8; ++i) { acc.X[i] = 0; acc.Y[i] = 0; acc.Z[i] = 0; }
+  CG_UNROLL for (int i = 0; i < 10; ++i) { acc.X.v[i] = 0; acc.Y.v[i] = 0; acc.Z.v[i] = 0; }
   acc.inf = 1;
   CG_NOUNROLL for (int i = 64; i >= 0; --i) {
     if (i != 64) {
@@ -357,9 +391,9 @@ CG_HD void ecdsa_joint(jpt& acc, uint32_t d1[9], uint32_t d2[9], GetQ&& getQ, Ge
     {
       const uint32_t neg = eq < 8, a = neg ? 8 - eq : eq - 8;
       getQ(a == 0 ? 1u : a, t);
-      uint32_t ny[8];
-      fp_neg<C>(ny, t.Y);
-      mp_select(t.Y, t.Y, ny, neg);
+      f26 ny;
+      f26_neg(ny, t.Y);
+      f26_select(t.Y, t.Y, ny, neg);
       t.inf = 0;
       ec_add<C, false>(acc, acc, t, a == 0);
     }
@@ -368,9 +402,9 @@ CG_HD void ecdsa_joint(jpt& acc, uint32_t d1[9], uint32_t d2[9], GetQ&& getQ, Ge
       constexpr uint32_t kHalf = 1u << (kGWin - 1);
       const uint32_t neg = eg < kHalf, a = neg ? kHalf - eg : eg - kHalf;
       getG(a == 0 ? 1u : a, t);
-      uint32_t ny[8];
-      fp_neg<C>(ny, t.Y);
-      mp_select(t.Y, t.Y, ny, neg);
+      f26 ny;
+      f26_neg(ny, t.Y);
+      f26_select(t.Y, t.Y, ny, neg);
       t.inf = 0;
       ec_add<C, true>(acc, acc, t, a == 0);
     }
@@ -498,21 +532,28 @@ CG_HD uint32_t glv_split(const uint32_t u2[8], uint32_t k1[8], uint32_t k2[8], u
   return nd < 33 ? 33u : nd;
 }
 
+// secp256k1 digits from (u1, u2) with the GLV split; returns aux (below).
+CG_HD uint32_t ecdsa_k1_digits(const uint32_t u1[8], const uint32_t u2[8], uint32_t dg[9], uint32_t dk1[9],
+                               uint32_t dk2[9]) {
+  uint32_t k1[8], k2[8], neg1, neg2;
+  const uint32_t nd = glv_split(u2, k1, k2, neg1, neg2);
+  recode_g(dg, u1);
+  recode16_65(dk1, k1);
+  recode16_65(dk2, k2);
+  return nd | neg1 << 8 | neg2 << 9;
+}
+
 // secp256k1 phase 1 with the GLV split: dg = recode_g(u1), dk1/dk2 = recode16_65 of
 // |k1|, |k2|; nd / signs returned through `aux` (nd | neg1 << 8 | neg2 << 9).
 CG_HD uint32_t ecdsa_prep_k1glv(const uint32_t qx[8], const uint32_t qy[8], uint32_t der_status, const uint32_t r[8],
                                 const uint32_t s[8], uint32_t sig_len, const uint8_t* msg, uint32_t msg_len,
                                 uint32_t mode, uint32_t dg[9], uint32_t dk1[9], uint32_t dk2[9], uint32_t& aux) {
-  uint32_t u1[8], u2[8], k1[8], k2[8], neg1, neg2;
+  uint32_t u1[8], u2[8];
   aux = 33;
   const uint32_t pre =
       ecdsa_prep_scalars<CurveK1>(qx, qy, der_status, r, s, sig_len, msg, msg_len, mode, u1, u2);
   if (pre != 0xff) return pre;
-  const uint32_t nd = glv_split(u2, k1, k2, neg1, neg2);
-  recode_g(dg, u1);
-  recode16_65(dk1, k1);
-  recode16_65(dk2, k2);
-  aux = nd | neg1 << 8 | neg2 << 9;
+  aux = ecdsa_k1_digits(u1, u2, dg, dk1, dk2);
   return 0xff;
 }
 
@@ -547,7 +588,7 @@ CG_HD void ecdsa_joint_glv(jpt& acc, uint32_t nd, uint32_t dk1[9], uint32_t dk2[
   shl_nibbles9(dk1, 72 - nd);  // digit nd-1 to the top nibble
   shl_nibbles9(dk2, 72 - nd);
   jpt t;
-  CG_UNROLL for (int i = 0; i < 8; ++i) { acc.X[i] = 0; acc.Y[i] = 0; acc.Z[i] = 0; }
+  CG_UNROLL for (int i = 0; i < 10; ++i) { acc.X.v[i] = 0; acc.Y.v[i] = 0; acc.Z.v[i] = 0; }
   acc.inf = 1;
   CG_NOUNROLL for (int i = (int)nd - 1; i >= 0; --i) {
     if (i != (int)nd - 1) {
@@ -567,14 +608,13 @@ CG_HD void ecdsa_joint_glv(jpt& acc, uint32_t nd, uint32_t dk1[9], uint32_t dk2[
       const uint32_t neg = (e < 8) ^ (slot ? neg2 : neg1), a = e < 8 ? 8 - e : e - 8;
       getQ(a == 0 ? 1u : a, t);
       if (slot) {
-        uint32_t beta[8], bx[8];
-        GlvK1::beta(beta);
-        fp_mul<C>(bx, t.X, beta);  // phi(X:Y:Z) = (beta X : Y : Z)
-        CG_UNROLL for (int w = 0; w < 8; ++w) t.X[w] = bx[w];
+        f26 beta;
+        F26<C>::beta(beta);
+        f26_mul<C>(t.X, t.X, beta);  // phi(X:Y:Z) = (beta X : Y : Z)
       }
-      uint32_t ny[8];
-      fp_neg<C>(ny, t.Y);
-      mp_select(t.Y, t.Y, ny, neg);
+      f26 ny;
+      f26_neg(ny, t.Y);
+      f26_select(t.Y, t.Y, ny, neg);
       t.inf = 0;
       ec_add<C, false>(acc, acc, t, a == 0);
     }
@@ -595,9 +635,9 @@ CG_HD void ecdsa_joint_glv(jpt& acc, uint32_t nd, uint32_t dk1[9], uint32_t dk2[
         const uint32_t e = tb ? eh : eg;
         const uint32_t neg = e < 0x8000u, a = neg ? 0x8000u - e : e - 0x8000u;
         getG(tb, a == 0 ? 1u : a, t);
-        uint32_t ny[8];
-        fp_neg<C>(ny, t.Y);
-        mp_select(t.Y, t.Y, ny, neg);
+        f26 ny;
+        f26_neg(ny, t.Y);
+        f26_select(t.Y, t.Y, ny, neg);
         t.inf = 0;
         ec_add<C, true>(acc, acc, t, a == 0);
       }
@@ -610,16 +650,21 @@ template <class C>
 CG_HD uint32_t ecdsa_x_check(const jpt& acc, const uint32_t r[8]) {
   if (acc.inf) return 1;
   // x(P) mod n == r  <=>  X == r Z^2  or  (r + n < p and X == (r + n) Z^2)
-  uint32_t z2[8], rz[8], nn[8], pp[8], rn[8];
-  fp_sqr<C>(z2, acc.Z);
-  fp_mul<C>(rz, r, z2);
-  if (mp_eq(rz, acc.X)) return 0;
+  f26 z2, rm, rz;
+  uint32_t nn[8], pp[8], rn[8];
+  f26_sqr<C>(z2, acc.Z);
+  f26_from_u256<C>(rm, r);
+  f26_mul<C>(rz, rm, z2);
+  f26_sub(rz, rz, acc.X);
+  if (f26_iszero<C>(rz)) return 0;
   C::n(nn);
   C::p(pp);
   const uint32_t carry = mp_add(rn, r, nn);
   if (!carry && mp_lt(rn, pp)) {
-    fp_mul<C>(rz, rn, z2);
-    if (mp_eq(rz, acc.X)) return 0;
+    f26_from_u256<C>(rm, rn);
+    f26_mul<C>(rz, rm, z2);
+    f26_sub(rz, rz, acc.X);
+    if (f26_iszero<C>(rz)) return 0;
   }
   return 1;
 }
@@ -636,8 +681,9 @@ CG_HD uint32_t ecdsa_msm_check(uint32_t d1[9], uint32_t d2[9], const uint32_t r[
 template <class C, typename Put>
 CG_HD void ecdsa_q_table(const uint32_t qx[8], const uint32_t qy[8], Put&& put) {
   jpt q1, cur, t;
-  CG_UNROLL for (int i = 0; i < 8; ++i) { q1.X[i] = qx[i]; q1.Y[i] = qy[i]; q1.Z[i] = 0; }
-  q1.Z[0] = 1;
+  f26_from_u256<C>(q1.X, qx);
+  f26_from_u256<C>(q1.Y, qy);
+  F26<C>::one(q1.Z);
   q1.inf = 0;
   put(1, q1);
   cur = q1;
@@ -648,49 +694,46 @@ CG_HD void ecdsa_q_table(const uint32_t qx[8], const uint32_t qy[8], Put&& put) 
   }
 }
 
-// Affine k*G (or k*2^128 G, shift128 = 1; 1 <= k < 2^17) for the shared generator
-// tables: left-to-right binary
-// with the exact formulas, then one inversion.  One lane per entry at context
-// creation (and on the host for the tests).
+// (X : Y : Z) -> affine (x, y), Montgomery form (table setup and tests only).
 template <class C>
-CG_HD void ecdsa_g_entry(uint32_t k, uint32_t x[8], uint32_t y[8], uint32_t shift128 = 0) {
+CG_HD void ec_to_affine(f26& x, f26& y, const jpt& p) {
+  f26 zi, zi2, zi3;
+  f26_inv<C>(zi, p.Z);
+  f26_sqr<C>(zi2, zi);
+  f26_mul<C>(zi3, zi2, zi);
+  f26_mul<C>(x, p.X, zi2);
+  f26_mul<C>(y, p.Y, zi3);
+}
+
+// Affine k*G (or k*2^128 G, shift128 = 1; 1 <= k < 2^17) in Montgomery form for the
+// shared generator tables: left-to-right binary with the exact formulas, then one
+// inversion.  One lane per entry at context creation (and on the host for the tests).
+template <class C>
+CG_HD void ecdsa_g_entry(uint32_t k, f26& x, f26& y, uint32_t shift128 = 0) {
   const uint32_t k1x[8] = {0x16F81798u, 0x59F2815Bu, 0x2DCE28D9u, 0x029BFCDBu, 0xCE870B07u, 0x55A06295u, 0xF9DCBBACu, 0x79BE667Eu};
   const uint32_t k1y[8] = {0xFB10D4B8u, 0x9C47D08Fu, 0xA6855419u, 0xFD17B448u, 0x0E1108A8u, 0x5DA4FBFCu, 0x26A3C465u, 0x483ADA77u};
   const uint32_t r1x[8] = {0xD898C296u, 0xF4A13945u, 0x2DEB33A0u, 0x77037D81u, 0x63A440F2u, 0xF8BCE6E5u, 0xE12C4247u, 0x6B17D1F2u};
   const uint32_t r1y[8] = {0x37BF51F5u, 0xCBB64068u, 0x6B315ECEu, 0x2BCE3357u, 0x7C0F9E16u, 0x8EE7EB4Au, 0xFE1A7F9Bu, 0x4FE342E2u};
   jpt g, acc;
-  CG_UNROLL for (int i = 0; i < 8; ++i) {
-    g.X[i] = C::kScheme == 2 ? k1x[i] : r1x[i];
-    g.Y[i] = C::kScheme == 2 ? k1y[i] : r1y[i];
-    g.Z[i] = i == 0;
-    acc.X[i] = acc.Y[i] = acc.Z[i] = 0;
-  }
+  f26_from_u256<C>(g.X, C::kScheme == 2 ? k1x : r1x);
+  f26_from_u256<C>(g.Y, C::kScheme == 2 ? k1y : r1y);
+  F26<C>::one(g.Z);
+  CG_UNROLL for (int i = 0; i < 10; ++i) acc.X.v[i] = acc.Y.v[i] = acc.Z.v[i] = 0;
   g.inf = 0;
   acc.inf = 1;
   CG_NOUNROLL for (uint32_t i = 0; i < 128 * shift128; ++i) ec_dbl<C>(g, g);  // 2^128 G (its own table)
   if (shift128) {  // back to affine: the table loop adds g with the mixed formula
-    uint32_t zi[8], zi2[8], zi3[8], gx[8], gy[8];
-    fp_inv<C>(zi, g.Z);
-    fp_sqr<C>(zi2, zi);
-    fp_mul<C>(zi3, zi2, zi);
-    fp_mul<C>(gx, g.X, zi2);
-    fp_mul<C>(gy, g.Y, zi3);
-    CG_UNROLL for (int i = 0; i < 8; ++i) {
-      g.X[i] = gx[i];
-      g.Y[i] = gy[i];
-      g.Z[i] = i == 0;
-    }
+    f26 gx, gy;
+    ec_to_affine<C>(gx, gy, g);
+    g.X = gx;
+    g.Y = gy;
+    F26<C>::one(g.Z);
   }
   CG_NOUNROLL for (int b = 16; b >= 0; --b) {
     ec_dbl<C>(acc, acc);
     if ((k >> b) & 1) ec_add<C, true>(acc, acc, g, 0);
   }
-  uint32_t zi[8], zi2[8], zi3[8];
-  fp_inv<C>(zi, acc.Z);
-  fp_sqr<C>(zi2, zi);
-  fp_mul<C>(zi3, zi2, zi);
-  fp_mul<C>(x, acc.X, zi2);
-  fp_mul<C>(y, acc.Y, zi3);
+  ec_to_affine<C>(x, y, acc);
 }
 
 }  // namespace cg

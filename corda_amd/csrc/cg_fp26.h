@@ -1,0 +1,339 @@
+// GF(p) arithmetic for the ECDSA kernels (P-256 and secp256k1): Montgomery form
+// with R = 2^260 over 10 signed 32-bit limbs of radix 2^26 (gfx950 VALU, no MFMA).
+//
+// Why not the saturated 8 x 32-bit limbs of cg_mp256.h: every limb product there
+// needs a carry instruction next to its v_mad_u64_u32, the NIST/Solinas fold is
+// ~100 64-bit adds, and each add/sub is a full carry chain plus a conditional
+// subtraction.  With 26-bit limbs a product is 100 full-rate v_mad_i64_i32 into
+// 64-bit column sums, add/sub/neg are 10 plain 32-bit ops with no carries, and
+// both primes are sparse in radix 2^26 (x = 2^26):
+//   P-256      p = -1 + 2^18 x^3 + 2^10 x^7 - 2^16 x^8 + 2^22 x^9,  -p^-1 = 1 mod x
+//   secp256k1  p = -977 - 2^6 x + 2^22 x^9,                        -p^-1 = 977^-1 mod x
+// so each of the ten Montgomery steps is a mask (or one mul_lo), a carry and 2-4
+// constant mads.  The result's top bits (>= 2^256) are folded back with the prime's
+// form (v - top p), which keeps every multiplication output below 2^256 (1 + 2^-21).
+//
+// Bounds (checked on the host with -DCG_CHECK_BOUNDS over the golden/random suites,
+// tests/test_native_host.py):
+//   * a "unit" value (f26_mul/f26_sqr output, f26_norm output, table entry, converted
+//     input) has |limb| <= 1.125 * 2^26 and value in (-2^102, 2^256 (1 + 2^-21)).
+//   * a linear combination of unit values whose coefficients' absolute values sum to c
+//     has |limb| <= 1.125 c 2^26; f26_mul/f26_sqr accept inputs with c_a c_b <= 150
+//     (10 column products of 1.125^2 c_a c_b 2^52 stay below 2^62), f26_norm accepts
+//     c <= 16.  The point formulas (cg_ecdsa.h) note the c of every multiplication.
+//
+// Constants: tools/gen_fp26_consts.py.
+#pragma once
+#include "cg_common.h"
+#include "cg_mp256.h"
+
+namespace cg {
+
+struct f26 {
+  int32_t v[10];
+};
+
+constexpr int32_t kF26Mask = (1 << 26) - 1;
+
+#if defined(CG_CHECK_BOUNDS) && !defined(__HIP_DEVICE_COMPILE__)
+struct CgBounds26 {
+  int64_t max_limb = 0;  // largest |input limb| of a multiplication
+  __int128 max_col = 0;  // largest |column sum| before reduction
+  int32_t max_top = 0;   // largest |folded top|
+};
+inline CgBounds26& cg_bounds26() {
+  static CgBounds26 b;
+  return b;
+}
+inline void cg_bounds26_mul(const f26& f, const f26& g) {
+  CgBounds26& b = cg_bounds26();
+  __int128 col[19] = {0};
+  for (int i = 0; i < 10; ++i) {
+    const int64_t af = f.v[i] < 0 ? -(int64_t)f.v[i] : f.v[i], ag = g.v[i] < 0 ? -(int64_t)g.v[i] : g.v[i];
+    if (af > b.max_limb) b.max_limb = af;
+    if (ag > b.max_limb) b.max_limb = ag;
+    for (int j = 0; j < 10; ++j) col[i + j] += (__int128)f.v[i] * g.v[j];
+  }
+  for (int k = 0; k < 19; ++k) {
+    const __int128 a = col[k] < 0 ? -col[k] : col[k];
+    if (a > b.max_col) b.max_col = a;
+    if (a >= ((__int128)1 << 62)) {
+      fprintf(stderr, "cg bounds (f26): column %d = 2^%.2f\n", k, __builtin_log2((double)a));
+      __builtin_trap();
+    }
+  }
+}
+inline void cg_bounds26_top(int32_t top) {
+  const int32_t a = top < 0 ? -top : top;
+  if (a > cg_bounds26().max_top) cg_bounds26().max_top = a;
+  if (a > 64) {
+    fprintf(stderr, "cg bounds (f26): fold top %d\n", top);
+    __builtin_trap();
+  }
+}
+#define CG_BOUNDS26_MUL(f, g) cg_bounds26_mul(f, g)
+#define CG_BOUNDS26_TOP(t) cg_bounds26_top(t)
+#else
+#define CG_BOUNDS26_MUL(f, g) ((void)0)
+#define CG_BOUNDS26_TOP(t) ((void)0)
+#endif
+
+// Keeps a derived limb (2 f_i in squaring) a 32-bit value so its products stay one
+// v_mad_i64_i32 (see fe_pin in cg_fe25519.h).
+CG_HD int32_t f26_pin(int32_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm("" : "+v"(x));
+#endif
+  return x;
+}
+
+// A wave-uniform constant hidden from the optimiser (kept in an SGPR): m * k + t
+// with k a power of two would otherwise become a 64-bit shift + add/sub pair (2-3
+// instructions) instead of one v_mad_i64_i32.
+CG_HD int32_t f26_kpin(int32_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm("" : "+s"(x));
+#endif
+  return x;
+}
+
+CG_HD void f26_load(f26& h, const int32_t (&c)[10]) {
+  CG_UNROLL for (int i = 0; i < 10; ++i) h.v[i] = c[i];
+}
+
+// ------------------------------------------------------------ per-curve forms
+template <class C>
+struct F26;
+
+template <>
+struct F26<CurveR1> {
+  // one Montgomery step: t[k] + m p == 0 mod 2^26 with m = t[k] mod 2^26; the
+  // exact quotient (t[k] - m) / 2^26 = t[k] >> 26 carries into t[k+1]
+  CG_HDM static void step(int64_t t[19], int k) {
+    const int32_t m = (int32_t)((uint32_t)t[k] & (uint32_t)kF26Mask);
+    t[k + 1] += t[k] >> 26;
+    t[k + 3] += (int64_t)m * f26_kpin(1 << 18);
+    t[k + 7] += (int64_t)m * f26_kpin(1 << 10);
+    t[k + 8] += (int64_t)m * f26_kpin(-(1 << 16));
+    t[k + 9] += (int64_t)m * f26_kpin(1 << 22);
+  }
+  // h - top p with top = h.v[9] >> 22: -top 2^256 + top (2^224 - 2^192 - 2^96 + 1)
+  CG_HDM static void fold(f26& h) {
+    const int32_t top = h.v[9] >> 22;
+    CG_BOUNDS26_TOP(top);
+    h.v[9] &= (1 << 22) - 1;
+    h.v[0] += top;
+    h.v[3] -= top * (1 << 18);
+    h.v[7] -= top * (1 << 10);
+    h.v[8] += top * (1 << 16);
+  }
+  CG_HDM static void p(f26& h) {
+    const int32_t c[10] = {0x3FFFFFF, 0x3FFFFFF, 0x3FFFFFF, 0x003FFFF, 0x0000000,
+                           0x0000000, 0x0000000, 0x0000400, 0x3FF0000, 0x03FFFFF};
+    f26_load(h, c);
+  }
+  CG_HDM static void one(f26& h) {  // R mod p
+    const int32_t c[10] = {0x0000010, 0x0000000, 0x0000000, 0x3C00000, 0x3FFFFFF,
+                           0x3FFFFFF, 0x3FFFFFF, 0x3FFBFFF, 0x00FFFFF, 0x0000000};
+    f26_load(h, c);
+  }
+  CG_HDM static void r2(f26& h) {  // R^2 mod p
+    const int32_t c[10] = {0x0000300, 0x0000000, 0x3F00000, 0x3FFFFFF, 0x3FFFFFB,
+                           0x3FFFFBF, 0x3FFFFFF, 0x3F7FFFF, 0x0FFFFFF, 0x0000001};
+    f26_load(h, c);
+  }
+  CG_HDM static void b(f26& h) {  // b R mod p
+    const int32_t c[10] = {0x04BDDFD, 0x37D88A7, 0x090D89C, 0x32A210C, 0x2CF005C,
+                           0x084BB5A, 0x220ABF7, 0x20D0568, 0x1DD4874, 0x030C018};
+    f26_load(h, c);
+  }
+};
+
+template <>
+struct F26<CurveK1> {
+  static constexpr uint32_t kPinv = 0x2253531u;  // 977^-1 = -p^-1 mod 2^26
+  CG_HDM static void step(int64_t t[19], int k) {
+    const int32_t m = (int32_t)(((uint32_t)t[k] * kPinv) & (uint32_t)kF26Mask);
+    t[k + 1] += (t[k] + (int64_t)m * f26_kpin(-977)) >> 26;
+    t[k + 1] += (int64_t)m * f26_kpin(-(1 << 6));
+    t[k + 9] += (int64_t)m * f26_kpin(1 << 22);
+  }
+  // h - top p = h - top 2^256 + top (2^32 + 977)
+  CG_HDM static void fold(f26& h) {
+    const int32_t top = h.v[9] >> 22;
+    CG_BOUNDS26_TOP(top);
+    h.v[9] &= (1 << 22) - 1;
+    h.v[0] += top * 977;
+    h.v[1] += top * (1 << 6);
+  }
+  CG_HDM static void p(f26& h) {
+    const int32_t c[10] = {0x3FFFC2F, 0x3FFFFBF, 0x3FFFFFF, 0x3FFFFFF, 0x3FFFFFF,
+                           0x3FFFFFF, 0x3FFFFFF, 0x3FFFFFF, 0x3FFFFFF, 0x03FFFFF};
+    f26_load(h, c);
+  }
+  CG_HDM static void one(f26& h) {
+    const int32_t c[10] = {0x0003D10, 0x0000400, 0, 0, 0, 0, 0, 0, 0, 0};
+    f26_load(h, c);
+  }
+  CG_HDM static void r2(f26& h) {
+    const int32_t c[10] = {0x290A100, 0x1E88003, 0x0100000, 0, 0, 0, 0, 0, 0, 0};
+    f26_load(h, c);
+  }
+  CG_HDM static void b(f26& h) {
+    const int32_t c[10] = {0x001AB70, 0x0001C00, 0, 0, 0, 0, 0, 0, 0, 0};
+    f26_load(h, c);
+  }
+  CG_HDM static void beta(f26& h) {  // beta R mod p (GLV endomorphism)
+    const int32_t c[10] = {0x018AF97, 0x0D873FA, 0x0AF58A4, 0x0C712E0, 0x03FDE16,
+                           0x0B8E414, 0x18978D0, 0x354FE3A, 0x2EBCBB3, 0x02928DA};
+    f26_load(h, c);
+  }
+};
+
+// ------------------------------------------------------------ limb-wise ops
+CG_HD void f26_add(f26& h, const f26& f, const f26& g) {
+  CG_UNROLL for (int i = 0; i < 10; ++i) h.v[i] = f.v[i] + g.v[i];
+}
+CG_HD void f26_sub(f26& h, const f26& f, const f26& g) {
+  CG_UNROLL for (int i = 0; i < 10; ++i) h.v[i] = f.v[i] - g.v[i];
+}
+CG_HD void f26_neg(f26& h, const f26& f) {
+  CG_UNROLL for (int i = 0; i < 10; ++i) h.v[i] = -f.v[i];
+}
+// h = c ? g : f   (c is 0/1)
+CG_HD void f26_select(f26& h, const f26& f, const f26& g, uint32_t c) {
+  CG_UNROLL for (int i = 0; i < 10; ++i) h.v[i] = c ? g.v[i] : f.v[i];
+}
+
+// Exact carry chain: limbs 0..8 into [0, 2^26), limb 9 takes the rest (floor).
+CG_HD void f26_carry(f26& h) {
+  CG_UNROLL for (int i = 0; i < 9; ++i) {
+    h.v[i + 1] += h.v[i] >> 26;
+    h.v[i] &= kF26Mask;
+  }
+}
+
+// Any combination with c <= 16 -> a unit value (same residue).
+template <class C>
+CG_HD void f26_norm(f26& h) {
+  f26_carry(h);
+  F26<C>::fold(h);
+}
+
+// ------------------------------------------------------------ Montgomery product
+// 64-bit column sums t[0..18] -> t R^-1 mod p as a unit value.
+template <class C>
+CG_HD void f26_redc(f26& h, int64_t t[19]) {
+  CG_UNROLL for (int k = 0; k < 10; ++k) F26<C>::step(t, k);
+  CG_UNROLL for (int k = 10; k < 18; ++k) {
+    t[k + 1] += t[k] >> 26;
+    h.v[k - 10] = (int32_t)((uint32_t)t[k] & (uint32_t)kF26Mask);
+  }
+  h.v[8] = (int32_t)((uint32_t)t[18] & (uint32_t)kF26Mask);
+  h.v[9] = (int32_t)(t[18] >> 26);
+  F26<C>::fold(h);
+}
+
+// h = f g R^-1 mod p
+template <class C>
+CG_HD void f26_mul(f26& h, const f26& f, const f26& g) {
+  CG_BOUNDS26_MUL(f, g);
+  int64_t t[19];
+  CG_UNROLL for (int k = 0; k < 19; ++k) t[k] = 0;
+  CG_UNROLL for (int i = 0; i < 10; ++i) {
+    CG_UNROLL for (int j = 0; j < 10; ++j) t[i + j] += (int64_t)f.v[i] * g.v[j];
+  }
+  f26_redc<C>(h, t);
+}
+
+// h = f^2 R^-1 mod p: 45 cross products against pre-doubled limbs + 10 squares
+template <class C>
+CG_HD void f26_sqr(f26& h, const f26& f) {
+  CG_BOUNDS26_MUL(f, f);
+  int32_t f2[10];
+  CG_UNROLL for (int i = 0; i < 10; ++i) f2[i] = f26_pin(2 * f.v[i]);
+  int64_t t[19];
+  CG_UNROLL for (int k = 0; k < 19; ++k) t[k] = 0;
+  CG_UNROLL for (int i = 0; i < 10; ++i) {
+    t[2 * i] += (int64_t)f.v[i] * f.v[i];
+    CG_UNROLL for (int j = i + 1; j < 10; ++j) t[i + j] += (int64_t)f2[i] * f.v[j];
+  }
+  f26_redc<C>(h, t);
+}
+
+// Two independent products interleaved (the scheduler overlaps their reductions).
+template <class C>
+CG_HD void f26_mul2(f26& h0, const f26& f0, const f26& g0, f26& h1, const f26& f1, const f26& g1) {
+  f26 a, b;
+  f26_mul<C>(a, f0, g0);
+  f26_mul<C>(b, f1, g1);
+  h0 = a;
+  h1 = b;
+}
+
+// ------------------------------------------------------------ predicates, conversion
+// value == 0 mod p?  (input: combination with c <= 16)
+template <class C>
+CG_HD uint32_t f26_iszero(const f26& a) {
+  f26 t = a, pp;
+  f26_norm<C>(t);   // value in (-2^102, 2^256 + 2^236): 0 mod p <=> value is 0 or p
+  f26_carry(t);     // unique limbs for the value
+  F26<C>::p(pp);
+  uint32_t z = 0, e = 0;
+  CG_UNROLL for (int i = 0; i < 10; ++i) {
+    z |= (uint32_t)t.v[i];
+    e |= (uint32_t)(t.v[i] ^ pp.v[i]);
+  }
+  return (z == 0) | (e == 0);
+}
+
+// canonical 256-bit integer (8 LE words, < 2^256) -> Montgomery form (unit value)
+template <class C>
+CG_HD void f26_from_u256(f26& h, const uint32_t a[8]) {
+  f26 u, r2;
+  CG_UNROLL for (int i = 0; i < 10; ++i) {
+    const int bit = 26 * i, w = bit >> 5, s = bit & 31;
+    uint32_t x = a[w] >> s;
+    if (s > 6 && w + 1 < 8) x |= a[w + 1] << (32 - s);
+    u.v[i] = (int32_t)(x & (uint32_t)kF26Mask);
+  }
+  F26<C>::r2(r2);
+  f26_mul<C>(h, u, r2);
+}
+
+// Montgomery form (unit value) -> canonical residue in [0, p), 8 LE words
+template <class C>
+CG_HD void f26_to_u256(uint32_t out[8], const f26& a) {
+  f26 one, t;
+  CG_UNROLL for (int i = 0; i < 10; ++i) one.v[i] = i == 0;
+  f26_mul<C>(t, a, one);  // a R^-1: value in [0, p]
+  f26_carry(t);
+  CG_UNROLL for (int w = 0; w < 8; ++w) out[w] = 0;
+  CG_UNROLL for (int i = 0; i < 10; ++i) {
+    const int bit = 26 * i, w = bit >> 5, s = bit & 31;
+    const uint32_t x = (uint32_t)t.v[i];
+    out[w] |= x << s;
+    if (s > 6 && w + 1 < 8) out[w + 1] |= x >> (32 - s);
+  }
+  uint32_t pp[8], d[8];
+  C::p(pp);
+  const uint32_t bw = mp_sub(d, out, pp);
+  mp_select(out, d, out, bw);
+}
+
+// a^-1 (Montgomery in, Montgomery out) by Fermat; table setup and tests only.
+template <class C>
+CG_HD void f26_inv(f26& r, const f26& a) {
+  uint32_t pp[8], e[8];
+  C::p(pp);
+  const uint32_t two[8] = {2, 0, 0, 0, 0, 0, 0, 0};
+  mp_sub(e, pp, two);
+  f26 acc = a;  // top bit of p - 2 is set
+  for (int bit = 254; bit >= 0; --bit) {
+    f26_sqr<C>(acc, acc);
+    if ((e[bit >> 5] >> (bit & 31)) & 1) f26_mul<C>(acc, acc, a);
+  }
+  r = acc;
+}
+
+}  // namespace cg

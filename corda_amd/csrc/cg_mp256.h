@@ -296,6 +296,15 @@ CG_HD void mn_mul(uint32_t r[8], const uint32_t a[8], const uint32_t b[8]) {
   mp_select(r, d, t, bw & (t[8] == 0));
 }
 
+// R mod n = 2^256 - n (the Montgomery form of 1).
+template <class C>
+CG_HD void mn_one(uint32_t r[8]) {
+  uint32_t nn[8];
+  const uint32_t z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  C::n(nn);
+  mp_sub(r, z, nn);
+}
+
 // R^2 mod n, for converting into the Montgomery domain.
 template <class C>
 CG_HD void mn_r2(uint32_t r[8]);

@@ -2,8 +2,11 @@
 // for gfx950, BouncyCastle 1.57 semantics (cg_ecdsa.h).
 //
 //   cg_der_parse<C>   staging-time pre-pass: strict DER -> r, s limbs + status
-//   cg_ecdsa_prep<C>  key check, SHA-256(M), s^-1 / u1 / u2 mod n, digits, k*Q table;
-//                     secp256k1 also splits u2 = k1 + k2 lambda (GLV, cg_ecdsa.h)
+//   cg_ecdsa_prep_a<C> key check, SHA-256(M) mod n, k*Q table, s into the batched
+//                     inversion (cg_inv_up / cg_inv_root / cg_inv_down: a product
+//                     tree over the chunk, ~3 multiplications per s^-1 mod n)
+//   cg_ecdsa_prep_b<C> u1 / u2 = (e, r) s^-1 mod n, digits; secp256k1 also splits
+//                     u2 = k1 + k2 lambda (GLV, cg_ecdsa.h)
 //   cg_ecdsa_msm<C>   P-256: u1 G + u2 Q over 256 bits (4-bit Q windows, 16-bit G
 //                     windows); secp256k1: u1 G + k1 Q + k2 phi(Q) over ~129 bits
 //                     (G and 2^128 G tables); then the projective x check
@@ -14,7 +17,8 @@
 //   words), rs[w*cap+i] (16 LE limbs: r then s), der[i], sig_len[i], msg_off[i],
 //   msg_len[i]; scratch status[i] (verdict | digit count << 8 | signs << 16 for
 //   secp256k1), digits[w*scap+i] (27 words: u1 G digits, then k1 / k2 or u2
-//   nibbles), qtab[(e*24+w)*scap+i] (e = k-1 for k*Q, k = 1..8, X|Y|Z).
+//   nibbles), qtab[(e*30+w)*scap+i] (e = k-1 for k*Q, k = 1..8, X|Y|Z as 10
+//   radix-2^26 Montgomery limbs each, cg_fp26.h).
 #include <vector>
 
 #include "cg_ecdsa.h"
@@ -26,11 +30,14 @@ using namespace cg;
 namespace cg {
 
 struct EcdsaConsts {
-  uint32_t* gtab[2] = {nullptr, nullptr};  // affine k*G [kGTabEntries][16]; K1 also k*2^128 G after it
+  uint32_t* gtab[2] = {nullptr, nullptr};  // affine k*G [kGTabEntries][kGStride]; K1 also k*2^128 G after it
   uint32_t scap = 0;
   uint32_t* status = nullptr;
   uint32_t* digits = nullptr;
   uint32_t* qtab = nullptr;
+  uint32_t* ework = nullptr;  // e mod n [8][scap]
+  uint32_t* inv = nullptr;    // batched inversion: leaves, tree levels, trees (element-major)
+  size_t inv_words = 0;
 };
 
 }  // namespace cg
@@ -38,7 +45,8 @@ struct EcdsaConsts {
 namespace {
 
 constexpr uint32_t kEcChunk = 1u << 20;
-constexpr int kQWords = 24;
+constexpr int kQWords = 30;
+constexpr int kGStride = 20;  // affine table entry: x then y, 10 Montgomery limbs each (80 bytes)
 constexpr int kDigitWordsEc = 27;
 
 CG_DEV uint32_t wave_max_u32(uint32_t v) {
@@ -70,46 +78,179 @@ __global__ __launch_bounds__(256) void cg_der_parse(const uint8_t* __restrict__ 
   der[i] = st;
 }
 
+// Phase 1a (one lane per signature): key check, verdict precedence, e mod n, the
+// k*Q table; s in Montgomery form (s 2^256 mod n) into the batched inversion's
+// leaves (element-major, 8 words), or 1 (2^256 mod n) for lanes already decided.
 template <class C>
-__global__ __launch_bounds__(256) void cg_ecdsa_prep(const uint32_t* __restrict__ q, const uint32_t* __restrict__ rs,
-                                                     const uint32_t* __restrict__ der,
-                                                     const uint32_t* __restrict__ sig_len,
-                                                     const uint8_t* __restrict__ arena,
-                                                     const uint64_t* __restrict__ msg_off,
-                                                     const uint32_t* __restrict__ msg_len, uint32_t n, uint32_t cap,
-                                                     uint32_t scap, uint32_t mode, uint32_t* __restrict__ status,
-                                                     uint32_t* __restrict__ digits, uint32_t* __restrict__ qtab) {
+__global__ __launch_bounds__(256) void cg_ecdsa_prep_a(const uint32_t* __restrict__ q, const uint32_t* __restrict__ rs,
+                                                       const uint32_t* __restrict__ der,
+                                                       const uint32_t* __restrict__ sig_len,
+                                                       const uint8_t* __restrict__ arena,
+                                                       const uint64_t* __restrict__ msg_off,
+                                                       const uint32_t* __restrict__ msg_len, uint32_t n, uint32_t cap,
+                                                       uint32_t scap, uint32_t mode, uint32_t* __restrict__ status,
+                                                       uint32_t* __restrict__ ework, uint32_t* __restrict__ inv_leaf,
+                                                       uint32_t* __restrict__ qtab) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  uint32_t qw[16], qx[8], qy[8], r[8], s[8], d1[9], d2[9];
+  uint32_t qw[16], qx[8], qy[8], s[8], e[8], a[8];
   CG_UNROLL for (int w = 0; w < 16; ++w) qw[w] = q[(size_t)w * cap + i];
   be_words_to_limbs(qx, qw);
   be_words_to_limbs(qy, qw + 8);
-  CG_UNROLL for (int w = 0; w < 8; ++w) {
-    r[w] = rs[(size_t)w * cap + i];
-    s[w] = rs[(size_t)(8 + w) * cap + i];
-  }
-  uint32_t pre, aux = 0, d3[9];
-  if constexpr (C::kScheme == 2) {
-    pre = ecdsa_prep_k1glv(qx, qy, der[i], r, s, sig_len[i], arena + msg_off[i], msg_len[i], mode, d1, d2, d3, aux);
+  const uint32_t pre = ecdsa_prep_front<C>(qx, qy, der[i], sig_len[i], arena + msg_off[i], msg_len[i], mode, e);
+  status[i] = pre;
+  if (pre == 0xff) {
+    uint32_t r2[8];
+    CG_UNROLL for (int w = 0; w < 8; ++w) s[w] = rs[(size_t)(8 + w) * cap + i];
+    mn_r2<C>(r2);
+    mn_mul<C>(a, s, r2);
   } else {
-    pre = ecdsa_prep<C>(qx, qy, der[i], r, s, sig_len[i], arena + msg_off[i], msg_len[i], mode, d1, d2);
+    mn_one<C>(a);
   }
-  status[i] = pre | aux << 8;
+  uint4* leaf = reinterpret_cast<uint4*>(inv_leaf + (size_t)i * 8);
+  leaf[0] = make_uint4(a[0], a[1], a[2], a[3]);
+  leaf[1] = make_uint4(a[4], a[5], a[6], a[7]);
   if (pre != 0xff) return;
-  CG_UNROLL for (int w = 0; w < 9; ++w) {
-    digits[(size_t)w * scap + i] = d1[w];
-    digits[(size_t)(9 + w) * scap + i] = d2[w];
-    if constexpr (C::kScheme == 2) digits[(size_t)(18 + w) * scap + i] = d3[w];
-  }
+  CG_UNROLL for (int w = 0; w < 8; ++w) ework[(size_t)w * scap + i] = e[w];
   ecdsa_q_table<C>(qx, qy, [&](int k, const jpt& p) {
     uint32_t* base = qtab + (size_t)(k - 1) * kQWords * scap + i;
-    CG_UNROLL for (int w = 0; w < 8; ++w) {
-      base[(size_t)w * scap] = p.X[w];
-      base[(size_t)(8 + w) * scap] = p.Y[w];
-      base[(size_t)(16 + w) * scap] = p.Z[w];
+    CG_UNROLL for (int w = 0; w < 10; ++w) {
+      base[(size_t)w * scap] = (uint32_t)p.X.v[w];
+      base[(size_t)(10 + w) * scap] = (uint32_t)p.Y.v[w];
+      base[(size_t)(20 + w) * scap] = (uint32_t)p.Z.v[w];
     }
   });
+}
+
+// Batched inversion mod n (Montgomery's trick as a product tree): every inverse
+// s^-1 of a chunk costs ~3 multiplications instead of a 383-multiplication Fermat
+// exponentiation per lane.  Values are Montgomery residues (x 2^256 mod n), element-
+// major 8 words.  Up: block b multiplies its 256 values pairwise in an LDS heap
+// (node k = node 2k * node 2k+1, leaves 256..511), keeps the 255 internal nodes in
+// tree[b][1..255] and writes the product to out[b].
+CG_DEV void lds_get8(uint32_t v[8], const uint32_t (*h)[8], uint32_t k) {
+  CG_UNROLL for (int w = 0; w < 8; ++w) v[w] = h[k][w];
+}
+CG_DEV void lds_put8(uint32_t (*h)[8], uint32_t k, const uint32_t v[8]) {
+  CG_UNROLL for (int w = 0; w < 8; ++w) h[k][w] = v[w];
+}
+CG_DEV void gl_get8(uint32_t v[8], const uint32_t* p) {
+  const uint4 a = reinterpret_cast<const uint4*>(p)[0], b = reinterpret_cast<const uint4*>(p)[1];
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+CG_DEV void gl_put8(uint32_t* p, const uint32_t v[8]) {
+  reinterpret_cast<uint4*>(p)[0] = make_uint4(v[0], v[1], v[2], v[3]);
+  reinterpret_cast<uint4*>(p)[1] = make_uint4(v[4], v[5], v[6], v[7]);
+}
+
+template <class C>
+__global__ __launch_bounds__(256) void cg_inv_up(const uint32_t* __restrict__ in, uint32_t n,
+                                                 uint32_t* __restrict__ tree, uint32_t* __restrict__ out) {
+  __shared__ uint32_t h[512][8];
+  const uint32_t t = threadIdx.x, b = blockIdx.x, i = b * 256 + t;
+  uint32_t x[8], y[8], z[8];
+  if (i < n) gl_get8(x, in + (size_t)i * 8); else mn_one<C>(x);
+  lds_put8(h, 256 + t, x);
+  __syncthreads();
+  for (uint32_t w = 128; w >= 1; w >>= 1) {
+    if (t < w) {
+      const uint32_t k = w + t;
+      lds_get8(x, h, 2 * k);
+      lds_get8(y, h, 2 * k + 1);
+      mn_mul<C>(z, x, y);
+      lds_put8(h, k, z);
+    }
+    __syncthreads();
+  }
+  lds_get8(x, h, t ? t : 1u);
+  if (t) gl_put8(tree + ((size_t)b * 256 + t) * 8, x);
+  else gl_put8(out + (size_t)b * 8, x);
+}
+
+// The single root: its inverse, in Montgomery form (one lane).
+template <class C>
+__global__ void cg_inv_root(uint32_t* __restrict__ v) {
+  if (blockIdx.x | threadIdx.x) return;
+  uint32_t x[8], p[8], pi[8], r2[8];
+  const uint32_t one[8] = {1, 0, 0, 0, 0, 0, 0, 0};
+  gl_get8(x, v);
+  mn_mul<C>(p, x, one);  // plain product (invertible: every leaf is)
+  mn_inv<C>(pi, p);
+  mn_r2<C>(r2);
+  mn_mul<C>(x, pi, r2);
+  gl_put8(v, x);
+}
+
+// Down: with the inverse of block b's product (out_inv[b]), each internal node's
+// inverse gives its children's: inv(2k) = inv(k) * node(2k+1), inv(2k+1) = inv(k) *
+// node(2k); the leaves' inverses overwrite in[] (same positions, read first).
+template <class C>
+__global__ __launch_bounds__(256) void cg_inv_down(uint32_t* __restrict__ in, uint32_t n,
+                                                   const uint32_t* __restrict__ tree,
+                                                   const uint32_t* __restrict__ out_inv) {
+  __shared__ uint32_t h[512][8], g[256][8];
+  const uint32_t t = threadIdx.x, b = blockIdx.x, i = b * 256 + t;
+  uint32_t x[8], y[8], z[8];
+  if (i < n) gl_get8(x, in + (size_t)i * 8); else mn_one<C>(x);
+  lds_put8(h, 256 + t, x);
+  if (t) {
+    gl_get8(x, tree + ((size_t)b * 256 + t) * 8);
+    lds_put8(h, t, x);
+  } else {
+    gl_get8(x, out_inv + (size_t)b * 8);
+    lds_put8(g, 1, x);
+  }
+  __syncthreads();
+  for (uint32_t w = 1; w <= 128; w <<= 1) {
+    if (t < w) {
+      const uint32_t k = w + t;
+      lds_get8(x, g, k);
+      lds_get8(y, h, 2 * k + 1);
+      mn_mul<C>(z, x, y);  // inverse of node 2k
+      lds_get8(y, h, 2 * k);
+      mn_mul<C>(y, x, y);  // inverse of node 2k + 1
+      if (w < 128) {
+        lds_put8(g, 2 * k, z);
+        lds_put8(g, 2 * k + 1, y);
+      } else if (2 * k - 256 + b * 256 < n) {  // leaves: straight out
+        gl_put8(in + ((size_t)b * 256 + 2 * k - 256) * 8, z);
+        if (2 * k + 1 - 256 + b * 256 < n) gl_put8(in + ((size_t)b * 256 + 2 * k + 1 - 256) * 8, y);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// Phase 1b: w = s^-1 (Montgomery form) -> u1 = e w, u2 = r w (one Montgomery product
+// each lands in the plain domain) -> digits; secp256k1 also splits u2 (GLV).
+template <class C>
+__global__ __launch_bounds__(256) void cg_ecdsa_prep_b(const uint32_t* __restrict__ rs, uint32_t n, uint32_t cap,
+                                                       uint32_t scap, uint32_t* __restrict__ status,
+                                                       const uint32_t* __restrict__ ework,
+                                                       const uint32_t* __restrict__ inv_leaf,
+                                                       uint32_t* __restrict__ digits) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || status[i] != 0xff) return;
+  uint32_t w[8], e[8], r[8], u1[8], u2[8], d1[9], d2[9], d3[9], aux = 0;
+  gl_get8(w, inv_leaf + (size_t)i * 8);
+  CG_UNROLL for (int k = 0; k < 8; ++k) {
+    e[k] = ework[(size_t)k * scap + i];
+    r[k] = rs[(size_t)k * cap + i];
+  }
+  mn_mul<C>(u1, e, w);
+  mn_mul<C>(u2, r, w);
+  if constexpr (C::kScheme == 2) {
+    aux = ecdsa_k1_digits(u1, u2, d1, d2, d3);
+  } else {
+    recode_g(d1, u1);
+    recode16_65(d2, u2);
+  }
+  status[i] = 0xff | aux << 8;
+  CG_UNROLL for (int k = 0; k < 9; ++k) {
+    digits[(size_t)k * scap + i] = d1[k];
+    digits[(size_t)(9 + k) * scap + i] = d2[k];
+    if constexpr (C::kScheme == 2) digits[(size_t)(18 + k) * scap + i] = d3[k];
+  }
 }
 
 // Two waves per SIMD (<= 256 VGPRs); the GLV loop keeps one add site per formula
@@ -148,26 +289,29 @@ void cg_ecdsa_msm(const uint32_t* __restrict__ rs,
   CG_UNROLL for (int w = 0; w < 8; ++w) r[w] = rs[(size_t)w * cap + i];
   auto getQ = [&](uint32_t k, jpt& p) CG_LINLINE {
         const uint32_t* base = qtab + (size_t)(k - 1) * kQWords * scap + i;
-        CG_UNROLL for (int w = 0; w < 8; ++w) {
-          p.X[w] = base[(size_t)w * scap];
-          p.Y[w] = base[(size_t)(8 + w) * scap];
-          p.Z[w] = base[(size_t)(16 + w) * scap];
+        CG_UNROLL for (int w = 0; w < 10; ++w) {
+          p.X.v[w] = (int32_t)base[(size_t)w * scap];
+          p.Y.v[w] = (int32_t)base[(size_t)(10 + w) * scap];
+          p.Z.v[w] = (int32_t)base[(size_t)(20 + w) * scap];
         }
         p.inf = 0;
       };
   auto getG = [&](uint32_t t, uint32_t k, jpt& p) CG_LINLINE {
-        // affine k*G (t = 0) or k*2^128 G (t = 1): 64 bytes, four 16-byte loads from the
-        // L2-resident shared table
-        const uint4* g = reinterpret_cast<const uint4*>(gtab_g + ((size_t)t * kGTabEntries + k) * 16);
-        CG_UNROLL for (int q = 0; q < 4; ++q) {
-          const uint4 v = g[q];
-          uint32_t* dst = q < 2 ? p.X + 4 * q : p.Y + 4 * (q - 2);
-          dst[0] = v.x;
-          dst[1] = v.y;
-          dst[2] = v.z;
-          dst[3] = v.w;
+        // affine k*G (t = 0) or k*2^128 G (t = 1): 80 bytes, five 16-byte loads from the
+        // L2-resident shared table (Z is implied; ec_add<C, true> never reads it)
+        const int4* g = reinterpret_cast<const int4*>(gtab_g + ((size_t)t * kGTabEntries + k) * kGStride);
+        int32_t v[kGStride];
+        CG_UNROLL for (int q = 0; q < kGStride / 4; ++q) {
+          const int4 x = g[q];
+          v[4 * q] = x.x;
+          v[4 * q + 1] = x.y;
+          v[4 * q + 2] = x.z;
+          v[4 * q + 3] = x.w;
         }
-        CG_UNROLL for (int w = 0; w < 8; ++w) p.Z[w] = w == 0;
+        CG_UNROLL for (int w = 0; w < 10; ++w) {
+          p.X.v[w] = v[w];
+          p.Y.v[w] = v[10 + w];
+        }
         p.inf = 0;
       };
   uint32_t v;
@@ -183,19 +327,43 @@ void cg_ecdsa_msm(const uint32_t* __restrict__ rs,
 
 inline dim3 grid_for(uint32_t n) { return dim3((n + 255) / 256); }
 
-// The shared generator table of curve C: entry k = affine k*G (16 words: x then y,
-// LE limbs), k = 1 .. kGTabEntries - 1; entry 0 unused (zero).  One lane per entry.
+// The shared generator table of curve C: entry k = affine k*G (20 words: x then y,
+// Montgomery limbs), k = 1 .. kGTabEntries - 1; entry 0 unused (zero).  One lane per entry.
 template <class C>
 __global__ __launch_bounds__(256) void cg_ecdsa_gtab_build(uint32_t* __restrict__ out, uint32_t tables) {
   const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= tables * kGTabEntries) return;
   const uint32_t t = e / kGTabEntries, k = e % kGTabEntries;
-  uint32_t x[8] = {0, 0, 0, 0, 0, 0, 0, 0}, y[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  f26 x, y;
+  CG_UNROLL for (int w = 0; w < 10; ++w) x.v[w] = y.v[w] = 0;
   if (k) ecdsa_g_entry<C>(k, x, y, t);
-  CG_UNROLL for (int w = 0; w < 8; ++w) {
-    out[(size_t)e * 16 + w] = x[w];
-    out[(size_t)e * 16 + 8 + w] = y[w];
+  CG_UNROLL for (int w = 0; w < 10; ++w) {
+    out[(size_t)e * kGStride + w] = (uint32_t)x.v[w];
+    out[(size_t)e * kGStride + 10 + w] = (uint32_t)y.v[w];
   }
+}
+
+// Batched-inversion buffer layout for n leaves: level l has n_l values (n_0 = n,
+// n_{l+1} = ceil(n_l / 256), up to a single root) at val[l], and the product trees of
+// its ceil(n_l / 256) blocks (256 slots x 8 words each) at tree[l].  Returns the
+// words needed; fills offsets (in words) and the level count when asked.
+constexpr int kInvMaxLevels = 6;
+size_t inv_layout(uint32_t n, size_t* val, size_t* tree, int* levels) {
+  size_t off = 0;
+  int l = 0;
+  uint32_t m = n;
+  while (true) {
+    if (val) val[l] = off;
+    off += (size_t)m * 8;
+    if (m == 1) break;
+    const uint32_t nb = (m + 255) / 256;
+    if (tree) tree[l] = off;
+    off += (size_t)nb * 256 * 8;
+    m = nb;
+    ++l;
+  }
+  if (levels) *levels = l;  // number of up/down passes
+  return off;
 }
 
 hipError_t ensure_scratch(EcdsaConsts* c, uint32_t need) {
@@ -204,11 +372,16 @@ hipError_t ensure_scratch(EcdsaConsts* c, uint32_t need) {
   if (c->status) (void)hipFree(c->status);
   if (c->digits) (void)hipFree(c->digits);
   if (c->qtab) (void)hipFree(c->qtab);
-  c->status = c->digits = c->qtab = nullptr;
+  if (c->ework) (void)hipFree(c->ework);
+  if (c->inv) (void)hipFree(c->inv);
+  c->status = c->digits = c->qtab = c->ework = c->inv = nullptr;
   c->scap = 0;
   hipError_t e = hipMalloc((void**)&c->status, (size_t)want * 4);
   if (e == hipSuccess) e = hipMalloc((void**)&c->digits, (size_t)kDigitWordsEc * want * 4);
   if (e == hipSuccess) e = hipMalloc((void**)&c->qtab, (size_t)8 * kQWords * want * 4);
+  if (e == hipSuccess) e = hipMalloc((void**)&c->ework, (size_t)8 * want * 4);
+  c->inv_words = inv_layout(want, nullptr, nullptr, nullptr);
+  if (e == hipSuccess) e = hipMalloc((void**)&c->inv, c->inv_words * 4);
   if (e == hipSuccess) c->scap = want;
   return e;
 }
@@ -216,9 +389,25 @@ hipError_t ensure_scratch(EcdsaConsts* c, uint32_t need) {
 template <class C>
 hipError_t launch_prep(const EcdsaBatch& b, EcdsaConsts* c, uint32_t base, uint32_t cnt, const uint8_t* arena,
                        uint32_t mode, hipStream_t s) {
-  hipLaunchKernelGGL(cg_ecdsa_prep<C>, grid_for(cnt), dim3(256), 0, s, b.q + base, b.rs + base, b.der + base,
+  size_t val[kInvMaxLevels + 1], tree[kInvMaxLevels];
+  int levels = 0;
+  if (inv_layout(cnt, val, tree, &levels) > c->inv_words || levels > kInvMaxLevels) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(cg_ecdsa_prep_a<C>, grid_for(cnt), dim3(256), 0, s, b.q + base, b.rs + base, b.der + base,
                      b.sig_len + base, arena, b.msg_off + base, b.msg_len + base, cnt, b.n, c->scap, mode, c->status,
-                     c->digits, c->qtab);
+                     c->ework, c->inv + val[0], c->qtab);
+  uint32_t m[kInvMaxLevels + 1];
+  m[0] = cnt;
+  for (int l = 0; l < levels; ++l) {
+    m[l + 1] = (m[l] + 255) / 256;
+    hipLaunchKernelGGL(cg_inv_up<C>, dim3(m[l + 1]), dim3(256), 0, s, c->inv + val[l], m[l], c->inv + tree[l],
+                       c->inv + val[l + 1]);
+  }
+  hipLaunchKernelGGL(cg_inv_root<C>, dim3(1), dim3(64), 0, s, c->inv + val[levels]);
+  for (int l = levels - 1; l >= 0; --l)
+    hipLaunchKernelGGL(cg_inv_down<C>, dim3(m[l + 1]), dim3(256), 0, s, c->inv + val[l], m[l], c->inv + tree[l],
+                       c->inv + val[l + 1]);
+  hipLaunchKernelGGL(cg_ecdsa_prep_b<C>, grid_for(cnt), dim3(256), 0, s, b.rs + base, cnt, b.n, c->scap, c->status,
+                     c->ework, c->inv + val[0], c->digits);
   return hipGetLastError();
 }
 
@@ -241,7 +430,7 @@ hipError_t ecdsa_consts_create(EcdsaConsts** out, hipStream_t s) {
   const uint32_t tables[2] = {2, 1};
   hipError_t e = hipSuccess;
   for (int k = 0; k < 2 && e == hipSuccess; ++k)
-    e = hipMalloc((void**)&c->gtab[k], (size_t)tables[k] * kGTabEntries * 16 * sizeof(uint32_t));
+    e = hipMalloc((void**)&c->gtab[k], (size_t)tables[k] * kGTabEntries * kGStride * sizeof(uint32_t));
   if (e == hipSuccess) {
     hipLaunchKernelGGL(cg_ecdsa_gtab_build<CurveK1>, dim3((2 * kGTabEntries + 255) / 256), dim3(256), 0, s,
                        c->gtab[0], tables[0]);
@@ -263,7 +452,7 @@ hipError_t ecdsa_consts_create(EcdsaConsts** out, hipStream_t s) {
 
 void ecdsa_consts_free(EcdsaConsts* c) {
   if (!c) return;
-  for (auto* p : {c->gtab[0], c->gtab[1], c->status, c->digits, c->qtab})
+  for (auto* p : {c->gtab[0], c->gtab[1], c->status, c->digits, c->qtab, c->ework, c->inv})
     if (p) (void)hipFree(p);
   delete c;
 }

@@ -111,7 +111,7 @@ static const jpt* g_table(uint32_t t = 0) {
     tab[t] = new jpt[kGTabEntries];
     for (uint32_t k = 1; k < kGTabEntries; ++k) {
       ecdsa_g_entry<C>(k, tab[t][k].X, tab[t][k].Y, t);
-      for (int i = 0; i < 8; ++i) tab[t][k].Z[i] = i == 0;
+      F26<C>::one(tab[t][k].Z);
       tab[t][k].inf = 0;
     }
   }
@@ -159,6 +159,41 @@ static int ecdsa_verify_host(const uint8_t* q_be, const uint8_t* sig, uint32_t s
                                  [&](uint32_t k, jpt& p) { p = gtab[k]; });
 }
 
+// The Montgomery radix-2^26 field of the ECDSA kernels (cg_fp26.h) on canonical
+// inputs a, b < 2^256: op 0 = a b, 1 = a^2, 2 = a^-1, 3 = (a - b) == 0 mod p,
+// 4 = a b through worst-case lazy inputs (3a - 2b) (5a) - ... checked by the caller.
+template <class C>
+static void f26_op(int op, const uint32_t* a, const uint32_t* b, uint32_t* out) {
+  f26 fa, fb, r;
+  f26_from_u256<C>(fa, a);
+  f26_from_u256<C>(fb, b);
+  switch (op) {
+    case 0: f26_mul<C>(r, fa, fb); break;
+    case 1: f26_sqr<C>(r, fa); break;
+    case 2: f26_inv<C>(r, fa); break;
+    case 3: {
+      f26 d;
+      f26_sub(d, fa, fb);
+      for (int i = 0; i < 8; ++i) out[i] = 0;
+      out[0] = f26_iszero<C>(d);
+      return;
+    }
+    default: {  // (3a - 2b) * (-5a + 7b - 2a) with negated, unnormalised limbs: c 5 x c 14
+      f26 x, y, t;
+      f26_add(x, fa, fa);
+      f26_add(x, x, fa);
+      f26_sub(x, x, fb);
+      f26_sub(x, x, fb);
+      f26_neg(y, fa);
+      for (int k = 0; k < 6; ++k) f26_sub(y, y, fa);
+      for (int k = 0; k < 7; ++k) f26_add(y, y, fb);
+      f26_mul<C>(r, x, y);
+      (void)t;
+    }
+  }
+  f26_to_u256<C>(out, r);
+}
+
 extern "C" {
 int cgh_ecdsa_verify(int scheme, const uint8_t* q_be, const uint8_t* sig, uint32_t sig_len, const uint8_t* msg,
                      uint32_t msg_len, uint32_t mode) {
@@ -168,6 +203,10 @@ int cgh_ecdsa_verify(int scheme, const uint8_t* q_be, const uint8_t* sig, uint32
 
 void cgh_fp_mul(int scheme, const uint32_t* a, const uint32_t* b, uint32_t* out) {
   if (scheme == 2) fp_mul<CurveK1>(out, a, b); else fp_mul<CurveR1>(out, a, b);
+}
+
+void cgh_f26_op(int scheme, int op, const uint32_t* a, const uint32_t* b, uint32_t* out) {
+  if (scheme == 2) f26_op<CurveK1>(op, a, b, out); else f26_op<CurveR1>(op, a, b, out);
 }
 
 void cgh_mn_inv(int scheme, const uint32_t* a, uint32_t* out) {
@@ -203,12 +242,10 @@ static int joint_host(const uint32_t* u1, const uint32_t* u2, const uint32_t* qx
     ecdsa_joint<C>(acc, d1, d2, [&](uint32_t k, jpt& p) { p = qtab[k]; }, [&](uint32_t k, jpt& p) { p = gtab[k]; });
   }
   if (acc.inf) return 1;
-  uint32_t zi[8], zi2[8], zi3[8];
-  fp_inv<C>(zi, acc.Z);
-  fp_sqr<C>(zi2, zi);
-  fp_mul<C>(zi3, zi2, zi);
-  fp_mul<C>(out, acc.X, zi2);
-  fp_mul<C>(out + 8, acc.Y, zi3);
+  f26 x, y;
+  ec_to_affine<C>(x, y, acc);
+  f26_to_u256<C>(out, x);
+  f26_to_u256<C>(out + 8, y);
   return 0;
 }
 
@@ -241,5 +278,13 @@ extern "C" void cgh_sha256_tail(const uint8_t* msg, uint32_t n, const uint8_t* t
 extern "C" void cgh_bounds_report(int64_t* max_limb, double* log2_max_col) {
   *max_limb = cg_bounds().max_limb;
   *log2_max_col = __builtin_log2((double)cg_bounds().max_col);
+}
+#endif
+
+#if defined(CG_CHECK_BOUNDS)
+extern "C" void cgh_bounds26_report(int64_t* max_limb, double* log2_max_col, int32_t* max_top) {
+  *max_limb = cg_bounds26().max_limb;
+  *log2_max_col = __builtin_log2((double)cg_bounds26().max_col);
+  *max_top = cg_bounds26().max_top;
 }
 #endif

@@ -314,3 +314,68 @@ def test_glv_split_properties(host):
         a, b = val(k1) * (-1 if n1.value else 1), val(k2) * (-1 if n2.value else 1)
         assert (a + b * lam - u) % n == 0, hex(u)
         assert max(val(k1).bit_length(), val(k2).bit_length()) <= 129 and nd == 33 or nd == 34, (hex(u), nd)
+
+
+def test_f26_field_ops(host):
+    """The ECDSA kernels' Montgomery radix-2^26 field (cg_fp26.h) against Python big
+    ints on both primes: products, squares, inverses, the zero test and a product of
+    lazy (unnormalised, negated) combinations at c_a c_b = 70, over random and edge
+    values (0, 1, p - 1, p .. 2^256 - 1, sparse limb patterns)."""
+    import ecdsa_bc as EC
+    host.cgh_f26_op.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    rnd = random.Random(26)
+    out = (ctypes.c_uint32 * 8)()
+    for scheme in (2, 3):
+        p = EC.CURVES[scheme].p
+        edge = [0, 1, 2, p - 1, p, p + 1, 2**256 - 1, 2**255, 2**224, 2**96 - 1, 2**26 - 1, 2**234, 3 * 2**254,
+                p - 2**26]
+        for t in range(1500):
+            a = rnd.getrandbits(256) if t % 3 else rnd.choice(edge)
+            b = rnd.getrandbits(256) if t % 4 else rnd.choice(edge)
+            host.cgh_f26_op(scheme, 0, w8(a), w8(b), out)
+            assert val(out) == a * b % p, (scheme, hex(a), hex(b))
+            host.cgh_f26_op(scheme, 1, w8(a), w8(b), out)
+            assert val(out) == a * a % p
+            host.cgh_f26_op(scheme, 3, w8(a), w8(b), out)
+            assert val(out) == int((a - b) % p == 0)
+            host.cgh_f26_op(scheme, 3, w8(a), w8((a + p) % 2**256 if t % 2 else a), out)
+            assert val(out) == int((a - (a + p) % 2**256 if t % 2 else 0) % p == 0)
+            host.cgh_f26_op(scheme, 4, w8(a), w8(b), out)
+            assert val(out) == (3 * a - 2 * b) * (7 * b - 7 * a) % p
+            if t % 25 == 0:
+                host.cgh_f26_op(scheme, 2, w8(a), w8(b), out)
+                assert val(out) == (pow(a, p - 2, p) if a % p else 0)
+
+
+def test_f26_bounds_ecdsa_pipeline(golden_ecdsa):
+    """The bound argument of cg_fp26.h on the real ECDSA operation sequences: a host
+    build with 128-bit shadow column sums (-DCG_CHECK_BOUNDS traps when a column
+    reaches 2^62 or a folded top exceeds 64) runs every ECDSA fixture (both curves, all
+    adversarial classes, both modes) and random joint multiplications."""
+    import ecdsa_bc as EC
+    so = os.path.join(ROOT, "tests", "native", "libcg_host_bounds26.so")
+    src = os.path.join(ROOT, "tests", "native", "cg_host.cpp")
+    subprocess.check_call(["g++", "-O1", "-std=c++17", "-shared", "-fPIC", "-DCG_CHECK_BOUNDS", "-I",
+                           os.path.join(ROOT, "corda_amd", "csrc"), src, "-o", so])
+    lib = ctypes.CDLL(so)
+    lib.cgh_ecdsa_verify.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32,
+                                     ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint32]
+    for i, e in enumerate(golden_ecdsa):
+        q, sig, msg = _q_bytes(e["q"]), bytes.fromhex(e["sig"]), bytes.fromhex(e["msg"])
+        if len(q) != 64 or i % 2:
+            continue
+        assert lib.cgh_ecdsa_verify(e["scheme"], q, sig, len(sig), msg, len(msg), 0) == e["is_valid"], e["cls"]
+    rnd = random.Random(27)
+    out = (ctypes.c_uint32 * 16)()
+    for scheme in (2, 3):
+        c = EC.CURVES[scheme]
+        for t in range(6):
+            qpt = EC._mul(c, rnd.randrange(1, c.n), c.g)
+            u1, u2 = rnd.randrange(c.n), rnd.randrange(1, c.n)
+            exp = EC._add(c, EC._mul(c, u1, c.g), EC._mul(c, u2, qpt))
+            assert lib.cgh_ecdsa_joint(scheme, w8(u1), w8(u2), w8(qpt[0]), w8(qpt[1]), out, 0) == 0
+            assert val(out) == exp[0] and val(out[8:], 8) == exp[1]
+    ml, lc, top = ctypes.c_int64(), ctypes.c_double(), ctypes.c_int32()
+    lib.cgh_bounds26_report(ctypes.byref(ml), ctypes.byref(lc), ctypes.byref(top))
+    # the documented envelope: inputs <= 1.125 * 14 * 2^26 (c <= 14 here), columns < 2^62
+    assert ml.value < 16 * 2**26 and lc.value < 62 and top.value <= 12, (ml.value / 2**26, lc.value, top.value)
