@@ -91,7 +91,7 @@ CG_HD uint32_t der_parse(Byte&& b, uint32_t n, const uint32_t order[8], uint32_t
 // ------------------------------------------------------------ points
 // Jacobian (X : Y : Z) over the Montgomery field of cg_fp26.h; every coordinate is a
 // "unit" value (a multiplication output or f26_norm'ed).  The comment next to each
-// product gives c_a x c_b of its inputs (<= 150 allowed), next to each f26_norm the
+// product gives c_a x c_b of its inputs (<= 80 allowed), next to each f26_norm the
 // c of its input (<= 16 allowed).
 struct jpt {
   f26 X, Y, Z;
@@ -357,7 +357,7 @@ CG_HD uint32_t ecdsa_prep(const uint32_t qx[8], const uint32_t qy[8], uint32_t d
   return 0xff;
 }
 
-// P = u1 G + u2 Q from the packed digits; getQ(k, jpt&) loads k*Q (k = 1..8),
+// P = u1 G + u2 Q from the packed digits; getQ(k, jpt&) loads affine k*Q (k = 1..8),
 // getG(k, jpt&) loads affine k*G (k = 1 .. 2^(kGWin-1)).
 template <class C, typename GetQ, typename GetG>
 CG_HD void ecdsa_joint(jpt& acc, uint32_t d1[9], uint32_t d2[9], GetQ&& getQ, GetG&& getG) {
@@ -395,7 +395,7 @@ CG_HD void ecdsa_joint(jpt& acc, uint32_t d1[9], uint32_t d2[9], GetQ&& getQ, Ge
       f26_neg(ny, t.Y);
       f26_select(t.Y, t.Y, ny, neg);
       t.inf = 0;
-      ec_add<C, false>(acc, acc, t, a == 0);
+      ec_add<C, true>(acc, acc, t, a == 0);
     }
     // G part (affine)
     if (has_g) {
@@ -573,7 +573,7 @@ CG_HD void shl_nibbles9(uint32_t x[9], uint32_t s) {
 
 // P = u1 G + k1 Q + k2 phi(Q) over nd nibble positions (nd uniform, >= 33).
 // dk1/dk2: recode16_65 digits of |k1|, |k2| (signs neg1/neg2); dg: recode_g digits of
-// u1.  getQ(k, jpt&) loads k*Q (k = 1..8); getG(t, k, jpt&) loads affine k*G (t = 0)
+// u1.  getQ(k, jpt&) loads affine k*Q (k = 1..8); getG(t, k, jpt&) loads affine k*G (t = 0)
 // or k*2^128 G (t = 1).
 template <typename GetQ, typename GetG>
 CG_HD void ecdsa_joint_glv(jpt& acc, uint32_t nd, uint32_t dk1[9], uint32_t dk2[9], uint32_t neg1, uint32_t neg2,
@@ -616,7 +616,7 @@ CG_HD void ecdsa_joint_glv(jpt& acc, uint32_t nd, uint32_t dk1[9], uint32_t dk2[
       f26_neg(ny, t.Y);
       f26_select(t.Y, t.Y, ny, neg);
       t.inf = 0;
-      ec_add<C, false>(acc, acc, t, a == 0);
+      ec_add<C, true>(acc, acc, t, a == 0);
     }
     // +-|digit| * (k G or k 2^128 G) from the shared tables: 16-bit windows at bits 16 j
     if ((i & 3) == 0 && i <= 32) {
@@ -694,7 +694,8 @@ CG_HD void ecdsa_q_table(const uint32_t qx[8], const uint32_t qy[8], Put&& put) 
   }
 }
 
-// (X : Y : Z) -> affine (x, y), Montgomery form (table setup and tests only).
+// (X : Y : Z) -> affine (x, y), Montgomery form (table setup and tests only; the
+// kernels convert the k*Q tables with a batched inversion, ecdsa_kernels.hip).
 template <class C>
 CG_HD void ec_to_affine(f26& x, f26& y, const jpt& p) {
   f26 zi, zi2, zi3;
@@ -703,6 +704,20 @@ CG_HD void ec_to_affine(f26& x, f26& y, const jpt& p) {
   f26_mul<C>(zi3, zi2, zi);
   f26_mul<C>(x, p.X, zi2);
   f26_mul<C>(y, p.Y, zi3);
+}
+
+// The k*Q table in affine form (what the joint multiplications take), one lane on
+// its own (host tests).
+template <class C, typename Put>
+CG_HD void ecdsa_q_table_affine(const uint32_t qx[8], const uint32_t qy[8], Put&& put) {
+  ecdsa_q_table<C>(qx, qy, [&](int k, const jpt& p) {
+    jpt a = p;
+    if (k > 1) {
+      ec_to_affine<C>(a.X, a.Y, p);
+      F26<C>::one(a.Z);
+    }
+    put(k, a);
+  });
 }
 
 // Affine k*G (or k*2^128 G, shift128 = 1; 1 <= k < 2^17) in Montgomery form for the

@@ -16,11 +16,12 @@
 // Bounds (checked on the host with -DCG_CHECK_BOUNDS over the golden/random suites,
 // tests/test_native_host.py):
 //   * a "unit" value (f26_mul/f26_sqr output, f26_norm output, table entry, converted
-//     input) has |limb| <= 1.125 * 2^26 and value in (-2^102, 2^256 (1 + 2^-21)).
+//     input) has |limb| <= 1.125 * 2^26 and value in (-2^229, 2^256 (1 + 2^-21)).
 //   * a linear combination of unit values whose coefficients' absolute values sum to c
-//     has |limb| <= 1.125 c 2^26; f26_mul/f26_sqr accept inputs with c_a c_b <= 150
-//     (10 column products of 1.125^2 c_a c_b 2^52 stay below 2^62), f26_norm accepts
-//     c <= 16.  The point formulas (cg_ecdsa.h) note the c of every multiplication.
+//     has |limb| <= 1.125 c 2^26; f26_mul/f26_sqr accept inputs with c_a c_b <= 80
+//     (10 column products of 1.125^2 c_a c_b 2^52 stay below 2^62, a bit of headroom
+//     under int64), f26_norm accepts c <= 16.  The point formulas (cg_ecdsa.h) note
+//     the c of every multiplication (at most 21).
 //
 // Constants: tools/gen_fp26_consts.py.
 #pragma once
@@ -97,8 +98,10 @@ CG_HD int32_t f26_kpin(int32_t x) {
   return x;
 }
 
+// Constants (p, R mod p, ...) as SGPR values: uniform, so they neither take VGPRs
+// nor get hoisted out of the hot loops into VGPRs.
 CG_HD void f26_load(f26& h, const int32_t (&c)[10]) {
-  CG_UNROLL for (int i = 0; i < 10; ++i) h.v[i] = c[i];
+  CG_UNROLL for (int i = 0; i < 10; ++i) h.v[i] = f26_kpin(c[i]);
 }
 
 // ------------------------------------------------------------ per-curve forms

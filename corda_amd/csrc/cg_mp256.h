@@ -296,6 +296,54 @@ CG_HD void mn_mul(uint32_t r[8], const uint32_t a[8], const uint32_t b[8]) {
   mp_select(r, d, t, bw & (t[8] == 0));
 }
 
+// r = a^-1 mod m (m odd, 0 < a < m, gcd 1) by the binary extended Euclidean
+// algorithm: variable time, for the single root of a batched inversion (one lane
+// per chunk; ~700 cheap iterations instead of a 383-multiplication exponentiation).
+CG_HD void mp_half_mod(uint32_t x[8], const uint32_t m[8]) {  // x / 2 mod m
+  uint32_t t[8], c = 0;
+  if (x[0] & 1) c = mp_add(t, x, m); else CG_UNROLL for (int i = 0; i < 8; ++i) t[i] = x[i];
+  CG_UNROLL for (int i = 0; i < 7; ++i) x[i] = t[i] >> 1 | t[i + 1] << 31;
+  x[7] = t[7] >> 1 | c << 31;
+}
+CG_HD void mp_sub_mod(uint32_t x[8], const uint32_t y[8], const uint32_t m[8]) {  // x - y mod m
+  uint32_t t[8];
+  if (mp_sub(x, x, y)) {
+    mp_add(t, x, m);
+    CG_UNROLL for (int i = 0; i < 8; ++i) x[i] = t[i];
+  }
+}
+CG_HD void mp_inv_binary(uint32_t r[8], const uint32_t a[8], const uint32_t m[8]) {
+  uint32_t u[8], v[8], x1[8], x2[8];
+  CG_UNROLL for (int i = 0; i < 8; ++i) {
+    u[i] = a[i];
+    v[i] = m[i];
+    x1[i] = i == 0;
+    x2[i] = 0;
+  }
+  const uint32_t one[8] = {1, 0, 0, 0, 0, 0, 0, 0};
+  while (!mp_eq(u, one) && !mp_eq(v, one)) {
+    while (!(u[0] & 1)) {
+      CG_UNROLL for (int i = 0; i < 7; ++i) u[i] = u[i] >> 1 | u[i + 1] << 31;
+      u[7] >>= 1;
+      mp_half_mod(x1, m);
+    }
+    while (!(v[0] & 1)) {
+      CG_UNROLL for (int i = 0; i < 7; ++i) v[i] = v[i] >> 1 | v[i + 1] << 31;
+      v[7] >>= 1;
+      mp_half_mod(x2, m);
+    }
+    if (!mp_lt(u, v)) {
+      mp_sub(u, u, v);
+      mp_sub_mod(x1, x2, m);
+    } else {
+      mp_sub(v, v, u);
+      mp_sub_mod(x2, x1, m);
+    }
+  }
+  const uint32_t* res = mp_eq(u, one) ? x1 : x2;
+  CG_UNROLL for (int i = 0; i < 8; ++i) r[i] = res[i];
+}
+
 // R mod n = 2^256 - n (the Montgomery form of 1).
 template <class C>
 CG_HD void mn_one(uint32_t r[8]) {

@@ -17,7 +17,7 @@
 //   words), rs[w*cap+i] (16 LE limbs: r then s), der[i], sig_len[i], msg_off[i],
 //   msg_len[i]; scratch status[i] (verdict | digit count << 8 | signs << 16 for
 //   secp256k1), digits[w*scap+i] (27 words: u1 G digits, then k1 / k2 or u2
-//   nibbles), qtab[(e*30+w)*scap+i] (e = k-1 for k*Q, k = 1..8, X|Y|Z as 10
+//   nibbles), qtab[(e*20+w)*scap+i] (e = k-1 for affine k*Q, k = 1..8, x|y as 10
 //   radix-2^26 Montgomery limbs each, cg_fp26.h).
 #include <vector>
 
@@ -36,8 +36,9 @@ struct EcdsaConsts {
   uint32_t* digits = nullptr;
   uint32_t* qtab = nullptr;
   uint32_t* ework = nullptr;  // e mod n [8][scap]
-  uint32_t* inv = nullptr;    // batched inversion: leaves, tree levels, trees (element-major)
-  size_t inv_words = 0;
+  uint32_t* inv = nullptr;    // batched inversion mod n: leaves, tree levels, trees (element-major)
+  uint32_t* invp = nullptr;   // batched inversion mod p (Z of the k*Q tables, 7 per lane)
+  size_t inv_words = 0, invp_words = 0;
 };
 
 }  // namespace cg
@@ -45,7 +46,7 @@ struct EcdsaConsts {
 namespace {
 
 constexpr uint32_t kEcChunk = 1u << 20;
-constexpr int kQWords = 30;
+constexpr int kQWords = 20;  // affine k*Q: X then Y, 10 Montgomery limbs each
 constexpr int kGStride = 20;  // affine table entry: x then y, 10 Montgomery limbs each (80 bytes)
 constexpr int kDigitWordsEc = 27;
 
@@ -78,9 +79,167 @@ __global__ __launch_bounds__(256) void cg_der_parse(const uint8_t* __restrict__ 
   der[i] = st;
 }
 
+// ------------------------------------------------------------ batched inversion
+// Montgomery's trick as a product tree over a whole chunk: every inverse costs ~3
+// multiplications instead of a per-lane exponentiation.  Two instances per chunk:
+//   InvN  s mod n (Montgomery 2^256, 8 words)      -> w = s^-1 for u1, u2
+//   InvP  Z of k*Q mod p (cg_fp26.h, 10 words)     -> affine k*Q tables, so the
+//         joint multiplication's Q additions are mixed (7M + 4S instead of 11M + 5S)
+// Values are element-major.  Up: block b multiplies its 256 values pairwise in an
+// LDS heap (node k = node 2k * node 2k+1, leaves 256..511), keeps the internal nodes
+// in tree[b][1..255] and writes the product to out[b]; the single root is inverted
+// by binary extended Euclid (cg_inv_roots); down: inv(2k) = inv(k) node(2k+1),
+// inv(2k+1) = inv(k) node(2k), the leaves' inverses overwrite the leaves.
+template <class C>
+struct InvN {
+  static constexpr int W = 8;
+  CG_DEV static void mul(uint32_t z[8], const uint32_t x[8], const uint32_t y[8]) { mn_mul<C>(z, x, y); }
+  CG_DEV static void one(uint32_t x[8]) { mn_one<C>(x); }
+  CG_DEV static void invert(uint32_t x[8]) {  // x R -> x^-1 R
+    uint32_t p[8], pi[8], r2[8], nn[8];
+    const uint32_t o[8] = {1, 0, 0, 0, 0, 0, 0, 0};
+    mn_mul<C>(p, x, o);
+    C::n(nn);
+    mp_inv_binary(pi, p, nn);
+    mn_r2<C>(r2);
+    mn_mul<C>(x, pi, r2);
+  }
+};
+
+template <class C>
+struct InvP {
+  static constexpr int W = 10;
+  CG_DEV static void mul(uint32_t z[10], const uint32_t x[10], const uint32_t y[10]) {
+    f26 a, b, c;
+    CG_UNROLL for (int i = 0; i < 10; ++i) {
+      a.v[i] = (int32_t)x[i];
+      b.v[i] = (int32_t)y[i];
+    }
+    f26_mul<C>(c, a, b);
+    CG_UNROLL for (int i = 0; i < 10; ++i) z[i] = (uint32_t)c.v[i];
+  }
+  CG_DEV static void one(uint32_t x[10]) {
+    f26 o;
+    F26<C>::one(o);
+    CG_UNROLL for (int i = 0; i < 10; ++i) x[i] = (uint32_t)o.v[i];
+  }
+  CG_DEV static void invert(uint32_t x[10]) {  // x R -> x^-1 R
+    f26 a;
+    uint32_t p[8], pi[8], pp[8];
+    CG_UNROLL for (int i = 0; i < 10; ++i) a.v[i] = (int32_t)x[i];
+    f26_to_u256<C>(p, a);
+    C::p(pp);
+    mp_inv_binary(pi, p, pp);
+    f26_from_u256<C>(a, pi);
+    CG_UNROLL for (int i = 0; i < 10; ++i) x[i] = (uint32_t)a.v[i];
+  }
+};
+
+template <int W>
+CG_DEV void gl_get(uint32_t v[W], const uint32_t* p) {
+  CG_UNROLL for (int q = 0; q < W / 2; ++q) {
+    const uint2 a = reinterpret_cast<const uint2*>(p)[q];
+    v[2 * q] = a.x;
+    v[2 * q + 1] = a.y;
+  }
+}
+template <int W>
+CG_DEV void gl_put(uint32_t* p, const uint32_t v[W]) {
+  CG_UNROLL for (int q = 0; q < W / 2; ++q) reinterpret_cast<uint2*>(p)[q] = make_uint2(v[2 * q], v[2 * q + 1]);
+}
+template <int W>
+CG_DEV void lds_get(uint32_t v[W], const uint32_t* h, uint32_t k) {
+  CG_UNROLL for (int w = 0; w < W; ++w) v[w] = h[k * W + w];
+}
+template <int W>
+CG_DEV void lds_put(uint32_t* h, uint32_t k, const uint32_t v[W]) {
+  CG_UNROLL for (int w = 0; w < W; ++w) h[k * W + w] = v[w];
+}
+
+template <class F>
+__global__ __launch_bounds__(256) void cg_inv_up(const uint32_t* __restrict__ in, uint32_t n,
+                                                 uint32_t* __restrict__ tree, uint32_t* __restrict__ out) {
+  constexpr int W = F::W;
+  __shared__ uint32_t h[512 * W];
+  const uint32_t t = threadIdx.x, b = blockIdx.x, i = b * 256 + t;
+  uint32_t x[W], y[W], z[W];
+  if (i < n) gl_get<W>(x, in + (size_t)i * W); else F::one(x);
+  lds_put<W>(h, 256 + t, x);
+  __syncthreads();
+  for (uint32_t w = 128; w >= 1; w >>= 1) {
+    if (t < w) {
+      const uint32_t k = w + t;
+      lds_get<W>(x, h, 2 * k);
+      lds_get<W>(y, h, 2 * k + 1);
+      F::mul(z, x, y);
+      lds_put<W>(h, k, z);
+    }
+    __syncthreads();
+  }
+  lds_get<W>(x, h, t ? t : 1u);
+  if (t) gl_put<W>(tree + ((size_t)b * 256 + t) * W, x);
+  else gl_put<W>(out + (size_t)b * W, x);
+}
+
+// The two roots of a chunk (s mod n, Z mod p) in parallel: wave 0 and wave 1.
+template <class C>
+__global__ void cg_inv_roots(uint32_t* __restrict__ vn, uint32_t* __restrict__ vp) {
+  if (threadIdx.x == 0) {
+    uint32_t x[8];
+    gl_get<8>(x, vn);
+    InvN<C>::invert(x);
+    gl_put<8>(vn, x);
+  } else if (threadIdx.x == 64) {
+    uint32_t x[10];
+    gl_get<10>(x, vp);
+    InvP<C>::invert(x);
+    gl_put<10>(vp, x);
+  }
+}
+
+template <class F>
+__global__ __launch_bounds__(256) void cg_inv_down(uint32_t* __restrict__ in, uint32_t n,
+                                                   const uint32_t* __restrict__ tree,
+                                                   const uint32_t* __restrict__ out_inv) {
+  constexpr int W = F::W;
+  __shared__ uint32_t h[512 * W], g[256 * W];
+  const uint32_t t = threadIdx.x, b = blockIdx.x, i = b * 256 + t;
+  uint32_t x[W], y[W], z[W];
+  if (i < n) gl_get<W>(x, in + (size_t)i * W); else F::one(x);
+  lds_put<W>(h, 256 + t, x);
+  if (t) {
+    gl_get<W>(x, tree + ((size_t)b * 256 + t) * W);
+    lds_put<W>(h, t, x);
+  } else {
+    gl_get<W>(x, out_inv + (size_t)b * W);
+    lds_put<W>(g, 1, x);
+  }
+  __syncthreads();
+  for (uint32_t w = 1; w <= 128; w <<= 1) {
+    if (t < w) {
+      const uint32_t k = w + t;
+      lds_get<W>(x, g, k);
+      lds_get<W>(y, h, 2 * k + 1);
+      F::mul(z, x, y);  // inverse of node 2k
+      lds_get<W>(y, h, 2 * k);
+      F::mul(y, x, y);  // inverse of node 2k + 1
+      if (w < 128) {
+        lds_put<W>(g, 2 * k, z);
+        lds_put<W>(g, 2 * k + 1, y);
+      } else {  // leaves: straight out
+        const uint32_t j = b * 256 + 2 * k - 256;
+        if (j < n) gl_put<W>(in + (size_t)j * W, z);
+        if (j + 1 < n) gl_put<W>(in + (size_t)(j + 1) * W, y);
+      }
+    }
+    __syncthreads();
+  }
+}
+
 // Phase 1a (one lane per signature): key check, verdict precedence, e mod n, the
-// k*Q table; s in Montgomery form (s 2^256 mod n) into the batched inversion's
-// leaves (element-major, 8 words), or 1 (2^256 mod n) for lanes already decided.
+// Jacobian k*Q table; leaves of the two inversions: s R mod n, and Z of k*Q
+// (k = 2..8, plane k-2 of cnt values; k = 1 is affine already), or ones for lanes
+// already decided.
 template <class C>
 __global__ __launch_bounds__(256) void cg_ecdsa_prep_a(const uint32_t* __restrict__ q, const uint32_t* __restrict__ rs,
                                                        const uint32_t* __restrict__ der,
@@ -89,8 +248,8 @@ __global__ __launch_bounds__(256) void cg_ecdsa_prep_a(const uint32_t* __restric
                                                        const uint64_t* __restrict__ msg_off,
                                                        const uint32_t* __restrict__ msg_len, uint32_t n, uint32_t cap,
                                                        uint32_t scap, uint32_t mode, uint32_t* __restrict__ status,
-                                                       uint32_t* __restrict__ ework, uint32_t* __restrict__ inv_leaf,
-                                                       uint32_t* __restrict__ qtab) {
+                                                       uint32_t* __restrict__ ework, uint32_t* __restrict__ leaf_n,
+                                                       uint32_t* __restrict__ leaf_p, uint32_t* __restrict__ qtab) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint32_t qw[16], qx[8], qy[8], s[8], e[8], a[8];
@@ -99,140 +258,48 @@ __global__ __launch_bounds__(256) void cg_ecdsa_prep_a(const uint32_t* __restric
   be_words_to_limbs(qy, qw + 8);
   const uint32_t pre = ecdsa_prep_front<C>(qx, qy, der[i], sig_len[i], arena + msg_off[i], msg_len[i], mode, e);
   status[i] = pre;
-  if (pre == 0xff) {
-    uint32_t r2[8];
-    CG_UNROLL for (int w = 0; w < 8; ++w) s[w] = rs[(size_t)(8 + w) * cap + i];
-    mn_r2<C>(r2);
-    mn_mul<C>(a, s, r2);
-  } else {
-    mn_one<C>(a);
+  if (pre != 0xff) {
+    uint32_t o[10];
+    InvN<C>::one(a);
+    gl_put<8>(leaf_n + (size_t)i * 8, a);
+    InvP<C>::one(o);
+    CG_UNROLL for (int k = 2; k <= 8; ++k) gl_put<10>(leaf_p + ((size_t)(k - 2) * n + i) * 10, o);
+    return;
   }
-  uint4* leaf = reinterpret_cast<uint4*>(inv_leaf + (size_t)i * 8);
-  leaf[0] = make_uint4(a[0], a[1], a[2], a[3]);
-  leaf[1] = make_uint4(a[4], a[5], a[6], a[7]);
-  if (pre != 0xff) return;
+  uint32_t r2[8];
+  CG_UNROLL for (int w = 0; w < 8; ++w) s[w] = rs[(size_t)(8 + w) * cap + i];
+  mn_r2<C>(r2);
+  mn_mul<C>(a, s, r2);
+  gl_put<8>(leaf_n + (size_t)i * 8, a);
   CG_UNROLL for (int w = 0; w < 8; ++w) ework[(size_t)w * scap + i] = e[w];
   ecdsa_q_table<C>(qx, qy, [&](int k, const jpt& p) {
     uint32_t* base = qtab + (size_t)(k - 1) * kQWords * scap + i;
     CG_UNROLL for (int w = 0; w < 10; ++w) {
       base[(size_t)w * scap] = (uint32_t)p.X.v[w];
       base[(size_t)(10 + w) * scap] = (uint32_t)p.Y.v[w];
-      base[(size_t)(20 + w) * scap] = (uint32_t)p.Z.v[w];
+    }
+    if (k > 1) {
+      uint32_t z[10];
+      CG_UNROLL for (int w = 0; w < 10; ++w) z[w] = (uint32_t)p.Z.v[w];
+      gl_put<10>(leaf_p + ((size_t)(k - 2) * n + i) * 10, z);
     }
   });
 }
 
-// Batched inversion mod n (Montgomery's trick as a product tree): every inverse
-// s^-1 of a chunk costs ~3 multiplications instead of a 383-multiplication Fermat
-// exponentiation per lane.  Values are Montgomery residues (x 2^256 mod n), element-
-// major 8 words.  Up: block b multiplies its 256 values pairwise in an LDS heap
-// (node k = node 2k * node 2k+1, leaves 256..511), keeps the 255 internal nodes in
-// tree[b][1..255] and writes the product to out[b].
-CG_DEV void lds_get8(uint32_t v[8], const uint32_t (*h)[8], uint32_t k) {
-  CG_UNROLL for (int w = 0; w < 8; ++w) v[w] = h[k][w];
-}
-CG_DEV void lds_put8(uint32_t (*h)[8], uint32_t k, const uint32_t v[8]) {
-  CG_UNROLL for (int w = 0; w < 8; ++w) h[k][w] = v[w];
-}
-CG_DEV void gl_get8(uint32_t v[8], const uint32_t* p) {
-  const uint4 a = reinterpret_cast<const uint4*>(p)[0], b = reinterpret_cast<const uint4*>(p)[1];
-  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-}
-CG_DEV void gl_put8(uint32_t* p, const uint32_t v[8]) {
-  reinterpret_cast<uint4*>(p)[0] = make_uint4(v[0], v[1], v[2], v[3]);
-  reinterpret_cast<uint4*>(p)[1] = make_uint4(v[4], v[5], v[6], v[7]);
-}
-
-template <class C>
-__global__ __launch_bounds__(256) void cg_inv_up(const uint32_t* __restrict__ in, uint32_t n,
-                                                 uint32_t* __restrict__ tree, uint32_t* __restrict__ out) {
-  __shared__ uint32_t h[512][8];
-  const uint32_t t = threadIdx.x, b = blockIdx.x, i = b * 256 + t;
-  uint32_t x[8], y[8], z[8];
-  if (i < n) gl_get8(x, in + (size_t)i * 8); else mn_one<C>(x);
-  lds_put8(h, 256 + t, x);
-  __syncthreads();
-  for (uint32_t w = 128; w >= 1; w >>= 1) {
-    if (t < w) {
-      const uint32_t k = w + t;
-      lds_get8(x, h, 2 * k);
-      lds_get8(y, h, 2 * k + 1);
-      mn_mul<C>(z, x, y);
-      lds_put8(h, k, z);
-    }
-    __syncthreads();
-  }
-  lds_get8(x, h, t ? t : 1u);
-  if (t) gl_put8(tree + ((size_t)b * 256 + t) * 8, x);
-  else gl_put8(out + (size_t)b * 8, x);
-}
-
-// The single root: its inverse, in Montgomery form (one lane).
-template <class C>
-__global__ void cg_inv_root(uint32_t* __restrict__ v) {
-  if (blockIdx.x | threadIdx.x) return;
-  uint32_t x[8], p[8], pi[8], r2[8];
-  const uint32_t one[8] = {1, 0, 0, 0, 0, 0, 0, 0};
-  gl_get8(x, v);
-  mn_mul<C>(p, x, one);  // plain product (invertible: every leaf is)
-  mn_inv<C>(pi, p);
-  mn_r2<C>(r2);
-  mn_mul<C>(x, pi, r2);
-  gl_put8(v, x);
-}
-
-// Down: with the inverse of block b's product (out_inv[b]), each internal node's
-// inverse gives its children's: inv(2k) = inv(k) * node(2k+1), inv(2k+1) = inv(k) *
-// node(2k); the leaves' inverses overwrite in[] (same positions, read first).
-template <class C>
-__global__ __launch_bounds__(256) void cg_inv_down(uint32_t* __restrict__ in, uint32_t n,
-                                                   const uint32_t* __restrict__ tree,
-                                                   const uint32_t* __restrict__ out_inv) {
-  __shared__ uint32_t h[512][8], g[256][8];
-  const uint32_t t = threadIdx.x, b = blockIdx.x, i = b * 256 + t;
-  uint32_t x[8], y[8], z[8];
-  if (i < n) gl_get8(x, in + (size_t)i * 8); else mn_one<C>(x);
-  lds_put8(h, 256 + t, x);
-  if (t) {
-    gl_get8(x, tree + ((size_t)b * 256 + t) * 8);
-    lds_put8(h, t, x);
-  } else {
-    gl_get8(x, out_inv + (size_t)b * 8);
-    lds_put8(g, 1, x);
-  }
-  __syncthreads();
-  for (uint32_t w = 1; w <= 128; w <<= 1) {
-    if (t < w) {
-      const uint32_t k = w + t;
-      lds_get8(x, g, k);
-      lds_get8(y, h, 2 * k + 1);
-      mn_mul<C>(z, x, y);  // inverse of node 2k
-      lds_get8(y, h, 2 * k);
-      mn_mul<C>(y, x, y);  // inverse of node 2k + 1
-      if (w < 128) {
-        lds_put8(g, 2 * k, z);
-        lds_put8(g, 2 * k + 1, y);
-      } else if (2 * k - 256 + b * 256 < n) {  // leaves: straight out
-        gl_put8(in + ((size_t)b * 256 + 2 * k - 256) * 8, z);
-        if (2 * k + 1 - 256 + b * 256 < n) gl_put8(in + ((size_t)b * 256 + 2 * k + 1 - 256) * 8, y);
-      }
-    }
-    __syncthreads();
-  }
-}
-
 // Phase 1b: w = s^-1 (Montgomery form) -> u1 = e w, u2 = r w (one Montgomery product
-// each lands in the plain domain) -> digits; secp256k1 also splits u2 (GLV).
+// each lands in the plain domain) -> digits (secp256k1 also splits u2, GLV); the
+// k*Q table to affine with the Z inverses: x = X / Z^2, y = Y / Z^3.
 template <class C>
 __global__ __launch_bounds__(256) void cg_ecdsa_prep_b(const uint32_t* __restrict__ rs, uint32_t n, uint32_t cap,
                                                        uint32_t scap, uint32_t* __restrict__ status,
                                                        const uint32_t* __restrict__ ework,
-                                                       const uint32_t* __restrict__ inv_leaf,
-                                                       uint32_t* __restrict__ digits) {
+                                                       const uint32_t* __restrict__ leaf_n,
+                                                       const uint32_t* __restrict__ leaf_p,
+                                                       uint32_t* __restrict__ digits, uint32_t* __restrict__ qtab) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n || status[i] != 0xff) return;
   uint32_t w[8], e[8], r[8], u1[8], u2[8], d1[9], d2[9], d3[9], aux = 0;
-  gl_get8(w, inv_leaf + (size_t)i * 8);
+  gl_get<8>(w, leaf_n + (size_t)i * 8);
   CG_UNROLL for (int k = 0; k < 8; ++k) {
     e[k] = ework[(size_t)k * scap + i];
     r[k] = rs[(size_t)k * cap + i];
@@ -250,6 +317,25 @@ __global__ __launch_bounds__(256) void cg_ecdsa_prep_b(const uint32_t* __restric
     digits[(size_t)k * scap + i] = d1[k];
     digits[(size_t)(9 + k) * scap + i] = d2[k];
     if constexpr (C::kScheme == 2) digits[(size_t)(18 + k) * scap + i] = d3[k];
+  }
+  CG_NOUNROLL for (int k = 2; k <= 8; ++k) {
+    uint32_t zw[10];
+    f26 zi, zi2, zi3, X, Y;
+    gl_get<10>(zw, leaf_p + ((size_t)(k - 2) * n + i) * 10);
+    uint32_t* base = qtab + (size_t)(k - 1) * kQWords * scap + i;
+    CG_UNROLL for (int v = 0; v < 10; ++v) {
+      zi.v[v] = (int32_t)zw[v];
+      X.v[v] = (int32_t)base[(size_t)v * scap];
+      Y.v[v] = (int32_t)base[(size_t)(10 + v) * scap];
+    }
+    f26_sqr<C>(zi2, zi);
+    f26_mul<C>(zi3, zi2, zi);
+    f26_mul<C>(X, X, zi2);
+    f26_mul<C>(Y, Y, zi3);
+    CG_UNROLL for (int v = 0; v < 10; ++v) {
+      base[(size_t)v * scap] = (uint32_t)X.v[v];
+      base[(size_t)(10 + v) * scap] = (uint32_t)Y.v[v];
+    }
   }
 }
 
@@ -289,10 +375,9 @@ void cg_ecdsa_msm(const uint32_t* __restrict__ rs,
   CG_UNROLL for (int w = 0; w < 8; ++w) r[w] = rs[(size_t)w * cap + i];
   auto getQ = [&](uint32_t k, jpt& p) CG_LINLINE {
         const uint32_t* base = qtab + (size_t)(k - 1) * kQWords * scap + i;
-        CG_UNROLL for (int w = 0; w < 10; ++w) {
+        CG_UNROLL for (int w = 0; w < 10; ++w) {  // affine (cg_ecdsa_prep_b): Z is implied
           p.X.v[w] = (int32_t)base[(size_t)w * scap];
           p.Y.v[w] = (int32_t)base[(size_t)(10 + w) * scap];
-          p.Z.v[w] = (int32_t)base[(size_t)(20 + w) * scap];
         }
         p.inf = 0;
       };
@@ -343,22 +428,22 @@ __global__ __launch_bounds__(256) void cg_ecdsa_gtab_build(uint32_t* __restrict_
   }
 }
 
-// Batched-inversion buffer layout for n leaves: level l has n_l values (n_0 = n,
+// Batched-inversion buffer layout for n leaves of `words` words: level l has n_l values (n_0 = n,
 // n_{l+1} = ceil(n_l / 256), up to a single root) at val[l], and the product trees of
 // its ceil(n_l / 256) blocks (256 slots x 8 words each) at tree[l].  Returns the
 // words needed; fills offsets (in words) and the level count when asked.
 constexpr int kInvMaxLevels = 6;
-size_t inv_layout(uint32_t n, size_t* val, size_t* tree, int* levels) {
+size_t inv_layout(uint32_t n, int words, size_t* val, size_t* tree, int* levels) {
   size_t off = 0;
   int l = 0;
   uint32_t m = n;
   while (true) {
     if (val) val[l] = off;
-    off += (size_t)m * 8;
+    off += (size_t)m * words;
     if (m == 1) break;
     const uint32_t nb = (m + 255) / 256;
     if (tree) tree[l] = off;
-    off += (size_t)nb * 256 * 8;
+    off += (size_t)nb * 256 * words;
     m = nb;
     ++l;
   }
@@ -374,40 +459,60 @@ hipError_t ensure_scratch(EcdsaConsts* c, uint32_t need) {
   if (c->qtab) (void)hipFree(c->qtab);
   if (c->ework) (void)hipFree(c->ework);
   if (c->inv) (void)hipFree(c->inv);
-  c->status = c->digits = c->qtab = c->ework = c->inv = nullptr;
+  if (c->invp) (void)hipFree(c->invp);
+  c->status = c->digits = c->qtab = c->ework = c->inv = c->invp = nullptr;
   c->scap = 0;
   hipError_t e = hipMalloc((void**)&c->status, (size_t)want * 4);
   if (e == hipSuccess) e = hipMalloc((void**)&c->digits, (size_t)kDigitWordsEc * want * 4);
   if (e == hipSuccess) e = hipMalloc((void**)&c->qtab, (size_t)8 * kQWords * want * 4);
   if (e == hipSuccess) e = hipMalloc((void**)&c->ework, (size_t)8 * want * 4);
-  c->inv_words = inv_layout(want, nullptr, nullptr, nullptr);
+  c->inv_words = inv_layout(want, 8, nullptr, nullptr, nullptr);
+  c->invp_words = inv_layout(7 * want, 10, nullptr, nullptr, nullptr);
   if (e == hipSuccess) e = hipMalloc((void**)&c->inv, c->inv_words * 4);
+  if (e == hipSuccess) e = hipMalloc((void**)&c->invp, c->invp_words * 4);
   if (e == hipSuccess) c->scap = want;
   return e;
+}
+
+template <class F>
+void launch_inv_up(uint32_t* buf, const size_t* val, const size_t* tree, const uint32_t* m, int levels,
+                   hipStream_t s) {
+  for (int l = 0; l < levels; ++l)
+    hipLaunchKernelGGL(cg_inv_up<F>, dim3(m[l + 1]), dim3(256), 0, s, buf + val[l], m[l], buf + tree[l],
+                       buf + val[l + 1]);
+}
+
+template <class F>
+void launch_inv_down(uint32_t* buf, const size_t* val, const size_t* tree, const uint32_t* m, int levels,
+                     hipStream_t s) {
+  for (int l = levels - 1; l >= 0; --l)
+    hipLaunchKernelGGL(cg_inv_down<F>, dim3(m[l + 1]), dim3(256), 0, s, buf + val[l], m[l], buf + tree[l],
+                       buf + val[l + 1]);
 }
 
 template <class C>
 hipError_t launch_prep(const EcdsaBatch& b, EcdsaConsts* c, uint32_t base, uint32_t cnt, const uint8_t* arena,
                        uint32_t mode, hipStream_t s) {
-  size_t val[kInvMaxLevels + 1], tree[kInvMaxLevels];
-  int levels = 0;
-  if (inv_layout(cnt, val, tree, &levels) > c->inv_words || levels > kInvMaxLevels) return hipErrorInvalidValue;
+  size_t vn[kInvMaxLevels + 1], tn[kInvMaxLevels], vp[kInvMaxLevels + 1], tp[kInvMaxLevels];
+  int ln = 0, lp = 0;
+  if (inv_layout(cnt, 8, vn, tn, &ln) > c->inv_words || ln > kInvMaxLevels ||
+      inv_layout(7 * cnt, 10, vp, tp, &lp) > c->invp_words || lp > kInvMaxLevels)
+    return hipErrorInvalidValue;
+  uint32_t mn[kInvMaxLevels + 1], mp[kInvMaxLevels + 1];
+  mn[0] = cnt;
+  mp[0] = 7 * cnt;
+  for (int l = 0; l < ln; ++l) mn[l + 1] = (mn[l] + 255) / 256;
+  for (int l = 0; l < lp; ++l) mp[l + 1] = (mp[l] + 255) / 256;
   hipLaunchKernelGGL(cg_ecdsa_prep_a<C>, grid_for(cnt), dim3(256), 0, s, b.q + base, b.rs + base, b.der + base,
                      b.sig_len + base, arena, b.msg_off + base, b.msg_len + base, cnt, b.n, c->scap, mode, c->status,
-                     c->ework, c->inv + val[0], c->qtab);
-  uint32_t m[kInvMaxLevels + 1];
-  m[0] = cnt;
-  for (int l = 0; l < levels; ++l) {
-    m[l + 1] = (m[l] + 255) / 256;
-    hipLaunchKernelGGL(cg_inv_up<C>, dim3(m[l + 1]), dim3(256), 0, s, c->inv + val[l], m[l], c->inv + tree[l],
-                       c->inv + val[l + 1]);
-  }
-  hipLaunchKernelGGL(cg_inv_root<C>, dim3(1), dim3(64), 0, s, c->inv + val[levels]);
-  for (int l = levels - 1; l >= 0; --l)
-    hipLaunchKernelGGL(cg_inv_down<C>, dim3(m[l + 1]), dim3(256), 0, s, c->inv + val[l], m[l], c->inv + tree[l],
-                       c->inv + val[l + 1]);
+                     c->ework, c->inv + vn[0], c->invp + vp[0], c->qtab);
+  launch_inv_up<InvN<C>>(c->inv, vn, tn, mn, ln, s);
+  launch_inv_up<InvP<C>>(c->invp, vp, tp, mp, lp, s);
+  hipLaunchKernelGGL(cg_inv_roots<C>, dim3(1), dim3(128), 0, s, c->inv + vn[ln], c->invp + vp[lp]);
+  launch_inv_down<InvN<C>>(c->inv, vn, tn, mn, ln, s);
+  launch_inv_down<InvP<C>>(c->invp, vp, tp, mp, lp, s);
   hipLaunchKernelGGL(cg_ecdsa_prep_b<C>, grid_for(cnt), dim3(256), 0, s, b.rs + base, cnt, b.n, c->scap, c->status,
-                     c->ework, c->inv + val[0], c->digits);
+                     c->ework, c->inv + vn[0], c->invp + vp[0], c->digits, c->qtab);
   return hipGetLastError();
 }
 
@@ -452,7 +557,7 @@ hipError_t ecdsa_consts_create(EcdsaConsts** out, hipStream_t s) {
 
 void ecdsa_consts_free(EcdsaConsts* c) {
   if (!c) return;
-  for (auto* p : {c->gtab[0], c->gtab[1], c->status, c->digits, c->qtab, c->ework, c->inv})
+  for (auto* p : {c->gtab[0], c->gtab[1], c->status, c->digits, c->qtab, c->ework, c->inv, c->invp})
     if (p) (void)hipFree(p);
   delete c;
 }

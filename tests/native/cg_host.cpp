@@ -146,7 +146,7 @@ static int ecdsa_verify_host(const uint8_t* q_be, const uint8_t* sig, uint32_t s
   const uint32_t pre = ecdsa_prep_scalars<C>(qx, qy, ds, r, s, sig_len, msg, msg_len, mode, u1, u2);
   if (pre != 0xff) return (int)pre;
   jpt qtab[9];
-  ecdsa_q_table<C>(qx, qy, [&](int k, const jpt& p) { qtab[k] = p; });
+  ecdsa_q_table_affine<C>(qx, qy, [&](int k, const jpt& p) { qtab[k] = p; });
   if (C::kScheme == 2) {
     jpt acc;
     joint_k1glv(acc, u1, u2, qtab, 0);
@@ -209,6 +209,8 @@ void cgh_f26_op(int scheme, int op, const uint32_t* a, const uint32_t* b, uint32
   if (scheme == 2) f26_op<CurveK1>(op, a, b, out); else f26_op<CurveR1>(op, a, b, out);
 }
 
+void cgh_mp_inv_binary(const uint32_t* a, const uint32_t* m, uint32_t* out) { mp_inv_binary(out, a, m); }
+
 void cgh_mn_inv(int scheme, const uint32_t* a, uint32_t* out) {
   if (scheme == 2) mn_inv<CurveK1>(out, a); else mn_inv<CurveR1>(out, a);
 }
@@ -232,7 +234,7 @@ static int joint_host(const uint32_t* u1, const uint32_t* u2, const uint32_t* qx
                       uint32_t force_nd) {
   jpt qtab[9], acc;
   const jpt* gtab = g_table<C>();
-  ecdsa_q_table<C>(qx, qy, [&](int k, const jpt& p) { qtab[k] = p; });
+  ecdsa_q_table_affine<C>(qx, qy, [&](int k, const jpt& p) { qtab[k] = p; });
   if (C::kScheme == 2) {
     joint_k1glv(acc, u1, u2, qtab, force_nd);
   } else {

@@ -379,3 +379,17 @@ def test_f26_bounds_ecdsa_pipeline(golden_ecdsa):
     lib.cgh_bounds26_report(ctypes.byref(ml), ctypes.byref(lc), ctypes.byref(top))
     # the documented envelope: inputs <= 1.125 * 14 * 2^26 (c <= 14 here), columns < 2^62
     assert ml.value < 16 * 2**26 and lc.value < 62 and top.value <= 12, (ml.value / 2**26, lc.value, top.value)
+
+
+def test_mp_inv_binary(host):
+    """The binary extended Euclid used for the single root of the kernels' batched
+    inversions (mod n and mod p of both curves) against pow(a, -1, m)."""
+    import ecdsa_bc as EC
+    host.cgh_mp_inv_binary.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    rnd = random.Random(31)
+    out = (ctypes.c_uint32 * 8)()
+    for c in (EC.CURVES[2], EC.CURVES[3]):
+        for m in (c.n, c.p):
+            for a in [1, 2, 3, m - 1, m - 2, 2**255 % m, (m + 1) // 2] + [rnd.randrange(1, m) for _ in range(300)]:
+                host.cgh_mp_inv_binary(w8(a), w8(m), out)
+                assert val(out) == pow(a, -1, m), (hex(m), hex(a))
