@@ -89,8 +89,9 @@ CG_HD uint32_t der_parse(Byte&& b, uint32_t n, const uint32_t order[8], uint32_t
 }
 
 // ------------------------------------------------------------ points
-// Jacobian (X : Y : Z) over the Montgomery field of cg_fp26.h; every coordinate is a
-// "unit" value (a multiplication output or f26_norm'ed).  The comment next to each
+// Jacobian (X : Y : Z) over the Montgomery field of cg_fp26.h; X and Y are "unit"
+// values (a multiplication output or f26_norm'ed), Z has c <= 3 (the a = -3 doubling
+// leaves it unnormalised).  The comment next to each
 // product gives c_a x c_b of its inputs (<= 80 allowed), next to each f26_norm the
 // c of its input (<= 16 allowed).
 struct jpt {
@@ -104,7 +105,7 @@ CG_HD void ec_dbl(jpt& r, const jpt& p) {
   if (C::kAMinus3) {
     // dbl-2001-b: delta = Z^2, gamma = Y^2, beta = X gamma, alpha = 3 (X - delta)(X + delta)
     f26 delta, gamma, beta, alpha;
-    f26_sqr<C>(delta, p.Z);
+    f26_sqr<C>(delta, p.Z);  // 3 x 3
     f26_sqr<C>(gamma, p.Y);
     f26_mul<C>(beta, p.X, gamma);
     f26_sub(t0, p.X, delta);
@@ -119,10 +120,9 @@ CG_HD void ec_dbl(jpt& r, const jpt& p) {
     f26_sub(x3, x3, t1);
     f26_norm<C>(x3);  // c 9
     f26_add(t2, p.Y, p.Z);
-    f26_sqr<C>(z3, t2);  // 2 x 2
+    f26_sqr<C>(z3, t2);  // 4 x 4
     f26_sub(z3, z3, gamma);
-    f26_sub(z3, z3, delta);
-    f26_norm<C>(z3);      // c 3
+    f26_sub(z3, z3, delta);  // c 3, left unnormalised: Z feeds only products (<= 4 x 4)
     f26_sub(t0, t0, x3);  // 4 beta - X3: c 5
     f26_mul<C>(y3, alpha, t0);  // 3 x 5
     f26_sqr<C>(t3, gamma);
@@ -199,12 +199,12 @@ CG_HD void ec_add(jpt& r, const jpt& p, const jpt& q, uint32_t q_skip) {
   f26_sub(y3, y3, t);
   f26_norm<C>(y3);       // c 2
   if (AFFINE) {
-    f26_mul<C>(z3, p.Z, h);  // 1 x 2
+    f26_mul<C>(z3, p.Z, h);  // 3 x 2
   } else {
     f26_mul<C>(t, p.Z, q.Z);
     f26_mul<C>(z3, t, h);    // 1 x 2
   }
-  const uint32_t hz = f26_iszero<C>(h), rz = f26_iszero<C>(rr);
+  const uint32_t hz = f26_iszero<C>(h);
   jpt out;
   out.X = x3;
   out.Y = y3;
@@ -212,7 +212,7 @@ CG_HD void ec_add(jpt& r, const jpt& p, const jpt& q, uint32_t q_skip) {
   out.inf = 0;
   const uint32_t live = !p.inf & !q_skip;
   if (live & hz) {  // P == +-Q: rare (crafted keys only); divergent branch, exact result
-    if (rz) {
+    if (f26_iszero<C>(rr)) {
       ec_dbl<C>(out, p);
     } else {
       out.inf = 1;

@@ -279,7 +279,7 @@ CG_HD void f26_mul2(f26& h0, const f26& f0, const f26& g0, f26& h1, const f26& f
 template <class C>
 CG_HD uint32_t f26_iszero(const f26& a) {
   f26 t = a, pp;
-  f26_norm<C>(t);   // value in (-2^102, 2^256 + 2^236): 0 mod p <=> value is 0 or p
+  f26_norm<C>(t);   // value in (-2^229, 2^256 + 2^236): 0 mod p <=> value is 0 or p
   f26_carry(t);     // unique limbs for the value
   F26<C>::p(pp);
   uint32_t z = 0, e = 0;
