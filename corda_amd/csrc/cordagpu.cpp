@@ -22,6 +22,7 @@
 #include <algorithm>
 #include <array>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -50,6 +51,7 @@ struct Stat {
 struct cg_ctx {
   int device = -1;
   hipStream_t stream = nullptr;
+  hipStream_t copy_stream = nullptr;  // host-to-device uploads overlapped with `stream` (tx pipeline)
   std::string err;
   int32_t* btab = nullptr;
   // Ed25519 chunk scratch
@@ -347,6 +349,10 @@ cg_status cg_open(int device, cg_ctx** out) {
     delete ctx;
     return CG_E_DEVICE;
   }
+  if (hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking) != hipSuccess) {
+    cg_close(ctx);
+    return CG_E_DEVICE;
+  }
   // the shared Ed25519 base tables (k*B, k*2^128 B) are built on the device, once per context
   if (dalloc(ctx, &ctx->btab, cg::ed25519_btab_words(), "alloc base table") != CG_OK ||
       cg::launch_ed25519_btab_build(ctx->btab, ctx->stream) != hipSuccess ||
@@ -367,6 +373,7 @@ void cg_close(cg_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->copy_stream) (void)hipStreamSynchronize(ctx->copy_stream);
   collect_timings(ctx);
   cg::ecdsa_consts_free(ctx->ec);
   for (auto& b : ctx->live_blocks) (void)hipFree(b.first);
@@ -374,6 +381,7 @@ void cg_close(cg_ctx* ctx) {
   release_cached(ctx);
   for (hipEvent_t e : ctx->event_pool) (void)hipEventDestroy(e);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  if (ctx->copy_stream) (void)hipStreamDestroy(ctx->copy_stream);
   delete ctx;
 }
 
@@ -767,9 +775,30 @@ struct TxDev {
 
 // Host-side validation is O(n_tx): monotone comp_start / sig_start.  Component
 // bounds are checked by the leaf kernel (error flag, read back by the caller).
+// Leaf hashes of the components of txs [t0, t1) and their Merkle roots (the arena
+// bytes of those components must be on the device, in stream order).
+cg_status hash_txs(cg_ctx* ctx, TxDev& d, size_t arena_bytes, const uint32_t* comp_start, size_t t0, size_t t1) {
+  const uint32_t c0 = comp_start[t0], c1 = comp_start[t1];
+  {
+    Timed t(ctx, "merkle_leaf", c1 - c0);
+    CG_TRY(ctx, cg::launch_merkle_leaf(d.arena, arena_bytes, d.comp_off, d.comp_len, d.comp_start, d.comp_tx, d.salts,
+                                       nullptr, c0, c1, d.leaves, ctx->err_flag, ctx->stream),
+           "launch merkle_leaf");
+  }
+  {
+    Timed t(ctx, "merkle_tree", t1 - t0);
+    CG_TRY(ctx, cg::launch_merkle_tree(d.leaves, d.comp_start + t0, (uint32_t)(t1 - t0), (uint32_t*)d.ids + 8 * t0,
+                                       ctx->stream),
+           "launch merkle_tree");
+  }
+  return CG_OK;
+}
+
+// upload_arena = false: everything but the arena upload and the hashing (the
+// pipelined cg_tx_verify_batch streams the arena in chunks and hashes per chunk).
 cg_status compute_txids(cg_ctx* ctx, size_t n_tx, const uint8_t* arena, size_t arena_bytes, const uint64_t* comp_off,
                         const uint32_t* comp_len, const uint32_t* comp_start, const uint8_t* salts,
-                        const uint32_t* sig_start, TxDev& d, bool* any_empty) {
+                        const uint32_t* sig_start, TxDev& d, bool* any_empty, bool upload_arena = true) {
   if (n_tx > 0xFFFFFFF0ull) return fail(ctx, CG_E_INVALID_ARGUMENT, "too many transactions");
   if (!comp_start || !salts || (comp_start[n_tx] && (!comp_off || !comp_len || !arena)))
     return fail(ctx, CG_E_INVALID_ARGUMENT, "null pointer");
@@ -779,7 +808,7 @@ cg_status compute_txids(cg_ctx* ctx, size_t n_tx, const uint8_t* arena, size_t a
     if (comp_start[t + 1] == comp_start[t]) *any_empty = true;
     if (sig_start && sig_start[t + 1] < sig_start[t]) return fail(ctx, CG_E_INVALID_ARGUMENT, "sig_start not monotone");
   }
-  const uint32_t c_begin = comp_start[0], c_end = comp_start[n_tx];
+  const uint32_t c_end = comp_start[n_tx];
   const size_t n_comp = c_end;
   const size_t n_sig = sig_start ? sig_start[n_tx] : 0;
   cg_status st;
@@ -796,23 +825,77 @@ cg_status compute_txids(cg_ctx* ctx, size_t n_tx, const uint8_t* arena, size_t a
                     (st = dalloc(ctx, &d.sig_moff, n_sig, "alloc sig msg_off")) != CG_OK ||
                     (st = dalloc(ctx, &d.sig_mlen, n_sig, "alloc sig msg_len")) != CG_OK))
     return st;
-  if (arena_bytes)
+  if (upload_arena && arena_bytes)
     CG_TRY(ctx, hipMemcpyAsync(d.arena, arena, arena_bytes, hipMemcpyHostToDevice, ctx->stream), "upload tx arena");
   CG_TRY(ctx, hipMemsetAsync(d.arena + arena_bytes, 0, 16, ctx->stream), "pad tx arena");
   CG_TRY(ctx, hipMemsetAsync(d.ids, 0, 32 * n_tx + 16, ctx->stream), "zero ids");
   CG_TRY(ctx, hipMemsetAsync(ctx->err_flag, 0, 4, ctx->stream), "zero error flag");
   CG_TRY(ctx, cg::launch_tx_index(d.comp_start, d.sig_start, (uint32_t)n_tx, d.comp_tx, d.sig_moff, d.sig_mlen,
                                   ctx->stream), "launch tx_index");
-  {
-    Timed t(ctx, "merkle_leaf", c_end - c_begin);
-    CG_TRY(ctx, cg::launch_merkle_leaf(d.arena, arena_bytes, d.comp_off, d.comp_len, d.comp_start, d.comp_tx, d.salts,
-                                       nullptr, c_begin, c_end, d.leaves, ctx->err_flag, ctx->stream),
-           "launch merkle_leaf");
+  if (upload_arena) return hash_txs(ctx, d, arena_bytes, comp_start, 0, n_tx);
+  return CG_OK;
+}
+
+// The transaction pipeline of cg_tx_verify_batch: the component arena is streamed
+// to the device in byte pieces on copy_stream, and tx-range chunk k is hashed
+// (leaves, roots) and its signatures verified against the fresh ids on ctx->stream
+// as soon as the arena prefix it reads is in, so the PCIe upload of the (large)
+// arena overlaps the kernels and the host-side staging.  Any layout works; a
+// component-ordered arena (what the JVM producer writes) makes the prefixes grow
+// evenly.  Verdicts land in verdict_d at their absolute signature positions.
+cg_status tx_pipeline(cg_ctx* ctx, int mode, size_t n_tx, const uint8_t* arena, size_t arena_bytes,
+                      const uint64_t* comp_off, const uint32_t* comp_len, const uint32_t* comp_start,
+                      const uint32_t* sig_start, const uint8_t* scheme_id, const uint8_t* pk, size_t pk_stride,
+                      const uint8_t* sig, size_t sig_stride, const uint32_t* sig_len, TxDev& d, uint8_t* verdict_d,
+                      std::vector<hipEvent_t>& ev) {
+  // chunks: enough to overlap the upload, few enough that each chunk's signature
+  // subsets still fill the device (CORDA_AMD_TX_CHUNKS overrides, for tuning)
+  size_t kmax = 3;
+  if (const char* e = std::getenv("CORDA_AMD_TX_CHUNKS")) kmax = std::max(1, std::atoi(e));
+  const size_t K = std::max<size_t>(1, std::min<size_t>(kmax, n_tx / 131072));
+  // the whole arena goes out at once in kB equal byte pieces (one event each), before
+  // any host-side scanning, so the copy engine starts immediately
+  const size_t kB = 8, piece = (arena_bytes + kB - 1) / kB;
+  ev.assign(kB, nullptr);
+  for (size_t j = 0; j < kB; ++j) {
+    CG_TRY(ctx, hipEventCreateWithFlags(&ev[j], hipEventDisableTiming), "tx pipeline event");
+    const size_t lo = std::min(arena_bytes, j * piece), hi = std::min(arena_bytes, (j + 1) * piece);
+    if (hi > lo)
+      CG_TRY(ctx, hipMemcpyAsync(d.arena + lo, arena + lo, hi - lo, hipMemcpyHostToDevice, ctx->copy_stream),
+             "upload tx arena");
+    CG_TRY(ctx, hipEventRecord(ev[j], ctx->copy_stream), "tx pipeline record");
   }
-  {
-    Timed t(ctx, "merkle_tree", n_tx);
-    CG_TRY(ctx, cg::launch_merkle_tree(d.leaves, d.comp_start, (uint32_t)n_tx, (uint32_t*)d.ids, ctx->stream),
-           "launch merkle_tree");
+  std::vector<size_t> tb(K + 1);
+  for (size_t k = 0; k <= K; ++k) tb[k] = n_tx * k / K;
+  uint64_t up_to = 0;
+  cg_status st;
+  for (size_t k = 0; k < K; ++k) {
+    for (uint32_t c = comp_start[tb[k]]; c < comp_start[tb[k + 1]]; ++c)  // arena prefix chunk k reads
+      up_to = std::max<uint64_t>(up_to, std::min<uint64_t>(comp_off[c] + comp_len[c], arena_bytes));
+    if (up_to) {
+      const size_t j = std::min(kB - 1, (size_t)((up_to - 1) / (piece ? piece : 1)));
+      CG_TRY(ctx, hipStreamWaitEvent(ctx->stream, ev[j], 0), "tx pipeline wait");
+    }
+    if ((st = hash_txs(ctx, d, arena_bytes, comp_start, tb[k], tb[k + 1])) != CG_OK) return st;
+    const size_t s0 = sig_start[tb[k]], s1 = sig_start[tb[k + 1]];
+    if (s1 > s0) {
+      MsgSrc m;
+      m.dev = d.ids;
+      m.bytes = 32 * n_tx;
+      m.off_dev = d.sig_moff + s0;
+      m.len_dev = d.sig_mlen + s0;
+      cg_batch* b = nullptr;
+      st = create_batch(ctx, s1 - s0, scheme_id ? scheme_id + s0 : nullptr, pk + s0 * pk_stride, pk_stride,
+                        sig + s0 * sig_stride, sig_stride, sig_len ? sig_len + s0 : nullptr, m, &b);
+      if (st == CG_OK) st = launch_verify(ctx, b, mode);
+      if (st == CG_OK) {
+        const hipError_t e =
+            hipMemcpyAsync(verdict_d + s0, b->verdict, s1 - s0, hipMemcpyDeviceToDevice, ctx->stream);
+        if (e != hipSuccess) st = hip_fail(ctx, e, "tx verdicts");
+      }
+      if (b) batch_free(ctx, b);  // blocks go back to the stream-ordered cache
+      if (st != CG_OK) return st;
+    }
   }
   return CG_OK;
 }
@@ -867,31 +950,28 @@ cg_status cg_tx_verify_batch(cg_ctx* ctx, int mode, size_t n_tx, const uint8_t* 
   TxDev d;
   bool any_empty = false;
   cg_status st = compute_txids(ctx, n_tx, arena, arena_bytes, comp_off, comp_len, comp_start, salts, sig_start, d,
-                               &any_empty);
+                               &any_empty, /*upload_arena=*/false);
   const size_t n_sig = sig_start[n_tx];
-  cg_batch* b = nullptr;
+  uint8_t* verdict_d = nullptr;
   int32_t* fb_d = nullptr;
-  if (st == CG_OK && n_sig) {
-    MsgSrc m;
-    m.dev = d.ids;
-    m.bytes = 32 * n_tx;
-    m.off_dev = d.sig_moff;
-    m.len_dev = d.sig_mlen;
-    st = create_batch(ctx, n_sig, scheme_id, pk, pk_stride, sig, sig_stride, sig_len, m, &b);
-    if (st == CG_OK) st = launch_verify(ctx, b, mode);
-  }
+  std::vector<hipEvent_t> ev;
+  if (st == CG_OK && n_sig) st = dalloc(ctx, &verdict_d, n_sig, "alloc tx verdicts");
+  if (st == CG_OK) st = tx_pipeline(ctx, mode, n_tx, arena, arena_bytes, comp_off, comp_len, comp_start, sig_start,
+                                    scheme_id, pk, pk_stride, sig, sig_stride, sig_len, d, verdict_d, ev);
   if (st == CG_OK && (st = dalloc(ctx, &fb_d, n_tx, "alloc first_bad")) == CG_OK) {
-    hipError_t e = cg::launch_first_bad(b ? b->verdict : nullptr, d.sig_start, (uint32_t)n_tx, fb_d, ctx->stream);
+    hipError_t e = cg::launch_first_bad(verdict_d, d.sig_start, (uint32_t)n_tx, fb_d, ctx->stream);
     if (e == hipSuccess) e = hipMemcpyAsync(first_bad_out, fb_d, 4 * n_tx, hipMemcpyDeviceToHost, ctx->stream);
-    if (e == hipSuccess && verdict_out && b)
-      e = hipMemcpyAsync(verdict_out, b->verdict, n_sig, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess && verdict_out && verdict_d)
+      e = hipMemcpyAsync(verdict_out, verdict_d, n_sig, hipMemcpyDeviceToHost, ctx->stream);
     if (e == hipSuccess && ids_out) e = hipMemcpyAsync(ids_out, d.ids, 32 * n_tx, hipMemcpyDeviceToHost, ctx->stream);
     if (e != hipSuccess) st = hip_fail(ctx, e, "first_bad");
   }
   if (st == CG_OK) st = read_err_flag(ctx);
+  (void)hipStreamSynchronize(ctx->copy_stream);
   (void)hipStreamSynchronize(ctx->stream);
+  for (hipEvent_t e : ev) (void)hipEventDestroy(e);
   dfree(ctx, fb_d);
-  if (b) batch_free(ctx, b);
+  dfree(ctx, verdict_d);
   d.release(ctx);
   collect_timings(ctx);
   if (st != CG_OK) return st;
