@@ -58,6 +58,29 @@ CG_HD void sha256_block(uint32_t h[8], uint32_t w[16]) {
   h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
 }
 
+// The 16 big-endian words of a block lying wholly inside the message (and with the
+// dword after it inside too), from 17 dwords m4[0..16] read as four 16-byte loads +
+// one dword: 5 memory instructions instead of 17 per-lane gathers, which matters
+// because each of them touches 64 different cache lines (one message per lane).
+// m4 is only 4-byte aligned; global_load_dwordx4 needs no more on gfx950.
+CG_HD void sha256_load_block(uint32_t w[16], const uint32_t* m4, uint32_t sh) {
+  uint32_t x[17];
+#if defined(__HIP_DEVICE_COMPILE__)
+  typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
+  CG_UNROLL for (int q = 0; q < 4; ++q) {
+    const u32x4_a4 v = reinterpret_cast<const u32x4_a4*>(m4)[q];
+    x[4 * q] = v.x;
+    x[4 * q + 1] = v.y;
+    x[4 * q + 2] = v.z;
+    x[4 * q + 3] = v.w;
+  }
+#else
+  for (int q = 0; q < 16; ++q) x[q] = m4[q];
+#endif
+  x[16] = m4[16];
+  CG_UNROLL for (int j = 0; j < 16; ++j) w[j] = bswap32_(alignbyte32(x[j + 1], x[j], sh));
+}
+
 // SHA-256 of msg[0..n) read from memory (any alignment; reads never go past the
 // dword holding byte n-1).  Digest as 8 big-endian-valued words (h[0] is bytes 0..3).
 CG_HD void sha256_mem(uint32_t out[8], const uint8_t* msg, uint32_t n) {
@@ -69,6 +92,12 @@ CG_HD void sha256_mem(uint32_t out[8], const uint8_t* msg, uint32_t n) {
   const int64_t ndw = ((int64_t)n + sh + 3) >> 2;
   const uint32_t nb = (uint32_t)(((uint64_t)n + 9 + 63) / 64);
   CG_NOUNROLL for (uint32_t blk = 0; blk < nb; ++blk) {
+    // whole block inside msg, and the dword after it readable
+    // (lanes of a wave may take different paths: only the message fetch diverges,
+    // the compression below is shared)
+    if (64 * (int64_t)blk + 64 <= (int64_t)n && 16 * (int64_t)blk + 16 < ndw) {
+      sha256_load_block(w, m4 + 16 * (size_t)blk, sh);
+    } else {
     CG_UNROLL for (int j = 0; j < 16; ++j) {
       const int64_t q = 64 * (int64_t)blk + 4 * j;  // message byte offset of this word
       const int64_t c = (int64_t)n - q;
@@ -89,6 +118,7 @@ CG_HD void sha256_mem(uint32_t out[8], const uint8_t* msg, uint32_t n) {
       if (blk == nb - 1 && j == 14) word = (uint32_t)(((uint64_t)n * 8) >> 32);
       if (blk == nb - 1 && j == 15) word = (uint32_t)((uint64_t)n * 8);
       w[j] = word;
+    }
     }
     sha256_block(h, w);
   }
@@ -115,6 +145,12 @@ CG_HD void sha256_mem_tail(uint32_t out[8], const uint8_t* msg, uint32_t n, TB&&
   const uint64_t total = (uint64_t)n + tail_n;
   const uint32_t nb = (uint32_t)((total + 9 + 63) / 64);
   CG_NOUNROLL for (uint32_t blk = 0; blk < nb; ++blk) {
+    // whole block inside ser_i (no tail bytes in it), and the dword after it readable
+    // (lanes of a wave may take different paths: only the message fetch diverges,
+    // the compression below is shared)
+    if (64 * (int64_t)blk + 64 <= (int64_t)n && 16 * (int64_t)blk + 16 < ndw) {
+      sha256_load_block(w, m4 + 16 * (size_t)blk, sh);
+    } else {
     CG_UNROLL for (int j = 0; j < 16; ++j) {
       const int64_t q = 64 * (int64_t)blk + 4 * j;
       const int64_t c = (int64_t)n - q;
@@ -135,6 +171,7 @@ CG_HD void sha256_mem_tail(uint32_t out[8], const uint8_t* msg, uint32_t n, TB&&
       if (blk == nb - 1 && j == 14) word = (uint32_t)((total * 8) >> 32);
       if (blk == nb - 1 && j == 15) word = (uint32_t)(total * 8);
       w[j] = word;
+    }
     }
     sha256_block(h, w);
   }
