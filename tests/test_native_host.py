@@ -393,3 +393,29 @@ def test_mp_inv_binary(host):
             for a in [1, 2, 3, m - 1, m - 2, 2**255 % m, (m + 1) // 2] + [rnd.randrange(1, m) for _ in range(300)]:
                 host.cgh_mp_inv_binary(w8(a), w8(m), out)
                 assert val(out) == pow(a, -1, m), (hex(m), hex(a))
+
+
+def test_ecdsa_joint_exceptional_cases(host):
+    """Crafted keys that drive the joint multiplication through its exceptional
+    additions (exact Jacobian formulas): Q = G with u1 = u2 (every
+    Q addition meets an equal partial sum -> the doubling branch), Q = -G with
+    u1 = u2 (partial sums cancel -> infinity, then additions from infinity), Q = 2G
+    with u1 = 2 u2, and u1 = n - u2 d (result infinity -> REJECT), on both curves;
+    compared point for point with Python arithmetic."""
+    import ecdsa_bc as EC
+    rnd = random.Random(41)
+    out = (ctypes.c_uint32 * 16)()
+    for scheme in (2, 3):
+        c = EC.CURVES[scheme]
+        for d in (1, c.n - 1, 2, 3):
+            qpt = EC._mul(c, d, c.g)
+            for t in range(6):
+                u2 = rnd.randrange(1, c.n) if t > 1 else (1, c.n - 1)[t]
+                u1 = [u2, (c.n - u2 * d) % c.n, 2 * u2 % c.n, (u2 * d) % c.n][t % 4]
+                exp = EC._add(c, EC._mul(c, u1, c.g), EC._mul(c, u2, qpt))
+                for force in (0, 40):
+                    inf = host.cgh_ecdsa_joint(scheme, w8(u1), w8(u2), w8(qpt[0]), w8(qpt[1]), out, force)
+                    if exp is None:
+                        assert inf == 1, (scheme, d, t)
+                    else:
+                        assert inf == 0 and val(out) == exp[0] and val(out[8:], 8) == exp[1], (scheme, d, t)
