@@ -28,9 +28,9 @@ void ecdsa_consts_free(EcdsaConsts* c);
 hipError_t ecdsa_batch_stage(const EcdsaBatch& b, const uint8_t* pk_raw_dev, size_t pk_stride,
                              const uint8_t* sig_raw_dev, size_t sig_stride, const uint32_t* sig_len_dev,
                              const uint64_t* msg_off_all_dev, const uint32_t* msg_len_all_dev, hipStream_t s);
-// Scratch is sized for min(n, chunk) elements; a batch is verified chunk by chunk:
+// Scratch (one set per curve) is sized for min(n, chunk) elements; a batch is verified chunk by chunk:
 // prep (key check, SHA-256, scalars, k*Q table) then msm (u1 G + u2 Q, x check).
-hipError_t ecdsa_scratch(EcdsaConsts* c, uint32_t n, uint32_t* chunk);
+hipError_t ecdsa_scratch(EcdsaConsts* c, int scheme, uint32_t n, uint32_t* chunk);
 hipError_t ecdsa_launch_prep(const EcdsaBatch& b, EcdsaConsts* c, uint32_t base, uint32_t cnt, const uint8_t* arena,
                              uint32_t mode, hipStream_t s);
 hipError_t ecdsa_launch_msm(const EcdsaBatch& b, EcdsaConsts* c, uint32_t base, uint32_t cnt, uint8_t* verdict,

@@ -52,6 +52,10 @@ struct cg_ctx {
   int device = -1;
   hipStream_t stream = nullptr;
   hipStream_t copy_stream = nullptr;  // host-to-device uploads overlapped with `stream` (tx pipeline)
+  // the two ECDSA curves' pipelines run on their own streams, concurrently with the
+  // Ed25519 kernels on `stream` (fork/join events, no host sync)
+  hipStream_t ec_stream[2] = {nullptr, nullptr};
+  hipEvent_t ev_fork = nullptr, ev_join[2] = {nullptr, nullptr};
   std::string err;
   int32_t* btab = nullptr;
   // Ed25519 chunk scratch
@@ -100,22 +104,24 @@ hipEvent_t take_event(cg_ctx* ctx) {
   return e;
 }
 
-// RAII timing scope around one kernel launch on the context stream.
+// RAII timing scope around one kernel launch on the context stream (or `s`).
 struct Timed {
   cg_ctx* ctx;
   const char* name;
   uint64_t items;
+  hipStream_t s;
   hipEvent_t a = nullptr, b = nullptr;
-  Timed(cg_ctx* c, const char* n, uint64_t it) : ctx(c), name(n), items(it) {
+  Timed(cg_ctx* c, const char* n, uint64_t it, hipStream_t st = nullptr)
+      : ctx(c), name(n), items(it), s(st ? st : c->stream) {
     if (ctx->profiling) {
       a = take_event(ctx);
       b = take_event(ctx);
-      if (a) (void)hipEventRecord(a, ctx->stream);
+      if (a) (void)hipEventRecord(a, s);
     }
   }
   ~Timed() {
     if (ctx->profiling && a && b) {
-      (void)hipEventRecord(b, ctx->stream);
+      (void)hipEventRecord(b, s);
       ctx->pending.push_back({name, {a, b}});
       ctx->stats[name].items += items;
     }
@@ -349,7 +355,12 @@ cg_status cg_open(int device, cg_ctx** out) {
     delete ctx;
     return CG_E_DEVICE;
   }
-  if (hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking) != hipSuccess) {
+  if (hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&ctx->ec_stream[0], hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&ctx->ec_stream[1], hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->ev_join[0], hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->ev_join[1], hipEventDisableTiming) != hipSuccess) {
     cg_close(ctx);
     return CG_E_DEVICE;
   }
@@ -374,6 +385,8 @@ void cg_close(cg_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->copy_stream) (void)hipStreamSynchronize(ctx->copy_stream);
+  for (hipStream_t es : ctx->ec_stream)
+    if (es) (void)hipStreamSynchronize(es);
   collect_timings(ctx);
   cg::ecdsa_consts_free(ctx->ec);
   for (auto& b : ctx->live_blocks) (void)hipFree(b.first);
@@ -382,6 +395,10 @@ void cg_close(cg_ctx* ctx) {
   for (hipEvent_t e : ctx->event_pool) (void)hipEventDestroy(e);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   if (ctx->copy_stream) (void)hipStreamDestroy(ctx->copy_stream);
+  for (hipStream_t es : ctx->ec_stream)
+    if (es) (void)hipStreamDestroy(es);
+  for (hipEvent_t e : {ctx->ev_fork, ctx->ev_join[0], ctx->ev_join[1]})
+    if (e) (void)hipEventDestroy(e);
   delete ctx;
 }
 
@@ -538,8 +555,41 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode) {
   cg_status st;
   // elements of unsupported schemes keep this value
   CG_TRY(ctx, hipMemsetAsync(b->verdict, CG_UNSUPPORTED, n, ctx->stream), "init verdict");
+  CG_TRY(ctx, hipEventRecord(ctx->ev_fork, ctx->stream), "fork ecdsa");
+  bool joins[2] = {false, false};
+  // ECDSA: each curve on its own stream, forked after the verdict init and joined
+  // before the bitmap (the verdict scatters touch disjoint positions); enqueued
+  // first so they overlap the Ed25519 kernels below in mixed batches (config 4:
+  // 14.9 -> 15.3 M tx/s; per-kernel times then include the overlap)
+  for (int c = 0; c < 2; ++c) {
+    if (!b->ec[c].n) continue;
+    const cg::EcdsaBatch& eb = b->ec[c];
+    const char* prep_name = eb.scheme == 2 ? "ecdsa_k1_prep" : "ecdsa_r1_prep";
+    const char* msm_name = eb.scheme == 2 ? "ecdsa_k1_msm" : "ecdsa_r1_msm";
+    hipStream_t es = ctx->ec_stream[c];
+    uint32_t chunk = 0;
+    CG_TRY(ctx, cg::ecdsa_scratch(ctx->ec, eb.scheme, eb.n, &chunk), "alloc ecdsa scratch");
+    CG_TRY(ctx, hipStreamWaitEvent(es, ctx->ev_fork, 0), "fork ecdsa");
+    for (uint32_t base = 0; base < eb.n; base += chunk) {
+      const uint32_t cnt = std::min(chunk, eb.n - base);
+      {
+        Timed t(ctx, prep_name, cnt, es);
+        CG_TRY(ctx, cg::ecdsa_launch_prep(eb, ctx->ec, base, cnt, b->arena, (uint32_t)mode, es), "launch ecdsa prep");
+      }
+      {
+        Timed t(ctx, msm_name, cnt, es);
+        CG_TRY(ctx, cg::ecdsa_launch_msm(eb, ctx->ec, base, cnt, b->verdict, es), "launch ecdsa msm");
+      }
+    }
+    CG_TRY(ctx, hipEventRecord(ctx->ev_join[c], es), "join ecdsa");
+    joins[c] = true;
+  }
   if (b->n_ed) {
-    if ((st = ensure_ed_scratch(ctx, b->n_ed)) != CG_OK) return st;
+    if ((st = ensure_ed_scratch(ctx, b->n_ed)) != CG_OK) {
+      for (int c = 0; c < 2; ++c)  // keep the caller's stream-ordered frees after the ECDSA work
+        if (joins[c]) (void)hipStreamWaitEvent(ctx->stream, ctx->ev_join[c], 0);
+      return st;
+    }
     for (uint32_t base = 0; base < b->n_ed; base += ctx->ed_scap) {
       const uint32_t cnt = std::min(ctx->ed_scap, b->n_ed - base);
       cg::Ed25519Dev d;
@@ -572,26 +622,8 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode) {
       }
     }
   }
-  for (int c = 0; c < 2; ++c) {
-    if (!b->ec[c].n) continue;
-    const cg::EcdsaBatch& eb = b->ec[c];
-    const char* prep_name = eb.scheme == 2 ? "ecdsa_k1_prep" : "ecdsa_r1_prep";
-    const char* msm_name = eb.scheme == 2 ? "ecdsa_k1_msm" : "ecdsa_r1_msm";
-    uint32_t chunk = 0;
-    CG_TRY(ctx, cg::ecdsa_scratch(ctx->ec, eb.n, &chunk), "alloc ecdsa scratch");
-    for (uint32_t base = 0; base < eb.n; base += chunk) {
-      const uint32_t cnt = std::min(chunk, eb.n - base);
-      {
-        Timed t(ctx, prep_name, cnt);
-        CG_TRY(ctx, cg::ecdsa_launch_prep(eb, ctx->ec, base, cnt, b->arena, (uint32_t)mode, ctx->stream),
-               "launch ecdsa prep");
-      }
-      {
-        Timed t(ctx, msm_name, cnt);
-        CG_TRY(ctx, cg::ecdsa_launch_msm(eb, ctx->ec, base, cnt, b->verdict, ctx->stream), "launch ecdsa msm");
-      }
-    }
-  }
+  for (int c = 0; c < 2; ++c)
+    if (joins[c]) CG_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_join[c], 0), "join ecdsa");
   CG_TRY(ctx, cg::launch_verdict_bitmap(b->verdict, (uint32_t)n, b->bitmap, ctx->stream), "launch bitmap");
   return CG_OK;
 }

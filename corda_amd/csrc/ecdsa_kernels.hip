@@ -29,8 +29,9 @@ using namespace cg;
 
 namespace cg {
 
-struct EcdsaConsts {
-  uint32_t* gtab[2] = {nullptr, nullptr};  // affine k*G [kGTabEntries][kGStride]; K1 also k*2^128 G after it
+// Per-curve chunk scratch (one set per curve, so the two curves' pipelines can run
+// concurrently on their own streams).
+struct EcScratch {
   uint32_t scap = 0;
   uint32_t* status = nullptr;
   uint32_t* digits = nullptr;
@@ -39,6 +40,11 @@ struct EcdsaConsts {
   uint32_t* inv = nullptr;    // batched inversion mod n: leaves, tree levels, trees (element-major)
   uint32_t* invp = nullptr;   // batched inversion mod p (Z of the k*Q tables, 7 per lane)
   size_t inv_words = 0, invp_words = 0;
+};
+
+struct EcdsaConsts {
+  uint32_t* gtab[2] = {nullptr, nullptr};  // affine k*G [kGTabEntries][kGStride]; K1 also k*2^128 G after it
+  EcScratch sc[2];                         // secp256k1, secp256r1
 };
 
 }  // namespace cg
@@ -451,7 +457,13 @@ size_t inv_layout(uint32_t n, int words, size_t* val, size_t* tree, int* levels)
   return off;
 }
 
-hipError_t ensure_scratch(EcdsaConsts* c, uint32_t need) {
+void free_scratch(EcScratch* c) {
+  for (auto* p : {c->status, c->digits, c->qtab, c->ework, c->inv, c->invp})
+    if (p) (void)hipFree(p);
+  *c = EcScratch();
+}
+
+hipError_t ensure_scratch(EcScratch* c, uint32_t need) {
   const uint32_t want = need < kEcChunk ? need : kEcChunk;
   if (c->scap >= want) return hipSuccess;
   if (c->status) (void)hipFree(c->status);
@@ -491,8 +503,9 @@ void launch_inv_down(uint32_t* buf, const size_t* val, const size_t* tree, const
 }
 
 template <class C>
-hipError_t launch_prep(const EcdsaBatch& b, EcdsaConsts* c, uint32_t base, uint32_t cnt, const uint8_t* arena,
+hipError_t launch_prep(const EcdsaBatch& b, EcdsaConsts* cc, uint32_t base, uint32_t cnt, const uint8_t* arena,
                        uint32_t mode, hipStream_t s) {
+  EcScratch* c = &cc->sc[C::kScheme == 2 ? 0 : 1];
   size_t vn[kInvMaxLevels + 1], tn[kInvMaxLevels], vp[kInvMaxLevels + 1], tp[kInvMaxLevels];
   int ln = 0, lp = 0;
   if (inv_layout(cnt, 8, vn, tn, &ln) > c->inv_words || ln > kInvMaxLevels ||
@@ -517,9 +530,10 @@ hipError_t launch_prep(const EcdsaBatch& b, EcdsaConsts* c, uint32_t base, uint3
 }
 
 template <class C>
-hipError_t launch_msm(const EcdsaBatch& b, EcdsaConsts* c, uint32_t base, uint32_t cnt, uint8_t* verdict,
+hipError_t launch_msm(const EcdsaBatch& b, EcdsaConsts* cc, uint32_t base, uint32_t cnt, uint8_t* verdict,
                       hipStream_t s) {
-  const uint32_t* gt = c->gtab[C::kScheme == 2 ? 0 : 1];
+  const uint32_t* gt = cc->gtab[C::kScheme == 2 ? 0 : 1];
+  const EcScratch* c = &cc->sc[C::kScheme == 2 ? 0 : 1];
   hipLaunchKernelGGL(cg_ecdsa_msm<C>, grid_for(cnt), dim3(256), 0, s, b.rs + base, c->status, c->digits, c->qtab, gt,
                      cnt, b.n, c->scap, b.index + base, verdict);
   return hipGetLastError();
@@ -557,8 +571,10 @@ hipError_t ecdsa_consts_create(EcdsaConsts** out, hipStream_t s) {
 
 void ecdsa_consts_free(EcdsaConsts* c) {
   if (!c) return;
-  for (auto* p : {c->gtab[0], c->gtab[1], c->status, c->digits, c->qtab, c->ework, c->inv, c->invp})
+  for (auto* p : {c->gtab[0], c->gtab[1]})
     if (p) (void)hipFree(p);
+  free_scratch(&c->sc[0]);
+  free_scratch(&c->sc[1]);
   delete c;
 }
 
@@ -589,9 +605,10 @@ hipError_t ecdsa_batch_stage(const EcdsaBatch& b, const uint8_t* pk_raw_dev, siz
   return e;
 }
 
-hipError_t ecdsa_scratch(EcdsaConsts* c, uint32_t n, uint32_t* chunk) {
-  const hipError_t e = ensure_scratch(c, n);
-  *chunk = c->scap;
+hipError_t ecdsa_scratch(EcdsaConsts* c, int scheme, uint32_t n, uint32_t* chunk) {
+  EcScratch* sc = &c->sc[scheme == 2 ? 0 : 1];
+  const hipError_t e = ensure_scratch(sc, n);
+  *chunk = sc->scap;
   return e;
 }
 
