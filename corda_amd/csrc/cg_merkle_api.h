@@ -13,11 +13,13 @@ hipError_t launch_tx_index(const uint32_t* comp_start, const uint32_t* sig_start
 // leaves[8c..8c+7] = leaf hash of component c for c in [c_begin, c_end); *err |= 1 when a
 // component lies outside [0, arena_bytes).  nonces == nullptr: WireTransaction leaves
 // (nonce from the tx salt, last component = privacy salt); otherwise FilteredLeaves
-// leaves SHA256(ser_c || nonces[8c..8c+7]) (memory-order words).
+// leaves SHA256(ser_c || nonces[8c..8c+7]) (memory-order words).  With order (>= c_end -
+// c_begin words) and hist (32 words) scratch, lanes take components grouped by length.
 hipError_t launch_merkle_leaf(const uint8_t* arena, uint64_t arena_bytes, const uint64_t* comp_off,
                               const uint32_t* comp_len, const uint32_t* comp_start, const uint32_t* comp_tx,
                               const uint32_t* salts, const uint32_t* nonces, uint32_t c_begin, uint32_t c_end,
-                              uint32_t* leaves, uint32_t* err, hipStream_t s);
+                              uint32_t* leaves, uint32_t* err, hipStream_t s, uint32_t* order = nullptr,
+                              uint32_t* hist = nullptr);
 // ids (8 words per tx, digest byte order) = Merkle root over the tx's leaves (in place).
 hipError_t launch_merkle_tree(uint32_t* leaves, const uint32_t* comp_start, uint32_t n_tx, uint32_t* ids,
                               hipStream_t s);

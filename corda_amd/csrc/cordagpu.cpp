@@ -796,10 +796,12 @@ struct TxDev {
   uint32_t* sig_start = nullptr;
   uint64_t* sig_moff = nullptr;
   uint32_t* sig_mlen = nullptr;
+  uint32_t *order = nullptr, *leaf_hist = nullptr;  // leaf kernel work order (length buckets)
   void release(cg_ctx* ctx) {
     for (const void* p : {(const void*)arena, (const void*)comp_off, (const void*)comp_len, (const void*)comp_start,
                           (const void*)comp_tx, (const void*)salts, (const void*)leaves, (const void*)ids,
-                          (const void*)sig_start, (const void*)sig_moff, (const void*)sig_mlen})
+                          (const void*)sig_start, (const void*)sig_moff, (const void*)sig_mlen, (const void*)order,
+                          (const void*)leaf_hist})
       dfree(ctx, p);
     *this = TxDev();
   }
@@ -814,7 +816,8 @@ cg_status hash_txs(cg_ctx* ctx, TxDev& d, size_t arena_bytes, const uint32_t* co
   {
     Timed t(ctx, "merkle_leaf", c1 - c0);
     CG_TRY(ctx, cg::launch_merkle_leaf(d.arena, arena_bytes, d.comp_off, d.comp_len, d.comp_start, d.comp_tx, d.salts,
-                                       nullptr, c0, c1, d.leaves, ctx->err_flag, ctx->stream),
+                                       nullptr, c0, c1, d.leaves, ctx->err_flag, ctx->stream, d.order + c0,
+                                       d.leaf_hist),
            "launch merkle_leaf");
   }
   {
@@ -851,6 +854,8 @@ cg_status compute_txids(cg_ctx* ctx, size_t n_tx, const uint8_t* arena, size_t a
       (st = upload(ctx, &d.salts, (const uint32_t*)salts, 8 * n_tx, "upload salts")) != CG_OK ||
       (st = dalloc(ctx, &d.comp_tx, n_comp, "alloc comp_tx")) != CG_OK ||
       (st = dalloc(ctx, &d.leaves, 8 * n_comp, "alloc leaves")) != CG_OK ||
+      (st = dalloc(ctx, &d.order, n_comp + 1, "alloc leaf order")) != CG_OK ||
+      (st = dalloc(ctx, &d.leaf_hist, 32, "alloc leaf bins")) != CG_OK ||
       (st = dalloc(ctx, &d.ids, 32 * n_tx + 16, "alloc ids")) != CG_OK)
     return st;
   if (sig_start && ((st = upload(ctx, &d.sig_start, sig_start, n_tx + 1, "upload sig_start")) != CG_OK ||
@@ -882,7 +887,7 @@ cg_status tx_pipeline(cg_ctx* ctx, int mode, size_t n_tx, const uint8_t* arena, 
                       std::vector<hipEvent_t>& ev) {
   // chunks: enough to overlap the upload, few enough that each chunk's signature
   // subsets still fill the device (CORDA_AMD_TX_CHUNKS overrides, for tuning)
-  size_t kmax = 3;
+  size_t kmax = 4;
   if (const char* e = std::getenv("CORDA_AMD_TX_CHUNKS")) kmax = std::max(1, std::atoi(e));
   const size_t K = std::max<size_t>(1, std::min<size_t>(kmax, n_tx / 131072));
   // the whole arena goes out at once in kB equal byte pieces (one event each), before

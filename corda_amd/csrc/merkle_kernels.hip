@@ -51,11 +51,12 @@ __global__ __launch_bounds__(256) void cg_merkle_leaf(const uint8_t* __restrict_
                                                       const uint32_t* __restrict__ comp_tx,
                                                       const uint32_t* __restrict__ salts,
                                                       const uint32_t* __restrict__ nonces, uint32_t c_begin,
-                                                      uint32_t c_end, uint32_t* __restrict__ leaves,
-                                                      uint32_t* __restrict__ err) {
+                                                      uint32_t c_end, const uint32_t* __restrict__ order,
+                                                      uint32_t* __restrict__ leaves, uint32_t* __restrict__ err) {
   __shared__ uint32_t tails[256 * kTailWords];
-  const uint32_t c = c_begin + blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= c_end) return;
+  const uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c_begin + idx >= c_end) return;
+  const uint32_t c = order ? order[idx] : c_begin + idx;
   const uint32_t t = comp_tx[c];
   const uint32_t i = c - comp_start[t];
   // WireTransaction: the last component is the serialized privacy salt.  FilteredLeaves
@@ -86,6 +87,58 @@ __global__ __launch_bounds__(256) void cg_merkle_leaf(const uint8_t* __restrict_
   sha256_mem_tail(h, arena + off, len, [&](uint32_t d) { return tb[d]; }, salt ? 0u : 32u);
   uint32_t* dst = leaves + (size_t)c * 8;
   CG_UNROLL for (int w = 0; w < 8; ++w) dst[w] = h[w];
+}
+
+// Length buckets for the leaf kernel: components of a tx differ a lot in size
+// (inputs ~50 B, outputs 300-700 B), and a wave runs as many SHA-256 blocks as its
+// longest lane, so lanes are handed components grouped by block count (a counting
+// sort by bin: per-block LDS histograms, one global reservation per bin and block).
+// Only the work assignment changes; every leaf lands in its own slot.
+constexpr int kLeafBins = 32;
+CG_DEV uint32_t leaf_bin(uint32_t len) {
+  const uint32_t nb = (len + 41u + 63u) >> 6;  // blocks of ser || nonce (+ padding)
+  return nb < kLeafBins - 1 ? nb : kLeafBins - 1;
+}
+
+__global__ __launch_bounds__(256) void k_leaf_hist(const uint32_t* __restrict__ comp_len, uint32_t c_begin,
+                                                   uint32_t c_end, uint32_t* __restrict__ hist) {
+  __shared__ uint32_t h[kLeafBins];
+  if (threadIdx.x < kLeafBins) h[threadIdx.x] = 0;
+  __syncthreads();
+  const uint32_t c = c_begin + blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < c_end) atomicAdd(&h[leaf_bin(comp_len[c])], 1u);
+  __syncthreads();
+  if (threadIdx.x < kLeafBins && h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], h[threadIdx.x]);
+}
+
+// hist -> exclusive bin offsets, in place (one lane; 32 bins, longest first so the
+// heaviest waves start earliest)
+__global__ void k_leaf_scan(uint32_t* __restrict__ hist) {
+  if (threadIdx.x) return;
+  uint32_t acc = 0;
+  for (int b = kLeafBins - 1; b >= 0; --b) {
+    const uint32_t v = hist[b];
+    hist[b] = acc;
+    acc += v;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_leaf_scatter(const uint32_t* __restrict__ comp_len, uint32_t c_begin,
+                                                      uint32_t c_end, uint32_t* __restrict__ cursor,
+                                                      uint32_t* __restrict__ order) {
+  __shared__ uint32_t h[kLeafBins], base[kLeafBins];
+  if (threadIdx.x < kLeafBins) h[threadIdx.x] = 0;
+  __syncthreads();
+  const uint32_t c = c_begin + blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t bin = 0, local = 0;
+  if (c < c_end) {
+    bin = leaf_bin(comp_len[c]);
+    local = atomicAdd(&h[bin], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x < kLeafBins && h[threadIdx.x]) base[threadIdx.x] = atomicAdd(&cursor[threadIdx.x], h[threadIdx.x]);
+  __syncthreads();
+  if (c < c_end) order[base[bin] + local] = c;
 }
 
 // leaves[c] (8 big-endian-valued words) for every component; the tree of tx t is
@@ -228,10 +281,20 @@ hipError_t launch_tx_index(const uint32_t* comp_start, const uint32_t* sig_start
 hipError_t launch_merkle_leaf(const uint8_t* arena, uint64_t arena_bytes, const uint64_t* comp_off,
                               const uint32_t* comp_len, const uint32_t* comp_start, const uint32_t* comp_tx,
                               const uint32_t* salts, const uint32_t* nonces, uint32_t c_begin, uint32_t c_end,
-                              uint32_t* leaves, uint32_t* err, hipStream_t s) {
+                              uint32_t* leaves, uint32_t* err, hipStream_t s, uint32_t* order, uint32_t* hist) {
   if (c_end <= c_begin) return hipSuccess;
-  hipLaunchKernelGGL(cg_merkle_leaf, grid_for(c_end - c_begin), dim3(256), 0, s, arena, arena_bytes, comp_off,
-                     comp_len, comp_start, comp_tx, salts, nonces, c_begin, c_end, leaves, err);
+  const uint32_t n = c_end - c_begin;
+  if (order && hist) {
+    hipError_t e = hipMemsetAsync(hist, 0, kLeafBins * sizeof(uint32_t), s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_leaf_hist, grid_for(n), dim3(256), 0, s, comp_len, c_begin, c_end, hist);
+    hipLaunchKernelGGL(k_leaf_scan, dim3(1), dim3(64), 0, s, hist);
+    hipLaunchKernelGGL(k_leaf_scatter, grid_for(n), dim3(256), 0, s, comp_len, c_begin, c_end, hist, order);
+  } else {
+    order = nullptr;
+  }
+  hipLaunchKernelGGL(cg_merkle_leaf, grid_for(n), dim3(256), 0, s, arena, arena_bytes, comp_off, comp_len,
+                     comp_start, comp_tx, salts, nonces, c_begin, c_end, order, leaves, err);
   return hipGetLastError();
 }
 
