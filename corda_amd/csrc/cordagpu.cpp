@@ -937,6 +937,10 @@ cg_status tx_pipeline(cg_ctx* ctx, int mode, size_t n_tx, const uint8_t* arena, 
   return CG_OK;
 }
 
+cg_status hip_ok(cg_ctx* ctx, hipError_t e, const char* what) {
+  return e == hipSuccess ? CG_OK : hip_fail(ctx, e, what);
+}
+
 cg_status read_err_flag(cg_ctx* ctx) {
   uint32_t flag = 0;
   CG_TRY(ctx, hipMemcpyAsync(&flag, ctx->err_flag, 4, hipMemcpyDeviceToHost, ctx->stream), "read error flag");
@@ -1071,7 +1075,7 @@ cg_status cg_ftx_verify_batch(cg_ctx* ctx, size_t n_ftx, const uint8_t* arena, s
       return fail(ctx, CG_E_INVALID_ARGUMENT, "comp_start / node_start not monotone");
   if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, CG_E_DEVICE, "hipSetDevice");
   std::vector<uint8_t> status(n_ftx);
-  const uint32_t depth = pmt_scan(n_ftx, node_start, node_kind, status.data());
+  uint32_t depth = 1;
   const size_t n_comp = comp_start[n_ftx], n_node = node_start[n_ftx];
   TxDev d;
   uint32_t *nonces_d = nullptr, *node_start_d = nullptr, *node_hash_d = nullptr, *roots_d = nullptr,
@@ -1089,10 +1093,14 @@ cg_status cg_ftx_verify_batch(cg_ctx* ctx, size_t n_ftx, const uint8_t* arena, s
       (st = upload(ctx, &kind_d, node_kind, n_node, "upload node_kind")) == CG_OK &&
       (st = upload(ctx, &node_hash_d, (const uint32_t*)node_hash, 8 * n_node, "upload node_hash")) == CG_OK &&
       (st = upload(ctx, &roots_d, (const uint32_t*)root_hashes, 8 * n_ftx, "upload roots")) == CG_OK &&
+      (st = (arena_bytes ? hip_ok(ctx, hipMemcpyAsync(d.arena, arena, arena_bytes, hipMemcpyHostToDevice, ctx->stream),
+                                  "upload ftx arena")
+                         : CG_OK)) == CG_OK &&
+      // the host pass over the node programs runs while the uploads above are in flight
+      (depth = pmt_scan(n_ftx, node_start, node_kind, status.data()), true) &&
       (st = upload(ctx, &status_d, status.data(), n_ftx, "upload status")) == CG_OK &&
       (st = dalloc(ctx, &stack_d, (size_t)8 * depth * n_ftx, "alloc pmt stack")) == CG_OK) {
-    hipError_t e = arena_bytes ? hipMemcpyAsync(d.arena, arena, arena_bytes, hipMemcpyHostToDevice, ctx->stream)
-                               : hipSuccess;
+    hipError_t e = hipSuccess;
     if (e == hipSuccess) e = hipMemsetAsync(d.arena + arena_bytes, 0, 16, ctx->stream);
     if (e == hipSuccess) e = hipMemsetAsync(ctx->err_flag, 0, 4, ctx->stream);
     if (e == hipSuccess)
