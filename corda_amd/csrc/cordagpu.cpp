@@ -886,10 +886,12 @@ cg_status tx_pipeline(cg_ctx* ctx, int mode, size_t n_tx, const uint8_t* arena, 
                       const uint8_t* sig, size_t sig_stride, const uint32_t* sig_len, TxDev& d, uint8_t* verdict_d,
                       std::vector<hipEvent_t>& ev) {
   // chunks: enough to overlap the upload, few enough that each chunk's signature
-  // subsets still fill the device (CORDA_AMD_TX_CHUNKS overrides, for tuning)
-  size_t kmax = 4;
+  // subsets still fill the device
+  // (CORDA_AMD_TX_CHUNKS / CORDA_AMD_TX_MIN_CHUNK override, for tuning and tests)
+  size_t kmax = 4, min_chunk = 131072;
   if (const char* e = std::getenv("CORDA_AMD_TX_CHUNKS")) kmax = std::max(1, std::atoi(e));
-  const size_t K = std::max<size_t>(1, std::min<size_t>(kmax, n_tx / 131072));
+  if (const char* e = std::getenv("CORDA_AMD_TX_MIN_CHUNK")) min_chunk = std::max(1, std::atoi(e));
+  const size_t K = std::max<size_t>(1, std::min<size_t>(kmax, n_tx / min_chunk));
   // the whole arena goes out at once in kB equal byte pieces (one event each), before
   // any host-side scanning, so the copy engine starts immediately
   const size_t kB = 8, piece = (arena_bytes + kB - 1) / kB;

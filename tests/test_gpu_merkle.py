@@ -55,7 +55,17 @@ def run_tx_verify(ctx, w, mode=MODE_DO_VERIFY):
     return first_bad, verdict, ids
 
 
-def test_config4_shape_vs_oracle(gpu_ctx, oracle):
+@pytest.fixture(params=["1", "5"], ids=["one_chunk", "pipelined_5_chunks"])
+def tx_chunks(request, monkeypatch):
+    """cg_tx_verify_batch as one chunk, and streamed through the copy-stream pipeline
+    in 5 tx-range chunks (the arena pieces, per-chunk hashing and signature subsets
+    of tx_pipeline in cordagpu.cpp) at this small size."""
+    monkeypatch.setenv("CORDA_AMD_TX_CHUNKS", request.param)
+    monkeypatch.setenv("CORDA_AMD_TX_MIN_CHUNK", "1000")
+    return int(request.param)
+
+
+def test_config4_shape_vs_oracle(gpu_ctx, oracle, tx_chunks):
     w = datagen.make_tx_batch(30_000, seed=8, tamper_frac=0.02)
     # one bad signature at a random position in some untampered txs
     rng = np.random.default_rng(2)
