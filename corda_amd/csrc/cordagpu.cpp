@@ -292,6 +292,12 @@ struct MsgSrc {
   const uint32_t* len_host = nullptr;
   uint64_t* off_dev = nullptr;
   uint32_t* len_dev = nullptr;
+  // tx pipeline: the element-major pk / sig / sig_len rows are already on the device
+  // (uploaded on copy_stream, complete once raw_ready fires); not owned by the batch
+  const uint8_t* pk_dev = nullptr;
+  const uint8_t* sig_dev = nullptr;
+  const uint32_t* sl_dev = nullptr;
+  hipEvent_t raw_ready = nullptr;
 };
 
 cg_status check_inputs(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const uint8_t* pk, size_t pk_stride,
@@ -447,11 +453,19 @@ cg_status create_batch(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const ui
   // raw element-major inputs (temporary)
   uint8_t *pk_raw = nullptr, *sig_raw = nullptr;
   uint32_t* sl_raw = nullptr;
+  const bool raw_owned = !m.pk_dev;
+  auto free_raw = [&]() {
+    if (raw_owned) {
+      dfree(ctx, pk_raw);
+      dfree(ctx, sig_raw);
+      dfree(ctx, sl_raw);
+    }
+    pk_raw = sig_raw = nullptr;
+    sl_raw = nullptr;
+  };
   auto bail = [&](cg_status s) {
     (void)hipStreamSynchronize(ctx->stream);
-    dfree(ctx, pk_raw);
-    dfree(ctx, sig_raw);
-    dfree(ctx, sl_raw);
+    free_raw();
     batch_free(ctx, b);
     return s;
   };
@@ -490,9 +504,19 @@ cg_status create_batch(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const ui
     if ((st = upload(ctx, &b->msg_off_all, m.off_host, n, "upload msg_off")) != CG_OK) return bail(st);
     if ((st = upload(ctx, &b->msg_len_all, m.len_host, n, "upload msg_len")) != CG_OK) return bail(st);
   }
-  if ((st = upload(ctx, &pk_raw, pk, n * pk_stride, "upload pk")) != CG_OK) return bail(st);
-  if ((st = upload(ctx, &sig_raw, sig, n * sig_stride, "upload sig")) != CG_OK) return bail(st);
-  if (sig_len && (st = upload(ctx, &sl_raw, sig_len, n, "upload sig_len")) != CG_OK) return bail(st);
+  if (!raw_owned) {
+    pk_raw = const_cast<uint8_t*>(m.pk_dev);
+    sig_raw = const_cast<uint8_t*>(m.sig_dev);
+    sl_raw = const_cast<uint32_t*>(m.sl_dev);
+    if (m.raw_ready) {
+      const hipError_t e = hipStreamWaitEvent(ctx->stream, m.raw_ready, 0);
+      if (e != hipSuccess) return bail(hip_fail(ctx, e, "wait raw rows"));
+    }
+  } else {
+    if ((st = upload(ctx, &pk_raw, pk, n * pk_stride, "upload pk")) != CG_OK) return bail(st);
+    if ((st = upload(ctx, &sig_raw, sig, n * sig_stride, "upload sig")) != CG_OK) return bail(st);
+    if (sig_len && (st = upload(ctx, &sl_raw, sig_len, n, "upload sig_len")) != CG_OK) return bail(st);
+  }
   {
     Timed t(ctx, "stage", n);
     // Ed25519 subset -> SoA
@@ -538,11 +562,7 @@ cg_status create_batch(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const ui
   }
   // the host index vectors die here: wait for the copies that read them
   hipError_t e = hipStreamSynchronize(ctx->stream);
-  dfree(ctx, pk_raw);
-  dfree(ctx, sig_raw);
-  dfree(ctx, sl_raw);
-  pk_raw = sig_raw = nullptr;
-  sl_raw = nullptr;
+  free_raw();
   if (e != hipSuccess) return bail(hip_fail(ctx, e, "stage sync"));
   collect_timings(ctx);
   *out = b;
@@ -797,11 +817,13 @@ struct TxDev {
   uint64_t* sig_moff = nullptr;
   uint32_t* sig_mlen = nullptr;
   uint32_t *order = nullptr, *leaf_hist = nullptr;  // leaf kernel work order (length buckets)
+  uint8_t *raw_pk = nullptr, *raw_sig = nullptr;     // tx pipeline: signature rows, element-major
+  uint32_t* raw_sl = nullptr;
   void release(cg_ctx* ctx) {
     for (const void* p : {(const void*)arena, (const void*)comp_off, (const void*)comp_len, (const void*)comp_start,
                           (const void*)comp_tx, (const void*)salts, (const void*)leaves, (const void*)ids,
                           (const void*)sig_start, (const void*)sig_moff, (const void*)sig_mlen, (const void*)order,
-                          (const void*)leaf_hist})
+                          (const void*)leaf_hist, (const void*)raw_pk, (const void*)raw_sig, (const void*)raw_sl})
       dfree(ctx, p);
     *this = TxDev();
   }
@@ -892,22 +914,45 @@ cg_status tx_pipeline(cg_ctx* ctx, int mode, size_t n_tx, const uint8_t* arena, 
   if (const char* e = std::getenv("CORDA_AMD_TX_CHUNKS")) kmax = std::max(1, std::atoi(e));
   if (const char* e = std::getenv("CORDA_AMD_TX_MIN_CHUNK")) min_chunk = std::max(1, std::atoi(e));
   const size_t K = std::max<size_t>(1, std::min<size_t>(kmax, n_tx / min_chunk));
-  // the whole arena goes out at once in kB equal byte pieces (one event each), before
-  // any host-side scanning, so the copy engine starts immediately
-  const size_t kB = 8, piece = (arena_bytes + kB - 1) / kB;
-  ev.assign(kB, nullptr);
-  for (size_t j = 0; j < kB; ++j) {
-    CG_TRY(ctx, hipEventCreateWithFlags(&ev[j], hipEventDisableTiming), "tx pipeline event");
-    const size_t lo = std::min(arena_bytes, j * piece), hi = std::min(arena_bytes, (j + 1) * piece);
-    if (hi > lo)
-      CG_TRY(ctx, hipMemcpyAsync(d.arena + lo, arena + lo, hi - lo, hipMemcpyHostToDevice, ctx->copy_stream),
-             "upload tx arena");
-    CG_TRY(ctx, hipEventRecord(ev[j], ctx->copy_stream), "tx pipeline record");
-  }
   std::vector<size_t> tb(K + 1);
   for (size_t k = 0; k <= K; ++k) tb[k] = n_tx * k / K;
-  uint64_t up_to = 0;
+  // Everything goes out on copy_stream before any host-side scanning, so the copy
+  // engine starts immediately: the arena in kB equal byte pieces (event ev[j] each)
+  // and, after the pieces of the arena share of chunk k, that chunk's signature rows
+  // (event ev[kB + k]).  The compute stream then never waits behind a host copy.
+  // The row buffers come from the block cache: every block in it is idle here (the
+  // API calls that freed them ended with a stream sync; compute_txids only enqueued
+  // work on live blocks).
+  const size_t n_sig = sig_start[n_tx];
   cg_status st;
+  if (n_sig && ((st = dalloc(ctx, &d.raw_pk, n_sig * pk_stride, "alloc pk rows")) != CG_OK ||
+                (st = dalloc(ctx, &d.raw_sig, n_sig * sig_stride, "alloc sig rows")) != CG_OK ||
+                (sig_len && (st = dalloc(ctx, &d.raw_sl, n_sig, "alloc sig_len rows")) != CG_OK)))
+    return st;
+  const size_t kB = 8, piece = (arena_bytes + kB - 1) / kB;
+  ev.assign(kB + K, nullptr);
+  for (hipEvent_t& e : ev) CG_TRY(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming), "tx pipeline event");
+  for (size_t k = 0; k < K; ++k) {
+    for (size_t j = kB * k / K; j < kB * (k + 1) / K; ++j) {
+      const size_t lo = std::min(arena_bytes, j * piece), hi = std::min(arena_bytes, (j + 1) * piece);
+      if (hi > lo)
+        CG_TRY(ctx, hipMemcpyAsync(d.arena + lo, arena + lo, hi - lo, hipMemcpyHostToDevice, ctx->copy_stream),
+               "upload tx arena");
+      CG_TRY(ctx, hipEventRecord(ev[j], ctx->copy_stream), "tx pipeline record");
+    }
+    const size_t s0 = sig_start[tb[k]], s1 = sig_start[tb[k + 1]];
+    if (s1 > s0) {
+      CG_TRY(ctx, hipMemcpyAsync(d.raw_pk + s0 * pk_stride, pk + s0 * pk_stride, (s1 - s0) * pk_stride,
+                                 hipMemcpyHostToDevice, ctx->copy_stream), "upload pk rows");
+      CG_TRY(ctx, hipMemcpyAsync(d.raw_sig + s0 * sig_stride, sig + s0 * sig_stride, (s1 - s0) * sig_stride,
+                                 hipMemcpyHostToDevice, ctx->copy_stream), "upload sig rows");
+      if (sig_len)
+        CG_TRY(ctx, hipMemcpyAsync(d.raw_sl + s0, sig_len + s0, (s1 - s0) * 4, hipMemcpyHostToDevice, ctx->copy_stream),
+               "upload sig_len rows");
+    }
+    CG_TRY(ctx, hipEventRecord(ev[kB + k], ctx->copy_stream), "tx pipeline record");
+  }
+  uint64_t up_to = 0;
   for (size_t k = 0; k < K; ++k) {
     for (uint32_t c = comp_start[tb[k]]; c < comp_start[tb[k + 1]]; ++c)  // arena prefix chunk k reads
       up_to = std::max<uint64_t>(up_to, std::min<uint64_t>(comp_off[c] + comp_len[c], arena_bytes));
@@ -923,6 +968,10 @@ cg_status tx_pipeline(cg_ctx* ctx, int mode, size_t n_tx, const uint8_t* arena, 
       m.bytes = 32 * n_tx;
       m.off_dev = d.sig_moff + s0;
       m.len_dev = d.sig_mlen + s0;
+      m.pk_dev = d.raw_pk + s0 * pk_stride;
+      m.sig_dev = d.raw_sig + s0 * sig_stride;
+      m.sl_dev = sig_len ? d.raw_sl + s0 : nullptr;
+      m.raw_ready = ev[kB + k];
       cg_batch* b = nullptr;
       st = create_batch(ctx, s1 - s0, scheme_id ? scheme_id + s0 : nullptr, pk + s0 * pk_stride, pk_stride,
                         sig + s0 * sig_stride, sig_stride, sig_len ? sig_len + s0 : nullptr, m, &b);
