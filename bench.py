@@ -291,7 +291,12 @@ def run_ed25519(args, dist):
         "roofline": {"bound": "valu_int32", "kernel": "ed25519_msm", "achieved": round(achieved, 3),
                      "peak": PEAK, "unit": "TOPS", "frac": round(achieved / PEAK, 4), "traffic": traffic,
                      "ops_per_unit": model["msm"], "units_per_launch": per_launch,
-                     "avg_launch_ms": round(avg_msm_s * 1e3, 3), "hw_valu": hw},
+                     "avg_launch_ms": round(avg_msm_s * 1e3, 3), "hw_valu": hw,
+                     "model_note": "achieved = SURVEY 8(d)'s fixed op model of the reference algorithm "
+                                   "(253 doublings + 84 adds + final inversion per verify) / kernel time; the "
+                                   "kernel decides the same predicate with ~130 doublings and no inversion "
+                                   "(half-size scalars), so frac > 1 is algorithmic saving. hw_valu.frac_of_peak "
+                                   "is the issued-VALU-instruction fraction of the INT32 peak"},
         "path_frac_of_int32_peak": round(value / world * model["total"] / 1e12 / PEAK, 4),
         "prep_kernels": {"kernels": list(ED_PREP_KERNELS), "achieved": round(achieved_prep, 3),
                          "avg_launch_ms": round(avg_prep_s * 1e3, 3)},
