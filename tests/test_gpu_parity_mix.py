@@ -1,0 +1,85 @@
+"""North-star parity run: BASELINE.json asks for verdicts bit-exact against
+Crypto.doVerify on a 10 M adversarial+valid Ed25519 mix.
+
+Shape: config 5, i.e. signatures over 32 B tx ids with distinct keys. 10 % of
+them are adversarial, spread over E1–E12 (tools/datagen). Every
+chunk is verified on the GPU in both modes (Crypto.isValid, Crypto.kt:534-541;
+Crypto.doVerify, Crypto.kt:472-483) and compared element by element with the
+C restatement of i2p eddsa 0.2.0 (oracle/, test infrastructure only).
+
+The default size, 2^19, takes about 10 s on the box. Set
+CORDA_AMD_PARITY_N=10000000 for the full 10 M run; its log is committed as
+profiles/r01q_parity_10m.txt.
+"""
+from __future__ import annotations
+
+import collections
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import pytest
+
+from corda_amd import crypto
+from corda_amd._lib import ACCEPT, MODE_DO_VERIFY, MODE_IS_VALID, ptr
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools", "datagen"))
+import datagen  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+N = int(os.environ.get("CORDA_AMD_PARITY_N", 1 << 19))
+CHUNK = 1 << 21
+ADV = 0.10
+
+
+def _oracle(oracle, w, mode, threads):
+    out = np.empty(max(w.n, 1), dtype=np.uint8)
+    oracle.oracle_verify_batch(ptr(w.scheme), ptr(w.pk), ctypes.c_size_t(w.pk_stride), ptr(w.sig),
+                               ctypes.c_size_t(w.sig_stride), ptr(w.sig_len), ptr(w.msg), ptr(w.msg_off),
+                               ptr(w.msg_len), ctypes.c_size_t(w.n), mode, threads, ptr(out))
+    return out[:w.n]
+
+
+def test_adversarial_mix_vs_oracle(gpu_ctx, oracle):
+    threads = min(16, os.cpu_count() or 1)
+    t0 = time.perf_counter()
+    mismatches = {MODE_IS_VALID: 0, MODE_DO_VERIFY: 0}
+    verdicts = {MODE_IS_VALID: collections.Counter(), MODE_DO_VERIFY: collections.Counter()}
+    accepts_by_class = collections.Counter()
+    first_bad = []
+    for c0 in range(0, N, CHUNK):
+        n = min(CHUNK, N - c0)
+        k = c0 // CHUNK
+        w = datagen.make_batch(n, msg_bytes=32, seed=9000 + k, key_base=60_000_000 + c0, threads=threads)
+        w = datagen.add_ed25519_adversarial(w, frac=ADV, seed=900 + k)
+        b = crypto.PackedBatch(w.n, w.scheme, w.pk, w.pk_stride, w.sig, w.sig_stride, w.sig_len, w.msg,
+                               w.msg_off, w.msg_len)
+        cls = np.array(w.classes)
+        for mode in (MODE_IS_VALID, MODE_DO_VERIFY):
+            got = crypto.verify_packed(gpu_ctx, b, mode)
+            exp = _oracle(oracle, w, mode, threads)
+            bad = np.flatnonzero(got != exp)
+            mismatches[mode] += int(bad.size)
+            first_bad += [(c0 + int(i), str(cls[i]), int(got[i]), int(exp[i])) for i in bad[:5]]
+            for v, c in enumerate(np.bincount(got, minlength=5)):
+                if c:
+                    verdicts[mode][v] += int(c)
+            if mode == MODE_IS_VALID:
+                for name in np.unique(cls):
+                    accepts_by_class[str(name)] += int((got[cls == name] == ACCEPT).sum())
+        print(f"parity chunk {k}: {c0 + n}/{N} signatures, mismatches {mismatches}, "
+              f"{time.perf_counter() - t0:.1f} s", flush=True)
+    summary = {"signatures": N, "adversarial_frac": ADV, "msg_bytes": 32,
+               "mismatches_is_valid": mismatches[MODE_IS_VALID],
+               "mismatches_do_verify": mismatches[MODE_DO_VERIFY],
+               "verdict_counts_is_valid": dict(sorted(verdicts[MODE_IS_VALID].items())),
+               "verdict_counts_do_verify": dict(sorted(verdicts[MODE_DO_VERIFY].items())),
+               "accepts_by_class_is_valid": dict(sorted(accepts_by_class.items())),
+               "seconds": round(time.perf_counter() - t0, 1)}
+    print("parity summary " + json.dumps(summary), flush=True)
+    assert mismatches[MODE_IS_VALID] == 0 and mismatches[MODE_DO_VERIFY] == 0, first_bad[:10]
