@@ -269,6 +269,7 @@ def run_ed25519(args, dist):
               "valu_lane_ops_T": round(lane_ops / 1e12, 2), "frac_of_peak": round(lane_ops / 1e12 / PEAK, 3),
               "pmc_clock_GHz": clk,
               "frac_of_peak_at_pmc_clock": round(lane_ops / (256 * 64 * clk * 1e9), 3) if clk else None,
+              "occupancy": pmc.get("ed25519_msm_occupancy"),
               "source": pmc.get("source")}
 
     cpu = None

@@ -32,6 +32,24 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 from prof_summary import short, trace  # noqa: E402
 
 PEAK_LANE_OPS_PER_CLK = 256 * 64  # CUs x lanes (full-rate VOP3 integer)
+SIMDS = 256 * 4
+
+
+def isa_regs():
+    path = os.path.join(ROOT, "profiles", "isa_registers.json")
+    return json.load(open(path))["kernels"] if os.path.exists(path) else {}
+
+
+def occupancy(e, c, regs):
+    """Register pressure (code object, tools/isa_regs.py) and the measured mean
+    residency: SQ_WAVE_CYCLES counts quad-cycles summed over waves, GRBM_GUI_ACTIVE
+    cycles summed over the 8 XCDs (MI355X_MICROARCH.md, PMC units)."""
+    r = regs.get(e.get("kernel_short", ""), {})
+    for key in ("vgpr", "agpr", "sgpr", "vgpr_spill", "scratch_bytes", "lds_bytes", "waves_per_simd_limit"):
+        if key in r:
+            e[key] = r[key]
+    if c.get("SQ_WAVE_CYCLES") and c.get("GRBM_GUI_ACTIVE"):
+        e["mean_waves_per_simd"] = round(4 * c["SQ_WAVE_CYCLES"] / (c["GRBM_GUI_ACTIVE"] / 8 * SIMDS), 3)
 
 
 def load_counters(paths, grid):
@@ -47,7 +65,42 @@ def load_counters(paths, grid):
     return agg, dur
 
 
+def occupancy_fields(kernels):
+    out = {}
+    for k in ("hash", "points", "msm"):
+        e = kernels.get(f"cg_ed25519_{k}", {})
+        out[f"ed25519_{k}_occupancy"] = {key: e.get(key) for key in
+                                         ("vgpr", "vgpr_spill", "waves_per_simd_limit", "mean_waves_per_simd")}
+    return out
+
+
+def augment(tag):
+    """Adds register pressure and mean residency to an existing summary (from its
+    stored counters): python tools/pmc_report.py --augment r01p"""
+    path = os.path.join(ROOT, "profiles", f"{tag}_pmc_summary.json")
+    summary = json.load(open(path))
+    regs = isa_regs()
+    for k, e in summary["kernels"].items():
+        e["kernel_short"] = k
+        occupancy(e, e.get("counters", {}), regs)
+        e.pop("kernel_short")
+        e["counters"] = e.pop("counters", {})
+    with open(path, "w") as f:
+        json.dump(summary, f, indent=1)
+    tpath = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(tpath):
+        traffic = json.load(open(tpath))
+        if traffic.get("source") == f"profiles/{tag}_pmc_summary.json":
+            traffic.update(occupancy_fields(summary["kernels"]))
+            with open(tpath, "w") as f:
+                json.dump(traffic, f, indent=1)
+    print(json.dumps({k: {kk: vv for kk, vv in v.items() if kk != "counters"} for k, v in summary["kernels"].items()},
+                     indent=1))
+
+
 def main():
+    if sys.argv[1] == "--augment":
+        return augment(sys.argv[2])
     src, tag = sys.argv[1], sys.argv[2]
     grid = int(sys.argv[sys.argv.index("--grid") + 1]) if "--grid" in sys.argv else 1 << 20
     prof = os.path.join(ROOT, "profiles")
@@ -65,6 +118,7 @@ def main():
     for p in pmc_csv:
         shutil.copy(p, os.path.join(raw_dir, os.path.basename(p)))
     agg, dur = load_counters(pmc_csv, grid)
+    regs = isa_regs()
     kernels = {}
     for k, cs in agg.items():
         c = {n: statistics.median(v) for n, v in cs.items()}
@@ -98,6 +152,9 @@ def main():
             e["hbm_GBps"] = round(b / avg_s / 1e9, 1)
         if "TCC_HIT_sum" in c:
             e["l2_hit_rate"] = round(c["TCC_HIT_sum"] / max(c["TCC_HIT_sum"] + c["TCC_MISS_sum"], 1), 4)
+        e["kernel_short"] = k
+        occupancy(e, c, regs)
+        e.pop("kernel_short")
         e["counters"] = c
         kernels[k] = e
     summary = {"source": f"rocprofv3 --pmc passes over `python3 bench.py --steps 3` (tools/profile_gpu.sh {tag}); "
@@ -115,6 +172,7 @@ def main():
         e = kernels.get(f"cg_ed25519_{k}", {})
         traffic[f"ed25519_{k}_bytes_per_launch"] = e.get("hbm_bytes_per_launch")
         traffic[f"ed25519_{k}_valu_instr_per_verify"] = e.get("valu_instr_per_verify")
+    traffic.update(occupancy_fields(kernels))
     if "--no-traffic" not in sys.argv:  # pmc_traffic.json feeds bench.py's default (Ed25519) line
         with open(os.path.join(prof, "pmc_traffic.json"), "w") as f:
             json.dump(traffic, f, indent=1)
