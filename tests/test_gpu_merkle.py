@@ -89,6 +89,32 @@ def test_config4_shape_vs_oracle(gpu_ctx, oracle, tx_chunks):
     assert (first_bad[w.tampered] == 0).all()
 
 
+def test_null_sig_len_stride_64_vs_oracle(gpu_ctx, oracle, tx_chunks):
+    """sig_len = NULL (every signature is sig_stride bytes) through both tx paths:
+    the signature rows of the pipelined path then carry no length row. Ed25519
+    signatures repacked at stride 64 verify; the ECDSA DER ones, cut to 64 bytes,
+    fail exactly as the oracle says."""
+    w = datagen.make_tx_batch(12_000, seed=21, tamper_frac=0.02)
+    n_tx, n_sig = w.n_tx, int(w.sig_start[-1])
+    sig64 = np.ascontiguousarray(w.sig[:, :64])
+    first_bad = np.zeros(n_tx, dtype=np.int32)
+    verdict = np.zeros(n_sig, dtype=np.uint8)
+    ids = np.zeros(32 * n_tx, dtype=np.uint8)
+    gpu_ctx.check(gpu_ctx.lib.cg_tx_verify_batch(gpu_ctx.h, MODE_DO_VERIFY, n_tx, ptr(w.arena), len(w.arena),
+                                                 ptr(w.comp_off), ptr(w.comp_len), ptr(w.comp_start),
+                                                 ptr(w.salts), ptr(w.sig_start), ptr(w.scheme), ptr(w.pk), 64,
+                                                 ptr(sig64), 64, None, ptr(first_bad), ptr(verdict), ptr(ids)))
+    exp_ids = oracle_ids(oracle, w)
+    assert np.array_equal(ids, exp_ids)
+    msg_off = np.repeat(np.arange(n_tx, dtype=np.uint64) * 32, np.diff(w.sig_start))
+    sw = datagen.Workload(n_sig, w.scheme, w.pk, 64, sig64, 64, np.full(n_sig, 64, np.uint32), exp_ids, msg_off,
+                          np.full(n_sig, 32, np.uint32))
+    exp_v = oracle_verdicts(oracle, sw, MODE_DO_VERIFY)
+    assert np.array_equal(verdict, exp_v)
+    ed = w.scheme == 4
+    assert (exp_v[ed] == ACCEPT).mean() > 0.9 and (exp_v[~ed] != ACCEPT).all()
+
+
 def test_python_mirror_raises_like_check_signatures_are_valid(gpu_ctx):
     w = datagen.make_tx_batch(50, seed=3, tamper_frac=0.0)
     stxs = []
