@@ -83,3 +83,52 @@ def test_adversarial_mix_vs_oracle(gpu_ctx, oracle):
                "seconds": round(time.perf_counter() - t0, 1)}
     print("parity summary " + json.dumps(summary), flush=True)
     assert mismatches[MODE_IS_VALID] == 0 and mismatches[MODE_DO_VERIFY] == 0, first_bad[:10]
+
+
+EC_N = int(os.environ.get("CORDA_AMD_PARITY_EC_N", 1 << 16))
+EC_CHUNK = 1 << 19
+
+
+def test_ecdsa_adversarial_mix_vs_oracle(gpu_ctx, oracle):
+    """The same run for ECDSA: K1 and R1 interleaved, 32 B ids, 10 % adversarial
+    over D1–D8, both modes, against the BC 1.57 restatement. Default 2^16;
+    CORDA_AMD_PARITY_EC_N raises it (log: profiles/r01q_parity_ecdsa_2m.txt)."""
+    threads = min(16, os.cpu_count() or 1)
+    t0 = time.perf_counter()
+    mismatches = {MODE_IS_VALID: 0, MODE_DO_VERIFY: 0}
+    verdicts = {MODE_IS_VALID: collections.Counter(), MODE_DO_VERIFY: collections.Counter()}
+    accepts_by_class = collections.Counter()
+    first_bad = []
+    for c0 in range(0, EC_N, EC_CHUNK):
+        n = min(EC_CHUNK, EC_N - c0)
+        k = c0 // EC_CHUNK
+        scheme = np.where(np.arange(n) % 2 == 0, 2, 3).astype(np.uint8)
+        w = datagen.make_batch(n, msg_bytes=32, scheme=scheme, seed=7000 + k, key_base=80_000_000 + c0,
+                               threads=threads)
+        w = datagen.add_ecdsa_adversarial(w, frac=ADV, seed=700 + k)
+        b = crypto.PackedBatch(w.n, w.scheme, w.pk, w.pk_stride, w.sig, w.sig_stride, w.sig_len, w.msg,
+                               w.msg_off, w.msg_len)
+        cls = np.array(w.classes)
+        for mode in (MODE_IS_VALID, MODE_DO_VERIFY):
+            got = crypto.verify_packed(gpu_ctx, b, mode)
+            exp = _oracle(oracle, w, mode, threads)
+            bad = np.flatnonzero(got != exp)
+            mismatches[mode] += int(bad.size)
+            first_bad += [(c0 + int(i), str(cls[i]), int(got[i]), int(exp[i])) for i in bad[:5]]
+            for v, c in enumerate(np.bincount(got, minlength=5)):
+                if c:
+                    verdicts[mode][v] += int(c)
+            if mode == MODE_IS_VALID:
+                for name in np.unique(cls):
+                    accepts_by_class[str(name)] += int((got[cls == name] == ACCEPT).sum())
+        print(f"ecdsa parity chunk {k}: {c0 + n}/{EC_N} signatures, mismatches {mismatches}, "
+              f"{time.perf_counter() - t0:.1f} s", flush=True)
+    summary = {"signatures": EC_N, "curves": "K1/R1 interleaved", "adversarial_frac": ADV, "msg_bytes": 32,
+               "mismatches_is_valid": mismatches[MODE_IS_VALID],
+               "mismatches_do_verify": mismatches[MODE_DO_VERIFY],
+               "verdict_counts_is_valid": dict(sorted(verdicts[MODE_IS_VALID].items())),
+               "verdict_counts_do_verify": dict(sorted(verdicts[MODE_DO_VERIFY].items())),
+               "accepts_by_class_is_valid": dict(sorted(accepts_by_class.items())),
+               "seconds": round(time.perf_counter() - t0, 1)}
+    print("ecdsa parity summary " + json.dumps(summary), flush=True)
+    assert mismatches[MODE_IS_VALID] == 0 and mismatches[MODE_DO_VERIFY] == 0, first_bad[:10]
