@@ -282,6 +282,11 @@ def run_ed25519(args, dist):
                          f"adversarial elements), C i2p-exact restatement (oracle/liboracle.so) on {threads} "
                          f"threads of '{host_cpu_model()}', {dt:.1f} s wall",
                "verdicts_match_gpu": bool(np.array_equal(cv, verdict[:sample.n]))}
+        # SURVEY 8(d) also asks for a single-thread run: 1/16 of the same sample on one core
+        one = w.subset(np.arange(max(1, sample.n // 16)))
+        cv1, dt1 = oracle_verify(one, 1)
+        cpu["single_thread"] = {"value": round(one.n / dt1, 1), "cores": 1, "sample": f"first {one.n} signatures",
+                                "verdicts_match_gpu": bool(np.array_equal(cv1, verdict[:one.n]))}
 
     line = base_line(args, dist, "Ed25519 verifies/sec", "verifies/s", value, elapsed * 1e3 / args.steps, {
         "workload": "BASELINE config 2: EDDSA_ED25519_SHA512 batch verify, distinct keys, "
