@@ -25,20 +25,34 @@ own JSON line; they are evidence for DESIGN.md, not the driver's line):
     ftx      SURVEY 8(f) row 1: 1M FilteredTransaction.verify (non-validating
              notary: filtered-leaf hashes + partial Merkle tree + multiset check)
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload ed25519|ecdsa|tx|backlog]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload ed25519|ecdsa|tx|backlog|ftx]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
-Prints ONE JSON line on rank 0.  See DESIGN.md "Measurement" for the op model
-behind `roofline` and the CPU baseline.
+Multi-GPU: under torchrun (WORLD_SIZE set) every process is one rank and
+WORLD_SIZE must equal --gpus (else exit 2).  Without WORLD_SIZE and --gpus N > 1
+this process is only a launcher: it starts N rank processes of itself (RANK /
+LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT in their env)
+before anything touches the GPU, waits for them, and exits with the first
+failing rank's code; rank 0 prints the line.  ``--dry-run`` runs the same
+launcher / barrier / max-over-ranks / all-gather logic over gloo on CPU tensors
+with a synthetic step (no GPU; tests/test_bench_launcher.py).
+
+Prints ONE JSON line on rank 0.  See DESIGN.md "Measurement" for the roofline
+(issued VALU lane-ops of the dominant kernel against the 78.6 T lane-op/s
+INT32 VALU peak, instruction counts from the committed rocprofv3 PMC pass of the
+same kernel sources) and the CPU baseline.
 """
 from __future__ import annotations
 
 import argparse
 import ctypes
+import hashlib
 import json
 import os
 import platform
+import socket
 import statistics
+import subprocess
 import sys
 import time
 
@@ -49,10 +63,25 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tools", "datagen"))
 
 # SURVEY.md §8(d) fixed algorithmic op model (INT32 ops per verify), committed
-# once in bench/roofline_model.json.
+# once in bench/roofline_model.json, and the INT32 VALU peak: 256 CUs x 4 SIMD-32
+# x 32 lanes x 2.4 GHz = 78.6 T lane-ops/s (MI355X_MICROARCH.md: "4 SIMD-32 vector
+# units" per CU, a wave64 VALU instruction in 2 cycles).
 with open(os.path.join(ROOT, "bench", "roofline_model.json")) as _f:
     OP_MODEL = json.load(_f)
 PEAK = OP_MODEL["peak_int32_tops"]
+
+
+def kernel_src_hash() -> str:
+    """Hash of the device sources + build file; the PMC summaries carry the same
+    hash, so a bench line can say whether its instruction counts belong to the
+    kernels it ran (tools/pmc_report.py writes it)."""
+    d = os.path.join(ROOT, "corda_amd", "csrc")
+    h = hashlib.sha256()
+    for name in sorted(os.listdir(d)):
+        if name.endswith((".hip", ".h", ".cpp")) or name == "Makefile":
+            with open(os.path.join(d, name), "rb") as f:
+                h.update(name.encode() + b"\0" + f.read())
+    return h.hexdigest()[:16]
 
 
 def parse():
@@ -63,14 +92,67 @@ def parse():
     p.add_argument("--workload", choices=["ed25519", "ecdsa", "tx", "backlog", "ftx"], default="ed25519")
     p.add_argument("--batch", type=int, default=None,
                    help="per-GPU units (default: 1M signatures / 1M per curve / 1M txs; backlog: 100M total)")
-    p.add_argument("--pool", type=int, default=131072,
-                   help="distinct signed tuples generated for ecdsa/tx/backlog and tiled to --batch")
+    p.add_argument("--pool", type=int, default=None,
+                   help="distinct signed tuples generated and tiled to --batch (default: ecdsa all distinct, "
+                        "tx 131072, backlog 1M per rank)")
     p.add_argument("--msg-bytes", type=int, default=None)
     p.add_argument("--adversarial", type=float, default=0.01)
     p.add_argument("--latency-runs", type=int, default=21)
     p.add_argument("--cpu-sample", type=int, default=None, help="units in the CPU-baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    return p.parse_args()
+    p.add_argument("--key-reuse", type=int, default=0,
+                   help="ed25519/backlog: draw signer keys from this many distinct keys (0 = all distinct)")
+    p.add_argument("--dry-run", action="store_true",
+                   help="launcher / barrier / all-gather logic over gloo on CPU, synthetic step (tests)")
+    a = p.parse_args()
+    a.pool_set = a.pool is not None
+    if a.pool is None:
+        a.pool = 131072
+    return a
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args) -> int | None:
+    """Returns None when this process is a rank (torchrun, or --gpus 1), else
+    starts --gpus rank processes of this script and returns the exit code to use.
+    Runs before anything touches the GPU: the children are fresh processes (no
+    exec from a process with an initialised device)."""
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != args.gpus:
+            print(f"bench.py: WORLD_SIZE={ws} but --gpus {args.gpus}; refusing to report a mislabelled line",
+                  file=sys.stderr)
+            return 2
+        return None
+    if args.gpus <= 1:
+        return None
+    port = _free_port()
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env))
+    rc = 0
+    alive = list(procs)
+    while alive:
+        for p in list(alive):
+            code = p.poll()
+            if code is None:
+                continue
+            alive.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 1
+                for q in alive:  # a dead rank leaves the others waiting in a collective
+                    q.terminate()
+        time.sleep(0.2)
+    return rc
 
 
 def host_cpu_model():
@@ -116,31 +198,38 @@ def oracle_verify(w, threads, mode=0):
 
 
 class Dist:
-    """torch.distributed over RCCL when launched by torchrun (one rank per GPU)."""
+    """One rank per GPU: torch.distributed over RCCL ("nccl") when WORLD_SIZE > 1
+    (launched by torchrun or by launch_ranks); gloo on CPU tensors for --dry-run."""
 
-    def __init__(self):
+    def __init__(self, cpu: bool = False):
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        self.cpu = cpu
+        self.device = "cpu" if cpu else "cuda"
         self.d = None
         if self.world > 1:
             import torch
             import torch.distributed as dist
-            torch.cuda.set_device(self.local_rank)
-            dist.init_process_group("nccl", device_id=torch.device("cuda", self.local_rank))
+            if cpu:
+                dist.init_process_group("gloo")
+            else:
+                torch.cuda.set_device(self.local_rank)
+                dist.init_process_group("nccl", device_id=torch.device("cuda", self.local_rank))
             self.d = dist
 
     def sync(self):
         if self.d is not None:
-            import torch
             self.d.barrier()
+        if not self.cpu:
+            import torch
             torch.cuda.synchronize()
 
     def max(self, x: float) -> float:
         if self.d is None:
             return x
         import torch
-        t = torch.tensor([x], dtype=torch.float64, device="cuda")
+        t = torch.tensor([x], dtype=torch.float64, device=self.device)
         self.d.all_reduce(t, op=self.d.ReduceOp.MAX)
         return float(t.item())
 
@@ -181,18 +270,110 @@ def kstats(ctx, names):
     return out
 
 
-def pmc_view():
-    tpath = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+def pmc_view(name="pmc_traffic.json"):
+    tpath = os.path.join(ROOT, "profiles", name)
     if os.path.exists(tpath):  # measured in separate rocprofv3 --pmc passes (tools/profile_gpu.sh)
         with open(tpath) as f:
             return json.load(f)
     return {}
 
 
+def valu_roofline(pmc, kernel, units_per_launch, avg_launch_s, model_ops=None):
+    """Roofline of one kernel against the INT32 VALU peak.
+
+    achieved = VALU lane-instructions the kernel issues per unit (SQ_INSTS_VALU /
+    SQ_WAVES of the committed rocprofv3 PMC pass, profiles/<tag>_pmc_summary.json)
+    x units per launch / the launch's average duration (HIP events on the stream
+    the kernel runs on, this run).  `pmc_src_hash_matches` says whether the PMC
+    pass profiled the very kernel sources this run built (tools/pmc_report.py
+    stamps the hash).  model_* = SURVEY 8(d)'s fixed op model of the reference
+    algorithm over the same time (it prices 253 doublings + an inversion; the
+    kernels do ~130 doublings and no inversion, so model_frac is not a roofline
+    fraction and can exceed 1)."""
+    e = pmc.get("kernels", {}).get(kernel, {})
+    instr = e.get("valu_instr_per_unit")
+    out = {"bound": "valu_int32", "kernel": kernel, "unit": "T lane-ops/s", "peak": PEAK,
+           "units_per_launch": units_per_launch, "avg_launch_ms": round(avg_launch_s * 1e3, 4),
+           "valu_instr_per_unit": instr, "achieved": None, "frac": None,
+           "traffic": e.get("hbm_bytes_per_unit") and round(e["hbm_bytes_per_unit"] * units_per_launch),
+           "traffic_note": "HBM bytes per launch from the PMC pass: (2 x FETCH_SIZE + WRITE_SIZE) x 1 KiB, "
+                           "FETCH doubled for the 16-B-per-lane table loads (MI355X_MICROARCH.md HBM section)",
+           "pmc_source": pmc.get("source"), "pmc_commit": pmc.get("commit"),
+           "pmc_src_hash_matches": pmc.get("src_hash") == kernel_src_hash() if pmc else False,
+           "pmc_clock_GHz": e.get("effective_clock_GHz"), "occupancy": e.get("occupancy")}
+    if instr and avg_launch_s > 0:
+        ach = instr * units_per_launch / avg_launch_s / 1e12
+        out["achieved"] = round(ach, 3)
+        out["frac"] = round(ach / PEAK, 4)
+    if model_ops and avg_launch_s > 0:
+        m = model_ops * units_per_launch / avg_launch_s / 1e12
+        out["model_ops_per_unit"] = model_ops
+        out["model_achieved"] = round(m, 3)
+        out["model_frac"] = round(m / PEAK, 4)
+    return out
+
+
 def base_line(args, dist, metric, unit, value, ms_per_step, config, scaling="weak"):
     return {"metric": metric, "value": round(value, 1), "unit": unit, "n_gpus": dist.world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
             "scaling": scaling, "vs_baseline": None, "dtype": "int32", "data": "synthetic", "config": config}
+
+
+def pcie_h2d_peak_GBps(device=0, mb=512, reps=5):
+    """Measured host-to-device rate from page-locked memory on this box (the
+    roofline of the paths that start from host buffers)."""
+    import torch
+    src = torch.empty(mb << 20, dtype=torch.uint8).pin_memory()
+    dst = torch.empty(mb << 20, dtype=torch.uint8, device=f"cuda:{device}")
+    dst.copy_(src, non_blocking=True)
+    torch.cuda.synchronize()
+    best = 0.0
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        dst.copy_(src, non_blocking=True)
+        b.record()
+        b.synchronize()
+        best = max(best, (mb << 20) / (a.elapsed_time(b) / 1e3) / 1e9)
+    del src, dst
+    return round(best, 2)
+
+
+# ------------------------------------------------------------------ --dry-run
+def run_dry(args, dist):
+    """The multi-rank plumbing without a GPU: every rank owns a synthetic index
+    shard, a step packs a verdict bitmap and all-gathers it (gloo), timing is the
+    max over ranks between barriers — what the real workloads do over RCCL."""
+    import torch
+    from corda_amd import dist as D
+    if os.environ.get("CORDA_AMD_DRY_FAIL_RANK") == str(dist.rank):
+        sys.exit(3)  # tests: a failing rank must fail the launcher
+    n = args.batch or 4096
+    bounds = D.shard_bounds(n * dist.world, dist.world)
+    lo, hi = bounds[dist.rank], bounds[dist.rank + 1]
+    accept = (np.arange(lo, hi) % 7) != 3
+    words = torch.from_numpy(D.pack_bits(accept).view(np.int32).copy())
+    got = [None]
+
+    def step():
+        got[0] = D.allgather_bitmap(words, bounds, dist.rank) if dist.d is not None else words
+
+    for _ in range(args.warmup):
+        step()
+    dist.sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    dist.sync()
+    elapsed = dist.max(time.perf_counter() - t0)
+    exp = D.pack_bits((np.arange(n * dist.world) % 7) != 3).view(np.int32)
+    line = base_line(args, dist, "dry-run bitmap all-gathers/sec", "steps/s", args.steps / max(elapsed, 1e-9),
+                     elapsed * 1e3 / args.steps, {"workload": "dry run (gloo, CPU)", "batch_per_gpu": n,
+                                                  "global_batch": n * dist.world,
+                                                  "parallelism": f"dp{dist.world}"})
+    line["checks"] = {"bitmap_matches": bool(np.array_equal(got[0].numpy(), exp)), "rank_pid_world": dist.world}
+    line["dry_run"] = True
+    return line
 
 
 # ------------------------------------------------------------------ config 2
@@ -205,7 +386,9 @@ def run_ed25519(args, dist):
     msg_bytes = args.msg_bytes or 1024
     rank, world = dist.rank, dist.world
     t_gen = time.perf_counter()
-    w = datagen.make_batch(n, msg_bytes=msg_bytes, seed=42 + rank, key_base=rank * n, threads=cpu_threads())
+    # distinct keys, every 4,096th one a reference test key (seeds 20..110)
+    w = datagen.make_batch(n, msg_bytes=msg_bytes, seed=42 + rank, key_base=rank * n, threads=cpu_threads(),
+                           key_reuse=args.key_reuse, ref_seed_stride=4096)
     if args.adversarial > 0:
         w = datagen.add_ed25519_adversarial(w, frac=args.adversarial, seed=1 + rank)
     t_gen = time.perf_counter() - t_gen
@@ -261,28 +444,19 @@ def run_ed25519(args, dist):
             lat_small[bn] = round(statistics.median(ts) * 1e3, 3)
 
     value = n * world * args.steps / elapsed
-    msm = ks.get("ed25519_msm", {})
-    per_launch = msm.get("units_per_launch", 0)
-    avg_msm_s = msm.get("avg_launch_ms", 0) / 1e3
-    # the op model's "prep" (SHA-512, scalars, key decode, table) is spread over the hash and points kernels
-    avg_prep_s = sum(ks.get(k, {}).get("avg_launch_ms", 0) for k in ED_PREP_KERNELS) / 1e3
     model = OP_MODEL["ed25519_1kb" if msg_bytes > 32 else "ed25519_32b"]
-    achieved = model["msm"] * per_launch / avg_msm_s / 1e12 if avg_msm_s > 0 else 0.0
-    achieved_prep = model["prep"] * per_launch / avg_prep_s / 1e12 if avg_prep_s > 0 else 0.0
-    pmc = pmc_view()
-    traffic = pmc.get("ed25519_msm_bytes_per_launch")
-    hw = None
-    if pmc.get("ed25519_msm_valu_instr_per_verify") and avg_msm_s > 0:
-        # hardware view: VALU lane-instructions actually issued per second (instruction count
-        # per verify from SQ_INSTS_VALU, time from this run's HIP events)
-        lane_ops = pmc["ed25519_msm_valu_instr_per_verify"] * per_launch / avg_msm_s
-        clk = pmc.get("ed25519_msm_effective_clock_GHz")
-        hw = {"valu_instr_per_verify": pmc["ed25519_msm_valu_instr_per_verify"],
-              "valu_lane_ops_T": round(lane_ops / 1e12, 2), "frac_of_peak": round(lane_ops / 1e12 / PEAK, 3),
-              "pmc_clock_GHz": clk,
-              "frac_of_peak_at_pmc_clock": round(lane_ops / (256 * 64 * clk * 1e9), 3) if clk else None,
-              "occupancy": pmc.get("ed25519_msm_occupancy"),
-              "source": pmc.get("source")}
+    pmc = pmc_view("pmc_ed25519.json")
+    msm = ks.get("ed25519_msm", {})
+    roof = valu_roofline(pmc, "cg_ed25519_msm", msm.get("units_per_launch", 0), msm.get("avg_launch_ms", 0) / 1e3,
+                         model["msm"])
+    prep = {k: valu_roofline(pmc, f"cg_{k}", ks.get(k, {}).get("units_per_launch", 0),
+                             ks.get(k, {}).get("avg_launch_ms", 0) / 1e3) for k in ED_PREP_KERNELS}
+    # whole path: VALU lane-instructions of the three kernels per verify x verifies/s
+    path_instr = sum((pmc.get("kernels", {}).get(f"cg_{k}", {}).get("valu_instr_per_unit") or 0) for k in ED_KERNELS)
+    path = {"valu_instr_per_verify": path_instr or None,
+            "achieved": round(path_instr * value / world / 1e12, 3) if path_instr else None,
+            "frac": round(path_instr * value / world / 1e12 / PEAK, 4) if path_instr else None,
+            "model_frac": round(value / world * model["total"] / 1e12 / PEAK, 4)}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -301,23 +475,17 @@ def run_ed25519(args, dist):
                                 "verdicts_match_gpu": bool(np.array_equal(cv1, verdict[:one.n]))}
 
     line = base_line(args, dist, "Ed25519 verifies/sec", "verifies/s", value, elapsed * 1e3 / args.steps, {
-        "workload": "BASELINE config 2: EDDSA_ED25519_SHA512 batch verify, distinct keys, "
-                    f"{msg_bytes} B messages, {args.adversarial:.0%} adversarial (E1-E12)",
+        "workload": "BASELINE config 2: EDDSA_ED25519_SHA512 batch verify, "
+                    + (f"keys drawn from {args.key_reuse} signers" if args.key_reuse else
+                       "distinct keys (every 4096th a reference test key, seeds 20..110)")
+                    + f", {msg_bytes} B messages, {args.adversarial:.0%} adversarial (E1-E12)",
         "batch_per_gpu": n, "global_batch": n * world, "msg_bytes": msg_bytes,
         "parallelism": f"dp{world} (signature-index shards" + (", RCCL all-gather of accept bitmaps)" if world > 1 else ")")})
     line.update({
-        "roofline": {"bound": "valu_int32", "kernel": "ed25519_msm", "achieved": round(achieved, 3),
-                     "peak": PEAK, "unit": "TOPS", "frac": round(achieved / PEAK, 4), "traffic": traffic,
-                     "ops_per_unit": model["msm"], "units_per_launch": per_launch,
-                     "avg_launch_ms": round(avg_msm_s * 1e3, 3), "hw_valu": hw,
-                     "model_note": "achieved = SURVEY 8(d)'s fixed op model of the reference algorithm "
-                                   "(253 doublings + 84 adds + final inversion per verify) / kernel time; the "
-                                   "kernel decides the same predicate with ~130 doublings and no inversion "
-                                   "(half-size scalars), so frac > 1 is algorithmic saving. hw_valu.frac_of_peak "
-                                   "is the issued-VALU-instruction fraction of the INT32 peak"},
-        "path_frac_of_int32_peak": round(value / world * model["total"] / 1e12 / PEAK, 4),
-        "prep_kernels": {"kernels": list(ED_PREP_KERNELS), "achieved": round(achieved_prep, 3),
-                         "avg_launch_ms": round(avg_prep_s * 1e3, 3)},
+        "roofline": roof,
+        "path_roofline": path,
+        "prep_kernels": {k: {"achieved": v["achieved"], "frac": v["frac"], "avg_launch_ms": v["avg_launch_ms"],
+                             "valu_instr_per_unit": v["valu_instr_per_unit"]} for k, v in prep.items()},
         "kernels": ks,
         "latency": {"p50_device_ms": round(statistics.median(lat_dev) * 1e3, 3) if lat_dev else None,
                     "p50_e2e_ms": round(statistics.median(lat_e2e) * 1e3, 3) if lat_e2e else None,
@@ -335,31 +503,37 @@ def run_ed25519(args, dist):
 def run_ecdsa(args, dist):
     import datagen
     from corda_amd import Context, crypto
+    from corda_amd import dist as D
     from corda_amd._lib import ACCEPT, MODE_IS_VALID
 
     n = args.batch or (1 << 20)  # per curve
     msg_bytes = args.msg_bytes or 1024
-    pool = min(args.pool, n)
+    pool = min(args.pool, n) if args.pool_set else n  # distinct keys unless --pool caps them
     rank, world = dist.rank, dist.world
     t_gen = time.perf_counter()
-    # pool of distinct keys per curve, tiled to n per curve; K1 elements first, then R1
+    # K1 elements first, then R1; distinct keys per curve (or a pool tiled to size)
     p = datagen.make_batch(2 * pool, msg_bytes=msg_bytes, scheme=np.repeat(np.array([2, 3], np.uint8), pool),
                            seed=42 + rank, key_base=(1 << 32) + rank * 2 * pool, threads=cpu_threads())
-    k1 = p.subset(np.arange(pool)).tiled(n)
-    r1 = p.subset(np.arange(pool, 2 * pool)).tiled(n)
-    w = datagen.Workload(2 * n, np.concatenate([k1.scheme, r1.scheme]), np.concatenate([k1.pk, r1.pk]), 64,
-                         np.concatenate([k1.sig, r1.sig]), k1.sig_stride, np.concatenate([k1.sig_len, r1.sig_len]),
-                         np.concatenate([k1.msg[:-16], r1.msg]),
-                         np.concatenate([k1.msg_off, r1.msg_off + np.uint64(len(k1.msg) - 16)]),
-                         np.concatenate([k1.msg_len, r1.msg_len]), ["valid"] * (2 * n))
-    del k1, r1, p
+    if pool == n:
+        w = p
+    else:
+        k1 = p.subset(np.arange(pool)).tiled(n)
+        r1 = p.subset(np.arange(pool, 2 * pool)).tiled(n)
+        w = datagen.Workload(2 * n, np.concatenate([k1.scheme, r1.scheme]), np.concatenate([k1.pk, r1.pk]), 64,
+                             np.concatenate([k1.sig, r1.sig]), k1.sig_stride, np.concatenate([k1.sig_len, r1.sig_len]),
+                             np.concatenate([k1.msg[:-16], r1.msg]),
+                             np.concatenate([k1.msg_off, r1.msg_off + np.uint64(len(k1.msg) - 16)]),
+                             np.concatenate([k1.msg_len, r1.msg_len]), ["valid"] * (2 * n))
+        del k1, r1
+    del p
     if args.adversarial > 0:
         w = datagen.add_ecdsa_adversarial(w, frac=args.adversarial, seed=1 + rank)
     t_gen = time.perf_counter() - t_gen
 
     ctx = Context(dist.local_rank)
-    pb = crypto.PreparedBatch(ctx, crypto.PackedBatch(w.n, w.scheme, w.pk, w.pk_stride, w.sig, w.sig_stride,
-                                                      w.sig_len, w.msg, w.msg_off, w.msg_len))
+    packed = crypto.PackedBatch(w.n, w.scheme, w.pk, w.pk_stride, w.sig, w.sig_stride, w.sig_len, w.msg, w.msg_off,
+                                w.msg_len)
+    pb = crypto.PreparedBatch(ctx, packed)
     bitmap_dev = gathered = None
     if dist.d is not None:
         import torch
@@ -375,7 +549,7 @@ def run_ecdsa(args, dist):
 
     elapsed = timed(dist, ctx, step, args.steps, args.warmup)
     names = ["ecdsa_k1_prep", "ecdsa_k1_msm", "ecdsa_r1_prep", "ecdsa_r1_msm"]
-    ks = kstats(ctx, names)
+    ks_mixed = kstats(ctx, names)
     verdict = pb.verify(MODE_IS_VALID)
     adv = np.array([c != "valid" for c in w.classes])
     untouched_ok = bool((verdict[~adv] == ACCEPT).all())
@@ -383,21 +557,40 @@ def run_ecdsa(args, dist):
     if rank == 0:
         for _ in range(args.latency_runs):
             t1 = time.perf_counter(); pb.verify(MODE_IS_VALID, want_verdicts=False); lat_dev.append(time.perf_counter() - t1)
+    pb.close()
+
+    # Kernel calibration outside the timed region: each curve's half verified alone,
+    # so its kernels' HIP-event times are not stretched by the other curve's stream
+    # (the mixed step runs both curves concurrently).
+    ks = {}
+    for lo, hi in ((0, n), (n, 2 * n)):
+        cb = crypto.PreparedBatch(ctx, D.slice_batch(packed, lo, hi))
+        cb.verify(MODE_IS_VALID, want_verdicts=False)
+        ctx.set_profiling(True)
+        ctx.reset_stats()
+        for _ in range(max(2, min(args.steps, 5))):
+            cb.verify(MODE_IS_VALID, want_verdicts=False)
+        ctx.set_profiling(False)
+        ks.update(kstats(ctx, names))
+        cb.close()
 
     value = w.n * world * args.steps / elapsed
     key = "1kb" if msg_bytes > 32 else "32b"
-    ops_k1, ops_r1 = OP_MODEL["ecdsa_secp256k1"][key], OP_MODEL["ecdsa_p256"][key]
+    ops = {"k1": OP_MODEL["ecdsa_secp256k1"][key], "r1": OP_MODEL["ecdsa_p256"][key]}
+    pmc = pmc_view("pmc_ecdsa.json")
     per_curve = {}
-    for cname, ops in (("k1", ops_k1), ("r1", ops_r1)):
-        pr, ms = ks.get(f"ecdsa_{cname}_prep", {}), ks.get(f"ecdsa_{cname}_msm", {})
-        t = (pr.get("avg_launch_ms", 0) * pr.get("launches", 0) + ms.get("avg_launch_ms", 0) * ms.get("launches", 0))
-        units = ms.get("units_per_launch", 0) * ms.get("launches", 0)
-        per_curve[cname] = {"ops_per_verify": ops, "kernel_ms_per_step": round(t / max(args.steps, 1), 3),
-                            "achieved_TOPS": round(ops * units / (t / 1e3) / 1e12, 3) if t else 0.0}
-    # dominant kernel: the heavier curve's msm (op model has no prep/msm split for ECDSA,
-    # so achieved is priced over that curve's prep+msm pair)
-    dom = max(per_curve, key=lambda c: per_curve[c]["kernel_ms_per_step"])
-    ach = per_curve[dom]["achieved_TOPS"]
+    for c in ("k1", "r1"):
+        ms = ks.get(f"ecdsa_{c}_msm", {})
+        per_curve[c] = valu_roofline(pmc, f"cg_ecdsa_msm_{c}", ms.get("units_per_launch", 0),
+                                     ms.get("avg_launch_ms", 0) / 1e3)
+        per_curve[c]["curve_kernel_ms"] = round(sum(ks.get(f"ecdsa_{c}_{k}", {}).get("avg_launch_ms", 0)
+                                                    for k in ("prep", "msm")), 3)
+    dom = max(per_curve, key=lambda c: per_curve[c]["avg_launch_ms"])  # the dominant kernel: the slower msm
+    roof = dict(per_curve[dom])
+    roof["other_curve"] = per_curve["k1" if dom == "r1" else "r1"]
+    kinstr = {c: sum((pmc.get("kernels", {}).get(f"cg_{k}_{c}", {}).get("valu_instr_per_unit") or 0)
+                     for k in ("ecdsa_prep_a", "ecdsa_prep_b", "ecdsa_msm")) for c in ("k1", "r1")}
+    path_instr = (kinstr["k1"] + kinstr["r1"]) / 2
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = cpu_threads()
@@ -412,22 +605,23 @@ def run_ecdsa(args, dist):
                "verdicts_match_gpu": bool(np.array_equal(cv, verdict[idx]))}
     line = base_line(args, dist, "ECDSA verifies/sec", "verifies/s", value, elapsed * 1e3 / args.steps, {
         "workload": f"BASELINE config 3: {n} ECDSA_SECP256K1_SHA256 + {n} ECDSA_SECP256R1_SHA256 per GPU, "
-                    f"{msg_bytes} B messages, {args.adversarial:.0%} adversarial (D1-D8); {pool} distinct "
-                    "signed tuples per curve tiled to size",
+                    f"{msg_bytes} B messages, {args.adversarial:.0%} adversarial (D1-D8); "
+                    + ("distinct keys" if pool == n else f"{pool} distinct signed tuples per curve tiled to size")
+                    + "; K4 DER pre-pass staged once with the batch (cg_batch_create), not in the step",
         "batch_per_gpu": w.n, "global_batch": w.n * world, "msg_bytes": msg_bytes,
         "parallelism": f"dp{world} (signature-index shards)"})
     line.update({
-        "roofline": {"bound": "valu_int32", "kernel": f"ecdsa_{dom} (prep+msm)", "achieved": ach, "peak": PEAK,
-                     "unit": "TOPS", "frac": round(ach / PEAK, 4), "traffic": None, "per_curve": per_curve},
-        "kernels": ks,
-        "path_frac_of_int32_peak": round(value / world * (ops_k1 + ops_r1) / 2 / 1e12 / PEAK, 4),
+        "roofline": roof,
+        "path_roofline": {"valu_instr_per_verify": round(path_instr) or None,
+                          "frac": round(path_instr * value / world / 1e12 / PEAK, 4) if path_instr else None,
+                          "model_frac": round(value / world * (ops["k1"] + ops["r1"]) / 2 / 1e12 / PEAK, 4)},
+        "kernels": ks, "kernels_mixed_step_overlapping": ks_mixed,
         "latency": {"p50_device_ms": round(statistics.median(lat_dev) * 1e3, 3) if lat_dev else None,
                     "runs": args.latency_runs},
         "cpu_baseline": cpu,
         "checks": {"untouched_all_accept": untouched_ok, "accepts": int((verdict == ACCEPT).sum()),
                    "datagen_s": round(t_gen, 1)},
     })
-    pb.close()
     ctx.close()
     return line
 
@@ -486,11 +680,17 @@ def run_tx(args, dist):
               "untampered_all_valid": bool((first_bad[~w.tampered] == -1).all()),
               "signatures": n_sig, "datagen_s": round(t_gen, 1)}
     value = n_tx * world * args.steps / elapsed
-    kernel_ms = sum(v["avg_launch_ms"] * v["launches"] for v in ks.values()) / args.steps
-    mk = ks.get("merkle_leaf", {}), ks.get("merkle_tree", {})
-    merkle_ms = sum(v.get("avg_launch_ms", 0) for v in mk)
+    # Merkle kernels: the whole batch's SHA-256 op model over the summed launch time of
+    # one step (the batch is hashed in several tx-range chunks, one launch pair each)
+    merkle_ms = sum(ks.get(k, {}).get("avg_launch_ms", 0) * ks.get(k, {}).get("launches", 0)
+                    for k in ("merkle_leaf", "merkle_tree")) / args.steps
     mops = merkle_ops(w)
-    ach_merkle = mops / (merkle_ms / 1e3) / 1e12 if merkle_ms else 0.0
+    # what binds this path: the host->device upload of the caller's buffers
+    h2d = (len(w.arena) + w.comp_off.nbytes + w.comp_len.nbytes + w.comp_start.nbytes + w.salts.nbytes +
+           w.sig_start.nbytes + w.scheme.nbytes + w.pk.nbytes + w.sig.nbytes + w.sig_len.nbytes)
+    d2h = first_bad.nbytes + verdict.nbytes + ids.nbytes
+    pcie = pcie_h2d_peak_GBps(dist.local_rank)
+    step_s = elapsed / args.steps
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from concurrent.futures import ThreadPoolExecutor
@@ -530,11 +730,16 @@ def run_tx(args, dist):
         "batch_per_gpu": n_tx, "global_batch": n_tx * world, "parallelism": f"dp{world} (tx-index shards)"})
     line.update({
         "signatures_per_s": round(n_sig * world * args.steps / elapsed, 1),
-        "roofline": {"bound": "valu_int32", "kernel": "merkle_leaf+merkle_tree", "achieved": round(ach_merkle, 3),
-                     "peak": PEAK, "unit": "TOPS", "frac": round(ach_merkle / PEAK, 4), "traffic": None,
-                     "ops_per_launch": mops},
-        "kernels": ks, "kernel_ms_per_step": round(kernel_ms, 3),
-        "host_and_copy_ms_per_step": round(elapsed * 1e3 / args.steps - kernel_ms, 3),
+        "roofline": {"bound": "pcie", "kernel": "whole step (host buffers in, results out)",
+                     "achieved": round(h2d / step_s / 1e9, 2), "peak": pcie, "unit": "GB/s",
+                     "frac": round(h2d / step_s / 1e9 / pcie, 4), "traffic": h2d + d2h,
+                     "h2d_bytes_per_step": h2d, "d2h_bytes_per_step": d2h,
+                     "peak_note": "measured pinned host-to-device copy rate on this box (512 MB, best of 5)"},
+        "merkle_kernels": {"ms_per_step": round(merkle_ms, 3), "model_ops_per_step": mops,
+                           "model_achieved_T": round(mops / (merkle_ms / 1e3) / 1e12, 3) if merkle_ms else None},
+        "kernels": ks,
+        "kernels_note": "HIP-event spans per kernel; the ECDSA curves run on their own streams beside the Ed25519 "
+                        "kernels, so spans overlap and do not add up to the step",
         "cpu_baseline": cpu, "checks": checks})
     ctx.close()
     return line
@@ -570,8 +775,10 @@ def run_ftx(args, dist):
     blocks = int(((w.comp_len.astype(np.int64) + 32 + 9 + 63) // 64).sum() + 2 * int((w.node_kind == 2).sum()))
     ops = blocks * OP_MODEL["primitives"]["sha256_block"]
     kms = sum(ks.get(k, {}).get("avg_launch_ms", 0) for k in ("merkle_leaf", "pmt_eval"))
-    ach = ops / (kms / 1e3) / 1e12 if kms else 0.0
     value = n * world * args.steps / elapsed
+    h2d = len(w.arena) + sum(x.nbytes for x in arrs[1:])
+    pcie = pcie_h2d_peak_GBps(dist.local_rank)
+    step_s = elapsed / args.steps
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         m = min(args.cpu_sample or 2097152, n)
@@ -592,9 +799,13 @@ def run_ftx(args, dist):
                     "host buffers (page-locked once) in, results out",
         "batch_per_gpu": n, "global_batch": n * world, "parallelism": f"dp{world} (ftx-index shards)"})
     line.update({
-        "roofline": {"bound": "valu_int32", "kernel": "merkle_leaf+pmt_eval", "achieved": round(ach, 3),
-                     "peak": PEAK, "unit": "TOPS", "frac": round(ach / PEAK, 4), "traffic": None,
-                     "ops_per_launch": ops, "sha256_blocks": blocks},
+        "roofline": {"bound": "pcie", "kernel": "whole step (host buffers in, results out)",
+                     "achieved": round(h2d / step_s / 1e9, 2), "peak": pcie, "unit": "GB/s",
+                     "frac": round(h2d / step_s / 1e9 / pcie, 4), "traffic": h2d + out.nbytes,
+                     "h2d_bytes_per_step": h2d,
+                     "peak_note": "measured pinned host-to-device copy rate on this box (512 MB, best of 5)"},
+        "sha256_kernels": {"ms_per_step": round(kms, 3), "model_ops_per_step": ops, "sha256_blocks": blocks,
+                           "model_achieved_T": round(ops / (kms / 1e3) / 1e12, 3) if kms else None},
         "kernels": ks, "cpu_baseline": cpu,
         "checks": {"results_match_generator": bool(np.array_equal(out, w.expected)), "false": int(out.sum()),
                    "components": int(w.comp_start[-1]), "nodes": int(w.node_start[-1]), "datagen_s": round(t_gen, 1)}})
@@ -608,16 +819,19 @@ def run_backlog(args, dist):
     from corda_amd import Context, crypto
     from corda_amd._lib import ACCEPT, MODE_IS_VALID
 
+    from corda_amd import dist as D
     total = args.batch or 100_000_000
     rank, world = dist.rank, dist.world
-    lo, hi = total * rank // world, total * (rank + 1) // world  # index shard of this rank
+    bounds = D.shard_bounds(total, world)  # 32-aligned index shards: bitmap words concatenate
+    lo, hi = bounds[rank], bounds[rank + 1]
     n = hi - lo
+    n_max = max(bounds[r + 1] - bounds[r] for r in range(world))
     chunk = 1 << 24
     pool = min(args.pool * 8, n)
     msg_bytes = args.msg_bytes or 32
     t_gen = time.perf_counter()
     p = datagen.make_batch(pool, msg_bytes=msg_bytes, seed=42 + rank, key_base=(2 << 32) + rank * pool,
-                           threads=cpu_threads())
+                           threads=cpu_threads(), key_reuse=args.key_reuse)
     t_gen = time.perf_counter() - t_gen
     ctx = Context(dist.local_rank)
     batches, sizes, adv_ok = [], [], True
@@ -640,7 +854,7 @@ def run_backlog(args, dist):
     bitmaps = gathered = None
     if dist.d is not None:
         import torch
-        nwords = (n + 31) // 32 + len(sizes)
+        nwords = (n_max + 31) // 32  # equal on every rank (all_gather_into_tensor)
         bitmaps = torch.zeros(nwords, dtype=torch.int32, device="cuda")
         gathered = torch.zeros(nwords * world, dtype=torch.int32, device="cuda")
 
@@ -658,7 +872,10 @@ def run_backlog(args, dist):
     value = total * args.steps / elapsed
     model = OP_MODEL["ed25519_32b" if msg_bytes <= 32 else "ed25519_1kb"]
     msm = ks.get("ed25519_msm", {})
-    ach = model["msm"] * msm.get("units_per_launch", 0) / (msm.get("avg_launch_ms", 1) / 1e3) / 1e12 if msm else 0
+    roof = valu_roofline(pmc_view("pmc_ed25519.json"), "cg_ed25519_msm", msm.get("units_per_launch", 0),
+                         msm.get("avg_launch_ms", 0) / 1e3, model["msm"])
+    roof["pmc_note"] = "instruction counts from the config-2 (1 KB message) PMC pass; the msm kernel does not " \
+                       "read messages, so its count per verify is the same for 32 B ids"
     line = base_line(args, dist, "Ed25519 verifies/sec (100M notary backlog)", "verifies/s", value,
                      elapsed * 1e3 / args.steps, {
                          "workload": f"BASELINE config 5: {total} EDDSA_ED25519_SHA512 signatures over {msg_bytes} B "
@@ -669,9 +886,7 @@ def run_backlog(args, dist):
                          "parallelism": f"dp{world} (index shards" + (", RCCL all-gather)" if world > 1 else ")")},
                      scaling="strong")
     line.update({
-        "roofline": {"bound": "valu_int32", "kernel": "ed25519_msm", "achieved": round(ach, 3), "peak": PEAK,
-                     "unit": "TOPS", "frac": round(ach / PEAK, 4), "traffic": None},
-        "path_frac_of_int32_peak": round(value / world * model["total"] / 1e12 / PEAK, 4),
+        "roofline": roof,
         "kernels": ks, "cpu_baseline": None,
         "checks": {"first_chunk_untouched_all_accept": adv_ok, "datagen_s": round(t_gen, 1),
                    "stage_s": round(t_stage, 1), "chunks": len(sizes)}})
@@ -683,14 +898,19 @@ def run_backlog(args, dist):
 
 def main():
     args = parse()
-    dist = Dist()
-    run = {"ed25519": run_ed25519, "ecdsa": run_ecdsa, "tx": run_tx, "backlog": run_backlog,
-           "ftx": run_ftx}[args.workload]
+    rc = launch_ranks(args)
+    if rc is not None:
+        return rc
+    dist = Dist(cpu=args.dry_run)
+    run = run_dry if args.dry_run else {"ed25519": run_ed25519, "ecdsa": run_ecdsa, "tx": run_tx,
+                                        "backlog": run_backlog, "ftx": run_ftx}[args.workload]
     line = run(args, dist)
     if dist.rank == 0:
+        line["kernel_src_hash"] = kernel_src_hash()
         print(json.dumps(line), flush=True)
     dist.close()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

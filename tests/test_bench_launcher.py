@@ -1,0 +1,81 @@
+"""bench.py's multi-GPU plumbing on CPU (no GPU): the --gpus N launcher starts N
+rank processes itself (so the driver's `python bench.py --gpus N` really runs N
+ranks), a WORLD_SIZE that disagrees with --gpus is refused, a failing rank fails
+the launcher, and the roofline helper reports fractions of the 78.6 T peak."""
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(ROOT, "bench.py")
+
+
+def _env(**kw):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(kw)
+    return env
+
+
+def _run(args, env, timeout=180):
+    return subprocess.run([sys.executable, BENCH, *args], env=env, capture_output=True, text=True,
+                          timeout=timeout, cwd="/tmp")
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_launcher_spawns_n_gloo_ranks(n):
+    r = _run(["--gpus", str(n), "--dry-run", "--steps", "3", "--warmup", "1", "--batch", "1000"], _env())
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1  # rank 0 only
+    line = lines[0]
+    assert line["n_gpus"] == n and line["steps"] == 3 and line["warmup"] == 1
+    assert line["config"]["global_batch"] == 1000 * n
+    assert line["checks"]["bitmap_matches"] is True
+
+
+def test_world_size_mismatch_is_refused():
+    r = _run(["--gpus", "2", "--dry-run"], _env(WORLD_SIZE="3", RANK="0", LOCAL_RANK="0"))
+    assert r.returncode == 2
+    assert "WORLD_SIZE=3" in r.stderr
+    assert not [x for x in r.stdout.splitlines() if x.startswith("{")]
+
+
+def test_failing_rank_fails_the_launcher():
+    r = _run(["--gpus", "2", "--dry-run", "--steps", "2"], _env(CORDA_AMD_DRY_FAIL_RANK="1"), timeout=240)
+    assert r.returncode != 0
+
+
+def test_single_rank_dry_run_without_launcher():
+    r = _run(["--dry-run", "--steps", "2"], _env())
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert json.loads(r.stdout.strip().splitlines()[-1])["n_gpus"] == 1
+
+
+def test_valu_roofline_fraction_of_peak():
+    sys.path.insert(0, ROOT)
+    import bench
+    assert bench.PEAK == pytest.approx(78.6)
+    pmc = {"source": "x", "src_hash": bench.kernel_src_hash(),
+           "kernels": {"cg_ed25519_msm": {"valu_instr_per_unit": 200000, "hbm_bytes_per_unit": 1000.0}}}
+    r = bench.valu_roofline(pmc, "cg_ed25519_msm", 1 << 20, 7.5e-3, model_ops=987510)
+    ach = 200000 * (1 << 20) / 7.5e-3 / 1e12
+    assert r["achieved"] == pytest.approx(ach, rel=1e-3)
+    assert r["frac"] == pytest.approx(ach / 78.6, rel=1e-3) and r["frac"] <= 1
+    assert r["pmc_src_hash_matches"] is True
+    assert r["traffic"] == 1000 * (1 << 20)
+    assert r["model_frac"] > 1  # the op model is not a roofline (see valu_roofline's docstring)
+    stale = dict(pmc, src_hash="0" * 16)
+    assert bench.valu_roofline(stale, "cg_ed25519_msm", 1, 1.0)["pmc_src_hash_matches"] is False
+
+
+def test_pmc_report_hash_matches_bench_hash():
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    sys.path.insert(0, ROOT)
+    import bench
+    import pmc_report
+    assert pmc_report.src_identity()[1] == bench.kernel_src_hash()

@@ -65,7 +65,18 @@ static void key_seed(uint8_t seed32[32], uint64_t idx) {
   memcpy(seed32, h, 32);
 }
 
-typedef struct {
+/* Key selection (dg_set_key_options): element i signs with key key_base + (i mod
+ * key_modulus) (0: all distinct), and every ref_stride-th element (0: none) with
+ * one of the reference's fixed test keys entropyToKeyPair(20, 30, ..., 110)
+ * (test-utils TestConstants.kt:32-71; Crypto.kt:733-739: seed = the big-endian
+ * minimal bytes of k, zero-padded on the right to 32 bytes). */
+static uint64_t g_key_modulus = 0, g_ref_stride = 0;
+void dg_set_key_options(uint64_t key_modulus, uint64_t ref_stride) {
+  g_key_modulus = key_modulus;
+  g_ref_stride = ref_stride;
+}
+
+typedef struct job_s {
   const uint8_t* scheme_arr;  /* 2 K1, 3 R1, 4 Ed25519 (NULL: all Ed25519) */
   size_t lo, hi;
   uint64_t key_base;
@@ -78,9 +89,18 @@ typedef struct {
   int err;
 } job;
 
+static void elem_seed(const struct job_s* j, size_t i, uint8_t seed[32]) {
+  if (g_ref_stride && i % g_ref_stride == 0) {
+    memset(seed, 0, 32);
+    seed[0] = (uint8_t)(20 + 10 * ((i / g_ref_stride) % 10));  /* k < 128: one byte */
+    return;
+  }
+  key_seed(seed, j->key_base + (g_key_modulus ? i % g_key_modulus : i));
+}
+
 static void sign_ed(job* j, size_t i, EVP_MD_CTX* mctx) {
   uint8_t seed[32];
-  key_seed(seed, j->key_base + i);
+  elem_seed(j, i, seed);
   EVP_PKEY* k = EVP_PKEY_new_raw_private_key(EVP_PKEY_ED25519, NULL, seed, 32);
   size_t pl = 32, sl = 64;
   if (!k || EVP_PKEY_get_raw_public_key(k, j->pk + i * j->pk_stride, &pl) != 1 ||
@@ -101,7 +121,7 @@ static void sign_ec(job* j, size_t i, int scheme, BN_CTX* bctx, EC_KEY* keys[2])
   if (!*slot) *slot = EC_KEY_new_by_curve_name(nid);
   EC_KEY* k = *slot;
   uint8_t seed[32], dig[32];
-  key_seed(seed, j->key_base + i);
+  elem_seed(j, i, seed);
   const EC_GROUP* g = EC_KEY_get0_group(k);
   BIGNUM* d = BN_bin2bn(seed, 32, NULL);
   const BIGNUM* order = EC_GROUP_get0_order(g);

@@ -30,6 +30,7 @@ def lib():
                                 ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                 ctypes.c_void_p, ctypes.c_int]
     c.dg_fill_bytes.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64]
+    c.dg_set_key_options.argtypes = [ctypes.c_uint64, ctypes.c_uint64]
     c.dg_txid_batch.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_size_t, ctypes.c_void_p]
     return c
 
@@ -71,9 +72,13 @@ class Workload:
 
 
 def make_batch(n: int, msg_bytes: int = 1024, scheme: int | np.ndarray = 4, seed: int = 42, key_base: int = 0,
-               threads: int | None = None, sig_stride: int = 72) -> Workload:
-    """n signed messages of msg_bytes each (fixed size), all valid."""
+               threads: int | None = None, sig_stride: int = 72, key_reuse: int = 0,
+               ref_seed_stride: int = 0) -> Workload:
+    """n signed messages of msg_bytes each (fixed size), all valid.  key_reuse > 0:
+    element i signs with key (i mod key_reuse); ref_seed_stride > 0: every such
+    element uses the reference's test keys entropyToKeyPair(20..110)."""
     c = lib()
+    c.dg_set_key_options(key_reuse, ref_seed_stride)
     threads = threads or min(16, os.cpu_count() or 1)
     sch = np.full(n, scheme, dtype=np.uint8) if np.isscalar(scheme) else np.asarray(scheme, dtype=np.uint8)
     msg = np.empty(n * msg_bytes + 1, dtype=np.uint8)
@@ -85,6 +90,7 @@ def make_batch(n: int, msg_bytes: int = 1024, scheme: int | np.ndarray = 4, seed
     sig_len = np.zeros(n, dtype=np.uint32)
     rc = c.dg_sign_batch(n, sch.ctypes.data, key_base, pk.ctypes.data, 64, sig.ctypes.data, sig_stride,
                          sig_len.ctypes.data, msg.ctypes.data, msg_off.ctypes.data, msg_len.ctypes.data, threads)
+    c.dg_set_key_options(0, 0)
     if rc != 0:
         raise RuntimeError("signature generation failed")
     return Workload(n, sch, pk, 64, sig, sig_stride, sig_len, msg, msg_off, msg_len, ["valid"] * n)

@@ -12,9 +12,10 @@ Conventions (MI355X_MICROARCH.md, HBM / rocprofv3 section):
   * SQ_INSTS_VALU counts wave instructions; per-lane (= per-verify) count is
     SQ_INSTS_VALU / SQ_WAVES.
   * effective clock = GRBM_GUI_ACTIVE / 8 XCDs / dispatch duration.
-  * FETCH_SIZE / WRITE_SIZE are KiB; HBM bytes = (FETCH_SIZE + WRITE_SIZE) * 1024.
-    No 2x correction is applied: these kernels gather 4-16 B per lane, not the
-    16-B streaming loads the correction is calibrated on.
+  * FETCH_SIZE / WRITE_SIZE are KiB; HBM bytes = (c * FETCH_SIZE + WRITE_SIZE) * 1024
+    with c = 2 for kernels whose dominant loads are 16 B per lane (the guide's gfx950
+    rule: FETCH_SIZE reports half of those bytes) and c = 1 otherwise.
+  * peak = 256 CUs x 4 SIMD-32 x 32 lanes x 2.4 GHz = 78.6 T lane-ops/s.
 """
 from __future__ import annotations
 
@@ -31,7 +32,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 from prof_summary import short, trace  # noqa: E402
 
-PEAK_LANE_OPS_PER_CLK = 256 * 64  # CUs x lanes (full-rate VOP3 integer)
+PEAK_LANE_OPS_PER_CLK = 256 * 4 * 32  # CUs x SIMD-32 units x lanes (MI355X_MICROARCH.md)
+PEAK_T = 78.6  # at 2.4 GHz
 SIMDS = 256 * 4
 
 
@@ -98,11 +100,44 @@ def augment(tag):
                      indent=1))
 
 
+def src_identity():
+    """(git commit, kernel source hash) of the tree being profiled; bench.py
+    recomputes the hash to tell whether a summary matches its kernels."""
+    import hashlib
+    src_hash = None
+    try:
+        d = os.path.join(ROOT, "corda_amd", "csrc")
+        h = hashlib.sha256()
+        for name in sorted(os.listdir(d)):
+            if name.endswith((".hip", ".h", ".cpp")) or name == "Makefile":
+                with open(os.path.join(d, name), "rb") as f:
+                    h.update(name.encode() + b"\0" + f.read())
+        src_hash = h.hexdigest()[:16]
+    except OSError:
+        pass
+    commit = os.environ.get("PROFILE_COMMIT")
+    if not commit:
+        try:
+            import subprocess
+            commit = subprocess.check_output(["git", "-C", ROOT, "rev-parse", "--short=12", "HEAD"],
+                                             stderr=subprocess.DEVNULL).decode().strip()
+        except Exception:  # noqa: BLE001 (no git on the box: the caller passes PROFILE_COMMIT)
+            commit = None
+    return commit, src_hash
+
+
+# kernels whose dominant loads are 16-B-per-lane (global_load_dwordx4): FETCH_SIZE
+# counts half of those bytes on gfx950 (MI355X_MICROARCH.md, HBM / rocprofv3)
+WIDE_LOAD_KERNELS = ("cg_ed25519_msm", "cg_ecdsa_msm_k1", "cg_ecdsa_msm_r1", "cg_merkle_leaf", "cg_ecdsa_prep_a_k1",
+                     "cg_ecdsa_prep_a_r1")
+
+
 def main():
     if sys.argv[1] == "--augment":
         return augment(sys.argv[2])
     src, tag = sys.argv[1], sys.argv[2]
     grid = int(sys.argv[sys.argv.index("--grid") + 1]) if "--grid" in sys.argv else 1 << 20
+    out_name = sys.argv[sys.argv.index("--out") + 1] if "--out" in sys.argv else "pmc_ed25519.json"
     prof = os.path.join(ROOT, "profiles")
     tr = glob.glob(os.path.join(src, "trace", "**", "*kernel_trace.csv"), recursive=True)
     st = glob.glob(os.path.join(src, "trace", "**", "*kernel_stats.csv"), recursive=True)
@@ -130,25 +165,27 @@ def main():
         if "SQ_INSTS_VALU" in c:
             per_lane = c["SQ_INSTS_VALU"] / waves
             lane_ops = per_lane * grid / avg_s
-            e["valu_instr_per_verify"] = round(per_lane)
+            e["valu_instr_per_unit"] = round(per_lane)
             e["valu_lane_ops_per_s_T"] = round(lane_ops / 1e12, 2)
-            e["frac_of_39.3T_nominal"] = round(lane_ops / 39.3e12, 3)
+            e["frac_of_78.6T_peak"] = round(lane_ops / (PEAK_T * 1e12), 4)
             if "SQ_INSTS_VALU_INT64" in c:
-                e["int64_instr_per_verify"] = round(c["SQ_INSTS_VALU_INT64"] / waves)
+                e["int64_instr_per_unit"] = round(c["SQ_INSTS_VALU_INT64"] / waves)
             if "GRBM_GUI_ACTIVE" in c and d.get("GRBM_GUI_ACTIVE"):
                 clk = c["GRBM_GUI_ACTIVE"] / 8 / d["GRBM_GUI_ACTIVE"]
                 e["effective_clock_GHz"] = round(clk / 1e9, 3)
-                e["frac_of_vop3_peak_at_measured_clock"] = round(
-                    c["SQ_INSTS_VALU"] * 64 / d["SQ_INSTS_VALU"] / (PEAK_LANE_OPS_PER_CLK * clk), 3)
+                e["frac_of_peak_at_measured_clock"] = round(
+                    c["SQ_INSTS_VALU"] * 64 / d["SQ_INSTS_VALU"] / (PEAK_LANE_OPS_PER_CLK * clk), 4)
         if "SQ_ACTIVE_INST_VALU" in c and "SQ_BUSY_CYCLES" in c:
             e["active_valu_per_busy_cycle"] = round(c["SQ_ACTIVE_INST_VALU"] / c["SQ_BUSY_CYCLES"], 3)
         if "SQ_WAIT_ANY" in c and "SQ_WAVE_CYCLES" in c:
             e["wait_any_frac"] = round(c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"], 3)
             e["wait_inst_any_frac"] = round(c.get("SQ_WAIT_INST_ANY", 0) / c["SQ_WAVE_CYCLES"], 3)
         if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
-            b = (c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024
+            fetch = c["FETCH_SIZE"] * (2 if k in WIDE_LOAD_KERNELS else 1)
+            b = (fetch + c["WRITE_SIZE"]) * 1024
+            e["fetch_correction"] = 2 if k in WIDE_LOAD_KERNELS else 1
             e["hbm_bytes_per_launch"] = round(b)
-            e["hbm_bytes_per_verify"] = round(b / grid, 1)
+            e["hbm_bytes_per_unit"] = round(b / grid, 1)
             e["hbm_GBps"] = round(b / avg_s / 1e9, 1)
         if "TCC_HIT_sum" in c:
             e["l2_hit_rate"] = round(c["TCC_HIT_sum"] / max(c["TCC_HIT_sum"] + c["TCC_MISS_sum"], 1), 4)
@@ -157,25 +194,27 @@ def main():
         e.pop("kernel_short")
         e["counters"] = c
         kernels[k] = e
+    commit, src_hash = src_identity()
     summary = {"source": f"rocprofv3 --pmc passes over `python3 bench.py --steps 3` (tools/profile_gpu.sh {tag}); "
                          f"raw CSVs in profiles/{tag}_pmc/",
+               "commit": commit, "src_hash": src_hash,
                "notes": __doc__.split("Conventions")[1].strip().splitlines(),
                "kernels": kernels}
     with open(os.path.join(prof, f"{tag}_pmc_summary.json"), "w") as f:
         json.dump(summary, f, indent=1)
-    msm = kernels.get("cg_ed25519_msm", {})
-    traffic = {"source": f"profiles/{tag}_pmc_summary.json",
-               "ed25519_msm_bytes_per_launch": msm.get("hbm_bytes_per_launch"),
-               "ed25519_msm_valu_instr_per_verify": msm.get("valu_instr_per_verify"),
-               "ed25519_msm_effective_clock_GHz": msm.get("effective_clock_GHz")}
-    for k in ("hash", "points"):
-        e = kernels.get(f"cg_ed25519_{k}", {})
-        traffic[f"ed25519_{k}_bytes_per_launch"] = e.get("hbm_bytes_per_launch")
-        traffic[f"ed25519_{k}_valu_instr_per_verify"] = e.get("valu_instr_per_verify")
-    traffic.update(occupancy_fields(kernels))
-    if "--no-traffic" not in sys.argv:  # pmc_traffic.json feeds bench.py's default (Ed25519) line
-        with open(os.path.join(prof, "pmc_traffic.json"), "w") as f:
-            json.dump(traffic, f, indent=1)
+    # the per-kernel view bench.py joins with its own HIP-event times
+    view = {"source": f"profiles/{tag}_pmc_summary.json", "commit": commit, "src_hash": src_hash,
+            "peak_T": PEAK_T, "kernels": {}}
+    for k, e in kernels.items():
+        if e.get("valu_instr_per_unit", 0) < 500:
+            continue  # staging / bitmap helpers
+        view["kernels"][k] = {key: e.get(key) for key in ("valu_instr_per_unit", "int64_instr_per_unit",
+                                                            "hbm_bytes_per_unit", "effective_clock_GHz",
+                                                            "frac_of_peak_at_measured_clock", "l2_hit_rate")}
+        view["kernels"][k]["occupancy"] = {key: e.get(key) for key in
+                                           ("vgpr", "vgpr_spill", "waves_per_simd_limit", "mean_waves_per_simd")}
+    with open(os.path.join(prof, out_name), "w") as f:
+        json.dump(view, f, indent=1)
     print(json.dumps({k: {kk: vv for kk, vv in v.items() if kk != "counters"} for k, v in kernels.items()},
                      indent=1))
 

@@ -16,8 +16,17 @@ from collections import defaultdict
 
 
 def short(name: str) -> str:
+    """Kernel name without the signature; template instances of the two ECDSA
+    curves (and the two batched-inversion moduli) get a suffix."""
     m = re.search(r"(cg_[a-z0-9_]+|k_[a-z0-9_]+|__amd_rocclr_[A-Za-z]+)", name)
-    return m.group(1) if m else name[:60]
+    base = m.group(1) if m else name[:60]
+    for tag, suf in (("InvN", "_n"), ("InvP", "_p")):
+        if tag in name:
+            base += suf
+    for tag, suf in (("CurveK1", "_k1"), ("CurveR1", "_r1")):
+        if tag in name:
+            base += suf
+    return base
 
 
 def trace(path):
