@@ -28,6 +28,11 @@ MODE_IS_VALID, MODE_DO_VERIFY = 0, 1
 FTX_TRUE, FTX_FALSE, FTX_NO_LEAVES, FTX_MALFORMED = 0, 1, 2, 3
 # CompositeKey fulfilment (cg_composite_eval_batch)
 COMPOSITE_LEAF, COMPOSITE_NODE, COMPOSITE_INVALID = 0, 1, 0x80
+# per-tx codes of cg_tx_verify_batch / cg_tx_verify_signatures_except (>= 0: first bad signature)
+TX_OK, TX_NO_SIGNATURES, TX_NO_COMPONENTS, TX_SIGNATURES_MISSING = -1, -2, -3, -4
+# cg_set_debug options (test hooks)
+DEBUG_FORCE_FULL_LENGTH, DEBUG_FAIL_ALLOC, DEBUG_THROW = 1, 2, 3
+ABI_VERSION = 2
 
 # exported symbols and their prototypes: (restype, argtypes)
 _u8p, _u32p, _u64p, _i32p = POINTER(c_uint8), POINTER(c_uint32), POINTER(c_uint64), POINTER(ctypes.c_int32)
@@ -50,6 +55,10 @@ PROTOTYPES = {
     "cg_tx_verify_batch": (c_int, [c_void_p, c_int, c_size_t, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p,
                                    c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p, c_size_t, c_void_p,
                                    c_void_p, c_void_p, c_void_p]),
+    "cg_tx_verify_signatures_except": (c_int, [c_void_p, c_int, c_size_t, c_void_p, c_size_t, c_void_p, c_void_p,
+                                               c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p,
+                                               c_size_t, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                               c_void_p, c_void_p]),
     "cg_ftx_verify_batch": (c_int, [c_void_p, c_size_t, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_void_p,
                                     c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "cg_composite_eval_batch": (c_int, [c_void_p, c_size_t, c_void_p, c_void_p, c_size_t, c_void_p, c_void_p,
@@ -60,6 +69,7 @@ PROTOTYPES = {
     "cg_set_profiling": (c_int, [c_void_p, c_int]),
     "cg_kernel_stats": (c_int, [c_void_p, c_char_p, POINTER(c_double), POINTER(c_uint64), POINTER(c_uint64)]),
     "cg_reset_stats": (c_int, [c_void_p]),
+    "cg_set_debug": (c_int, [c_void_p, c_int, ctypes.c_int64]),
 }
 
 _lib = None
@@ -96,6 +106,8 @@ def load() -> ctypes.CDLL:
             raise OSError(f"{LIB_PATH} not built: run __graft_entry__.build() or make -C corda_amd/csrc")
         _share_torch_hip_runtime()
         lib = ctypes.CDLL(LIB_PATH)
+        if lib.cg_abi_version() != ABI_VERSION:
+            raise OSError(f"{LIB_PATH}: ABI version {lib.cg_abi_version()}, binding expects {ABI_VERSION} (rebuild)")
         for name, (res, args) in PROTOTYPES.items():
             fn = getattr(lib, name)
             fn.restype = res
@@ -156,6 +168,11 @@ class Context:
 
     def reset_stats(self):
         self.check(self.lib.cg_reset_stats(self.h))
+
+    def set_debug(self, option: int, value: int):
+        """Test hooks (cg_set_debug): forced full-length Ed25519 scalars, injected
+        allocation failures, an injected exception."""
+        self.check(self.lib.cg_set_debug(self.h, option, value))
 
     def register_host(self, *arrays):
         """Page-locks numpy arrays the caller will pass again (cg_register_host)."""

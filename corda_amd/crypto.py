@@ -76,6 +76,25 @@ def _scheme_id(s) -> int:
     return int(s)
 
 
+KEY_BYTES = {ECDSA_SECP256K1_SHA256.scheme_number_id: 64, ECDSA_SECP256R1_SHA256.scheme_number_id: 64,
+             EDDSA_ED25519_SHA512.scheme_number_id: 32}
+
+
+def key_length_ok(scheme_id: int, key) -> bool:
+    """The key bytes must be the scheme's wire form: 32-byte A for Ed25519 (i2p's
+    EdDSAPublicKeySpec refuses any other length, so the key object cannot exist),
+    64-byte X||Y for ECDSA (see corda_amd.keys for X.509 decoding).  Keys are never
+    truncated or zero-padded into that form."""
+    want = KEY_BYTES.get(scheme_id)
+    return want is None or len(bytes(key)) == want
+
+
+def _check_key_length(scheme_id: int, key, index: int | None = None):
+    if not key_length_ok(scheme_id, key):
+        raise InvalidKeyException(f"public key of scheme {scheme_id} must be {KEY_BYTES[scheme_id]} bytes, "
+                                  f"got {len(bytes(key))}", index)
+
+
 @dataclass
 class PackedBatch:
     """Element-major host buffers in the C ABI's layout."""
@@ -90,6 +109,9 @@ class PackedBatch:
     msg: np.ndarray
     msg_off: np.ndarray
     msg_len: np.ndarray
+    # elements whose key bytes are not the scheme's wire form: the key object cannot
+    # be constructed, so their verdict is KEY_INVALID whatever the device computes
+    key_invalid: np.ndarray | None = None
 
 
 def pack(schemes, public_keys: Sequence[bytes], signatures: Sequence[bytes], clear_data: Sequence[bytes]) -> PackedBatch:
@@ -105,8 +127,12 @@ def pack(schemes, public_keys: Sequence[bytes], signatures: Sequence[bytes], cle
         scheme = np.array([_scheme_id(s) for s in schemes], dtype=np.uint8)
     pk_stride = 64
     pk = np.zeros((max(n, 1), pk_stride), dtype=np.uint8)
+    bad_keys = []
     for i, k in enumerate(public_keys):
-        kb = bytes(k)[:pk_stride]
+        kb = bytes(k)
+        if not key_length_ok(int(scheme[i]), kb):
+            bad_keys.append(i)
+            continue  # the row stays zero; the verdict is overridden
         pk[i, :len(kb)] = np.frombuffer(kb, dtype=np.uint8)
     maxlen = max([len(s) for s in signatures] + [64])
     sig_stride = (maxlen + 3) // 4 * 4
@@ -121,7 +147,8 @@ def pack(schemes, public_keys: Sequence[bytes], signatures: Sequence[bytes], cle
     if n:
         msg_off[1:n] = np.cumsum(msg_len[:n - 1], dtype=np.uint64)
     arena = np.frombuffer(b"".join(bytes(m) for m in clear_data) or b"\0", dtype=np.uint8).copy()
-    return PackedBatch(n, scheme, pk, pk_stride, sig, sig_stride, sig_len, arena, msg_off, msg_len)
+    return PackedBatch(n, scheme, pk, pk_stride, sig, sig_stride, sig_len, arena, msg_off, msg_len,
+                       np.array(bad_keys, dtype=np.int64) if bad_keys else None)
 
 
 def verify_packed(ctx: _lib.Context, b: PackedBatch, mode: int, bitmap: bool = False):
@@ -131,13 +158,41 @@ def verify_packed(ctx: _lib.Context, b: PackedBatch, mode: int, bitmap: bool = F
                                       _lib.ptr(b.sig), b.sig_stride, _lib.ptr(b.sig_len), _lib.ptr(b.msg),
                                       len(b.msg), _lib.ptr(b.msg_off), _lib.ptr(b.msg_len), _lib.ptr(verdict),
                                       _lib.ptr(bm)))
+    if b.key_invalid is not None:  # KEY_INVALID outranks every other outcome (JVM order)
+        verdict[b.key_invalid] = KEY_INVALID
+        if bm is not None:
+            bm[b.key_invalid // 32] &= ~(np.uint32(1) << (b.key_invalid % 32).astype(np.uint32))
     return (verdict[:b.n], bm) if bitmap else verdict[:b.n]
 
 
-def is_valid_batch(ctx: _lib.Context, schemes, public_keys, signatures, clear_data) -> np.ndarray:
+# Schemes Crypto supports (Crypto.kt:176-183) that the device does not run: RSA_SHA256 (1),
+# SPHINCS-256_SHA512 (5) and COMPOSITE (6) are verified by the host's own JCA path.
+HOST_SCHEMES = {1: "RSA_SHA256", 5: "SPHINCS-256_SHA512", 6: "COMPOSITE"}
+
+
+def _verify_mixed(ctx, schemes, public_keys, signatures, clear_data, mode, host_verify):
+    """Device batch for schemes 2/3/4; elements of HOST_SCHEMES go to
+    ``host_verify(scheme_id, key, signature, data, mode) -> verdict code`` (on the JVM:
+    Crypto.isValid / doVerify under try/catch) and are merged back in index order, so
+    first-failure-wins still holds.  Without a host_verifier such elements raise
+    IllegalArgumentException — they are not silently reported UNSUPPORTED."""
+    b = pack(schemes, public_keys, signatures, clear_data)
+    host = np.flatnonzero(np.isin(b.scheme[:b.n], list(HOST_SCHEMES)))
+    if host.size and host_verify is None:
+        i = int(host[0])
+        raise IllegalArgumentException(f"scheme {HOST_SCHEMES[int(b.scheme[i])]} is verified on the host JCA path: "
+                                       "pass host_verify", i)
+    v = verify_packed(ctx, b, mode)
+    for i in host:
+        i = int(i)
+        v[i] = host_verify(int(b.scheme[i]), bytes(public_keys[i]), bytes(signatures[i]), bytes(clear_data[i]), mode)
+    return v
+
+
+def is_valid_batch(ctx: _lib.Context, schemes, public_keys, signatures, clear_data, host_verify=None) -> np.ndarray:
     """Per-element verdict codes of ``Crypto.isValid`` (ACCEPT=0 means ``true``,
     REJECT=1 ``false``; 2/3/5 mean isValid would have thrown)."""
-    return verify_packed(ctx, pack(schemes, public_keys, signatures, clear_data), MODE_IS_VALID)
+    return _verify_mixed(ctx, schemes, public_keys, signatures, clear_data, MODE_IS_VALID, host_verify)
 
 
 def raise_for_verdict(code: int, index: int):
@@ -154,10 +209,10 @@ def raise_for_verdict(code: int, index: int):
         raise IllegalArgumentException("Unsupported key/algorithm", index)
 
 
-def do_verify_batch(ctx: _lib.Context, schemes, public_keys, signatures, clear_data) -> bool:
+def do_verify_batch(ctx: _lib.Context, schemes, public_keys, signatures, clear_data, host_verify=None) -> bool:
     """``for i in range(n): Crypto.doVerify(...)``: returns True or raises the
     exception of the lowest failing index."""
-    v = verify_packed(ctx, pack(schemes, public_keys, signatures, clear_data), MODE_DO_VERIFY)
+    v = _verify_mixed(ctx, schemes, public_keys, signatures, clear_data, MODE_DO_VERIFY, host_verify)
     bad = np.flatnonzero(v != ACCEPT)
     if bad.size:
         i = int(bad[0])

@@ -73,11 +73,12 @@ CG_HD void ed25519_abyte(uint32_t ab[8], const uint32_t pk[8]) {
 
 // Hash phase for one signature.  Returns the pre-verdict and fills dig / the
 // digit count and R sign (packed into the status word by the caller).
-// FULL_LENGTH (tests only) forces the (h, 1) fallback of the half-size reduction.
+// FULL_LENGTH / force_full (tests only; force_full per lane through the
+// cg_set_debug hook) force the (h, 1) fallback of the half-size reduction.
 template <bool FULL_LENGTH = false>
 CG_HD uint32_t ed25519_hash_stage(const uint32_t pk[8], const uint32_t sig[16], uint32_t sig_len, const uint8_t* msg,
                                   uint32_t msg_len, uint32_t mode, uint32_t dig[kDigitWords], uint32_t& ndig,
-                                  uint32_t& rneg) {
+                                  uint32_t& rneg, bool force_full = false) {
   ndig = kMinDigits;
   rneg = 0;
   const uint32_t pre = ed25519_precheck_sig(sig_len, msg_len, mode);
@@ -88,7 +89,7 @@ CG_HD uint32_t ed25519_hash_stage(const uint32_t pk[8], const uint32_t sig[16], 
   sc_reduce512(h, hd);
   sc_effective_s(s, sig + 8);
   uint32_t c1neg = 0;
-  if (FULL_LENGTH) {
+  if (FULL_LENGTH || force_full) {
     CG_UNROLL for (int w = 0; w < 8; ++w) {
       c0[w] = h[w];
       c1[w] = w == 0;

@@ -21,6 +21,8 @@ struct Ed25519Dev {
   uint32_t* digits = nullptr;    // [24][scap]
   int32_t* table = nullptr;      // [scap][18][40] lane-contiguous k*(-A), k*R
   const int32_t* btab = nullptr; // [2][kBTabEntries][30] shared k*B, k*2^128 B tables
+  uint32_t full_mod = 0;         // test hook: lanes with (index_base + i) % full_mod == 0 take (c0, c1) = (h, 1)
+  uint32_t index_base = 0;       // index of this chunk's first element in the Ed25519 subset
 };
 
 size_t ed25519_btab_words();

@@ -52,9 +52,37 @@ __global__ __launch_bounds__(256) void cg_composite_eval(const uint32_t* __restr
   out[q] = (uint8_t)((stack[q] >> 31) | all_valid << 1);
 }
 
+// getMissingSignatures - allowedToBeMissing per tx (TransactionWithSignatures.kt:
+// 41-47, 72-77), after checkSignaturesAreValid: status[t] arrives as the first-bad
+// code; only a tx whose signatures all verified (-1) can report missing keys.
+__global__ __launch_bounds__(256) void cg_tx_missing(int32_t* __restrict__ status,
+                                                     const uint32_t* __restrict__ req_start,
+                                                     const uint8_t* __restrict__ fulfilled,
+                                                     const uint8_t* __restrict__ allowed, uint32_t n_tx,
+                                                     uint8_t* __restrict__ missing) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n_tx) return;
+  const int32_t st = status[t];
+  uint32_t any = 0;
+  for (uint32_t r = req_start[t]; r < req_start[t + 1]; ++r) {
+    const uint32_t m = st == -1 && !(fulfilled[r] & 1u) && !(allowed && allowed[r]);
+    missing[r] = (uint8_t)m;
+    any |= m;
+  }
+  if (any) status[t] = -4;  // SignaturesMissingException
+}
+
 }  // namespace
 
 namespace cg {
+
+hipError_t launch_tx_missing(int32_t* status, const uint32_t* req_start, const uint8_t* fulfilled,
+                             const uint8_t* allowed, uint32_t n_tx, uint8_t* missing, hipStream_t s) {
+  if (n_tx == 0) return hipSuccess;
+  hipLaunchKernelGGL(cg_tx_missing, dim3((n_tx + 255) / 256), dim3(256), 0, s, status, req_start, fulfilled, allowed,
+                     n_tx, missing);
+  return hipGetLastError();
+}
 
 hipError_t launch_composite_eval(const uint32_t* prog_start, const int32_t* prog, const uint32_t* sig_start,
                                  const uint8_t* verdicts, uint32_t n, uint32_t* stack, uint8_t* out, hipStream_t s) {

@@ -72,6 +72,12 @@ struct cg_ctx {
   // device block cache: size -> free block; live block -> size
   std::multimap<size_t, void*> free_blocks;
   std::unordered_map<void*, size_t> live_blocks;
+  // test hooks (cg_set_debug): Ed25519 lanes forced onto the full-length (h, 1)
+  // scalar pair when index % debug_full_mod == 0; the debug_fail_alloc-th device
+  // allocation from now fails as out of memory; the next guarded call throws.
+  uint32_t debug_full_mod = 0;
+  int64_t debug_fail_alloc = 0;
+  int debug_throw = 0;
 };
 
 namespace {
@@ -160,8 +166,14 @@ void release_cached(cg_ctx* ctx) {
   ctx->free_blocks.clear();
 }
 
+bool debug_alloc_fails(cg_ctx* ctx) {
+  if (ctx->debug_fail_alloc <= 0) return false;
+  return --ctx->debug_fail_alloc == 0;
+}
+
 cg_status dalloc_bytes(cg_ctx* ctx, void** p, size_t bytes, const char* what) {
   *p = nullptr;
+  if (debug_alloc_fails(ctx)) return fail(ctx, CG_E_OUT_OF_MEMORY, std::string(what) + ": injected allocation failure");
   const size_t want = round_block(bytes ? bytes : 1);
   auto it = ctx->free_blocks.lower_bound(want);
   if (it != ctx->free_blocks.end() && it->first <= 2 * want) {
@@ -327,6 +339,47 @@ cg_status check_inputs(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const ui
   return CG_OK;
 }
 
+// Every extern "C" entry point runs inside CG_API_BEGIN / CG_API_END: a C++
+// exception (std::bad_alloc from a host-side vector or string, or anything else)
+// never unwinds into the caller (a JVM through JNI); it becomes a status code, and
+// the context's streams are drained first so no in-flight kernel still uses a
+// buffer the caller is about to reuse.
+cg_status api_guard_fail(cg_ctx* ctx) noexcept {
+  cg_status st = CG_E_DEVICE;
+  const char* msg = "internal error (exception caught at the C ABI)";
+  try {
+    throw;
+  } catch (const std::bad_alloc&) {
+    st = CG_E_OUT_OF_MEMORY;
+    msg = "host allocation failed";
+  } catch (...) {
+  }
+  if (ctx) {
+    (void)hipSetDevice(ctx->device);
+    for (hipStream_t s : {ctx->stream, ctx->copy_stream, ctx->ec_stream[0], ctx->ec_stream[1]})
+      if (s) (void)hipStreamSynchronize(s);
+    try {
+      ctx->err = msg;
+    } catch (...) {
+    }
+  }
+  return st;
+}
+
+void debug_throw_point(cg_ctx* ctx) {
+  if (ctx && ctx->debug_throw) {
+    ctx->debug_throw = 0;
+    throw std::bad_alloc();
+  }
+}
+
+#define CG_API_BEGIN try {
+#define CG_API_END(ctx_)          \
+  }                               \
+  catch (...) {                   \
+    return api_guard_fail(ctx_);  \
+  }
+
 }  // namespace
 
 extern "C" {
@@ -343,6 +396,7 @@ int cg_device_count(void) {
 }
 
 cg_status cg_open(int device, cg_ctx** out) {
+  CG_API_BEGIN
   if (!out) return CG_E_INVALID_ARGUMENT;
   *out = nullptr;
   int count = 0;
@@ -384,54 +438,65 @@ cg_status cg_open(int device, cg_ctx** out) {
   }
   *out = ctx;
   return CG_OK;
+  CG_API_END(nullptr)
 }
 
 void cg_close(cg_ctx* ctx) {
-  if (!ctx) return;
-  (void)hipSetDevice(ctx->device);
-  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-  if (ctx->copy_stream) (void)hipStreamSynchronize(ctx->copy_stream);
-  for (hipStream_t es : ctx->ec_stream)
-    if (es) (void)hipStreamSynchronize(es);
-  collect_timings(ctx);
-  cg::ecdsa_consts_free(ctx->ec);
-  for (auto& b : ctx->live_blocks) (void)hipFree(b.first);
-  ctx->live_blocks.clear();
-  release_cached(ctx);
-  for (hipEvent_t e : ctx->event_pool) (void)hipEventDestroy(e);
-  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
-  if (ctx->copy_stream) (void)hipStreamDestroy(ctx->copy_stream);
-  for (hipStream_t es : ctx->ec_stream)
-    if (es) (void)hipStreamDestroy(es);
-  for (hipEvent_t e : {ctx->ev_fork, ctx->ev_join[0], ctx->ev_join[1]})
-    if (e) (void)hipEventDestroy(e);
-  delete ctx;
+  try {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->copy_stream) (void)hipStreamSynchronize(ctx->copy_stream);
+    for (hipStream_t es : ctx->ec_stream)
+      if (es) (void)hipStreamSynchronize(es);
+    collect_timings(ctx);
+    cg::ecdsa_consts_free(ctx->ec);
+    for (auto& b : ctx->live_blocks) (void)hipFree(b.first);
+    ctx->live_blocks.clear();
+    release_cached(ctx);
+    for (hipEvent_t e : ctx->event_pool) (void)hipEventDestroy(e);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    if (ctx->copy_stream) (void)hipStreamDestroy(ctx->copy_stream);
+    for (hipStream_t es : ctx->ec_stream)
+      if (es) (void)hipStreamDestroy(es);
+    for (hipEvent_t e : {ctx->ev_fork, ctx->ev_join[0], ctx->ev_join[1]})
+      if (e) (void)hipEventDestroy(e);
+    delete ctx;
+  } catch (...) {
+    // nothing to report from a destructor-like call; never unwind into the caller
+  }
 }
 
 const char* cg_last_error(const cg_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
 
 cg_status cg_register_host(cg_ctx* ctx, void* ptr, size_t bytes) {
+  CG_API_BEGIN
   if (!ctx) return CG_E_INVALID_ARGUMENT;
   if (!ptr || !bytes) return fail(ctx, CG_E_INVALID_ARGUMENT, "null pointer or empty range");
   if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, CG_E_DEVICE, "hipSetDevice");
   CG_TRY(ctx, hipHostRegister(ptr, bytes, hipHostRegisterDefault), "hipHostRegister");
   return CG_OK;
+  CG_API_END(ctx)
 }
 
 cg_status cg_unregister_host(cg_ctx* ctx, void* ptr) {
+  CG_API_BEGIN
   if (!ctx) return CG_E_INVALID_ARGUMENT;
   if (!ptr) return fail(ctx, CG_E_INVALID_ARGUMENT, "null pointer");
   if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, CG_E_DEVICE, "hipSetDevice");
   CG_TRY(ctx, hipHostUnregister(ptr), "hipHostUnregister");
   return CG_OK;
+  CG_API_END(ctx)
 }
 
 cg_status cg_release_cached(cg_ctx* ctx) {
+  CG_API_BEGIN
   if (!ctx) return CG_E_INVALID_ARGUMENT;
   (void)hipSetDevice(ctx->device);
   (void)hipStreamSynchronize(ctx->stream);
   release_cached(ctx);
   return CG_OK;
+  CG_API_END(ctx)
 }
 
 }  // extern "C"
@@ -471,6 +536,7 @@ cg_status create_batch(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const ui
   };
   // host-side partition by scheme
   std::vector<uint32_t> idx[3];  // 0: ed25519, 1: K1, 2: R1
+  debug_throw_point(ctx);
   bool ed_identity = true;
   for (size_t i = 0; i < n; ++i) {
     const uint8_t s = scheme_id ? scheme_id[i] : CG_SCHEME_EDDSA_ED25519_SHA512;
@@ -569,81 +635,113 @@ cg_status create_batch(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const ui
   return CG_OK;
 }
 
+// ECDSA scratch for one curve; on out-of-memory the context's cached blocks are
+// returned to the device and the allocation retried once (as dalloc_bytes does).
+cg_status ecdsa_scratch_retry(cg_ctx* ctx, int scheme, uint32_t n, uint32_t* chunk) {
+  hipError_t e = debug_alloc_fails(ctx) ? hipErrorOutOfMemory : cg::ecdsa_scratch(ctx->ec, scheme, n, chunk);
+  if (e == hipErrorOutOfMemory) {
+    (void)hipGetLastError();
+    for (hipStream_t s : {ctx->stream, ctx->ec_stream[0], ctx->ec_stream[1]}) (void)hipStreamSynchronize(s);
+    release_cached(ctx);
+    e = debug_alloc_fails(ctx) ? hipErrorOutOfMemory : cg::ecdsa_scratch(ctx->ec, scheme, n, chunk);
+  }
+  return e == hipSuccess ? CG_OK : hip_fail(ctx, e, "alloc ecdsa scratch");
+}
+
 // Launches the verify kernels of a staged batch and the accept bitmap; no sync.
+// Every exit — success or error — leaves ctx->stream ordered after the ECDSA
+// streams it forked, so the caller's stream-ordered frees (batch_free, the block
+// cache) can never hand a buffer to new work while an ECDSA kernel still writes it.
 cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode) {
   const size_t n = b->n;
-  cg_status st;
-  // elements of unsupported schemes keep this value
-  CG_TRY(ctx, hipMemsetAsync(b->verdict, CG_UNSUPPORTED, n, ctx->stream), "init verdict");
-  CG_TRY(ctx, hipEventRecord(ctx->ev_fork, ctx->stream), "fork ecdsa");
   bool joins[2] = {false, false};
-  // ECDSA: each curve on its own stream, forked after the verdict init and joined
-  // before the bitmap (the verdict scatters touch disjoint positions); enqueued
-  // first so they overlap the Ed25519 kernels below in mixed batches (config 4:
-  // 14.9 -> 15.3 M tx/s; per-kernel times then include the overlap)
-  for (int c = 0; c < 2; ++c) {
-    if (!b->ec[c].n) continue;
-    const cg::EcdsaBatch& eb = b->ec[c];
-    const char* prep_name = eb.scheme == 2 ? "ecdsa_k1_prep" : "ecdsa_r1_prep";
-    const char* msm_name = eb.scheme == 2 ? "ecdsa_k1_msm" : "ecdsa_r1_msm";
-    hipStream_t es = ctx->ec_stream[c];
-    uint32_t chunk = 0;
-    CG_TRY(ctx, cg::ecdsa_scratch(ctx->ec, eb.scheme, eb.n, &chunk), "alloc ecdsa scratch");
-    CG_TRY(ctx, hipStreamWaitEvent(es, ctx->ev_fork, 0), "fork ecdsa");
-    for (uint32_t base = 0; base < eb.n; base += chunk) {
-      const uint32_t cnt = std::min(chunk, eb.n - base);
-      {
-        Timed t(ctx, prep_name, cnt, es);
-        CG_TRY(ctx, cg::ecdsa_launch_prep(eb, ctx->ec, base, cnt, b->arena, (uint32_t)mode, es), "launch ecdsa prep");
+  cg_status st = CG_OK;
+  auto join = [&]() {
+    for (int c = 0; c < 2; ++c)
+      if (joins[c]) {  // recorded here, after whatever this curve's stream got (all of it, or up to a failure)
+        hipError_t e = hipEventRecord(ctx->ev_join[c], ctx->ec_stream[c]);
+        if (e == hipSuccess) e = hipStreamWaitEvent(ctx->stream, ctx->ev_join[c], 0);
+        if (e != hipSuccess) {  // cannot order the streams: wait on the host instead
+          (void)hipGetLastError();
+          (void)hipStreamSynchronize(ctx->ec_stream[c]);
+          if (st == CG_OK) st = hip_fail(ctx, e, "join ecdsa");
+        }
+        joins[c] = false;
       }
-      {
-        Timed t(ctx, msm_name, cnt, es);
-        CG_TRY(ctx, cg::ecdsa_launch_msm(eb, ctx->ec, base, cnt, b->verdict, es), "launch ecdsa msm");
-      }
-    }
-    CG_TRY(ctx, hipEventRecord(ctx->ev_join[c], es), "join ecdsa");
-    joins[c] = true;
-  }
-  if (b->n_ed) {
-    if ((st = ensure_ed_scratch(ctx, b->n_ed)) != CG_OK) {
-      for (int c = 0; c < 2; ++c)  // keep the caller's stream-ordered frees after the ECDSA work
-        if (joins[c]) (void)hipStreamWaitEvent(ctx->stream, ctx->ev_join[c], 0);
-      return st;
-    }
-    for (uint32_t base = 0; base < b->n_ed; base += ctx->ed_scap) {
-      const uint32_t cnt = std::min(ctx->ed_scap, b->n_ed - base);
-      cg::Ed25519Dev d;
-      d.cap = b->n_ed;
-      d.scap = ctx->ed_scap;
-      d.pk = b->ed_pk + base;
-      d.sig = b->ed_sig + base;
-      d.sig_len = b->ed_sig_len + base;
-      d.arena = b->arena;
-      d.msg_off = b->ed_msg_off + base;
-      d.msg_len = b->ed_msg_len + base;
-      d.status = ctx->ed_status;
-      d.digits = ctx->ed_digits;
-      d.table = ctx->ed_table;
-      d.btab = ctx->btab;
-      {
-        Timed t(ctx, "ed25519_hash", cnt);
-        CG_TRY(ctx, cg::launch_ed25519_hash(d, cnt, (uint32_t)mode, ctx->stream), "launch ed25519_hash");
-      }
-      {
-        Timed t(ctx, "ed25519_points", cnt);
-        CG_TRY(ctx, cg::launch_ed25519_points(d, cnt, ctx->stream), "launch ed25519_points");
-      }
-      {
-        Timed t(ctx, "ed25519_msm", cnt);
-        CG_TRY(ctx,
-               cg::launch_ed25519_msm(d, cnt, b->ed_index ? b->ed_index + base : nullptr,
-                                      b->ed_index ? b->verdict : b->verdict + base, ctx->stream),
-               "launch ed25519_msm");
+  };
+  auto run = [&]() -> cg_status {
+    // elements of unsupported schemes keep this value
+    CG_TRY(ctx, hipMemsetAsync(b->verdict, CG_UNSUPPORTED, n, ctx->stream), "init verdict");
+    CG_TRY(ctx, hipEventRecord(ctx->ev_fork, ctx->stream), "fork ecdsa");
+    // ECDSA: each curve on its own stream, forked after the verdict init and joined
+    // before the bitmap (the verdict scatters touch disjoint positions); enqueued
+    // first so they overlap the Ed25519 kernels below in mixed batches (config 4:
+    // 14.9 -> 15.3 M tx/s; per-kernel times then include the overlap)
+    for (int c = 0; c < 2; ++c) {
+      if (!b->ec[c].n) continue;
+      const cg::EcdsaBatch& eb = b->ec[c];
+      const char* prep_name = eb.scheme == 2 ? "ecdsa_k1_prep" : "ecdsa_r1_prep";
+      const char* msm_name = eb.scheme == 2 ? "ecdsa_k1_msm" : "ecdsa_r1_msm";
+      hipStream_t es = ctx->ec_stream[c];
+      uint32_t chunk = 0;
+      cg_status s2 = ecdsa_scratch_retry(ctx, eb.scheme, eb.n, &chunk);
+      if (s2 != CG_OK) return s2;
+      CG_TRY(ctx, hipStreamWaitEvent(es, ctx->ev_fork, 0), "fork ecdsa");
+      joins[c] = true;  // from here on this curve's stream may hold work: the exit path joins it
+      for (uint32_t base = 0; base < eb.n; base += chunk) {
+        const uint32_t cnt = std::min(chunk, eb.n - base);
+        {
+          Timed t(ctx, prep_name, cnt, es);
+          CG_TRY(ctx, cg::ecdsa_launch_prep(eb, ctx->ec, base, cnt, b->arena, (uint32_t)mode, es), "launch ecdsa prep");
+        }
+        {
+          Timed t(ctx, msm_name, cnt, es);
+          CG_TRY(ctx, cg::ecdsa_launch_msm(eb, ctx->ec, base, cnt, b->verdict, es), "launch ecdsa msm");
+        }
       }
     }
-  }
-  for (int c = 0; c < 2; ++c)
-    if (joins[c]) CG_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_join[c], 0), "join ecdsa");
+    if (b->n_ed) {
+      cg_status s2 = ensure_ed_scratch(ctx, b->n_ed);
+      if (s2 != CG_OK) return s2;
+      for (uint32_t base = 0; base < b->n_ed; base += ctx->ed_scap) {
+        const uint32_t cnt = std::min(ctx->ed_scap, b->n_ed - base);
+        cg::Ed25519Dev d;
+        d.cap = b->n_ed;
+        d.scap = ctx->ed_scap;
+        d.pk = b->ed_pk + base;
+        d.sig = b->ed_sig + base;
+        d.sig_len = b->ed_sig_len + base;
+        d.arena = b->arena;
+        d.msg_off = b->ed_msg_off + base;
+        d.msg_len = b->ed_msg_len + base;
+        d.status = ctx->ed_status;
+        d.digits = ctx->ed_digits;
+        d.table = ctx->ed_table;
+        d.btab = ctx->btab;
+        d.full_mod = ctx->debug_full_mod;
+        d.index_base = base;
+        {
+          Timed t(ctx, "ed25519_hash", cnt);
+          CG_TRY(ctx, cg::launch_ed25519_hash(d, cnt, (uint32_t)mode, ctx->stream), "launch ed25519_hash");
+        }
+        {
+          Timed t(ctx, "ed25519_points", cnt);
+          CG_TRY(ctx, cg::launch_ed25519_points(d, cnt, ctx->stream), "launch ed25519_points");
+        }
+        {
+          Timed t(ctx, "ed25519_msm", cnt);
+          CG_TRY(ctx,
+                 cg::launch_ed25519_msm(d, cnt, b->ed_index ? b->ed_index + base : nullptr,
+                                        b->ed_index ? b->verdict : b->verdict + base, ctx->stream),
+                 "launch ed25519_msm");
+        }
+      }
+    }
+    return CG_OK;
+  };
+  st = run();
+  join();
+  if (st != CG_OK) return st;
   CG_TRY(ctx, cg::launch_verdict_bitmap(b->verdict, (uint32_t)n, b->bitmap, ctx->stream), "launch bitmap");
   return CG_OK;
 }
@@ -655,16 +753,19 @@ extern "C" {
 cg_status cg_batch_create(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const uint8_t* pk, size_t pk_stride,
                           const uint8_t* sig, size_t sig_stride, const uint32_t* sig_len, const uint8_t* msg,
                           size_t msg_bytes, const uint64_t* msg_off, const uint32_t* msg_len, cg_batch** out) {
+  CG_API_BEGIN
   MsgSrc m;
   m.host = msg;
   m.bytes = msg_bytes;
   m.off_host = msg_off;
   m.len_host = msg_len;
   return create_batch(ctx, n, scheme_id, pk, pk_stride, sig, sig_stride, sig_len, m, out);
+  CG_API_END(ctx)
 }
 
 cg_status cg_batch_verify(cg_ctx* ctx, cg_batch* b, int mode, uint8_t* verdict_out, uint32_t* accept_bitmap_out,
                           void* device_bitmap_out) {
+  CG_API_BEGIN
   if (!ctx || !b) return fail(ctx, CG_E_INVALID_ARGUMENT, "null context or batch");
   if (mode != CG_MODE_IS_VALID && mode != CG_MODE_DO_VERIFY) return fail(ctx, CG_E_INVALID_ARGUMENT, "bad mode");
   if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, CG_E_DEVICE, "hipSetDevice");
@@ -684,21 +785,27 @@ cg_status cg_batch_verify(cg_ctx* ctx, cg_batch* b, int mode, uint8_t* verdict_o
   CG_TRY(ctx, hipStreamSynchronize(ctx->stream), "verify sync");
   collect_timings(ctx);
   return CG_OK;
+  CG_API_END(ctx)
 }
 
 size_t cg_batch_size(const cg_batch* b) { return b ? b->n : 0; }
 
 void cg_batch_destroy(cg_ctx* ctx, cg_batch* b) {
-  if (!ctx) return;
-  (void)hipSetDevice(ctx->device);
-  (void)hipStreamSynchronize(ctx->stream);
-  batch_free(ctx, b);
+  try {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    batch_free(ctx, b);
+  } catch (...) {
+    api_guard_fail(ctx);
+  }
 }
 
 cg_status cg_verify_batch(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme_id, const uint8_t* pk,
                           size_t pk_stride, const uint8_t* sig, size_t sig_stride, const uint32_t* sig_len,
                           const uint8_t* msg, size_t msg_bytes, const uint64_t* msg_off, const uint32_t* msg_len,
                           uint8_t* verdict_out, uint32_t* accept_bitmap_out) {
+  CG_API_BEGIN
   if (!ctx) return CG_E_INVALID_ARGUMENT;
   if (n && !verdict_out) return fail(ctx, CG_E_INVALID_ARGUMENT, "null verdict_out");
   if (n == 0) return CG_OK;
@@ -709,10 +816,12 @@ cg_status cg_verify_batch(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
   st = cg_batch_verify(ctx, b, mode, verdict_out, accept_bitmap_out, nullptr);
   cg_batch_destroy(ctx, b);
   return st;
+  CG_API_END(ctx)
 }
 
 cg_status cg_der_parse_batch(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const uint8_t* sig,
                              size_t sig_stride, const uint32_t* sig_len, uint8_t* rs_out, uint8_t* status_out) {
+  CG_API_BEGIN
   if (!ctx) return CG_E_INVALID_ARGUMENT;
   if (n == 0) return CG_OK;
   if (!sig || !rs_out || !status_out) return fail(ctx, CG_E_INVALID_ARGUMENT, "null pointer");
@@ -775,16 +884,20 @@ cg_status cg_der_parse_batch(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, co
   cleanup();
   collect_timings(ctx);
   return CG_OK;
+  CG_API_END(ctx)
 }
 
 cg_status cg_set_profiling(cg_ctx* ctx, int enable) {
+  CG_API_BEGIN
   if (!ctx) return CG_E_INVALID_ARGUMENT;
   collect_timings(ctx);
   ctx->profiling = enable != 0;
   return CG_OK;
+  CG_API_END(ctx)
 }
 
 cg_status cg_kernel_stats(cg_ctx* ctx, const char* kernel, double* total_ms, uint64_t* launches, uint64_t* items) {
+  CG_API_BEGIN
   if (!ctx || !kernel) return CG_E_INVALID_ARGUMENT;
   collect_timings(ctx);
   auto it = ctx->stats.find(kernel);
@@ -793,13 +906,36 @@ cg_status cg_kernel_stats(cg_ctx* ctx, const char* kernel, double* total_ms, uin
   if (launches) *launches = s.launches;
   if (items) *items = s.items;
   return CG_OK;
+  CG_API_END(ctx)
 }
 
 cg_status cg_reset_stats(cg_ctx* ctx) {
+  CG_API_BEGIN
   if (!ctx) return CG_E_INVALID_ARGUMENT;
   collect_timings(ctx);
   ctx->stats.clear();
   return CG_OK;
+  CG_API_END(ctx)
+}
+
+cg_status cg_set_debug(cg_ctx* ctx, int option, int64_t value) {
+  CG_API_BEGIN
+  if (!ctx) return CG_E_INVALID_ARGUMENT;
+  switch (option) {
+    case CG_DEBUG_FORCE_FULL_LENGTH:
+      if (value < 0 || value > 0xffffffffll) return fail(ctx, CG_E_INVALID_ARGUMENT, "bad modulus");
+      ctx->debug_full_mod = (uint32_t)value;
+      return CG_OK;
+    case CG_DEBUG_FAIL_ALLOC:
+      ctx->debug_fail_alloc = value;
+      return CG_OK;
+    case CG_DEBUG_THROW:
+      ctx->debug_throw = value != 0;
+      return CG_OK;
+    default:
+      return fail(ctx, CG_E_INVALID_ARGUMENT, "unknown debug option");
+  }
+  CG_API_END(ctx)
 }
 
 }  // extern "C"
@@ -1000,6 +1136,56 @@ cg_status read_err_flag(cg_ctx* ctx) {
   return CG_OK;
 }
 
+uint32_t composite_scan(size_t n, const uint32_t* prog_start, const int32_t* prog, size_t n_sig, uint8_t* out);
+
+// One cg_tx_verify_batch-style run: ids, every signature's verdict and the
+// per-tx first failing signature, all left in device memory.
+struct TxRun {
+  TxDev d;
+  uint8_t* verdict_d = nullptr;
+  int32_t* fb_d = nullptr;
+  std::vector<hipEvent_t> ev;
+  bool any_empty = false;
+  size_t n_sig = 0;
+  void release(cg_ctx* ctx) {
+    (void)hipStreamSynchronize(ctx->copy_stream);
+    (void)hipStreamSynchronize(ctx->stream);
+    for (hipEvent_t e : ev)
+      if (e) (void)hipEventDestroy(e);
+    ev.clear();
+    dfree(ctx, fb_d);
+    dfree(ctx, verdict_d);
+    fb_d = nullptr;
+    verdict_d = nullptr;
+    d.release(ctx);
+  }
+};
+
+cg_status tx_run(cg_ctx* ctx, int mode, size_t n_tx, const uint8_t* arena, size_t arena_bytes,
+                 const uint64_t* comp_off, const uint32_t* comp_len, const uint32_t* comp_start, const uint8_t* salts,
+                 const uint32_t* sig_start, const uint8_t* scheme_id, const uint8_t* pk, size_t pk_stride,
+                 const uint8_t* sig, size_t sig_stride, const uint32_t* sig_len, TxRun& r) {
+  cg_status st = compute_txids(ctx, n_tx, arena, arena_bytes, comp_off, comp_len, comp_start, salts, sig_start, r.d,
+                               &r.any_empty, /*upload_arena=*/false);
+  if (st != CG_OK) return st;
+  r.n_sig = sig_start[n_tx];
+  if (r.n_sig && (st = dalloc(ctx, &r.verdict_d, r.n_sig, "alloc tx verdicts")) != CG_OK) return st;
+  st = tx_pipeline(ctx, mode, n_tx, arena, arena_bytes, comp_off, comp_len, comp_start, sig_start, scheme_id, pk,
+                   pk_stride, sig, sig_stride, sig_len, r.d, r.verdict_d, r.ev);
+  if (st != CG_OK) return st;
+  if ((st = dalloc(ctx, &r.fb_d, n_tx, "alloc first_bad")) != CG_OK) return st;
+  CG_TRY(ctx, cg::launch_first_bad(r.verdict_d, r.d.sig_start, (uint32_t)n_tx, r.fb_d, ctx->stream), "first_bad");
+  return CG_OK;
+}
+
+// A tx with no component has no id: CG_TX_NO_COMPONENTS (MerkleTreeException).
+cg_status finish_empty_txs(cg_ctx* ctx, size_t n_tx, const uint32_t* comp_start, bool any_empty, int32_t* out) {
+  if (!any_empty) return CG_OK;
+  for (size_t t = 0; t < n_tx; ++t)
+    if (comp_start[t + 1] == comp_start[t]) out[t] = CG_TX_NO_COMPONENTS;
+  return fail(ctx, CG_E_MERKLE_EMPTY, "Cannot calculate Merkle root on empty hash list.");
+}
+
 }  // namespace
 
 extern "C" {
@@ -1007,6 +1193,7 @@ extern "C" {
 cg_status cg_txid_batch(cg_ctx* ctx, size_t n_tx, const uint8_t* arena, size_t arena_bytes,
                         const uint64_t* comp_off, const uint32_t* comp_len, const uint32_t* comp_start,
                         const uint8_t* salts, uint8_t* ids_out) {
+  CG_API_BEGIN
   if (!ctx) return CG_E_INVALID_ARGUMENT;
   if (n_tx == 0) return CG_OK;
   if (!ids_out) return fail(ctx, CG_E_INVALID_ARGUMENT, "null ids_out");
@@ -1026,6 +1213,7 @@ cg_status cg_txid_batch(cg_ctx* ctx, size_t n_tx, const uint8_t* arena, size_t a
   if (st == CG_OK && any_empty)
     return fail(ctx, CG_E_MERKLE_EMPTY, "Cannot calculate Merkle root on empty hash list.");
   return st;
+  CG_API_END(ctx)
 }
 
 cg_status cg_tx_verify_batch(cg_ctx* ctx, int mode, size_t n_tx, const uint8_t* arena, size_t arena_bytes,
@@ -1034,46 +1222,107 @@ cg_status cg_tx_verify_batch(cg_ctx* ctx, int mode, size_t n_tx, const uint8_t* 
                              const uint8_t* pk, size_t pk_stride, const uint8_t* sig, size_t sig_stride,
                              const uint32_t* sig_len, int32_t* first_bad_out, uint8_t* verdict_out,
                              uint8_t* ids_out) {
+  CG_API_BEGIN
   if (!ctx) return CG_E_INVALID_ARGUMENT;
   if (n_tx == 0) return CG_OK;
   if (!sig_start || !first_bad_out) return fail(ctx, CG_E_INVALID_ARGUMENT, "null pointer");
   if (mode != CG_MODE_IS_VALID && mode != CG_MODE_DO_VERIFY) return fail(ctx, CG_E_INVALID_ARGUMENT, "bad mode");
   if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, CG_E_DEVICE, "hipSetDevice");
-  TxDev d;
-  bool any_empty = false;
-  cg_status st = compute_txids(ctx, n_tx, arena, arena_bytes, comp_off, comp_len, comp_start, salts, sig_start, d,
-                               &any_empty, /*upload_arena=*/false);
-  const size_t n_sig = sig_start[n_tx];
-  uint8_t* verdict_d = nullptr;
-  int32_t* fb_d = nullptr;
-  std::vector<hipEvent_t> ev;
-  if (st == CG_OK && n_sig) st = dalloc(ctx, &verdict_d, n_sig, "alloc tx verdicts");
-  if (st == CG_OK) st = tx_pipeline(ctx, mode, n_tx, arena, arena_bytes, comp_off, comp_len, comp_start, sig_start,
-                                    scheme_id, pk, pk_stride, sig, sig_stride, sig_len, d, verdict_d, ev);
-  if (st == CG_OK && (st = dalloc(ctx, &fb_d, n_tx, "alloc first_bad")) == CG_OK) {
-    hipError_t e = cg::launch_first_bad(verdict_d, d.sig_start, (uint32_t)n_tx, fb_d, ctx->stream);
-    if (e == hipSuccess) e = hipMemcpyAsync(first_bad_out, fb_d, 4 * n_tx, hipMemcpyDeviceToHost, ctx->stream);
-    if (e == hipSuccess && verdict_out && verdict_d)
-      e = hipMemcpyAsync(verdict_out, verdict_d, n_sig, hipMemcpyDeviceToHost, ctx->stream);
-    if (e == hipSuccess && ids_out) e = hipMemcpyAsync(ids_out, d.ids, 32 * n_tx, hipMemcpyDeviceToHost, ctx->stream);
+  TxRun r;
+  cg_status st = tx_run(ctx, mode, n_tx, arena, arena_bytes, comp_off, comp_len, comp_start, salts, sig_start,
+                        scheme_id, pk, pk_stride, sig, sig_stride, sig_len, r);
+  if (st == CG_OK) {
+    hipError_t e = hipMemcpyAsync(first_bad_out, r.fb_d, 4 * n_tx, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess && verdict_out && r.verdict_d)
+      e = hipMemcpyAsync(verdict_out, r.verdict_d, r.n_sig, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess && ids_out) e = hipMemcpyAsync(ids_out, r.d.ids, 32 * n_tx, hipMemcpyDeviceToHost, ctx->stream);
     if (e != hipSuccess) st = hip_fail(ctx, e, "first_bad");
   }
   if (st == CG_OK) st = read_err_flag(ctx);
-  (void)hipStreamSynchronize(ctx->copy_stream);
-  (void)hipStreamSynchronize(ctx->stream);
-  for (hipEvent_t e : ev) (void)hipEventDestroy(e);
-  dfree(ctx, fb_d);
-  dfree(ctx, verdict_d);
-  d.release(ctx);
+  r.release(ctx);
   collect_timings(ctx);
   if (st != CG_OK) return st;
-  // a tx with no component has no id: report it as -3 (MerkleTreeException)
-  if (any_empty) {
-    for (size_t t = 0; t < n_tx; ++t)
-      if (comp_start[t + 1] == comp_start[t]) first_bad_out[t] = -3;
-    return fail(ctx, CG_E_MERKLE_EMPTY, "Cannot calculate Merkle root on empty hash list.");
+  return finish_empty_txs(ctx, n_tx, comp_start, r.any_empty, first_bad_out);
+  CG_API_END(ctx)
+}
+
+cg_status cg_tx_verify_signatures_except(cg_ctx* ctx, int mode, size_t n_tx, const uint8_t* arena, size_t arena_bytes,
+                                         const uint64_t* comp_off, const uint32_t* comp_len,
+                                         const uint32_t* comp_start, const uint8_t* salts, const uint32_t* sig_start,
+                                         const uint8_t* scheme_id, const uint8_t* pk, size_t pk_stride,
+                                         const uint8_t* sig, size_t sig_stride, const uint32_t* sig_len,
+                                         const uint32_t* req_start, const uint32_t* prog_start, const int32_t* prog,
+                                         const uint8_t* allowed, int32_t* status_out, uint8_t* missing_out,
+                                         uint8_t* ids_out) {
+  CG_API_BEGIN
+  if (!ctx) return CG_E_INVALID_ARGUMENT;
+  if (n_tx == 0) return CG_OK;
+  if (!sig_start || !status_out || !req_start || !prog_start) return fail(ctx, CG_E_INVALID_ARGUMENT, "null pointer");
+  if (mode != CG_MODE_IS_VALID && mode != CG_MODE_DO_VERIFY) return fail(ctx, CG_E_INVALID_ARGUMENT, "bad mode");
+  for (size_t t = 0; t < n_tx; ++t)
+    if (req_start[t + 1] < req_start[t] || sig_start[t + 1] < sig_start[t])
+      return fail(ctx, CG_E_INVALID_ARGUMENT, "req_start / sig_start not monotone");
+  const size_t n_req = req_start[n_tx];
+  for (size_t q = 0; q < n_req; ++q)
+    if (prog_start[q + 1] < prog_start[q]) return fail(ctx, CG_E_INVALID_ARGUMENT, "prog_start not monotone");
+  if (prog_start[n_req] && !prog) return fail(ctx, CG_E_INVALID_ARGUMENT, "null prog");
+  // host pass: CompositeKey construction rules; leaf signature indices are within the tx
+  std::vector<uint8_t> cstat(n_req ? n_req : 1, 0);
+  uint32_t depth = 1;
+  for (size_t t = 0; t < n_tx; ++t) {
+    const uint32_t r0 = req_start[t], r1 = req_start[t + 1];
+    if (r1 == r0) continue;
+    const uint32_t dd = composite_scan(r1 - r0, prog_start + r0, prog, sig_start[t + 1] - sig_start[t],
+                                       cstat.data() + r0);
+    depth = std::max(depth, dd);
   }
-  return CG_OK;
+  for (size_t q = 0; q < n_req; ++q)
+    if (cstat[q] == cg::kCompositeInvalid)
+      return fail(ctx, CG_E_INVALID_ARGUMENT, "required key " + std::to_string(q) +
+                                                  " violates CompositeKey construction rules");
+  if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, CG_E_DEVICE, "hipSetDevice");
+  TxRun r;
+  cg_status st = tx_run(ctx, mode, n_tx, arena, arena_bytes, comp_off, comp_len, comp_start, salts, sig_start,
+                        scheme_id, pk, pk_stride, sig, sig_stride, sig_len, r);
+  uint32_t *rs_d = nullptr, *ps_d = nullptr, *stack_d = nullptr;
+  int32_t* prog_d = nullptr;
+  uint8_t *allowed_d = nullptr, *ful_d = nullptr, *missing_d = nullptr;
+  if (st == CG_OK && n_req) {
+    if ((st = upload(ctx, &rs_d, req_start, n_tx + 1, "upload req_start")) == CG_OK &&
+        (st = upload(ctx, &ps_d, prog_start, n_req + 1, "upload prog_start")) == CG_OK &&
+        (st = upload(ctx, &prog_d, prog, 4 * (size_t)prog_start[n_req], "upload prog")) == CG_OK &&
+        (st = (allowed ? upload(ctx, &allowed_d, allowed, n_req, "upload allowed") : CG_OK)) == CG_OK &&
+        (st = upload(ctx, &ful_d, cstat.data(), n_req, "upload composite status")) == CG_OK &&
+        (st = dalloc(ctx, &missing_d, n_req, "alloc missing")) == CG_OK &&
+        (st = dalloc(ctx, &stack_d, (size_t)depth * n_req, "alloc composite stack")) == CG_OK) {
+      hipError_t e;
+      {
+        Timed tm(ctx, "composite_eval", n_req);
+        e = cg::launch_composite_eval(ps_d, prog_d, nullptr, nullptr, (uint32_t)n_req, stack_d, ful_d, ctx->stream);
+      }
+      if (e == hipSuccess)
+        e = cg::launch_tx_missing(r.fb_d, rs_d, ful_d, allowed_d, (uint32_t)n_tx, missing_d, ctx->stream);
+      if (e == hipSuccess && missing_out)
+        e = hipMemcpyAsync(missing_out, missing_d, n_req, hipMemcpyDeviceToHost, ctx->stream);
+      if (e != hipSuccess) st = hip_fail(ctx, e, "missing signatures");
+    }
+  } else if (st == CG_OK && missing_out && n_req) {
+    std::memset(missing_out, 0, n_req);
+  }
+  if (st == CG_OK) {
+    hipError_t e = hipMemcpyAsync(status_out, r.fb_d, 4 * n_tx, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess && ids_out) e = hipMemcpyAsync(ids_out, r.d.ids, 32 * n_tx, hipMemcpyDeviceToHost, ctx->stream);
+    if (e != hipSuccess) st = hip_fail(ctx, e, "tx status");
+  }
+  if (st == CG_OK) st = read_err_flag(ctx);
+  r.release(ctx);
+  for (const void* p : {(const void*)rs_d, (const void*)ps_d, (const void*)stack_d, (const void*)prog_d,
+                        (const void*)allowed_d, (const void*)ful_d, (const void*)missing_d})
+    dfree(ctx, p);
+  collect_timings(ctx);
+  if (st != CG_OK) return st;
+  return finish_empty_txs(ctx, n_tx, comp_start, r.any_empty, status_out);
+  CG_API_END(ctx)
 }
 
 }  // extern "C"
@@ -1115,6 +1364,7 @@ cg_status cg_ftx_verify_batch(cg_ctx* ctx, size_t n_ftx, const uint8_t* arena, s
                               const uint64_t* comp_off, const uint32_t* comp_len, const uint32_t* comp_start,
                               const uint8_t* nonces, const uint32_t* node_start, const uint8_t* node_kind,
                               const uint8_t* node_hash, const uint8_t* root_hashes, uint8_t* result_out) {
+  CG_API_BEGIN
   if (!ctx) return CG_E_INVALID_ARGUMENT;
   if (n_ftx == 0) return CG_OK;
   if (n_ftx > 0xFFFFFFF0ull) return fail(ctx, CG_E_INVALID_ARGUMENT, "too many transactions");
@@ -1208,6 +1458,7 @@ cg_status cg_ftx_verify_batch(cg_ctx* ctx, size_t n_ftx, const uint8_t* arena, s
   d.release(ctx);
   collect_timings(ctx);
   return st;
+  CG_API_END(ctx)
 }
 
 }  // extern "C"
@@ -1256,6 +1507,7 @@ extern "C" {
 
 cg_status cg_composite_eval_batch(cg_ctx* ctx, size_t n_q, const uint32_t* prog_start, const int32_t* prog,
                                   size_t n_sig, const uint32_t* sig_start, const uint8_t* verdicts, uint8_t* out) {
+  CG_API_BEGIN
   if (!ctx) return CG_E_INVALID_ARGUMENT;
   if (n_q == 0) return CG_OK;
   if (n_q > 0xFFFFFFF0ull) return fail(ctx, CG_E_INVALID_ARGUMENT, "too many queries");
@@ -1292,6 +1544,7 @@ cg_status cg_composite_eval_batch(cg_ctx* ctx, size_t n_q, const uint32_t* prog_
     dfree(ctx, p);
   collect_timings(ctx);
   return st;
+  CG_API_END(ctx)
 }
 
 }  // extern "C"

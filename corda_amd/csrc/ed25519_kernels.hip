@@ -44,14 +44,16 @@ __global__ __launch_bounds__(256) void cg_ed25519_hash(const uint32_t* __restric
                                                        const uint64_t* __restrict__ msg_off,
                                                        const uint32_t* __restrict__ msg_len, uint32_t n, uint32_t cap,
                                                        uint32_t scap, uint32_t mode, uint32_t* __restrict__ status,
-                                                       uint32_t* __restrict__ digits) {
+                                                       uint32_t* __restrict__ digits, uint32_t full_mod,
+                                                       uint32_t index_base) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint32_t pkw[8], sw[16], dig[kDigitWords], ndig, rneg;
   CG_UNROLL for (int w = 0; w < 8; ++w) pkw[w] = pk[(size_t)w * cap + i];
   CG_UNROLL for (int w = 0; w < 16; ++w) sw[w] = sig[(size_t)w * cap + i];
+  const bool force_full = full_mod != 0 && (index_base + i) % full_mod == 0;  // cg_set_debug test hook
   const uint32_t pre =
-      ed25519_hash_stage(pkw, sw, sig_len[i], arena + msg_off[i], msg_len[i], mode, dig, ndig, rneg);
+      ed25519_hash_stage(pkw, sw, sig_len[i], arena + msg_off[i], msg_len[i], mode, dig, ndig, rneg, force_full);
   status[i] = pre | ndig << 8 | rneg << 16;
   if (pre != V_COMPUTE) return;
   CG_UNROLL for (int w = 0; w < kDigitWords; ++w) digits[(size_t)w * scap + i] = dig[w];
@@ -193,7 +195,7 @@ hipError_t launch_ed25519_btab_build(int32_t* btab, hipStream_t s) {
 hipError_t launch_ed25519_hash(const Ed25519Dev& d, uint32_t n, uint32_t mode, hipStream_t s) {
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(cg_ed25519_hash, dim3((n + 255) / 256), dim3(256), 0, s, d.pk, d.sig, d.sig_len, d.arena,
-                     d.msg_off, d.msg_len, n, d.cap, d.scap, mode, d.status, d.digits);
+                     d.msg_off, d.msg_len, n, d.cap, d.scap, mode, d.status, d.digits, d.full_mod, d.index_base);
   return hipGetLastError();
 }
 

@@ -24,7 +24,7 @@ from typing import Sequence
 import numpy as np
 
 from . import _lib
-from .crypto import IllegalArgumentException, SignatureException, _scheme_id, raise_for_verdict
+from .crypto import IllegalArgumentException, SignatureException, _check_key_length, _scheme_id, raise_for_verdict
 
 
 class MerkleTreeException(Exception):
@@ -71,12 +71,7 @@ def tx_ids(ctx: _lib.Context, txs: Sequence[WireTx]) -> list[bytes]:
     return [bytes(ids[32 * i:32 * i + 32]) for i in range(len(txs))]
 
 
-def check_signatures_batch(ctx: _lib.Context, stxs: Sequence[SignedTx], mode: int = _lib.MODE_DO_VERIFY):
-    """Runs checkSignaturesAreValid for every tx in one device batch.
-    Returns (first_bad[n_tx], verdicts[n_sig], ids): first_bad[t] = -1 when all of
-    tx t's signatures verify, the index of the first failing signature otherwise,
-    -2 for a tx without signatures, -3 for a tx without components."""
-    arena, off, ln, start, salts = _pack_txs([s.wire for s in stxs])
+def _pack_sigs(stxs: Sequence[SignedTx]):
     sig_start = np.zeros(len(stxs) + 1, dtype=np.uint32)
     sig_start[1:] = np.cumsum([len(s.sigs) for s in stxs])
     flat = [x for s in stxs for x in s.sigs]
@@ -86,10 +81,21 @@ def check_signatures_batch(ctx: _lib.Context, stxs: Sequence[SignedTx], mode: in
     sig_stride = (max([len(x[2]) for x in flat] + [64]) + 3) // 4 * 4
     sig = np.zeros((max(n_sig, 1), sig_stride), dtype=np.uint8)
     sig_len = np.zeros(max(n_sig, 1), dtype=np.uint32)
-    for i, (_, k, s) in enumerate(flat):
+    for i, (sch, k, s) in enumerate(flat):
+        _check_key_length(_scheme_id(sch), k)
         pk[i, :len(k)] = np.frombuffer(bytes(k)[:64], dtype=np.uint8)
         sig[i, :len(s)] = np.frombuffer(bytes(s), dtype=np.uint8)
         sig_len[i] = len(s)
+    return sig_start, scheme, pk, sig, sig_stride, sig_len, n_sig
+
+
+def check_signatures_batch(ctx: _lib.Context, stxs: Sequence[SignedTx], mode: int = _lib.MODE_DO_VERIFY):
+    """Runs checkSignaturesAreValid for every tx in one device batch.
+    Returns (first_bad[n_tx], verdicts[n_sig], ids): first_bad[t] = -1 when all of
+    tx t's signatures verify, the index of the first failing signature otherwise,
+    -2 for a tx without signatures, -3 for a tx without components."""
+    arena, off, ln, start, salts = _pack_txs([s.wire for s in stxs])
+    sig_start, scheme, pk, sig, sig_stride, sig_len, n_sig = _pack_sigs(stxs)
     first_bad = np.zeros(max(len(stxs), 1), dtype=np.int32)
     verdict = np.zeros(max(n_sig, 1), dtype=np.uint8)
     ids = np.zeros(max(len(stxs), 1) * 32, dtype=np.uint8)
@@ -100,6 +106,83 @@ def check_signatures_batch(ctx: _lib.Context, stxs: Sequence[SignedTx], mode: in
     if st not in (_lib.CG_OK, _lib.CG_E_MERKLE_EMPTY):
         ctx.check(st)
     return first_bad[:len(stxs)], verdict[:n_sig], [bytes(ids[32 * i:32 * i + 32]) for i in range(len(stxs))]
+
+
+class SignaturesMissingException(Exception):
+    """SignedTransaction.SignaturesMissingException (SignedTransaction.kt): required keys
+    neither fulfilled by the signatures' keys nor allowed to be missing."""
+
+    def __init__(self, missing: list, tx_index: int):
+        super().__init__(f"Missing signatures for {len(missing)} required key(s) on transaction {tx_index}")
+        self.missing, self.tx_index = missing, tx_index
+
+
+def verify_signatures_except_batch(ctx: _lib.Context, stxs: Sequence[SignedTx], required: Sequence[Sequence[object]],
+                                   allowed_to_be_missing: Sequence[Sequence[object]] | None = None,
+                                   mode: int = _lib.MODE_DO_VERIFY):
+    """``stx.verifySignaturesExcept(*allowed)`` for every tx in ONE device call
+    (cg_tx_verify_signatures_except; TransactionWithSignatures.kt:41-47): ids
+    recomputed, every signature verified, then getMissingSignatures (:72-77) — each of
+    the tx's ``requiredSigningKeys`` (plain key bytes or a composite.CompositeKey)
+    evaluated with isFulfilledBy against the tx's signature keys, minus the allowed
+    keys — with the verdicts kept on the device.
+
+    Returns (status[n_tx], missing): status per tx as the _lib.TX_* codes (>= 0 = first
+    failing signature); missing[t] = the required keys of tx t in the exception's set."""
+    from .composite import _ident, _program
+    arena, off, ln, start, salts = _pack_txs([s.wire for s in stxs])
+    sig_start, scheme, pk, sig, sig_stride, sig_len, n_sig = _pack_sigs(stxs)
+    allowed_to_be_missing = allowed_to_be_missing or [[] for _ in stxs]
+    prog, prog_start, req_start, allowed = [], [0], [0], []
+    for t, s in enumerate(stxs):
+        index = {}
+        for i, (_, k, _sig) in enumerate(s.sigs):
+            index.setdefault(bytes(k), i)  # sigKeys = sigs.map { it.by }.toSet(): leaf -> a signature by it
+        ok = {_ident(a) for a in allowed_to_be_missing[t]}
+        for key in required[t]:
+            _program(key, index, prog)
+            prog_start.append(len(prog))
+            allowed.append(1 if _ident(key) in ok else 0)
+        req_start.append(len(prog_start) - 1)
+    n_tx, n_req = len(stxs), len(allowed)
+    status = np.zeros(max(n_tx, 1), dtype=np.int32)
+    missing = np.zeros(max(n_req, 1), dtype=np.uint8)
+    p = np.array(prog or [(0, 0, 0, 0)], dtype=np.int32)
+    ps, rs = np.array(prog_start, dtype=np.uint32), np.array(req_start, dtype=np.uint32)
+    al = np.array(allowed or [0], dtype=np.uint8)
+    st = ctx.lib.cg_tx_verify_signatures_except(
+        ctx.h, mode, n_tx, _lib.ptr(arena), len(arena), _lib.ptr(off), _lib.ptr(ln), _lib.ptr(start), _lib.ptr(salts),
+        _lib.ptr(sig_start), _lib.ptr(scheme), _lib.ptr(pk), 64, _lib.ptr(sig), sig_stride, _lib.ptr(sig_len),
+        _lib.ptr(rs), _lib.ptr(ps), _lib.ptr(p), _lib.ptr(al), _lib.ptr(status), _lib.ptr(missing), None)
+    if st == _lib.CG_E_INVALID_ARGUMENT:
+        raise IllegalArgumentException((ctx.lib.cg_last_error(ctx.h) or b"").decode())
+    if st not in (_lib.CG_OK, _lib.CG_E_MERKLE_EMPTY):
+        ctx.check(st)
+    miss = [[required[t][r - req_start[t]] for r in range(req_start[t], req_start[t + 1]) if missing[r]]
+            for t in range(n_tx)]
+    return status[:n_tx], miss
+
+
+def verify_signatures_except(ctx: _lib.Context, stxs: Sequence[SignedTx], required: Sequence[Sequence[object]],
+                             allowed_to_be_missing: Sequence[Sequence[object]] | None = None) -> None:
+    """Loop of ``stx.verifySignaturesExcept(*allowed)``: raises what the first failing
+    tx would raise (SignatureException & co. for its first bad signature, else
+    SignaturesMissingException)."""
+    status, miss = verify_signatures_except_batch(ctx, stxs, required, allowed_to_be_missing)
+    first_bad, verdict, _ = None, None, None
+    for t, st in enumerate(status):
+        st = int(st)
+        if st == _lib.TX_OK:
+            continue
+        if st == _lib.TX_NO_COMPONENTS:
+            raise MerkleTreeException("Cannot calculate Merkle root on empty hash list.")
+        if st == _lib.TX_NO_SIGNATURES:
+            raise IllegalArgumentException("Tried to instantiate a SignedTransaction without any signatures ", t)
+        if st == _lib.TX_SIGNATURES_MISSING:
+            raise SignaturesMissingException(miss[t], t)
+        if first_bad is None:  # the failing signature's verdict code decides the exception class
+            first_bad, verdict, _ = check_signatures_batch(ctx, [stxs[t]])
+        raise_for_verdict(int(verdict[st]), st)
 
 
 def check_signatures_are_valid(ctx: _lib.Context, stxs: Sequence[SignedTx]) -> None:

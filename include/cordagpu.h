@@ -40,6 +40,10 @@
  *       the given nonces, MerkleTransaction.kt:23-27,153) and
  *       core/.../crypto/PartialMerkleTree.kt:130-155 (root of the partial tree, multiset
  *       of included leaves == filtered component hashes).
+ *   cg_tx_verify_signatures_except
+ *       SignedTransaction.verifySignaturesExcept / verifyRequiredSignatures in one call:
+ *       TransactionWithSignatures.kt:26,41-47 = checkSignaturesAreValid (:58-62) then
+ *       getMissingSignatures (:72-77) minus allowedToBeMissing, verdicts kept on the device.
  *   cg_composite_eval_batch
  *       PublicKey.isFulfilledBy / CompositeKey.isFulfilledBy over the signers of a
  *       batch (core/.../crypto/CryptoUtils.kt:78-82, composite/CompositeKey.kt:186-209),
@@ -69,7 +73,7 @@
 extern "C" {
 #endif
 
-#define CG_ABI_VERSION 1
+#define CG_ABI_VERSION 2
 
 typedef int32_t cg_status;
 enum {
@@ -175,17 +179,53 @@ cg_status cg_txid_batch(cg_ctx* ctx, size_t n_tx, const uint8_t* arena, size_t a
  * verify each tx's signatures over its 32-byte id.  Signatures of tx t are
  * sig_start[t] .. sig_start[t+1]-1 (n_tx + 1 entries) in the tx's `sigs` order; the
  * per-signature inputs are laid out as for cg_verify_batch (msg is implied = id).
- * first_bad_out (n_tx): -1 when every signature of the tx verifies, else the index
- * (within the tx) of the first failing one — the signature checkSignaturesAreValid
- * would throw on.  verdict_out (optional, total sigs): per-signature verdicts.
- * ids_out (optional): 32 bytes per tx.
+ * first_bad_out (n_tx), per tx:
+ *   -1  every signature verifies (the ONLY success value; test `== CG_TX_OK`, never `< 0`)
+ *   >=0 the index (within the tx) of the first failing signature — the one
+ *       checkSignaturesAreValid would throw SignatureException on
+ *   -2  the tx has no signatures: SignedTransaction's constructor throws
+ *       IllegalArgumentException (SignedTransaction.kt:39-41)
+ *   -3  the tx has no components: its id cannot be computed (MerkleTreeException,
+ *       MerkleTree.kt:29-30); the call then also returns CG_E_MERKLE_EMPTY
+ * verdict_out (optional, total sigs): per-signature verdicts.  ids_out (optional):
+ * 32 bytes per tx.
  */
+enum { CG_TX_OK = -1, CG_TX_NO_SIGNATURES = -2, CG_TX_NO_COMPONENTS = -3, CG_TX_SIGNATURES_MISSING = -4 };
 cg_status cg_tx_verify_batch(cg_ctx* ctx, int mode, size_t n_tx, const uint8_t* arena, size_t arena_bytes,
                              const uint64_t* comp_off, const uint32_t* comp_len, const uint32_t* comp_start,
                              const uint8_t* salts, const uint32_t* sig_start, const uint8_t* scheme_id,
                              const uint8_t* pk, size_t pk_stride, const uint8_t* sig, size_t sig_stride,
                              const uint32_t* sig_len, int32_t* first_bad_out, uint8_t* verdict_out,
                              uint8_t* ids_out);
+
+/*
+ * Fused signature phase of SignedTransaction.verify / verifySignaturesExcept
+ * (TransactionWithSignatures.kt:41-47): every tx id recomputed and every signature
+ * verified as cg_tx_verify_batch does, then — with the verdicts still in device
+ * memory — getMissingSignatures (:72-77): each required signing key of the tx
+ * (requiredSigningKeys, plain or composite) evaluated with isFulfilledBy against the
+ * keys of the tx's signatures, minus allowedToBeMissing.
+ * Required keys of tx t: req_start[t] .. req_start[t+1]-1 (n_tx + 1 entries); key r is
+ * a post-order op program prog[prog_start[r] .. prog_start[r+1]) in the format of
+ * cg_composite_eval_batch, whose leaf `sig` field is the index WITHIN THE TX of a
+ * signature by that leaf key (or -1); allowed[r] != 0 marks keys passed in
+ * allowedToBeMissing.  status_out (n_tx) per tx, in the JVM's order:
+ *   CG_TX_OK, >= 0, CG_TX_NO_SIGNATURES, CG_TX_NO_COMPONENTS  as cg_tx_verify_batch
+ *   CG_TX_SIGNATURES_MISSING  all signatures valid but some required key neither
+ *                             fulfilled nor allowed: SignaturesMissingException
+ * missing_out (optional, req_start[n_tx] bytes): 1 for every required key in the
+ * exception's `missing` set (only for txs whose status is CG_TX_SIGNATURES_MISSING).
+ * A required-key program violating CompositeKey's construction rules returns
+ * CG_E_INVALID_ARGUMENT.
+ */
+cg_status cg_tx_verify_signatures_except(cg_ctx* ctx, int mode, size_t n_tx, const uint8_t* arena, size_t arena_bytes,
+                                         const uint64_t* comp_off, const uint32_t* comp_len,
+                                         const uint32_t* comp_start, const uint8_t* salts, const uint32_t* sig_start,
+                                         const uint8_t* scheme_id, const uint8_t* pk, size_t pk_stride,
+                                         const uint8_t* sig, size_t sig_stride, const uint32_t* sig_len,
+                                         const uint32_t* req_start, const uint32_t* prog_start, const int32_t* prog,
+                                         const uint8_t* allowed, int32_t* status_out, uint8_t* missing_out,
+                                         uint8_t* ids_out);
 
 /*
  * FilteredTransaction batch (non-validating notary).  n_ftx filtered transactions.
@@ -246,6 +286,21 @@ cg_status cg_set_profiling(cg_ctx* ctx, int enable);
 cg_status cg_kernel_stats(cg_ctx* ctx, const char* kernel, double* total_ms, uint64_t* launches,
                           uint64_t* items);
 cg_status cg_reset_stats(cg_ctx* ctx);
+
+/*
+ * Test hooks (not needed by callers; parity and fault-injection tests use them).
+ *   CG_DEBUG_FORCE_FULL_LENGTH  value m > 0: Ed25519 elements whose index in the
+ *       batch's Ed25519 subset is a multiple of m take the full-length scalar pair
+ *       (c0, c1) = (h, 1) instead of the half-size reduction (the fallback the
+ *       reduction takes when its quotient overflows); 0 turns it off.  Verdicts must
+ *       not change.
+ *   CG_DEBUG_FAIL_ALLOC  value k > 0: the k-th device allocation from now fails as
+ *       out of memory (CG_E_OUT_OF_MEMORY must come back, nothing may crash).
+ *   CG_DEBUG_THROW  value 1: the next batch staging throws std::bad_alloc inside the
+ *       library (it must come back as CG_E_OUT_OF_MEMORY, not unwind).
+ */
+enum { CG_DEBUG_FORCE_FULL_LENGTH = 1, CG_DEBUG_FAIL_ALLOC = 2, CG_DEBUG_THROW = 3 };
+cg_status cg_set_debug(cg_ctx* ctx, int option, int64_t value);
 
 #ifdef __cplusplus
 }

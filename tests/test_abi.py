@@ -43,7 +43,7 @@ def test_python_binding_covers_header():
 def test_abi_version_and_no_fallback_without_gpu():
     from corda_amd import _lib
     lib = _lib.load()
-    assert lib.cg_abi_version() == 1
+    assert lib.cg_abi_version() == _lib.ABI_VERSION == 2
     if lib.cg_device_count() > 0:
         pytest.skip("a GPU is present")
     h = ctypes.c_void_p()
@@ -79,3 +79,24 @@ def test_single_hip_runtime_per_process():
     assert out.returncode == 0, out.stderr
     libs = eval(out.stdout.strip().splitlines()[-1])
     assert len(libs) == 1, libs
+
+
+def _native(name):
+    path = os.path.join(ROOT, "tests", "native", name)
+    if not os.path.exists(path):
+        pytest.skip(f"{name} not built (__graft_entry__.build())")
+    return path
+
+
+def test_c_program_error_paths_without_device():
+    """A plain C99 caller linked through include/cordagpu.h: null contexts and the
+    missing device come back as statuses (tests/native/abi_errors.c)."""
+    out = subprocess.run([_native("abi_errors.bin"), "cpu"], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stdout + out.stderr
+
+
+def test_jni_glue_compiles_and_runs_against_stub_env():
+    """integration/jvm/cordagpu_jni.c compiled against the stub jni.h and driven by a
+    fake JNIEnv (tests/native/jni_harness.c): handles, statuses, error strings."""
+    out = subprocess.run([_native("jni_harness.bin"), "cpu"], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stdout + out.stderr

@@ -42,3 +42,21 @@ def test_mixed_scheme_pack():
     b = crypto.pack([2, 3, 4], [b"\0" * 64] * 3, [b"\x30\x06\x02\x01\x01\x02\x01\x01", b"", b"\0" * 64], [b"a"] * 3)
     assert list(b.scheme) == [2, 3, 4]
     assert np.array_equal(b.sig_len, [8, 0, 64])
+
+
+def test_wrong_length_keys_are_key_invalid_not_truncated():
+    """A 31/33-byte Ed25519 key or a 65-byte ECDSA key cannot be a key object: its
+    verdict is KEY_INVALID (never verified as a truncated / zero-padded key)."""
+    b = crypto.pack([4, 4, 4, 3], [b"\1" * 31, b"\1" * 33, b"\1" * 32, b"\2" * 65], [b"\3" * 64] * 4, [b"m"] * 4)
+    assert list(b.key_invalid) == [0, 1, 3]
+    assert not b.pk[0].any() and not b.pk[1].any() and not b.pk[3].any()
+    assert crypto.key_length_ok(4, b"x" * 32) and not crypto.key_length_ok(2, b"x" * 32)
+
+
+def test_host_schemes_need_a_host_verifier():
+    """RSA / SPHINCS / COMPOSITE (Crypto.kt:176-183) are supported by the reference
+    through JCA: the batch routes them to the caller's host verifier instead of
+    reporting them UNSUPPORTED, and refuses to guess without one."""
+    with pytest.raises(crypto.IllegalArgumentException) as ei:
+        crypto._verify_mixed(None, [4, 1], [b"\1" * 32, b"k"], [b"s" * 64, b"s"], [b"m", b"m"], 0, None)
+    assert ei.value.index == 1

@@ -117,13 +117,7 @@ def test_null_sig_len_stride_64_vs_oracle(gpu_ctx, oracle, tx_chunks):
 
 def test_python_mirror_raises_like_check_signatures_are_valid(gpu_ctx):
     w = datagen.make_tx_batch(50, seed=3, tamper_frac=0.0)
-    stxs = []
-    for t in range(w.n_tx):
-        comps = [w.arena[int(w.comp_off[c]):int(w.comp_off[c]) + int(w.comp_len[c])].tobytes()
-                 for c in range(int(w.comp_start[t]), int(w.comp_start[t + 1]))]
-        sigs = [(int(w.scheme[s]), w.pk[s].tobytes(), w.sig[s, :w.sig_len[s]].tobytes())
-                for s in range(int(w.sig_start[t]), int(w.sig_start[t + 1]))]
-        stxs.append(T.SignedTx(T.WireTx(comps, w.salts[32 * t:32 * t + 32].tobytes()), sigs))
+    stxs = _stxs_from(w)
     T.check_signatures_are_valid(gpu_ctx, stxs)  # all valid: no exception
     ids = T.tx_ids(gpu_ctx, [s.wire for s in stxs])
     assert b"".join(ids) == w.ids.tobytes()
@@ -228,3 +222,112 @@ def test_ftx_notary_shapes_vs_oracle(gpu_ctx, oracle):
     oracle.oracle_ftx_verify_batch(*(x.ctypes.data for x in a), w.n, exp.ctypes.data)
     assert np.array_equal(exp, w.expected)
     assert np.array_equal(got, exp)
+
+
+def _stxs_from(w):
+    stxs = []
+    for t in range(w.n_tx):
+        comps = [w.arena[int(w.comp_off[c]):int(w.comp_off[c]) + int(w.comp_len[c])].tobytes()
+                 for c in range(int(w.comp_start[t]), int(w.comp_start[t + 1]))]
+        sigs = [(int(w.scheme[s]), w.pk[s].tobytes()[:32 if w.scheme[s] == 4 else 64],
+                 w.sig[s, :w.sig_len[s]].tobytes()) for s in range(int(w.sig_start[t]), int(w.sig_start[t + 1]))]
+        stxs.append(T.SignedTx(T.WireTx(comps, w.salts[32 * t:32 * t + 32].tobytes()), sigs))
+    return stxs
+
+
+def test_verify_signatures_except_vs_oracle_loop(gpu_ctx, oracle):
+    """cg_tx_verify_signatures_except (one device call) against a sequential
+    verifySignaturesExcept loop (TransactionWithSignatures.kt:41-47,72-77) driven by
+    the oracle's ids + verdicts and the Python isFulfilledBy: required keys plain,
+    composite (fulfilled / not, nested), keys allowed to be missing, bad signatures
+    (which win over missing keys), tampered txs."""
+    import composite as OC  # oracle/py (test infrastructure)
+    from corda_amd import composite as C
+    w = datagen.make_tx_batch(4000, seed=31, tamper_frac=0.02)
+    rng = np.random.default_rng(5)
+    for t in rng.choice(np.flatnonzero(~w.tampered), size=60, replace=False):
+        s = int(rng.integers(w.sig_start[t], w.sig_start[t + 1]))
+        w.sig[s, 5] ^= 0x10
+    stxs = _stxs_from(w)
+    others = [bytes(rng.integers(0, 256, 32, dtype=np.uint8)) for _ in range(8)]
+
+    def both(th, kids):  # the same tree for the device mirror and the oracle
+        return (C.CompositeKey(th, [(k[0], wt) for k, wt in kids]),
+                OC.CompositeKey(th, [(k[1], wt) for k, wt in kids]))
+
+    required, required_o, allowed = [], [], []
+    for t, s in enumerate(stxs):
+        keys = list(dict.fromkeys(k for _, k, _ in s.sigs))
+        x, y = others[t % 8], others[(t + 3) % 8]
+        r = [(k, k) for k in keys]
+        al = []
+        kind = t % 7
+        if kind == 1:
+            r.append((x, x))
+        elif kind == 2:
+            r.append((x, x)); al.append(x)
+        elif kind == 3:
+            r.append(both(1, [((keys[0], keys[0]), 1), ((x, x), 1)]))
+        elif kind == 4:
+            r.append(both(2, [((keys[0], keys[0]), 1), ((x, x), 1)]))
+        elif kind == 5:
+            inner = both(1, [((x, x), 1), ((keys[-1], keys[-1]), 1)]) if keys[-1] != keys[0] else ((y, y))
+            r.append(both(3, [((keys[0], keys[0]), 2), (inner, 1)]))
+        elif kind == 6:
+            ck = both(2, [((x, x), 1), ((y, y), 1)])
+            r.append(ck); al.append(ck[0])
+        required.append([a for a, _ in r])
+        required_o.append([b for _, b in r])
+        allowed.append(al)
+    status, missing = T.verify_signatures_except_batch(gpu_ctx, stxs, required, allowed)
+
+    exp_ids = oracle_ids(oracle, w)
+    n_sig = int(w.sig_start[-1])
+    msg_off = np.repeat(np.arange(w.n_tx, dtype=np.uint64) * 32, np.diff(w.sig_start))
+    sw = datagen.Workload(n_sig, w.scheme, w.pk, 64, w.sig, 72, w.sig_len, exp_ids, msg_off,
+                          np.full(n_sig, 32, np.uint32))
+    exp_v = oracle_verdicts(oracle, sw, MODE_DO_VERIFY)
+    n_missing = 0
+    for t, s in enumerate(stxs):
+        a, b = int(w.sig_start[t]), int(w.sig_start[t + 1])
+        bad = [i - a for i in range(a, b) if exp_v[i] != ACCEPT]
+        if bad:  # checkSignaturesAreValid throws first
+            assert status[t] == bad[0], t
+            continue
+        sig_keys = {k for _, k, _ in s.sigs}
+        allowed_ids = {C._ident(k) for k in allowed[t]}
+        exp_missing = [required[t][j] for j, ko in enumerate(required_o[t])
+                       if not OC.is_fulfilled_by(ko, sig_keys) and C._ident(required[t][j]) not in allowed_ids]
+        if exp_missing:
+            n_missing += 1
+            assert status[t] == -4, t
+            assert [C._ident(k) for k in missing[t]] == [C._ident(k) for k in exp_missing], t
+        else:
+            assert status[t] == -1, t
+            assert missing[t] == []
+    assert n_missing > 500 and (status >= 0).sum() > 100
+
+    # the mirror raises like the loop: first failing tx, its exception
+    first = next(t for t in range(w.n_tx) if status[t] != -1)
+    exc = T.SignaturesMissingException if status[first] == -4 else T.SignatureException
+    with pytest.raises(exc):
+        T.verify_signatures_except(gpu_ctx, stxs, required, allowed)
+
+
+def test_verify_signatures_except_invalid_composite(gpu_ctx):
+    """A required-key program that breaks CompositeKey's construction rules is an
+    argument error of the whole call (no such key object can exist)."""
+    w = datagen.make_tx_batch(4, seed=2, tamper_frac=0.0)
+    stxs = _stxs_from(w)
+    lib, ctx = gpu_ctx.lib, gpu_ctx
+    arena, off, ln, start, salts = T._pack_txs([s.wire for s in stxs])
+    sig_start, scheme, pk, sig, sig_stride, sig_len, _ = T._pack_sigs(stxs)
+    req_start = np.array([0, 1, 1, 1, 1], np.uint32)
+    prog = np.array([[0, 0, 1, 0], [0, -1, 1, 0], [1, 2, 1, 3]], np.int32)  # threshold 3 > total weight 2
+    prog_start = np.array([0, 3], np.uint32)
+    status = np.zeros(4, np.int32)
+    st = lib.cg_tx_verify_signatures_except(ctx.h, MODE_DO_VERIFY, 4, ptr(arena), len(arena), ptr(off), ptr(ln),
+                                            ptr(start), ptr(salts), ptr(sig_start), ptr(scheme), ptr(pk), 64,
+                                            ptr(sig), sig_stride, ptr(sig_len), ptr(req_start), ptr(prog_start),
+                                            ptr(prog), None, ptr(status), None, None)
+    assert st == -1  # CG_E_INVALID_ARGUMENT

@@ -87,7 +87,33 @@ OP32(sub_u32, "v_sub_u32 %0, %0, %1")
 OP32(lshlrev_b32, "v_lshlrev_b32 %0, 3, %0")
 OP32(ashrrev_i32, "v_ashrrev_i32 %0, 3, %0")
 OP32(mul_i32_i24, "v_mul_i32_i24 %0, %0, %1")
+OP32(lshrrev_b32, "v_lshrrev_b32 %0, 3, %0")
+OP32(and_b32, "v_and_b32 %0, %0, %1")
+OP32(or_b32, "v_or_b32 %0, %0, %1")
+OP32(add_const, "v_add_u32 %0, 64, %0")
+OP32(add_self, "v_add_u32 %0, %0, %0")
+OP32(subrev_u32, "v_subrev_u32 %0, %0, %1")
+OP32(max_i32, "v_max_i32 %0, %0, %1")
+OP32(min_u32, "v_min_u32 %0, %0, %1")
+OP32(bfe_i32, "v_bfe_i32 %0, %0, 0, 26")
+OP32(mov_b32, "v_mov_b32 %0, %1")
+OP32(not_b32, "v_not_b32 %0, %0")
+OP32(mad_i32_i24, "v_mad_i32_i24 %0, %0, %1, %1")
+OP32(mul_lo_c19, "v_mul_lo_u32 %0, %0, 19")
+OP32(mul_u32_u24_c, "v_mul_u32_u24 %0, 19, %0")
+OP32(add_f32, "v_add_f32 %0, %0, %1")
+OP32(fma_f32, "v_fma_f32 %0, %0, %1, %1")
+OP32(sub_co_u32, "v_sub_co_u32 %0, vcc, %0, %1")
+OP32(ashrrev_e64, "v_ashrrev_i32_e64 %0, 3, %0")
+OP32(add_e64, "v_add_u32_e64 %0, %0, %1")
+OP32(lshl_or, "v_lshl_or_b32 %0, %0, 3, %1")
+OP32(xad, "v_xad_u32 %0, %0, %1, %1")
+OP32(bitop3, "v_bitop3_b32 %0, %0, %1, %1 bitop3:0x96")
+OP32(bcnt, "v_bcnt_u32_b32 %0, %0, %1")
 OP64(mad_u64_u32, "v_mad_u64_u32 %0, vcc, %1, %1, %0", unsigned long long)
+OP64(lshrrev_b64, "v_lshrrev_b64 %0, 3, %0", unsigned long long)
+OP64(pk_add_f32, "v_pk_add_f32 %0, %0, %0", unsigned long long)
+OP64(pk_fma_f32, "v_pk_fma_f32 %0, %0, %0, %0", unsigned long long)
 OP64(mad_i64_i32, "v_mad_i64_i32 %0, vcc, %1, %1, %0", unsigned long long)
 OP64(lshl_add_u64, "v_lshl_add_u64 %0, %0, 0, %0", unsigned long long)
 OP64(ashr_i64, "v_ashrrev_i64 %0, 3, %0", unsigned long long)
@@ -105,7 +131,10 @@ int main() {
                  E(mul_lo_u32), E(mul_hi_u32), E(mul_u32_u24), E(mul_hi_u32_u24), E(mad_u32_u24),
                  E(mad_u32_u16), E(pk_mad_u16), E(dot2_u32_u16), E(dot4_u32_u8), E(add_co_u32),
                  E(addc_co_u32), E(mul_f32), E(cndmask), E(cndmask_s), E(bfi_b32), E(perm_b32), E(xor_b32), E(and_or), E(sub_u32), E(lshlrev_b32), E(ashrrev_i32), E(mul_i32_i24), E(mad_u64_u32), E(mad_i64_i32), E(lshl_add_u64), E(ashr_i64), E(mov_b64), E(lshlrev_b64), E(add_f64),
-                 E(fma_f64), E(mul_f64)};
+                 E(fma_f64), E(mul_f64), E(lshrrev_b32), E(and_b32), E(or_b32), E(add_const), E(add_self),
+                 E(subrev_u32), E(max_i32), E(min_u32), E(bfe_i32), E(mov_b32), E(not_b32), E(mad_i32_i24),
+                 E(mul_lo_c19), E(mul_u32_u24_c), E(add_f32), E(fma_f32), E(sub_co_u32), E(ashrrev_e64), E(add_e64),
+                 E(lshl_or), E(xad), E(bitop3), E(bcnt), E(lshrrev_b64), E(pk_add_f32), E(pk_fma_f32)};
   hipDeviceProp_t prop;
   CHK(hipGetDeviceProperties(&prop, 0));
   const int cus = prop.multiProcessorCount;
