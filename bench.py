@@ -834,38 +834,36 @@ def run_backlog(args, dist):
                            threads=cpu_threads(), key_reuse=args.key_reuse)
     t_gen = time.perf_counter() - t_gen
     ctx = Context(dist.local_rank)
-    batches, sizes, adv_ok = [], [], True
+    adv_ok = [True]
     t_stage = time.perf_counter()
-    for c0 in range(0, n, chunk):
-        m = min(chunk, n - c0)
-        w = p.tiled(m)
-        if args.adversarial > 0:
-            w = datagen.add_ed25519_adversarial(w, frac=args.adversarial, seed=1000 * rank + c0 // chunk)
-        pb = crypto.PreparedBatch(ctx, crypto.PackedBatch(w.n, w.scheme, w.pk, w.pk_stride, w.sig, w.sig_stride,
-                                                          w.sig_len, w.msg, w.msg_off, w.msg_len))
-        if c0 == 0:  # verdict spot check on the first chunk
-            v = pb.verify(MODE_IS_VALID)
-            adv = np.array([c != "valid" for c in w.classes])
-            adv_ok = bool((v[~adv] == ACCEPT).all())
-        batches.append(pb)
-        sizes.append(m)
-        del w
+
+    def chunks():
+        for c0 in range(0, n, chunk):
+            m = min(chunk, n - c0)
+            w = p.tiled(m)
+            if args.adversarial > 0:
+                w = datagen.add_ed25519_adversarial(w, frac=args.adversarial, seed=1000 * rank + c0 // chunk)
+            pb = crypto.PackedBatch(w.n, w.scheme, w.pk, w.pk_stride, w.sig, w.sig_stride, w.sig_len, w.msg,
+                                    w.msg_off, w.msg_len)
+            if c0 == 0:  # verdict spot check on the first chunk
+                v = crypto.verify_packed(ctx, pb, MODE_IS_VALID)
+                adv = np.array([c != "valid" for c in w.classes])
+                adv_ok[0] = bool((v[~adv] == ACCEPT).all())
+            yield pb
+
+    # the rank's shard staged as 2^24-element chunks verified into one device bitmap (C1 input)
+    backlog = D.ShardBacklog(ctx, chunks(), words=(n_max + 31) // 32)
     t_stage = time.perf_counter() - t_stage
-    bitmaps = gathered = None
+    sizes = backlog.sizes
+    gathered = None
     if dist.d is not None:
         import torch
-        nwords = (n_max + 31) // 32  # equal on every rank (all_gather_into_tensor)
-        bitmaps = torch.zeros(nwords, dtype=torch.int32, device="cuda")
-        gathered = torch.zeros(nwords * world, dtype=torch.int32, device="cuda")
+        gathered = torch.zeros(backlog.words * world, dtype=torch.int32, device="cuda")
 
     def step():
-        off = 0
-        for pb, m in zip(batches, sizes):
-            pb.verify(MODE_IS_VALID, want_verdicts=False,
-                      device_bitmap_ptr=None if bitmaps is None else bitmaps.data_ptr() + 4 * off)
-            off += (m + 31) // 32
+        backlog.verify(MODE_IS_VALID)
         if dist.d is not None:
-            dist.d.all_gather_into_tensor(gathered, bitmaps)  # C1 over the whole shard's bitmap
+            backlog.allgather(gathered)  # C1 over the whole shard's bitmap
 
     elapsed = timed(dist, ctx, step, args.steps, args.warmup)
     ks = kstats(ctx, ED_KERNELS)
@@ -888,10 +886,9 @@ def run_backlog(args, dist):
     line.update({
         "roofline": roof,
         "kernels": ks, "cpu_baseline": None,
-        "checks": {"first_chunk_untouched_all_accept": adv_ok, "datagen_s": round(t_gen, 1),
+        "checks": {"first_chunk_untouched_all_accept": adv_ok[0], "datagen_s": round(t_gen, 1),
                    "stage_s": round(t_stage, 1), "chunks": len(sizes)}})
-    for pb in batches:
-        pb.close()
+    backlog.close()
     ctx.close()
     return line
 

@@ -113,8 +113,9 @@ CG_HD uint32_t ed25519_hash_stage(const uint32_t pk[8], const uint32_t sig[16], 
     x1[w] = w < 8 ? c1[w] : 0u;
   }
   const uint32_t bl = mp9_bitlen(x0) > mp9_bitlen(x1) ? mp9_bitlen(x0) : mp9_bitlen(x1);
-  // digits in [-8, 7]: the carry out of the top nonzero nibble needs one more digit
-  const uint32_t nd = (bl + 7) / 4;
+  // digits in [-8, 7]: the carry out of the top nonzero nibble needs one more digit;
+  // 64 digits hold any value < 2^255 (its top nibble plus a carry stays below 8)
+  const uint32_t nd = (bl + 7) / 4 < 64u ? (bl + 7) / 4 : 64u;
   ndig = nd > (uint32_t)kMinDigits ? nd : (uint32_t)kMinDigits;
   return V_COMPUTE;
 }

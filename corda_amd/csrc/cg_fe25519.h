@@ -100,6 +100,25 @@ CG_HD int32_t fe_pin(int32_t x) {
   return x;
 }
 
+// 2x / 4x / 8x of a limb as pinned 32-bit values through v_add_u32 (x + x): gfx950
+// issues v_add_u32 at the 2-cycle rate (72 T lane-ops/s measured) but v_lshlrev_b32,
+// which LLVM would pick for 2 * x, at the 4-cycle rate (38 T;
+// profiles/r02a_isa_rates.json); 4x and 8x are chained doublings of the 2x / 4x
+// values a squaring needs anyway.
+#ifndef CG_FE_X2_ADD
+#define CG_FE_X2_ADD 0  // A/B r02: the asm add version measured 0.8 % slower (more s_nop between dependent mads)
+#endif
+CG_HD int32_t fe_pin(int32_t x);
+CG_HD int32_t fe_x2(int32_t x) {
+#if defined(__HIP_DEVICE_COMPILE__) && CG_FE_X2_ADD
+  int32_t r;
+  asm("v_add_u32 %0, %1, %1" : "=v"(r) : "v"(x));
+  return r;
+#else
+  return fe_pin((int32_t)((uint32_t)x * 2u));
+#endif
+}
+
 // Signed carry chain (round-to-nearest) on 64-bit column sums -> reduced limbs.
 // With rounding carries c = (t + 2^(w-1)) >> w, the residue t - c*2^w is exactly
 // the sign-extended low w bits of t, so it costs one v_bfe_i32 instead of a
@@ -182,7 +201,7 @@ struct FeMulOp {
       f[j] = F.v[j];
       g[j] = G.v[j];
       g19[j] = fe_pin(19 * G.v[j]);
-      f2[j] = (j & 1) ? fe_pin(2 * F.v[j]) : F.v[j];
+      f2[j] = (j & 1) ? fe_x2(F.v[j]) : F.v[j];
     }
   }
   CG_HDM int64_t operator()(int k, int i, int64_t acc) const {
@@ -201,9 +220,9 @@ struct FeSqOp {
     CG_UNROLL for (int j = 0; j < 10; ++j) {
       f[j] = F.v[j];
       f19[j] = fe_pin(19 * F.v[j]);
-      f2[j] = fe_pin(2 * F.v[j]);
-      f4[j] = fe_pin(4 * F.v[j]);
-      f8[j] = fe_pin(8 * F.v[j]);
+      f2[j] = fe_x2(F.v[j]);
+      f4[j] = fe_x2(f2[j]);
+      f8[j] = fe_x2(f4[j]);
     }
   }
   // column k: products i <= j, i + j = k (mod 10), by rank n: i = n for

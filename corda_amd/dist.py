@@ -29,6 +29,35 @@ def shard_bounds(n: int, world: int, align: int = 32) -> list[int]:
     return b
 
 
+# Relative device cost of one verification per scheme id (measured kernel time per
+# signature on MI355X, 1 KB messages: Ed25519 hash+points+msm 12.4 ms / 1M; secp256k1
+# prep+msm 14.0 ms / 1M; P-256 20.2 ms / 1M — profiles/r01q_bench_*.json; the op model
+# of SURVEY 8(e) gives the same ordering, 1.18 M vs 1.56 / 1.69 M ops).
+SCHEME_COST = {4: 1.0, 2: 1.13, 3: 1.63}
+
+
+def shard_bounds_weighted(scheme: np.ndarray, world: int, align: int = 32, cost: dict | None = None) -> list[int]:
+    """Contiguous 32-aligned index shards of a mixed-scheme batch with equal device
+    COST per rank (Ed25519 and ECDSA differ by ~1.4x), so the slowest rank
+    — the one the max-over-ranks timing waits for — does not carry all the ECDSA work.
+    Elements of other schemes cost nothing on the device (they are rejected up front)."""
+    if world < 1:
+        raise ValueError("world must be >= 1")
+    cost = cost or SCHEME_COST
+    n = len(scheme)
+    w = np.zeros(n, dtype=np.float64)
+    for sid, c in cost.items():
+        w[scheme[:n] == sid] = c
+    cum = np.concatenate([[0.0], np.cumsum(w)])
+    total = cum[-1]
+    b = [0]
+    for r in range(1, world):
+        i = int(np.searchsorted(cum, total * r / world, side="left"))
+        b.append(max(b[-1], min(n, i // align * align)))
+    b.append(n)
+    return b
+
+
 def slice_batch(b: PackedBatch, lo: int, hi: int) -> PackedBatch:
     """Shard [lo, hi) of a packed batch, with its own compacted message arena."""
     if hi <= lo:
@@ -71,7 +100,8 @@ def verify_sharded(ctx: _lib.Context, batch: PackedBatch, rank: int, world: int,
     receive the global accept bitmap.  Returns (local verdicts, global bitmap
     as a torch tensor on the rank's device, bounds)."""
     import torch
-    bounds = shard_bounds(batch.n, world)
+    mixed = batch.n and len(np.unique(batch.scheme[:batch.n])) > 1
+    bounds = shard_bounds_weighted(batch.scheme, world) if mixed else shard_bounds(batch.n, world)
     lo, hi = bounds[rank], bounds[rank + 1]
     shard = slice_batch(batch, lo, hi)
     nwords = (shard.n + 31) // 32
@@ -83,3 +113,50 @@ def verify_sharded(ctx: _lib.Context, batch: PackedBatch, rank: int, world: int,
         pb.close()
     glob = allgather_bitmap(local[:nwords], bounds, rank, group)
     return verdicts, glob, bounds
+
+
+class ShardBacklog:
+    """Config 5 on one rank: the rank's index shard of a notary backlog, staged in
+    HBM as a sequence of PreparedBatch chunks (each a multiple of 32 elements but
+    the last, so chunk c's accept words land at word offset sum(len_j / 32, j < c) of
+    ONE device bitmap), verified chunk after chunk into that bitmap, then the C1
+    all-gather over RCCL.  Chunks bound the library's scratch (SURVEY 8d config 5:
+    streamed in 2^24 pieces); the bitmap never leaves the device."""
+
+    def __init__(self, ctx: _lib.Context, chunks, words: int | None = None):
+        import torch
+        self.ctx = ctx
+        self.batches, self.sizes = [], []
+        for b in chunks:
+            if self.sizes and self.sizes[-1] % 32:
+                raise ValueError("only the last chunk may have a length that is not a multiple of 32")
+            self.batches.append(PreparedBatch(ctx, b))
+            self.sizes.append(b.n)
+        self.n = sum(self.sizes)
+        need = (self.n + 31) // 32
+        self.words = max(need, words or 0, 1)
+        self.bitmap = torch.zeros(self.words, dtype=torch.int32, device=f"cuda:{ctx.device}")
+
+    def verify(self, mode: int = _lib.MODE_IS_VALID):
+        """Every chunk verified into its slice of the device bitmap (no host copy)."""
+        off = 0
+        for pb, m in zip(self.batches, self.sizes):
+            pb.verify(mode, want_verdicts=False, device_bitmap_ptr=self.bitmap.data_ptr() + 4 * off)
+            off += (m + 31) // 32
+        return self.bitmap
+
+    def allgather(self, out=None, group=None):
+        """C1: the ranks' bitmaps concatenated (equal word counts per rank: pass
+        `words` = the largest shard's word count when shards differ)."""
+        import torch
+        import torch.distributed as dist
+        world = dist.get_world_size(group)
+        if out is None:
+            out = torch.zeros(self.words * world, dtype=torch.int32, device=self.bitmap.device)
+        dist.all_gather_into_tensor(out, self.bitmap, group=group)
+        return out
+
+    def close(self):
+        for pb in self.batches:
+            pb.close()
+        self.batches = []

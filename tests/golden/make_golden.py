@@ -278,6 +278,37 @@ def ecdsa_cases():
         add("key_off_curve", scheme, (q[0], (q[1] + 1) % c.p), EC.der_encode(r, s), msg)
         add("key_x_ge_p", scheme, (q[0] + c.p, q[1]), EC.der_encode(r, s), msg) if q[0] + c.p < 2**256 else None
         add("key_zero", scheme, (0, 0), EC.der_encode(r, s), msg)
+    # Appendix B.4 exceptional points, realised as signatures (a separate RNG keeps the
+    # rows above unchanged).  With e = SHA-256(M) mod n, (r, s) fixes u1 = e/s and
+    # u2 = r/s exactly, so any (u1, u2, Q = dG) relation maps to a signature:
+    rx = random.Random(4242)
+    for scheme in (2, 3):
+        c = EC.CURVES[scheme]
+        for t in range(4):
+            msg = b"B4-%d-%d" % (scheme, t)
+            e = int.from_bytes(hashlib.sha256(msg).digest(), "big") % c.n
+            # u1 G + u2 Q = infinity (u1 + d u2 = 0 mod n: r = -e/d) -> REJECT (B.4)
+            for d in (1, 2, 3, c.n - 1):
+                r = (-e * pow(d, -1, c.n)) % c.n
+                add("B4_infinity", scheme, EC.pubkey(scheme, d), EC.der_encode(r, rx.randrange(1, c.n)), msg)
+            # u1 = u2 with Q = G (r = e): every Q addition of the device's joint
+            # multiplication meets an equal partial sum (its doubling branch;
+            # tests/test_native_host.py::test_ecdsa_joint_exceptional_cases)
+            add("B4_doubling_q_eq_g", scheme, EC.pubkey(scheme, 1), EC.der_encode(e, rx.randrange(1, c.n)), msg)
+            # Q = -G, u1 = u2: partial sums cancel to infinity mid-loop, then grow again
+            add("B4_cancel_q_eq_minus_g", scheme, EC.pubkey(scheme, c.n - 1),
+                EC.der_encode(e, rx.randrange(1, c.n)), msg)
+            # Q = 2G, u1 = 2 u2 (r = e/2)
+            add("B4_q_eq_2g_u1_eq_2u2", scheme, EC.pubkey(scheme, 2),
+                EC.der_encode(e * pow(2, -1, c.n) % c.n, rx.randrange(1, c.n)), msg)
+            # a VALID signature whose two halves are the same point, u1 G == u2 Q:
+            # key d = e/r, s = k^-1 (e + r d) = 2e/k -> ACCEPT
+            k = rx.randrange(1, c.n)
+            r = EC._mul(c, k, c.g)[0] % c.n
+            d = e * pow(r, -1, c.n) % c.n
+            s2 = 2 * e * pow(k, -1, c.n) % c.n
+            add("B4_equal_halves_valid", scheme, EC.pubkey(scheme, d), EC.der_encode(r, s2), msg)
+            assert EC.is_valid(scheme, EC.pubkey(scheme, d), EC.der_encode(r, s2), msg) == EC.ACCEPT
     return cases
 
 

@@ -95,3 +95,23 @@ def test_pack_bits_matches_device_layout():
     w = pack_bits(m)
     assert w.dtype == np.uint32 and len(w) == 3
     assert w[0] == (1 | 1 << 5 | 1 << 31) and w[1] == 1 and w[2] == 1 << 5
+
+
+def test_cost_weighted_shards_balance_mixed_batches():
+    """Mixed Ed25519 / ECDSA batches split by device cost, not count: the
+    per-rank cost differs by at most one aligned block from the ideal share, every
+    interior boundary is a multiple of 32, and a uniform batch splits like shard_bounds."""
+    from corda_amd import dist as D
+    rng = np.random.default_rng(3)
+    # ECDSA clustered at the end (config 3 / 4 layouts put curves in runs)
+    scheme = np.concatenate([np.full(60_000, 4), rng.choice([2, 3], 40_000)]).astype(np.uint8)
+    for world in (2, 3, 8):
+        b = D.shard_bounds_weighted(scheme, world)
+        assert b[0] == 0 and b[-1] == len(scheme) and all(x % 32 == 0 for x in b[1:-1])
+        costs = [sum(D.SCHEME_COST[int(s)] for s in scheme[b[r]:b[r + 1]]) for r in range(world)]
+        ideal = sum(costs) / world
+        assert max(costs) - ideal <= 32 * max(D.SCHEME_COST.values()) + 1e-6
+        counts = np.diff(b)
+        assert counts[-1] < counts[0]  # the ECDSA-heavy tail gets fewer elements
+    same = np.full(10_000, 4, np.uint8)
+    assert D.shard_bounds_weighted(same, 4) == D.shard_bounds(10_000, 4)

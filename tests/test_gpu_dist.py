@@ -37,3 +37,37 @@ def test_verify_sharded_rccl_world1(gpu_ctx):
         assert np.array_equal(glob.cpu().numpy(), exp)
     finally:
         dist.destroy_process_group()
+
+
+def test_backlog_chunks_into_one_device_bitmap_world1(gpu_ctx, oracle):
+    """Config 5's chunked path (corda_amd.dist.ShardBacklog, what bench.py
+    --workload backlog runs): several PreparedBatch chunks verified into consecutive
+    word slices of ONE device bitmap, then the RCCL all-gather; compared bit for bit
+    with the oracle's verdicts of the whole shard (32-aligned chunks + a ragged last)."""
+    import torch
+    import torch.distributed as dist
+    import datagen
+    from corda_amd import dist as D
+    from corda_amd.crypto import PackedBatch
+    from test_gpu_ed25519 import oracle_verdicts
+    n = 50_013
+    w = datagen.add_ed25519_adversarial(datagen.make_batch(n, msg_bytes=32, seed=17, key_base=31337), 0.05, seed=8)
+    full = PackedBatch(w.n, w.scheme, w.pk, w.pk_stride, w.sig, w.sig_stride, w.sig_len, w.msg, w.msg_off,
+                       w.msg_len)
+    with pytest.raises(ValueError):
+        D.ShardBacklog(gpu_ctx, [D.slice_batch(full, 0, 100), D.slice_batch(full, 100, 200)])
+    s = socket.socket(); s.bind(("127.0.0.1", 0)); port = s.getsockname()[1]; s.close()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(gpu_ctx.device)
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    try:
+        chunk = 8192
+        bl = D.ShardBacklog(gpu_ctx, (D.slice_batch(full, c, min(n, c + chunk)) for c in range(0, n, chunk)))
+        assert bl.sizes[:-1] == [chunk] * (len(bl.sizes) - 1) and bl.n == n
+        bl.verify()
+        glob = bl.allgather()
+        exp = D.pack_bits(oracle_verdicts(oracle, w, 0) == 0).view(np.int32)
+        assert np.array_equal(glob.cpu().numpy()[:len(exp)], exp)
+        bl.close()
+    finally:
+        dist.destroy_process_group()

@@ -96,3 +96,29 @@ def test_config3_shape(gpu_ctx, oracle):
         assert (got[~adv] == ACCEPT).all()
         sub = w.subset(np.flatnonzero(adv))
         assert np.array_equal(got[adv], oracle_verdicts(oracle, sub, MODE_IS_VALID))
+
+
+def test_config3_full_size_mixed_batch(gpu_ctx, oracle):
+    """BASELINE config 3 at full size in ONE batch: 2^20 secp256k1 + 2^20 P-256
+    signatures, 1 KB messages, 1 % adversarial over D1-D8 (both curves' pipelines
+    concurrently on their streams, several ECDSA scratch chunks).  Size-independent
+    properties at full size: every untouched signature accepts; the adversarial
+    subset's verdicts equal the oracle's element for element."""
+    n, pool = 1 << 20, 1 << 15
+    p = datagen.make_batch(2 * pool, msg_bytes=1024, scheme=np.repeat(np.array([2, 3], np.uint8), pool), seed=77,
+                           key_base=7_000_000)
+    k1 = p.subset(np.arange(pool)).tiled(n)
+    r1 = p.subset(np.arange(pool, 2 * pool)).tiled(n)
+    w = datagen.Workload(2 * n, np.concatenate([k1.scheme, r1.scheme]), np.concatenate([k1.pk, r1.pk]), 64,
+                         np.concatenate([k1.sig, r1.sig]), k1.sig_stride, np.concatenate([k1.sig_len, r1.sig_len]),
+                         np.concatenate([k1.msg[:-16], r1.msg]),
+                         np.concatenate([k1.msg_off, r1.msg_off + np.uint64(len(k1.msg) - 16)]),
+                         np.concatenate([k1.msg_len, r1.msg_len]), ["valid"] * (2 * n))
+    del k1, r1, p
+    w = datagen.add_ecdsa_adversarial(w, frac=0.01, seed=13)
+    got = gpu_verdicts(gpu_ctx, w, MODE_IS_VALID)
+    adv = np.array([c != "valid" for c in w.classes])
+    assert (got[~adv] == ACCEPT).all()
+    idx = np.flatnonzero(adv)
+    assert np.array_equal(got[idx], oracle_verdicts(oracle, w.subset(idx), MODE_IS_VALID))
+    assert idx.size > 15000 and (w.scheme[idx] == 2).any() and (w.scheme[idx] == 3).any()

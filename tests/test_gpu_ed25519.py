@@ -186,3 +186,32 @@ def test_empty_batch_is_ok(gpu_ctx):
     st = gpu_ctx.lib.cg_verify_batch(gpu_ctx.h, 0, MODE_IS_VALID, None, None, 64, None, 64, None, None, 0, None, None,
                                      ptr(v), None)
     assert st == 0
+
+
+@pytest.mark.parametrize("mod", [7, 1])
+def test_forced_full_length_fallback_vs_oracle(gpu_ctx, oracle, golden_ed25519, mod):
+    """The half-size reduction's fallback (c0, c1) = (h, 1) (cg_halfscalar.h; taken
+    when the Lehmer quotient overflows, ~1e-8 of hash-derived h) forced on the device
+    through cg_set_debug for every mod-th element — golden E1-E12 fixtures plus a
+    mutated random batch — must give the oracle's verdicts (the full-length loop
+    decides the same i2p predicate).  The waves holding a forced lane run 64 radix-16
+    digits instead of ~33."""
+    from corda_amd._lib import DEBUG_FORCE_FULL_LENGTH
+    g = golden_ed25519
+    pks = [bytes.fromhex(e["pk"]) for e in g]
+    sigs = [bytes.fromhex(e["sig"]) for e in g]
+    msgs = [bytes.fromhex(e["msg"]) for e in g]
+    w = datagen.add_ed25519_adversarial(datagen.make_batch(4000, msg_bytes=64, seed=21, key_base=777), frac=0.3,
+                                        seed=9)
+    gpu_ctx.set_debug(DEBUG_FORCE_FULL_LENGTH, mod)
+    try:
+        for mode, key in ((MODE_IS_VALID, "is_valid"), (MODE_DO_VERIFY, "do_verify")):
+            v = crypto.verify_packed(gpu_ctx, crypto.pack(crypto.EDDSA_ED25519_SHA512, pks, sigs, msgs), mode)
+            exp = np.array([e[key] for e in g], dtype=np.uint8)
+            bad = np.flatnonzero(v != exp)
+            assert bad.size == 0, [(g[i]["cls"], int(v[i]), int(exp[i])) for i in bad[:10]]
+            got = gpu_verdicts(gpu_ctx, w, mode)
+            assert np.array_equal(got, oracle_verdicts(oracle, w, mode))
+        assert (got == ACCEPT).sum() > 2000
+    finally:
+        gpu_ctx.set_debug(DEBUG_FORCE_FULL_LENGTH, 0)
