@@ -75,7 +75,11 @@ CG_HD void ed25519_abyte(uint32_t ab[8], const uint32_t pk[8]) {
 // digit count and R sign (packed into the status word by the caller).
 // FULL_LENGTH / force_full (tests only; force_full per lane through the
 // cg_set_debug hook) force the (h, 1) fallback of the half-size reduction.
-template <bool FULL_LENGTH = false>
+// REUSE selects the key-reuse split (cg_halfscalar.h TB = 192): c0 in four 64-bit
+// chunks over per-key tables, |c1| < 2^66, B digits over four tables 2^(64 t) B;
+// ndig then carries the number of low windows in which chunk 3 (digits 48..63 of
+// c0) is nonzero, plus 32 when c1 needs a 17th digit (ed_status_* decode it).
+template <bool FULL_LENGTH = false, bool REUSE = false>
 CG_HD uint32_t ed25519_hash_stage(const uint32_t pk[8], const uint32_t sig[16], uint32_t sig_len, const uint8_t* msg,
                                   uint32_t msg_len, uint32_t mode, uint32_t dig[kDigitWords], uint32_t& ndig,
                                   uint32_t& rneg, bool force_full = false) {
@@ -94,6 +98,8 @@ CG_HD uint32_t ed25519_hash_stage(const uint32_t pk[8], const uint32_t sig[16], 
       c0[w] = h[w];
       c1[w] = w == 0;
     }
+  } else if (REUSE) {
+    ed25519_half_scalars<192, 66>(h, c0, c1, c1neg);
   } else {
     ed25519_half_scalars(h, c0, c1, c1neg);
   }
@@ -111,6 +117,17 @@ CG_HD uint32_t ed25519_hash_stage(const uint32_t pk[8], const uint32_t sig[16], 
   CG_UNROLL for (int w = 0; w < 9; ++w) {
     x0[w] = w < 8 ? c0[w] : 0u;
     x1[w] = w < 8 ? c1[w] : 0u;
+  }
+  if (REUSE) {
+    // chunk-3 windows: 1 + the highest nonzero digit among 48..63 (e = d + 8 per nibble)
+    uint32_t c3w = 0;
+    CG_UNROLL for (int j = 0; j < 16; ++j) {
+      const uint32_t e = (dig[6 + (j >> 3)] >> (4 * (j & 7))) & 15u;
+      c3w = e != 8u ? (uint32_t)j + 1 : c3w;
+    }
+    const uint32_t c1_17 = (dig[10] & 15u) != 8u;  // digit 16 of c1
+    ndig = c3w | c1_17 << 5;
+    return V_COMPUTE;
   }
   const uint32_t bl = mp9_bitlen(x0) > mp9_bitlen(x1) ? mp9_bitlen(x0) : mp9_bitlen(x1);
   // digits in [-8, 7]: the carry out of the top nonzero nibble needs one more digit;
@@ -162,6 +179,15 @@ CG_HD uint32_t ed25519_points_stage(const uint32_t pk[8], const uint32_t r[8], u
   return V_COMPUTE;
 }
 
+// Points phase of the key-reuse path: the key was decoded once for its distinct-key
+// slot (key_ok), only R is decoded here.  Same precedence as ed25519_points_stage.
+CG_HD uint32_t ed25519_points_stage_r(const uint32_t r[8], uint32_t pre, uint32_t key_ok, ge_p3& R) {
+  if (!key_ok) return V_KEY_INVALID;
+  if (pre != V_COMPUTE) return pre;
+  if (!ge_frombytes_strict(R, r)) return V_REJECT;
+  return V_COMPUTE;
+}
+
 // Table entry k*P (k = 0..8) in cached form, P given as p3; writes via `put`.
 template <typename Put>
 CG_HD void ed25519_build_table(const ge_p3& P, Put&& put) {
@@ -181,9 +207,32 @@ CG_HD void ed25519_build_table(const ge_p3& P, Put&& put) {
   }
 }
 
+// Per distinct key of the key-reuse path: decode A once (i2p, A.2) and build the
+// tables k * 2^(64 t) (-A), t = 0..3, k = 0..8; put(t, k, cached).  Returns 0 when
+// the key has no square root (KEY_INVALID for every signature by it).
+template <typename Put>
+CG_HD uint32_t ed25519_key_tables(const uint32_t pk[8], Put&& put) {
+  ge_p3 P;
+  if (!ge_frombytes_i2p(P, pk)) return 0;
+  fe_neg(P.X, P.X);
+  fe_neg(P.T, P.T);
+  ge_p1p1 x;
+  CG_NOUNROLL for (int t = 0; t < 4; ++t) {
+    if (t) {
+      CG_NOUNROLL for (int i = 0; i < 64; ++i) {
+        ge_p3_dbl(x, P);
+        ge_p1p1_to_p3(P, x);
+      }
+    }
+    ed25519_build_table(P, [&](int k, const ge_cached& c) CG_LINLINE { put(t, k, c); });
+  }
+  return 1;
+}
+
 // Entry k (0 <= k <= 2^(kBWin-1)) of shared table t in affine precomputed form:
-// k*B (t = 0) or k*2^128 B (t = 1).  One call per lane of the table-building
-// kernel at context creation (and on the host for the tests).
+// k * 2^(64 t) B, t = 0..3 (the balanced split uses t = 0 and 2; the key-reuse
+// split all four).  One call per lane of the table-building kernel at context
+// creation (and on the host for the tests).
 CG_HD void ed25519_btab_entry(ge_precomp& out, uint32_t t, uint32_t k) {
   const uint32_t benc[8] = {0x66666658u, 0x66666666u, 0x66666666u, 0x66666666u,
                             0x66666666u, 0x66666666u, 0x66666666u, 0x66666666u};
@@ -191,7 +240,7 @@ CG_HD void ed25519_btab_entry(ge_precomp& out, uint32_t t, uint32_t k) {
   ge_p3 P, R;
   ge_p1p1 x;
   ge_frombytes_i2p(P, benc);
-  CG_NOUNROLL for (uint32_t i = 0; i < 128 * t; ++i) {
+  CG_NOUNROLL for (uint32_t i = 0; i < 64 * t; ++i) {
     ge_p3_dbl(x, P);
     ge_p1p1_to_p3(P, x);
   }
@@ -237,7 +286,7 @@ CG_HD void shl_nibbles(uint32_t x[8], uint32_t n) {
 
 // MSM phase: P = [b]B + [c0](-A) + [c1](+-R) over ndig radix-16 positions (ndig
 // uniform across the wave, >= 32).  getA(k, cached&) loads k*(-A), getR(k,
-// cached&) loads k*R, getB(t, k, precomp&) loads k*B (t = 0) or k*2^128 B (t = 1),
+// cached&) loads k*R, getB(t, k, precomp&) loads k * 2^(64 t) B (t = 0 or 2 here),
 // k <= 2^(kBWin-1).
 // Returns 1 iff P is the identity.
 template <typename GetA, typename GetR, typename GetB>
@@ -298,12 +347,96 @@ CG_HD uint32_t ed25519_msm(uint32_t ndig, const uint32_t dig[kDigitWords], uint3
       getB(0, nl ? kHalf - el : el - kHalf, pb);
       ge_p1p1_to_p3(r3, t);
       ge_madd(t, r3, pb, nl);
-      getB(1, nh ? kHalf - eh : eh - kHalf, pb);
+      getB(2, nh ? kHalf - eh : eh - kHalf, pb);
       ge_p1p1_to_p3(r3, t);
       ge_madd(t, r3, pb, nh);
     }
   }
   // identity <=> x = X/Z = 0 and y = Y/T = 1
+  fe d;
+  fe_sub(d, t.Y, t.T);
+  return fe_iszero(t.X) & fe_iszero(d);
+}
+
+// MSM phase of the key-reuse split: P = [b]B + sum_t [c0_t](2^(64 t) (-A)) +
+// [c1](+-R) with 16-digit chunks c0_t of c0's signed radix-16 digits (t = 0..3) and
+// |c1| < 2^66: 16 (or 17 when some lane's c1 needs a 17th digit) windows — ~64
+// doublings instead of ~130 — four per-key A tables (getA(t, k, .)), the lane's R
+// table, and 16-bit B windows over the four shared tables 2^(64 t) B (getB(t, k, .)).
+// c3w (wave-uniform): chunk 3 is added in the c3w lowest windows only (its digits
+// are zero above; 16 for a fallback lane's 253-bit c0).  Returns 1 iff P is the
+// identity.
+template <typename GetA, typename GetR, typename GetB>
+CG_HD uint32_t ed25519_msm_reuse(uint32_t c3w, uint32_t win17, const uint32_t dig[kDigitWords], uint32_t rneg,
+                                 GetA&& getA, GetR&& getR, GetB&& getB) {
+  uint64_t da[4], bt[4];
+  CG_UNROLL for (int t = 0; t < 4; ++t) {
+    da[t] = (uint64_t)dig[2 * t] | (uint64_t)dig[2 * t + 1] << 32;                  // digits 16t .. 16t+15
+    bt[t] = (uint64_t)dig[16 + 2 * (3 - t)] | (uint64_t)dig[17 + 2 * (3 - t)] << 32;  // B digits 4t+3 .. 4t
+  }
+  uint64_t dr = (uint64_t)dig[8] | (uint64_t)dig[9] << 32;  // c1 digits 0..15
+  const uint32_t dr16 = dig[10] & 15u;                       // c1 digit 16
+  ge_p2 r2;
+  ge_p3 r3;
+  ge_p1p1 t;
+  ge_cached ca;
+  ge_precomp pb;
+  fe_0(t.X);
+  fe_1(t.Y);
+  fe_1(t.Z);
+  fe_1(t.T);
+  const int top = win17 ? 64 : 60;
+  CG_NOUNROLL for (int pos = top; pos >= 0; --pos) {
+    if (pos != top) {
+      ge_p1p1_to_p2(r2, t);
+      ge_p2_dbl(t, r2);
+    }
+    if ((pos & 3) == 0) {
+      const uint32_t j = (uint32_t)pos >> 2;
+      if (j < 16) {
+        // rolled over the chunks; the digit registers rotate so every access is
+        // static (a runtime index into a register array would go to scratch)
+        CG_NOUNROLL for (int c = 0; c < 4; ++c) {
+          const uint32_t e = (uint32_t)(da[0] >> 60);
+          const uint64_t nx = da[0] << 4;
+          da[0] = da[1];
+          da[1] = da[2];
+          da[2] = da[3];
+          da[3] = nx;
+          if (c < 3 || j < c3w) {  // wave-uniform
+            const uint32_t n = e < 8;
+            getA(c, n ? 8 - e : e - 8, ca);
+            ge_p1p1_to_p3(r3, t);
+            ge_add_cached(t, r3, ca, n);
+          }
+        }
+      }
+      uint32_t er = dr16;
+      if (j < 16) {
+        er = (uint32_t)(dr >> 60);
+        dr <<= 4;
+      }
+      const uint32_t nr = er < 8;
+      getR(nr ? 8 - er : er - 8, ca);
+      ge_p1p1_to_p3(r3, t);
+      ge_add_cached(t, r3, ca, nr ^ rneg);
+    }
+    if ((pos & 15) == 0 && pos < 64) {
+      constexpr uint32_t kHalf = 1u << 15;
+      CG_NOUNROLL for (int c = 0; c < 4; ++c) {
+        const uint32_t e = (uint32_t)bt[0] & 0xffffu;
+        const uint64_t nx = bt[0] >> 16;
+        bt[0] = bt[1];
+        bt[1] = bt[2];
+        bt[2] = bt[3];
+        bt[3] = nx;
+        const uint32_t n = e < kHalf;
+        getB(c, n ? kHalf - e : e - kHalf, pb);
+        ge_p1p1_to_p3(r3, t);
+        ge_madd(t, r3, pb, n);
+      }
+    }
+  }
   fe d;
   fe_sub(d, t.Y, t.T);
   return fe_iszero(t.X) & fe_iszero(d);

@@ -173,13 +173,14 @@ CG_HD void mp9_lincomb(uint32_t out[9], const uint32_t x[9], const uint32_t y[9]
 // can get close to 2^128, so the exact single steps find the first remainder
 // below 2^128 — the same (a, b, ta, tb) the plain step-by-step loop reaches.
 // Returns 0 when no quotient was emulated (the caller takes an exact step).
+template <int TB = 128>
 CG_HD uint32_t hs_lehmer(uint32_t a[9], uint32_t b[9], uint32_t ta[9], uint32_t tb[9]) {
-  const uint32_t s = mp9_bitlen(a) - 52;  // caller guarantees bitlen(a) > 132
+  const uint32_t s = mp9_bitlen(a) - 52;  // caller guarantees bitlen(a) > TB + 4
   int64_t uh = (int64_t)mp9_shr64(a, s), vh = (int64_t)mp9_shr64(b, s);
   // An emulated remainder T stands for a true one in (T - |C| - |D|, T + |C| + |D|)
-  // * 2^s with |C|, |D| < 2^31: T >= 2^(129-s) + 2^33 keeps every emulated
-  // remainder above 2^128 (s ranges over 81..204).
-  const int64_t thr = (s < 129 ? (int64_t)1 << (129 - s) : (int64_t)0) + ((int64_t)1 << 33);
+  // * 2^s with |C|, |D| < 2^31: T >= 2^(TB+1-s) + 2^33 keeps every emulated
+  // remainder above 2^TB (s ranges over TB-47..204).
+  const int64_t thr = (s < (uint32_t)TB + 1 ? (int64_t)1 << (TB + 1 - s) : (int64_t)0) + ((int64_t)1 << 33);
   int64_t A = 1, B = 0, C = 0, D = 1;
   CG_NOUNROLL for (int it = 0; it < 48; ++it) {
     const int64_t y1 = vh + C, y2 = vh + D, x1 = uh + A, x2 = uh + B;
@@ -219,9 +220,20 @@ CG_HD uint32_t hs_lehmer(uint32_t a[9], uint32_t b[9], uint32_t ta[9], uint32_t 
   return 1;
 }
 
-// c0 = c1 h mod 8L with c1 odd; c0 >= 0 and |c1| returned with its sign.  Both
-// are < 2^253 on success (typically ~2^128).  Returns 0 when the caller must
-// fall back to (h, 1).
+// b >= 2^TB for TB a multiple of 32 plus TB % 32 bits
+template <int TB>
+CG_HD uint32_t mp9_ge_pow2(const uint32_t b[9]) {
+  uint32_t x = b[TB / 32] >> (TB % 32);
+  CG_UNROLL for (int w = TB / 32 + 1; w < 9; ++w) x |= b[w];
+  return x != 0;
+}
+
+// c0 = c1 h mod 8L with c1 odd; c0 >= 0 and |c1| returned with its sign.
+// TB = 128 (the balanced split, c0, |c1| ~ 2^128) or TB = 192 (the key-reuse
+// split: c0 ~ 2^192 in 64-bit chunks over the per-key tables A, 2^64 A, 2^128 A,
+// 2^192 A, |c1| ~ 2^63 in at most 17 signed radix-16 digits).  C1BITS bounds |c1|
+// (252 / 66).  Returns 0 when the caller must fall back to (h, 1).
+template <int TB = 128, int C1BITS = 252>
 CG_HD uint32_t ed25519_half_scalars(const uint32_t h[8], uint32_t c0[8], uint32_t c1[8], uint32_t& c1neg) {
   uint32_t a[9] = CG_8L_WORDS, b[9], ta[9], tb[9];
   CG_UNROLL for (int w = 0; w < 9; ++w) {
@@ -230,28 +242,33 @@ CG_HD uint32_t ed25519_half_scalars(const uint32_t h[8], uint32_t c0[8], uint32_
     tb[w] = w == 0;
   }
   uint32_t ok = 1, steps = 0;
-  CG_NOUNROLL while ((b[4] | b[5] | b[6] | b[7] | b[8]) != 0) {  // b >= 2^128
+  CG_NOUNROLL while (mp9_ge_pow2<TB>(b)) {  // b >= 2^TB
     if (++steps > 160) {
       ok = 0;
       break;
     }
-    if (mp9_bitlen(a) > 132 && hs_lehmer(a, b, ta, tb)) continue;
+    if (mp9_bitlen(a) > TB + 4 && hs_lehmer<TB>(a, b, ta, tb)) continue;
     if (!hs_exact_step(a, b, ta, tb)) {
       ok = 0;
       break;
     }
   }
   // candidates: (b, tb) when tb is odd; else (a, ta) and one more step (both odd,
-  // since consecutive cofactors are coprime) — keep the shorter one
+  // since consecutive cofactors are coprime) — keep the shorter one (balanced
+  // split: the longer of the two scalars; key-reuse split: the shorter c0 among the
+  // candidates whose |c1| fits C1BITS)
   uint32_t x0[9], x1[9], s1 = 0;
   CG_UNROLL for (int w = 0; w < 9; ++w) {
     x0[w] = b[w];
     x1[w] = tb[w];
   }
+  auto cost = [](uint32_t l0, uint32_t l1) CG_LINLINE -> uint32_t {
+    return TB == 128 ? (l0 > l1 ? l0 : l1) : (l1 > (uint32_t)C1BITS ? 1000u : l0);
+  };
   if (ok && !(tb[0] & 1)) {
     uint32_t ua[9], un[9], r[9], tn[9];
     mp9_abs(ua, ta);
-    uint32_t best = mp9_bitlen(a) > mp9_bitlen(ua) ? mp9_bitlen(a) : mp9_bitlen(ua);
+    uint32_t best = cost(mp9_bitlen(a), mp9_bitlen(ua));
     CG_UNROLL for (int w = 0; w < 9; ++w) {
       x0[w] = a[w];
       x1[w] = ta[w];
@@ -272,7 +289,7 @@ CG_HD uint32_t ed25519_half_scalars(const uint32_t h[8], uint32_t c0[8], uint32_
       }
       if (!neg && !mp9_ge(r, b)) {
         mp9_abs(un, tn);
-        const uint32_t l = mp9_bitlen(r) > mp9_bitlen(un) ? mp9_bitlen(r) : mp9_bitlen(un);
+        const uint32_t l = cost(mp9_bitlen(r), mp9_bitlen(un));
         if (l < best) {
           CG_UNROLL for (int w = 0; w < 9; ++w) {
             x0[w] = r[w];
@@ -284,7 +301,7 @@ CG_HD uint32_t ed25519_half_scalars(const uint32_t h[8], uint32_t c0[8], uint32_
   }
   uint32_t m1[9];
   s1 = mp9_abs(m1, x1);
-  if (!ok || !(m1[0] & 1) || mp9_bitlen(x0) > 252 || mp9_bitlen(m1) > 252) {
+  if (!ok || !(m1[0] & 1) || mp9_bitlen(x0) > 252 || mp9_bitlen(m1) > C1BITS) {
     CG_UNROLL for (int w = 0; w < 8; ++w) {
       c0[w] = h[w];
       c1[w] = w == 0;

@@ -21,6 +21,11 @@ struct Ed25519Dev {
   uint32_t* digits = nullptr;    // [24][scap]
   int32_t* table = nullptr;      // [scap][18][40] lane-contiguous k*(-A), k*R
   const int32_t* btab = nullptr; // [2][kBTabEntries][30] shared k*B, k*2^128 B tables
+  // key-reuse path (null key_index: the balanced path): per-signature index of the
+  // signer's distinct-key slot, the per-key tables k * 2^(64 t) (-A) and key status
+  const uint32_t* key_index = nullptr;
+  const int32_t* ktab = nullptr;
+  const uint32_t* kstat = nullptr;
   uint32_t full_mod = 0;         // test hook: lanes with (index_base + i) % full_mod == 0 take (c0, c1) = (h, 1)
   uint32_t index_base = 0;       // index of this chunk's first element in the Ed25519 subset
 };
@@ -31,6 +36,14 @@ size_t ed25519_digit_words();
 hipError_t launch_ed25519_btab_build(int32_t* btab, hipStream_t s);
 hipError_t launch_ed25519_hash(const Ed25519Dev& d, uint32_t n, uint32_t mode, hipStream_t s);
 hipError_t launch_ed25519_points(const Ed25519Dev& d, uint32_t n, hipStream_t s);
+size_t ed25519_key_table_bytes(uint32_t n_keys);
+hipError_t launch_ed25519_keyprep(const Ed25519Dev& d, const uint32_t* key_first, uint32_t n_keys, hipStream_t s);
+// Key dedupe at staging: key_index[i] = dense id of element i's 32-byte key among the
+// n Ed25519 keys (SoA pk[8][cap]), key_first[id] = an element holding that key,
+// *n_keys_dev = the number of ids.  table: tsize (power of 2) zeroed words.
+hipError_t launch_key_dedupe(const uint32_t* pk, uint32_t n, uint32_t cap, uint32_t* table, uint32_t tsize,
+                             uint32_t* slot_of, uint32_t* owner_id, uint32_t* counter, uint32_t* key_index,
+                             uint32_t* key_first, hipStream_t s);
 hipError_t launch_ed25519_msm(const Ed25519Dev& d, uint32_t n, const uint32_t* out_index, uint8_t* verdict,
                               hipStream_t s);
 

@@ -63,6 +63,10 @@ struct cg_ctx {
   uint32_t* ed_status = nullptr;
   uint32_t* ed_digits = nullptr;
   int32_t* ed_table = nullptr;
+  // key-reuse path scratch: per-key tables and decode status
+  uint32_t ed_kcap = 0;
+  int32_t* ed_ktab = nullptr;
+  uint32_t* ed_kstat = nullptr;
   uint32_t* err_flag = nullptr;  // device word raised by kernels on malformed layouts
   bool profiling = false;
   std::map<std::string, Stat> stats;
@@ -265,6 +269,11 @@ struct cg_batch {
   uint32_t* ed_sig_len = nullptr;
   uint64_t* ed_msg_off = nullptr;
   uint32_t* ed_msg_len = nullptr;
+  // key-reuse path (see key_reuse_mode): distinct-key slot of every Ed25519 element
+  // and one element per slot; null key_index = the balanced per-signature path
+  uint32_t n_keys = 0;
+  uint32_t* ed_key_index = nullptr;
+  uint32_t* ed_key_first = nullptr;
   // ECDSA subsets (K1, R1)
   cg::EcdsaBatch ec[2];
 };
@@ -286,6 +295,8 @@ void batch_free(cg_ctx* ctx, cg_batch* b) {
   dfree(ctx, b->ed_sig_len);
   dfree(ctx, b->ed_msg_off);
   dfree(ctx, b->ed_msg_len);
+  dfree(ctx, b->ed_key_index);
+  dfree(ctx, b->ed_key_first);
   for (auto& e : b->ec)
     for (const void* p : {(const void*)e.index, (const void*)e.q, (const void*)e.rs, (const void*)e.der,
                           (const void*)e.sig_len, (const void*)e.msg_off, (const void*)e.msg_len})
@@ -503,6 +514,77 @@ cg_status cg_release_cached(cg_ctx* ctx) {
 
 namespace {
 
+// Key-reuse decision (CORDA_AMD_KEY_REUSE: 0 never, 1 always, else automatic):
+// the per-key path pays a decode and four 9-entry tables (~190 doublings) per
+// distinct key and saves ~70 doublings, the A decode and the A table per
+// signature, so it wins once keys repeat a few times; automatic = n / n_keys >= 8.
+int key_reuse_forced() {
+  const char* e = std::getenv("CORDA_AMD_KEY_REUSE");
+  return e && (e[0] == '0' || e[0] == '1') ? e[0] - '0' : -1;
+}
+
+bool key_reuse_mode(uint32_t n, uint32_t n_keys) {
+  const int forced = key_reuse_forced();
+  if (forced >= 0) return forced == 1;
+  return n_keys > 0 && (uint64_t)n_keys * 8 <= n;
+}
+
+// Distinct Ed25519 keys of a staged batch (device hash table, stage_kernels.hip);
+// keeps key_index / key_first only when the key-reuse path will be used.
+cg_status stage_key_dedupe(cg_ctx* ctx, cg_batch* b) {
+  const uint32_t ne = b->n_ed;
+  const int forced = key_reuse_forced();
+  if (forced == 0 || (ne < 64 && forced != 1)) return CG_OK;
+  uint32_t tsize = 1;
+  while (tsize < 2 * ne) tsize <<= 1;
+  uint32_t *table = nullptr, *slot_of = nullptr, *owner = nullptr, *counter = nullptr;
+  cg_status st = CG_OK;
+  auto done = [&](cg_status r) {
+    (void)hipStreamSynchronize(ctx->stream);
+    for (const void* p : {(const void*)table, (const void*)slot_of, (const void*)owner, (const void*)counter})
+      dfree(ctx, p);
+    return r;
+  };
+  if ((st = dalloc(ctx, &table, tsize, "alloc key table")) != CG_OK || (st = dalloc(ctx, &slot_of, ne, "alloc key slots")) != CG_OK ||
+      (st = dalloc(ctx, &owner, tsize, "alloc key owners")) != CG_OK || (st = dalloc(ctx, &counter, 1, "alloc key counter")) != CG_OK ||
+      (st = dalloc(ctx, &b->ed_key_index, ne, "alloc key index")) != CG_OK ||
+      (st = dalloc(ctx, &b->ed_key_first, ne, "alloc key first")) != CG_OK)
+    return done(st);
+  hipError_t e = hipMemsetAsync(table, 0, (size_t)tsize * 4, ctx->stream);
+  if (e == hipSuccess) e = hipMemsetAsync(counter, 0, 4, ctx->stream);
+  if (e == hipSuccess)
+    e = cg::launch_key_dedupe(b->ed_pk, ne, ne, table, tsize, slot_of, owner, counter, b->ed_key_index,
+                              b->ed_key_first, ctx->stream);
+  uint32_t n_keys = 0;
+  if (e == hipSuccess) e = hipMemcpyAsync(&n_keys, counter, 4, hipMemcpyDeviceToHost, ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  if (e != hipSuccess) return done(hip_fail(ctx, e, "key dedupe"));
+  if (!key_reuse_mode(ne, n_keys)) {
+    dfree(ctx, b->ed_key_index);
+    dfree(ctx, b->ed_key_first);
+    b->ed_key_index = b->ed_key_first = nullptr;
+    return done(CG_OK);
+  }
+  b->n_keys = n_keys;
+  return done(CG_OK);
+}
+
+cg_status ensure_key_scratch(cg_ctx* ctx, uint32_t n_keys) {
+  if (ctx->ed_kcap >= n_keys) return CG_OK;
+  (void)hipStreamSynchronize(ctx->stream);
+  dfree(ctx, ctx->ed_ktab);
+  dfree(ctx, ctx->ed_kstat);
+  ctx->ed_ktab = nullptr;
+  ctx->ed_kstat = nullptr;
+  ctx->ed_kcap = 0;
+  cg_status st;
+  if ((st = dalloc(ctx, (uint8_t**)&ctx->ed_ktab, cg::ed25519_key_table_bytes(n_keys), "alloc key tables")) != CG_OK ||
+      (st = dalloc(ctx, &ctx->ed_kstat, n_keys, "alloc key status")) != CG_OK)
+    return st;
+  ctx->ed_kcap = n_keys;
+  return CG_OK;
+}
+
 // Stages a batch (see MsgSrc for where its clear data lives).
 cg_status create_batch(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const uint8_t* pk, size_t pk_stride,
                        const uint8_t* sig, size_t sig_stride, const uint32_t* sig_len, const MsgSrc& m,
@@ -605,6 +687,7 @@ cg_status create_batch(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const ui
       if (e == hipSuccess) e = cg::launch_gather_u64(b->msg_off_all, b->ed_index, ne, b->ed_msg_off, ctx->stream);
       if (e == hipSuccess) e = cg::launch_gather_u32(b->msg_len_all, b->ed_index, ne, b->ed_msg_len, 0, ctx->stream);
       if (e != hipSuccess) return bail(hip_fail(ctx, e, "stage ed25519"));
+      if ((st = stage_key_dedupe(ctx, b)) != CG_OK) return bail(st);
     }
     for (int c = 0; c < 2; ++c) {
       const std::vector<uint32_t>& ix = idx[1 + c];
@@ -703,6 +786,16 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode) {
     if (b->n_ed) {
       cg_status s2 = ensure_ed_scratch(ctx, b->n_ed);
       if (s2 != CG_OK) return s2;
+      if (b->ed_key_index) {  // key-reuse path: every distinct key decoded once, its tables built once
+        if ((s2 = ensure_key_scratch(ctx, b->n_keys)) != CG_OK) return s2;
+        cg::Ed25519Dev kd;
+        kd.pk = b->ed_pk;
+        kd.cap = b->n_ed;
+        kd.ktab = ctx->ed_ktab;
+        kd.kstat = ctx->ed_kstat;
+        Timed t(ctx, "ed25519_keyprep", b->n_keys);
+        CG_TRY(ctx, cg::launch_ed25519_keyprep(kd, b->ed_key_first, b->n_keys, ctx->stream), "launch ed25519_keyprep");
+      }
       for (uint32_t base = 0; base < b->n_ed; base += ctx->ed_scap) {
         const uint32_t cnt = std::min(ctx->ed_scap, b->n_ed - base);
         cg::Ed25519Dev d;
@@ -720,6 +813,11 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode) {
         d.btab = ctx->btab;
         d.full_mod = ctx->debug_full_mod;
         d.index_base = base;
+        if (b->ed_key_index) {
+          d.key_index = b->ed_key_index + base;
+          d.ktab = ctx->ed_ktab;
+          d.kstat = ctx->ed_kstat;
+        }
         {
           Timed t(ctx, "ed25519_hash", cnt);
           CG_TRY(ctx, cg::launch_ed25519_hash(d, cnt, (uint32_t)mode, ctx->stream), "launch ed25519_hash");

@@ -38,6 +38,7 @@ CG_DEV int4* lane_table(int32_t* table, uint32_t i) {
   return reinterpret_cast<int4*>(table + (size_t)i * (kLaneEntries * kTabLimbs));
 }
 
+template <bool REUSE>
 __global__ __launch_bounds__(256) void cg_ed25519_hash(const uint32_t* __restrict__ pk, const uint32_t* __restrict__ sig,
                                                        const uint32_t* __restrict__ sig_len,
                                                        const uint8_t* __restrict__ arena,
@@ -52,8 +53,8 @@ __global__ __launch_bounds__(256) void cg_ed25519_hash(const uint32_t* __restric
   CG_UNROLL for (int w = 0; w < 8; ++w) pkw[w] = pk[(size_t)w * cap + i];
   CG_UNROLL for (int w = 0; w < 16; ++w) sw[w] = sig[(size_t)w * cap + i];
   const bool force_full = full_mod != 0 && (index_base + i) % full_mod == 0;  // cg_set_debug test hook
-  const uint32_t pre =
-      ed25519_hash_stage(pkw, sw, sig_len[i], arena + msg_off[i], msg_len[i], mode, dig, ndig, rneg, force_full);
+  const uint32_t pre = ed25519_hash_stage<false, REUSE>(pkw, sw, sig_len[i], arena + msg_off[i], msg_len[i], mode, dig,
+                                                       ndig, rneg, force_full);
   status[i] = pre | ndig << 8 | rneg << 16;
   if (pre != V_COMPUTE) return;
   CG_UNROLL for (int w = 0; w < kDigitWords; ++w) digits[(size_t)w * scap + i] = dig[w];
@@ -112,13 +113,52 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_POINTS_W
   });
 }
 
-// The shared B tables: entry k of table t = k * 2^(128 t) B in affine form,
-// one lane per entry (2 * (2^(kBWin-1) + 1) lanes), at context creation.
+// Key-reuse path, once per distinct key and verify call: decode A and build its
+// four tables k * 2^(64 t) (-A) (lane-contiguous, kKeyEntries entries per key).
+constexpr int kKeyEntries = 4 * kATabEntries;
+CG_DEV int4* key_table(int32_t* ktab, uint32_t j) {
+  return reinterpret_cast<int4*>(ktab + (size_t)j * (kKeyEntries * kTabLimbs));
+}
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_POINTS_WAVES, 8))) void cg_ed25519_keyprep(
+    const uint32_t* __restrict__ pk, uint32_t cap, const uint32_t* __restrict__ key_first, uint32_t n_keys,
+    int32_t* __restrict__ ktab, uint32_t* __restrict__ kstat) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n_keys) return;
+  const uint32_t e = key_first[j];
+  uint32_t pkw[8];
+  CG_UNROLL for (int w = 0; w < 8; ++w) pkw[w] = pk[(size_t)w * cap + e];
+  int4* kt = key_table(ktab, j);
+  kstat[j] = ed25519_key_tables(pkw, [&](int t, int k, const ge_cached& c) CG_LINLINE {
+    store_cached(kt + (t * kATabEntries + k) * (kTabLimbs / 4), c);
+  });
+}
+
+// Key-reuse path, per signature: decode R only (the key's verdict comes from its
+// distinct-key slot) and build k*R in the lane table.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_POINTS_WAVES, 8))) void cg_ed25519_points_r(
+    const uint32_t* __restrict__ sig, uint32_t n, uint32_t cap, const uint32_t* __restrict__ key_index,
+    const uint32_t* __restrict__ kstat, uint32_t* __restrict__ status, int32_t* __restrict__ table) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t rw[8];
+  CG_UNROLL for (int w = 0; w < 8; ++w) rw[w] = sig[(size_t)w * cap + i];
+  const uint32_t st = status[i];
+  ge_p3 R;
+  const uint32_t v = ed25519_points_stage_r(rw, ed_status_verdict(st), kstat[key_index[i]], R);
+  if (v != ed_status_verdict(st)) status[i] = (st & ~0xffu) | v;
+  if (v != V_COMPUTE) return;
+  int4* lt = lane_table(table, i);
+  ed25519_build_table(R, [&](int k, const ge_cached& c) { store_cached(lt + k * (kTabLimbs / 4), c); });
+}
+
+// The shared B tables: entry k of table t = k * 2^(64 t) B in affine form, t = 0..3,
+// one lane per entry (4 * (2^(kBWin-1) + 1) lanes), at context creation.
+constexpr int kBTables = 4;
 __global__ __launch_bounds__(256) void cg_ed25519_btab_build(int32_t* __restrict__ btab) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= 2 * (uint32_t)kBTabEntries) return;
+  if (i >= kBTables * (uint32_t)kBTabEntries) return;
   ge_precomp e;
-  ed25519_btab_entry(e, i / kBTabEntries, i % kBTabEntries);
+  ed25519_btab_entry(e, i / kBTabEntries, i % kBTabEntries);  // table t = k * 2^(64 t) B
   int32_t* o = btab + (size_t)i * kBStride;
   CG_UNROLL for (int l = 0; l < 10; ++l) {
     o[l] = e.yplusx.v[l];
@@ -178,39 +218,112 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_MSM_WAVE
   verdict[dst] = ok ? (uint8_t)V_ACCEPT : (uint8_t)V_REJECT;
 }
 
+CG_DEV void load_bentry(const int32_t* btab_g, uint32_t t, uint32_t k, ge_precomp& p) {
+  // one 128-byte line per entry: eight 16-byte loads (L2 / MALL resident table)
+  const int4* b = reinterpret_cast<const int4*>(btab_g + ((size_t)t * kBTabEntries + k) * kBStride);
+  int32_t v[kBStride];
+  CG_UNROLL for (int q = 0; q < kBStride / 4; ++q) {
+    const int4 x = b[q];
+    v[4 * q] = x.x;
+    v[4 * q + 1] = x.y;
+    v[4 * q + 2] = x.z;
+    v[4 * q + 3] = x.w;
+  }
+  CG_UNROLL for (int l = 0; l < 10; ++l) {
+    p.yplusx.v[l] = v[l];
+    p.yminusx.v[l] = v[10 + l];
+    p.xy2d.v[l] = v[20 + l];
+  }
+}
+
+CG_DEV uint32_t wave_or(uint32_t v) { return __ballot(v != 0) != 0ull; }
+
+// MSM of the key-reuse split (cg_ed25519.h ed25519_msm_reuse): per-key A tables,
+// per-lane R table, four shared B tables; 60 doublings.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_MSM_WAVES, CG_MSM_WAVES))) void cg_ed25519_msm_r(
+    const uint32_t* __restrict__ status, const uint32_t* __restrict__ digits, const int32_t* __restrict__ table,
+    const int32_t* __restrict__ ktab, const uint32_t* __restrict__ key_index, const int32_t* __restrict__ btab_g,
+    uint32_t n, uint32_t scap, const uint32_t* __restrict__ out_index, uint8_t* __restrict__ verdict) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t st = i < n ? status[i] : 0u;
+  const bool live = i < n && ed_status_verdict(st) == V_COMPUTE;
+  // wave-uniform loop shape: the most chunk-3 windows and a 17th c1 digit in any lane
+  const uint32_t shape = live ? ed_status_ndig(st) : 0u;
+  const uint32_t c3w = wave_max(shape & 31u), win17 = wave_or(shape >> 5);
+  if (i >= n) return;
+  const uint32_t dst = out_index ? out_index[i] : i;
+  if (!live) {
+    verdict[dst] = (uint8_t)ed_status_verdict(st);
+    return;
+  }
+  uint32_t dig[kDigitWords];
+  CG_UNROLL for (int w = 0; w < kDigitWords; ++w) dig[w] = digits[(size_t)w * scap + i];
+  const int4* lt = lane_table(const_cast<int32_t*>(table), i);
+  const int4* kt = key_table(const_cast<int32_t*>(ktab), key_index[i]);
+  const uint32_t ok = ed25519_msm_reuse(
+      c3w, win17, dig, ed_status_rneg(st),
+      [&](uint32_t t, uint32_t k, ge_cached& c) CG_LINLINE {
+        load_cached(kt + (t * kATabEntries + k) * (kTabLimbs / 4), c);
+      },
+      [&](uint32_t k, ge_cached& c) CG_LINLINE { load_cached(lt + k * (kTabLimbs / 4), c); },
+      [&](uint32_t t, uint32_t k, ge_precomp& p) CG_LINLINE { load_bentry(btab_g, t, k, p); });
+  verdict[dst] = ok ? (uint8_t)V_ACCEPT : (uint8_t)V_REJECT;
+}
+
 }  // namespace
 
 namespace cg {
 
 size_t ed25519_table_bytes(uint32_t scap) { return (size_t)kLaneEntries * kTabLimbs * scap * sizeof(int32_t); }
 size_t ed25519_digit_words() { return kDigitWords; }
-size_t ed25519_btab_words() { return (size_t)2 * kBTabEntries * kBStride; }
+size_t ed25519_btab_words() { return (size_t)kBTables * kBTabEntries * kBStride; }
+size_t ed25519_key_table_bytes(uint32_t n_keys) { return (size_t)kKeyEntries * kTabLimbs * n_keys * sizeof(int32_t); }
 
 hipError_t launch_ed25519_btab_build(int32_t* btab, hipStream_t s) {
-  const uint32_t n = 2 * kBTabEntries;
+  const uint32_t n = kBTables * kBTabEntries;
   hipLaunchKernelGGL(cg_ed25519_btab_build, dim3((n + 255) / 256), dim3(256), 0, s, btab);
   return hipGetLastError();
 }
 
 hipError_t launch_ed25519_hash(const Ed25519Dev& d, uint32_t n, uint32_t mode, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(cg_ed25519_hash, dim3((n + 255) / 256), dim3(256), 0, s, d.pk, d.sig, d.sig_len, d.arena,
-                     d.msg_off, d.msg_len, n, d.cap, d.scap, mode, d.status, d.digits, d.full_mod, d.index_base);
+  if (d.key_index)
+    hipLaunchKernelGGL(cg_ed25519_hash<true>, dim3((n + 255) / 256), dim3(256), 0, s, d.pk, d.sig, d.sig_len, d.arena,
+                       d.msg_off, d.msg_len, n, d.cap, d.scap, mode, d.status, d.digits, d.full_mod, d.index_base);
+  else
+    hipLaunchKernelGGL(cg_ed25519_hash<false>, dim3((n + 255) / 256), dim3(256), 0, s, d.pk, d.sig, d.sig_len,
+                       d.arena, d.msg_off, d.msg_len, n, d.cap, d.scap, mode, d.status, d.digits, d.full_mod,
+                       d.index_base);
+  return hipGetLastError();
+}
+
+hipError_t launch_ed25519_keyprep(const Ed25519Dev& d, const uint32_t* key_first, uint32_t n_keys, hipStream_t s) {
+  if (n_keys == 0) return hipSuccess;
+  hipLaunchKernelGGL(cg_ed25519_keyprep, dim3((n_keys + 255) / 256), dim3(256), 0, s, d.pk, d.cap, key_first, n_keys,
+                     const_cast<int32_t*>(d.ktab), const_cast<uint32_t*>(d.kstat));
   return hipGetLastError();
 }
 
 hipError_t launch_ed25519_points(const Ed25519Dev& d, uint32_t n, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(cg_ed25519_points, dim3((n + 255) / 256), dim3(256), 0, s, d.pk, d.sig, n, d.cap, d.status,
-                     d.table);
+  if (d.key_index)
+    hipLaunchKernelGGL(cg_ed25519_points_r, dim3((n + 255) / 256), dim3(256), 0, s, d.sig, n, d.cap, d.key_index,
+                       d.kstat, d.status, d.table);
+  else
+    hipLaunchKernelGGL(cg_ed25519_points, dim3((n + 255) / 256), dim3(256), 0, s, d.pk, d.sig, n, d.cap, d.status,
+                       d.table);
   return hipGetLastError();
 }
 
 hipError_t launch_ed25519_msm(const Ed25519Dev& d, uint32_t n, const uint32_t* out_index, uint8_t* verdict,
                               hipStream_t s) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(cg_ed25519_msm, dim3((n + 255) / 256), dim3(256), 0, s, d.sig, d.status, d.digits, d.table,
-                     d.btab, n, d.cap, d.scap, out_index, verdict);
+  if (d.key_index)
+    hipLaunchKernelGGL(cg_ed25519_msm_r, dim3((n + 255) / 256), dim3(256), 0, s, d.status, d.digits, d.table, d.ktab,
+                       d.key_index, d.btab, n, d.scap, out_index, verdict);
+  else
+    hipLaunchKernelGGL(cg_ed25519_msm, dim3((n + 255) / 256), dim3(256), 0, s, d.sig, d.status, d.digits, d.table,
+                       d.btab, n, d.cap, d.scap, out_index, verdict);
   return hipGetLastError();
 }
 

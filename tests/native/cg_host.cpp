@@ -61,19 +61,22 @@ int cgh_half_scalars(const uint32_t* h, uint32_t* c0, uint32_t* c1, uint32_t* c1
   return (int)ed25519_half_scalars(h, c0, c1, *c1neg);
 }
 
-static ge_precomp g_btab[2][kBTabEntries];  // the device's shared tables, built with the same code
+static ge_precomp g_btab[4][kBTabEntries];  // the device's shared tables k * 2^(64 t) B, built with the same code
 static int g_init;
+
+static void init_btab() {
+  if (g_init) return;
+  for (uint32_t t = 0; t < 4; ++t)
+    for (uint32_t k = 0; k < (uint32_t)kBTabEntries; ++k) ed25519_btab_entry(g_btab[t][k], t, k);
+  g_init = 1;
+}
 
 // The three device phases in sequence (hash -> points -> msm) for one signature;
 // the digit count is the lane's own (on the device it is the wave maximum, which
 // only adds leading zero digits).  force_ndig > 0 overrides it.
 int cgh_ed25519_verify_nd(const uint8_t* pk_bytes, const uint8_t* sig_bytes, uint32_t sig_len, const uint8_t* msg,
                           uint32_t msg_len, uint32_t mode, uint32_t force_ndig, uint32_t full_length) {
-  if (!g_init) {
-    for (uint32_t t = 0; t < 2; ++t)
-      for (uint32_t k = 0; k < (uint32_t)kBTabEntries; ++k) ed25519_btab_entry(g_btab[t][k], t, k);
-    g_init = 1;
-  }
+  init_btab();
   uint32_t pk[8], sig[16] = {0};
   memcpy(pk, pk_bytes, 32);
   memcpy(sig, sig_bytes, sig_len < 64 ? sig_len : 64);
@@ -96,6 +99,34 @@ int cgh_ed25519_verify_nd(const uint8_t* pk_bytes, const uint8_t* sig_bytes, uin
 int cgh_ed25519_verify(const uint8_t* pk_bytes, const uint8_t* sig_bytes, uint32_t sig_len, const uint8_t* msg,
                        uint32_t msg_len, uint32_t mode) {
   return cgh_ed25519_verify_nd(pk_bytes, sig_bytes, sig_len, msg, msg_len, mode, 0, 0);
+}
+
+// The key-reuse path's phases (keyprep -> hash<REUSE> -> points_r -> msm_reuse) for
+// one signature; wide forces the all-chunk loop a fallback lane elsewhere in the
+// wave would cause; full_length forces this lane's own (h, 1) fallback.
+int cgh_ed25519_verify_reuse(const uint8_t* pk_bytes, const uint8_t* sig_bytes, uint32_t sig_len, const uint8_t* msg,
+                             uint32_t msg_len, uint32_t mode, uint32_t wide, uint32_t full_length) {
+  init_btab();
+  uint32_t pk[8], sig[16] = {0};
+  memcpy(pk, pk_bytes, 32);
+  memcpy(sig, sig_bytes, sig_len < 64 ? sig_len : 64);
+  static ge_cached kt[4][kATabEntries];
+  const uint32_t key_ok = ed25519_key_tables(pk, [&](int t, int k, const ge_cached& c) { kt[t][k] = c; });
+  uint32_t dig[kDigitWords], w, rneg;
+  uint32_t pre = ed25519_hash_stage<false, true>(pk, sig, sig_len, msg, msg_len, mode, dig, w, rneg, full_length != 0);
+  ge_p3 R;
+  pre = ed25519_points_stage_r(sig, pre, key_ok, R);
+  if (pre != V_COMPUTE) return (int)pre;
+  ge_cached tr[kATabEntries];
+  ed25519_build_table(R, [&](int k, const ge_cached& c) { tr[k] = c; });
+  const uint32_t ok = ed25519_msm_reuse(
+      wide ? 16u : (w & 31u), wide ? 1u : (w >> 5), dig, rneg, [&](uint32_t t, uint32_t k, ge_cached& c) { c = kt[t][k]; },
+      [&](uint32_t k, ge_cached& c) { c = tr[k]; }, [&](uint32_t t, uint32_t k, ge_precomp& p) { p = g_btab[t][k]; });
+  return ok ? (int)V_ACCEPT : (int)V_REJECT;
+}
+
+int cgh_half_scalars_reuse(const uint32_t* h, uint32_t* c0, uint32_t* c1, uint32_t* c1neg) {
+  return (int)ed25519_half_scalars<192, 66>(h, c0, c1, *c1neg);
 }
 }
 

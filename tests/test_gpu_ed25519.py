@@ -215,3 +215,67 @@ def test_forced_full_length_fallback_vs_oracle(gpu_ctx, oracle, golden_ed25519, 
         assert (got == ACCEPT).sum() > 2000
     finally:
         gpu_ctx.set_debug(DEBUG_FORCE_FULL_LENGTH, 0)
+
+
+@pytest.fixture
+def key_reuse(monkeypatch, request):
+    """CORDA_AMD_KEY_REUSE: '1' forces the key-reuse path, '0' the balanced one,
+    unset = automatic (distinct keys <= n / 8)."""
+    if request.param is None:
+        monkeypatch.delenv("CORDA_AMD_KEY_REUSE", raising=False)
+    else:
+        monkeypatch.setenv("CORDA_AMD_KEY_REUSE", request.param)
+    return request.param
+
+
+@pytest.mark.parametrize("key_reuse", ["1"], indirect=True)
+def test_key_reuse_path_golden_fixtures(gpu_ctx, golden_ed25519, key_reuse):
+    """Every golden class E1-E12 through the key-reuse path (device key dedupe,
+    per-key decode + tables 2^(64 t)(-A), R-only points kernel, 64-doubling msm):
+    torsion / mixed-order / non-canonical keys, KEY_INVALID from the per-key decode
+    taking precedence over ARG_EMPTY / SIG_MALFORMED of each signature."""
+    g = golden_ed25519 * 3  # every key at least three times
+    pks = [bytes.fromhex(e["pk"]) for e in g]
+    sigs = [bytes.fromhex(e["sig"]) for e in g]
+    msgs = [bytes.fromhex(e["msg"]) for e in g]
+    for mode, key in ((MODE_IS_VALID, "is_valid"), (MODE_DO_VERIFY, "do_verify")):
+        v = crypto.verify_packed(gpu_ctx, crypto.pack(crypto.EDDSA_ED25519_SHA512, pks, sigs, msgs), mode)
+        exp = np.array([e[key] for e in g], dtype=np.uint8)
+        bad = np.flatnonzero(v != exp)
+        assert bad.size == 0, [(g[i]["cls"], int(v[i]), int(exp[i])) for i in bad[:10]]
+
+
+@pytest.mark.parametrize("key_reuse", [None, "1"], indirect=True)
+@pytest.mark.parametrize("n_keys", [1, 16, 300])
+def test_key_reuse_random_signers_vs_oracle(gpu_ctx, oracle, key_reuse, n_keys):
+    """A notary-backlog shape: 20k signatures by n_keys signers (automatic mode picks
+    the key-reuse path), 25 % mutated over E1-E12, both modes, against the oracle;
+    and again with the (h, 1) fallback forced on every 5th signature (wide waves)."""
+    from corda_amd._lib import DEBUG_FORCE_FULL_LENGTH
+    w = datagen.make_batch(20_000, msg_bytes=48, seed=n_keys, key_base=4_000_000, key_reuse=n_keys)
+    w = datagen.add_ed25519_adversarial(w, frac=0.25, seed=n_keys + 1)
+    for mod in (0, 5):
+        gpu_ctx.set_debug(DEBUG_FORCE_FULL_LENGTH, mod)
+        try:
+            for mode in (MODE_IS_VALID, MODE_DO_VERIFY):
+                got = gpu_verdicts(gpu_ctx, w, mode)
+                assert np.array_equal(got, oracle_verdicts(oracle, w, mode)), (mod, mode)
+        finally:
+            gpu_ctx.set_debug(DEBUG_FORCE_FULL_LENGTH, 0)
+    assert (got == ACCEPT).sum() > 14000
+
+
+@pytest.mark.parametrize("key_reuse", [None], indirect=True)
+def test_key_reuse_prepared_batch_bitmap(gpu_ctx, oracle, key_reuse):
+    """Prepared batch on the reuse path verified twice (per-key tables rebuilt each
+    call) with the device bitmap, plus a distinct-key batch in the same context
+    (balanced path) in between."""
+    w = datagen.add_ed25519_adversarial(datagen.make_batch(70_001, msg_bytes=32, seed=3, key_reuse=40), 0.02, seed=2)
+    pb = crypto.PreparedBatch(gpu_ctx, crypto.PackedBatch(w.n, w.scheme, w.pk, w.pk_stride, w.sig, w.sig_stride,
+                                                          w.sig_len, w.msg, w.msg_off, w.msg_len))
+    exp = oracle_verdicts(oracle, w, MODE_IS_VALID)
+    assert np.array_equal(pb.verify(MODE_IS_VALID), exp)
+    d = datagen.make_batch(3000, msg_bytes=32, seed=4, key_base=99)
+    assert (gpu_verdicts(gpu_ctx, d, MODE_IS_VALID) == ACCEPT).all()
+    assert np.array_equal(pb.verify(MODE_IS_VALID), exp)
+    pb.close()

@@ -32,6 +32,8 @@ def host():
                                        ctypes.c_uint32, ctypes.c_uint32]
     lib.cgh_ed25519_verify_nd.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p,
                                           ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]
+    lib.cgh_ed25519_verify_reuse.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p,
+                                             ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]
     return lib
 
 
@@ -161,12 +163,15 @@ def test_half_scalars_property(host):
             assert (C0, C1) == (h, 1)
 
 
-def _half_scalars_euclid(h):
-    """Plain step-by-step Euclid on (8L, h) to the first remainder below 2^128 and
+def _half_scalars_euclid(h, tb_bits=128, c1_bits=252):
+    def cost(l0, l1):
+        return max(l0, l1) if tb_bits == 128 else (1000 if l1 > c1_bits else l0)
+
+    """Plain step-by-step Euclid on (8L, h) to the first remainder below 2^tb_bits and
     the candidate choice of cg_halfscalar.h: the device's Lehmer version must land
     on exactly these (c0, |c1|, sign), or return None for the (h, 1) fallback."""
     a, b, ta, tb = 8 * L, h, 0, 1
-    while b >= 1 << 128:
+    while b >= 1 << tb_bits:
         q = a // b
         if q >= 1 << 31:
             return None
@@ -174,14 +179,14 @@ def _half_scalars_euclid(h):
     x0, x1 = b, tb
     if tb % 2 == 0:
         x0, x1 = a, ta
-        best = max(a.bit_length(), abs(ta).bit_length())
+        best = cost(a.bit_length(), abs(ta).bit_length())
         if b:
             q = a // b
             if q < 1 << 31:
                 r, tn = a - q * b, ta - q * tb
-                if max(r.bit_length(), abs(tn).bit_length()) < best:
+                if cost(r.bit_length(), abs(tn).bit_length()) < best:
                     x0, x1 = r, tn
-    if x1 % 2 == 0 or x0.bit_length() > 252 or abs(x1).bit_length() > 252:
+    if x1 % 2 == 0 or x0.bit_length() > 252 or abs(x1).bit_length() > c1_bits:
         return None
     return x0, abs(x1), int(x1 < 0)
 
@@ -419,3 +424,58 @@ def test_ecdsa_joint_exceptional_cases(host):
                         assert inf == 1, (scheme, d, t)
                     else:
                         assert inf == 0 and val(out) == exp[0] and val(out[8:], 8) == exp[1], (scheme, d, t)
+
+
+def test_half_scalars_reuse_split_equals_euclid(host):
+    """The key-reuse split (TB = 192): c0 = c1 h (mod 8L), c1 odd, c0 ~ 2^192 (four
+    64-bit chunks over the per-key tables, chunk 3 only in its low windows),
+    |c1| < 2^66 (at most 17 signed radix-16 digits) — the Lehmer result equal to
+    plain Euclid's, or the (h, 1) fallback."""
+    host.cgh_half_scalars_reuse.argtypes = [ctypes.c_void_p] * 4
+    N = 8 * L
+    rnd = random.Random(23)
+    edge = [0, 1, 2, L - 1, 2**192 - 1, 2**192, 2**252, N // 3 % L]
+    hs = edge + [rnd.randrange(L) for _ in range(4000)]
+    uniform = set(hs[len(edge):])  # what SHA-512 mod L produces
+    hs += [rnd.randrange(1 << rnd.randrange(180, 253)) for _ in range(1000)]  # (h < 2^224: quotient >= 2^31)
+    n_fallback = 0
+    for h in hs:
+        c0, c1, neg = (ctypes.c_uint32 * 8)(), (ctypes.c_uint32 * 8)(), ctypes.c_uint32()
+        ok = host.cgh_half_scalars_reuse(w8(h), c0, c1, ctypes.byref(neg))
+        C0, C1 = val(c0), val(c1) * (-1 if neg.value else 1)
+        assert C1 % 2 == 1 and (C0 - C1 * h) % N == 0 and C0 >= 0, hex(h)
+        exp = _half_scalars_euclid(h, 192, 66)
+        if exp is None:
+            n_fallback += h in uniform
+            assert ok == 0 and (C0, C1) == (h, 1), hex(h)
+        else:
+            assert ok == 1 and (val(c0), val(c1), neg.value) == exp, hex(h)
+            # correct but long for an edge value with a huge partial quotient (the msm then
+            # runs every chunk-3 window: the hash phase flags c0 >= 2^196 as "wide")
+            assert abs(C1).bit_length() <= 66 and (h in edge or C0.bit_length() <= 200), hex(h)
+    assert n_fallback <= 2
+
+
+def test_verify_reuse_path_golden_and_random(host, golden_ed25519, oracle):
+    """The key-reuse path (per-key tables 2^(64 t)(-A), per-lane R only, 60
+    doublings): every golden class E1-E12 — torsion / mixed-order / non-canonical
+    keys included, KEY_INVALID from the per-key decode — with and without the wide
+    (fallback-in-wave) loop and the lane's own (h, 1) fallback, plus random
+    mutated signatures against the oracle."""
+    for e in golden_ed25519:
+        pk, sig, msg = (bytes.fromhex(e[k]) for k in ("pk", "sig", "msg"))
+        if len(pk) != 32:
+            continue
+        for wide, full in ((0, 0), (1, 0), (1, 1)):
+            assert host.cgh_ed25519_verify_reuse(pk, sig, len(sig), msg, len(msg), 0, wide, full) == e["is_valid"], \
+                (e["cls"], wide, full)
+        assert host.cgh_ed25519_verify_reuse(pk, sig, len(sig), msg, len(msg), 1, 0, 0) == e["do_verify"], e["cls"]
+    rnd = random.Random(9)
+    for _ in range(150):
+        seed, msg = rnd.randbytes(32), rnd.randbytes(rnd.randint(0, 90))
+        pk, sig = ED.sign(seed, msg)
+        s = int.from_bytes(sig[32:], "little")
+        cases = [(pk, sig), (pk, bytes([sig[0] ^ 4]) + sig[1:]), (pk, sig[:32] + ((s + L) % 2**256).to_bytes(32, "little"))]
+        for p, sg in cases:
+            assert host.cgh_ed25519_verify_reuse(p, sg, len(sg), msg, len(msg), 0, 0, 0) == \
+                oracle.oracle_ed25519_verify(p, sg, len(sg), msg, len(msg), 0)
