@@ -56,6 +56,7 @@ struct cg_ctx {
   // Ed25519 kernels on `stream` (fork/join events, no host sync)
   hipStream_t ec_stream[2] = {nullptr, nullptr};
   hipEvent_t ev_fork = nullptr, ev_join[2] = {nullptr, nullptr};
+  hipEvent_t ev_keys = nullptr;  // key-reuse path: per-key tables ready (keyprep runs on ec_stream[0])
   std::string err;
   int32_t* btab = nullptr;
   // Ed25519 chunk scratch
@@ -431,7 +432,8 @@ cg_status cg_open(int device, cg_ctx** out) {
       hipStreamCreateWithFlags(&ctx->ec_stream[1], hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_join[0], hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&ctx->ev_join[1], hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&ctx->ev_join[1], hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->ev_keys, hipEventDisableTiming) != hipSuccess) {
     cg_close(ctx);
     return CG_E_DEVICE;
   }
@@ -470,7 +472,7 @@ void cg_close(cg_ctx* ctx) {
     if (ctx->copy_stream) (void)hipStreamDestroy(ctx->copy_stream);
     for (hipStream_t es : ctx->ec_stream)
       if (es) (void)hipStreamDestroy(es);
-    for (hipEvent_t e : {ctx->ev_fork, ctx->ev_join[0], ctx->ev_join[1]})
+    for (hipEvent_t e : {ctx->ev_fork, ctx->ev_join[0], ctx->ev_join[1], ctx->ev_keys})
       if (e) (void)hipEventDestroy(e);
     delete ctx;
   } catch (...) {
@@ -756,6 +758,28 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode) {
     // elements of unsupported schemes keep this value
     CG_TRY(ctx, hipMemsetAsync(b->verdict, CG_UNSUPPORTED, n, ctx->stream), "init verdict");
     CG_TRY(ctx, hipEventRecord(ctx->ev_fork, ctx->stream), "fork ecdsa");
+    bool keys_pending = false;
+    if (b->n_ed && b->ed_key_index) {
+      // key-reuse path: every distinct key decoded once and its tables built once, on
+      // ec_stream[0] beside the hash kernel (one wave per 64 keys: latency-bound, it
+      // would otherwise serialize ~0.6 ms on the main stream); the points kernel waits
+      cg_status s2 = ensure_key_scratch(ctx, b->n_keys);
+      if (s2 != CG_OK) return s2;
+      hipStream_t ks = ctx->ec_stream[0];
+      CG_TRY(ctx, hipStreamWaitEvent(ks, ctx->ev_fork, 0), "fork keyprep");
+      joins[0] = true;
+      cg::Ed25519Dev kd;
+      kd.pk = b->ed_pk;
+      kd.cap = b->n_ed;
+      kd.ktab = ctx->ed_ktab;
+      kd.kstat = ctx->ed_kstat;
+      {
+        Timed t(ctx, "ed25519_keyprep", b->n_keys, ks);
+        CG_TRY(ctx, cg::launch_ed25519_keyprep(kd, b->ed_key_first, b->n_keys, ks), "launch ed25519_keyprep");
+      }
+      CG_TRY(ctx, hipEventRecord(ctx->ev_keys, ks), "keyprep ready");
+      keys_pending = true;
+    }
     // ECDSA: each curve on its own stream, forked after the verdict init and joined
     // before the bitmap (the verdict scatters touch disjoint positions); enqueued
     // first so they overlap the Ed25519 kernels below in mixed batches (config 4:
@@ -786,16 +810,6 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode) {
     if (b->n_ed) {
       cg_status s2 = ensure_ed_scratch(ctx, b->n_ed);
       if (s2 != CG_OK) return s2;
-      if (b->ed_key_index) {  // key-reuse path: every distinct key decoded once, its tables built once
-        if ((s2 = ensure_key_scratch(ctx, b->n_keys)) != CG_OK) return s2;
-        cg::Ed25519Dev kd;
-        kd.pk = b->ed_pk;
-        kd.cap = b->n_ed;
-        kd.ktab = ctx->ed_ktab;
-        kd.kstat = ctx->ed_kstat;
-        Timed t(ctx, "ed25519_keyprep", b->n_keys);
-        CG_TRY(ctx, cg::launch_ed25519_keyprep(kd, b->ed_key_first, b->n_keys, ctx->stream), "launch ed25519_keyprep");
-      }
       for (uint32_t base = 0; base < b->n_ed; base += ctx->ed_scap) {
         const uint32_t cnt = std::min(ctx->ed_scap, b->n_ed - base);
         cg::Ed25519Dev d;
@@ -821,6 +835,10 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode) {
         {
           Timed t(ctx, "ed25519_hash", cnt);
           CG_TRY(ctx, cg::launch_ed25519_hash(d, cnt, (uint32_t)mode, ctx->stream), "launch ed25519_hash");
+        }
+        if (keys_pending) {
+          CG_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_keys, 0), "wait keyprep");
+          keys_pending = false;
         }
         {
           Timed t(ctx, "ed25519_points", cnt);
