@@ -46,7 +46,8 @@ def occupancy(e, c, regs):
     """Register pressure (code object, tools/isa_regs.py) and the measured mean
     residency: SQ_WAVE_CYCLES counts quad-cycles summed over waves, GRBM_GUI_ACTIVE
     cycles summed over the 8 XCDs (MI355X_MICROARCH.md, PMC units)."""
-    r = regs.get(e.get("kernel_short", ""), {})
+    k = e.get("kernel_short", "")
+    r = regs.get(k) or next((v for n, v in regs.items() if n.startswith(k + "<")), {})
     for key in ("vgpr", "agpr", "sgpr", "vgpr_spill", "scratch_bytes", "lds_bytes", "waves_per_simd_limit"):
         if key in r:
             e[key] = r[key]
