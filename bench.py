@@ -72,13 +72,14 @@ PEAK = OP_MODEL["peak_int32_tops"]
 
 
 def kernel_src_hash() -> str:
-    """Hash of the device sources + build file; the PMC summaries carry the same
-    hash, so a bench line can say whether its instruction counts belong to the
-    kernels it ran (tools/pmc_report.py writes it)."""
+    """Hash of the device sources (*.hip, *.h) + build file; the PMC summaries carry
+    the same hash, so a bench line can say whether its instruction counts belong to
+    the kernels it ran (tools/pmc_report.py writes it; host-side cordagpu.cpp does
+    not change a kernel's instruction stream and is left out)."""
     d = os.path.join(ROOT, "corda_amd", "csrc")
     h = hashlib.sha256()
     for name in sorted(os.listdir(d)):
-        if name.endswith((".hip", ".h", ".cpp")) or name == "Makefile":
+        if name.endswith((".hip", ".h")) or name == "Makefile":
             with open(os.path.join(d, name), "rb") as f:
                 h.update(name.encode() + b"\0" + f.read())
     return h.hexdigest()[:16]

@@ -110,7 +110,7 @@ def src_identity():
         d = os.path.join(ROOT, "corda_amd", "csrc")
         h = hashlib.sha256()
         for name in sorted(os.listdir(d)):
-            if name.endswith((".hip", ".h", ".cpp")) or name == "Makefile":
+            if name.endswith((".hip", ".h")) or name == "Makefile":
                 with open(os.path.join(d, name), "rb") as f:
                     h.update(name.encode() + b"\0" + f.read())
         src_hash = h.hexdigest()[:16]
