@@ -102,7 +102,7 @@ def parse():
     p.add_argument("--cpu-sample", type=int, default=None, help="units in the CPU-baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--key-reuse", type=int, default=0,
-                   help="ed25519/backlog: draw signer keys from this many distinct keys (0 = all distinct)")
+                   help="ed25519/backlog/tx: draw signer keys from this many distinct keys (0 = all distinct)")
     p.add_argument("--dry-run", action="store_true",
                    help="launcher / barrier / all-gather logic over gloo on CPU, synthetic step (tests)")
     a = p.parse_args()
@@ -651,7 +651,7 @@ def run_tx(args, dist):
     rank, world = dist.rank, dist.world
     t_gen = time.perf_counter()
     p = datagen.make_tx_batch(pool, seed=4 + rank, key_base=9_000_000 + rank * 4 * pool, threads=cpu_threads(),
-                              tamper_frac=0.0)
+                              tamper_frac=0.0, key_reuse=args.key_reuse)
     w = datagen.tile_tx_batch(p, n_tx, tamper_frac=args.adversarial, seed=5 + rank)
     t_gen = time.perf_counter() - t_gen
     n_sig = int(w.sig_start[-1])
@@ -727,8 +727,9 @@ def run_tx(args, dist):
     line = base_line(args, dist, "SignedTransaction verifies/sec", "tx/s", value, elapsed * 1e3 / args.steps, {
         "workload": f"BASELINE config 4: {n_tx} SignedTransactions per GPU (trader-demo/loadtest shapes, "
                     f"{n_sig} signatures, 70/15/15 % Ed25519/R1/K1 over the 32 B id, {args.adversarial:.0%} "
-                    f"tampered); {pool} distinct txs tiled to size; host buffers (page-locked once via "
-                    "cg_register_host) in, per-tx first-bad out",
+                    f"tampered); {pool} distinct txs tiled to size; "
+                    + (f"signers drawn from {args.key_reuse} keys per scheme mix; " if args.key_reuse else "")
+                    + "host buffers (page-locked once via cg_register_host) in, per-tx first-bad out",
         "batch_per_gpu": n_tx, "global_batch": n_tx * world, "parallelism": f"dp{world} (tx-index shards)"})
     line.update({
         "signatures_per_s": round(n_sig * world * args.steps / elapsed, 1),

@@ -279,7 +279,7 @@ def _tx_components(n_tx: int, rng, seed: int):
 
 
 def make_tx_batch(n_tx: int, seed: int = 4, key_base: int = 9_000_000, threads: int | None = None,
-                  tamper_frac: float = 0.01) -> TxWorkload:
+                  tamper_frac: float = 0.01, key_reuse: int = 0) -> TxWorkload:
     """Trader-demo / loadtest shapes: inputs U{0..3},
     attachments U{0..1}, outputs U{1..3}, commands U{1..2}, notary 1,
     timeWindow p=0.3, salt 1; estimated Kryo sizes; signers = distinct command
@@ -303,9 +303,12 @@ def make_tx_batch(n_tx: int, seed: int = 4, key_base: int = 9_000_000, threads: 
     pk = np.zeros((total, 64), dtype=np.uint8)
     sig = np.zeros((total, 72), dtype=np.uint8)
     sig_len = np.zeros(total, dtype=np.uint32)
-    assert c.dg_sign_batch(total, scheme.ctypes.data, key_base, pk.ctypes.data, 64, sig.ctypes.data, 72,
-                           sig_len.ctypes.data, ids.ctypes.data, msg_off.ctypes.data, msg_len.ctypes.data,
-                           threads or min(16, os.cpu_count() or 1)) == 0
+    c.dg_set_key_options(key_reuse, 0)
+    rc = c.dg_sign_batch(total, scheme.ctypes.data, key_base, pk.ctypes.data, 64, sig.ctypes.data, 72,
+                         sig_len.ctypes.data, ids.ctypes.data, msg_off.ctypes.data, msg_len.ctypes.data,
+                         threads or min(16, os.cpu_count() or 1))
+    c.dg_set_key_options(0, 0)
+    assert rc == 0
     tampered = rng.random(n_tx) < tamper_frac
     for t in np.flatnonzero(tampered):
         c0 = int(comp_start[t])
