@@ -52,8 +52,14 @@ struct cg_ctx {
   int device = -1;
   hipStream_t stream = nullptr;
   hipStream_t copy_stream = nullptr;  // host-to-device uploads overlapped with `stream` (tx pipeline)
-  // the two ECDSA curves' pipelines run on their own streams, concurrently with the
-  // Ed25519 kernels on `stream` (fork/join events, no host sync)
+  hipStream_t hash_stream = nullptr;  // tx pipeline: Merkle ids of chunk k+1 beside chunk k's signatures
+  // the ECDSA curves' kernels run on their own streams, concurrently with the Ed25519
+  // kernels on `stream` (fork/join events, no host sync).  HIP maps streams onto
+  // GPU_MAX_HW_QUEUES hardware queues (default 4): stream, copy_stream, hash_stream
+  // and one ECDSA stream fill four, and a fifth stream would share a queue and
+  // serialize behind another stream's work (measured: the two curves of a tx chunk
+  // alternated).  So the curves get a stream each only when the process allows >= 5
+  // queues; otherwise ec_stream[1] aliases ec_stream[0].
   hipStream_t ec_stream[2] = {nullptr, nullptr};
   hipEvent_t ev_fork = nullptr, ev_join[2] = {nullptr, nullptr};
   hipEvent_t ev_keys = nullptr;  // key-reuse path: per-key tables ready (keyprep runs on ec_stream[0])
@@ -69,6 +75,13 @@ struct cg_ctx {
   int32_t* ed_ktab = nullptr;
   uint32_t* ed_kstat = nullptr;
   uint32_t* err_flag = nullptr;  // device word raised by kernels on malformed layouts
+  // page-locked staging for the host-built index vectors of the tx pipeline, so their
+  // uploads are truly asynchronous (a pageable hipMemcpyAsync waits for the stream);
+  // grow-only, handed out front to back while pin_active, reset per call
+  uint8_t* pin = nullptr;
+  size_t pin_cap = 0, pin_used = 0;
+  bool pin_active = false;
+  uint64_t pin_fallbacks = 0;  // uploads that found the staging area full
   bool profiling = false;
   std::map<std::string, Stat> stats;
   std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending;
@@ -140,6 +153,23 @@ struct Timed {
 };
 
 void collect_timings(cg_ctx* ctx) {
+  // CORDA_AMD_TIMELINE=<file>: every timed span of the call appended as
+  // "name items start_ms end_ms" relative to the call's first span (tools/timeline.py)
+  static const char* tl_path = std::getenv("CORDA_AMD_TIMELINE");
+  if (tl_path && !ctx->pending.empty()) {
+    if (FILE* f = std::fopen(tl_path, "a")) {
+      const hipEvent_t ref = ctx->pending.front().second.first;
+      std::fprintf(f, "# call\n");
+      for (auto& p : ctx->pending) {
+        float t0 = 0, t1 = 0;
+        if (hipEventSynchronize(p.second.second) == hipSuccess &&
+            hipEventElapsedTime(&t0, ref, p.second.first) == hipSuccess &&
+            hipEventElapsedTime(&t1, ref, p.second.second) == hipSuccess)
+          std::fprintf(f, "%s %.4f %.4f\n", p.first.c_str(), t0, t1);
+      }
+      std::fclose(f);
+    }
+  }
   for (auto& p : ctx->pending) {
     float ms = 0;
     if (hipEventSynchronize(p.second.second) == hipSuccess &&
@@ -230,6 +260,24 @@ cg_status upload(cg_ctx* ctx, T** dst, const T* src, size_t count, const char* w
   return CG_OK;
 }
 
+// upload() of a host vector that dies before the copy runs: through the pinned
+// staging area when the tx pipeline has one active (the copy then never blocks the
+// host), else a plain upload followed by the caller's stream sync.
+cg_status upload_idx(cg_ctx* ctx, uint32_t** dst, const uint32_t* src, size_t count, const char* what) {
+  const size_t bytes = (count * 4 + 255) & ~(size_t)255;
+  if (!ctx->pin_active || ctx->pin_used + bytes > ctx->pin_cap) {
+    ctx->pin_fallbacks += ctx->pin_active;
+    return upload(ctx, dst, src, count, what);
+  }
+  cg_status st = dalloc(ctx, dst, count, what);
+  if (st != CG_OK) return st;
+  uint8_t* h = ctx->pin + ctx->pin_used;
+  ctx->pin_used += bytes;
+  std::memcpy(h, src, count * 4);
+  if (count) CG_TRY(ctx, hipMemcpyAsync(*dst, h, count * 4, hipMemcpyHostToDevice, ctx->stream), what);
+  return CG_OK;
+}
+
 cg_status ensure_ed_scratch(cg_ctx* ctx, uint32_t need) {
   const uint32_t want = std::min(need, kEdChunk);
   if (ctx->ed_scap >= want) return CG_OK;
@@ -256,6 +304,7 @@ cg_status ensure_ed_scratch(cg_ctx* ctx, uint32_t need) {
 struct cg_batch {
   size_t n = 0;
   uint8_t* verdict = nullptr;   // [n]
+  bool verdict_owned = true;    // false: a slice of the tx pipeline's verdict array
   uint32_t* bitmap = nullptr;   // [ceil(n/32)]
   uint8_t* arena = nullptr;     // message arena (+16 pad)
   bool arena_owned = true;
@@ -283,7 +332,7 @@ namespace {
 
 void batch_free(cg_ctx* ctx, cg_batch* b) {
   if (!b) return;
-  dfree(ctx, b->verdict);
+  if (b->verdict_owned) dfree(ctx, b->verdict);
   dfree(ctx, b->bitmap);
   if (b->arena_owned) dfree(ctx, b->arena);
   if (b->meta_owned) {
@@ -322,6 +371,10 @@ struct MsgSrc {
   const uint8_t* sig_dev = nullptr;
   const uint32_t* sl_dev = nullptr;
   hipEvent_t raw_ready = nullptr;
+  // tx pipeline: verdicts straight into this device slice; staging ends without a
+  // host sync (the caller keeps the batch until its own final sync)
+  uint8_t* verdict_dev = nullptr;
+  bool async = false;
 };
 
 cg_status check_inputs(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const uint8_t* pk, size_t pk_stride,
@@ -368,7 +421,7 @@ cg_status api_guard_fail(cg_ctx* ctx) noexcept {
   }
   if (ctx) {
     (void)hipSetDevice(ctx->device);
-    for (hipStream_t s : {ctx->stream, ctx->copy_stream, ctx->ec_stream[0], ctx->ec_stream[1]})
+    for (hipStream_t s : {ctx->stream, ctx->copy_stream, ctx->hash_stream, ctx->ec_stream[0], ctx->ec_stream[1]})
       if (s) (void)hipStreamSynchronize(s);
     try {
       ctx->err = msg;
@@ -428,8 +481,8 @@ cg_status cg_open(int device, cg_ctx** out) {
     return CG_E_DEVICE;
   }
   if (hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&ctx->hash_stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&ctx->ec_stream[0], hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&ctx->ec_stream[1], hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_join[0], hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_join[1], hipEventDisableTiming) != hipSuccess ||
@@ -437,6 +490,10 @@ cg_status cg_open(int device, cg_ctx** out) {
     cg_close(ctx);
     return CG_E_DEVICE;
   }
+  const char* hwq = std::getenv("GPU_MAX_HW_QUEUES");
+  if (!hwq || std::atoi(hwq) < 5 ||
+      hipStreamCreateWithFlags(&ctx->ec_stream[1], hipStreamNonBlocking) != hipSuccess)
+    ctx->ec_stream[1] = ctx->ec_stream[0];
   // the shared Ed25519 base tables (k*B, k*2^128 B) are built on the device, once per context
   if (dalloc(ctx, &ctx->btab, cg::ed25519_btab_words(), "alloc base table") != CG_OK ||
       cg::launch_ed25519_btab_build(ctx->btab, ctx->stream) != hipSuccess ||
@@ -460,6 +517,7 @@ void cg_close(cg_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->copy_stream) (void)hipStreamSynchronize(ctx->copy_stream);
+    if (ctx->hash_stream) (void)hipStreamSynchronize(ctx->hash_stream);
     for (hipStream_t es : ctx->ec_stream)
       if (es) (void)hipStreamSynchronize(es);
     collect_timings(ctx);
@@ -470,10 +528,12 @@ void cg_close(cg_ctx* ctx) {
     for (hipEvent_t e : ctx->event_pool) (void)hipEventDestroy(e);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     if (ctx->copy_stream) (void)hipStreamDestroy(ctx->copy_stream);
-    for (hipStream_t es : ctx->ec_stream)
-      if (es) (void)hipStreamDestroy(es);
+    if (ctx->hash_stream) (void)hipStreamDestroy(ctx->hash_stream);
+    if (ctx->ec_stream[1] && ctx->ec_stream[1] != ctx->ec_stream[0]) (void)hipStreamDestroy(ctx->ec_stream[1]);
+    if (ctx->ec_stream[0]) (void)hipStreamDestroy(ctx->ec_stream[0]);
     for (hipEvent_t e : {ctx->ev_fork, ctx->ev_join[0], ctx->ev_join[1], ctx->ev_keys})
       if (e) (void)hipEventDestroy(e);
+    if (ctx->pin) (void)hipHostFree(ctx->pin);
     delete ctx;
   } catch (...) {
     // nothing to report from a destructor-like call; never unwind into the caller
@@ -533,10 +593,32 @@ bool key_reuse_mode(uint32_t n, uint32_t n_keys) {
 
 // Distinct Ed25519 keys of a staged batch (device hash table, stage_kernels.hip);
 // keeps key_index / key_first only when the key-reuse path will be used.
-cg_status stage_key_dedupe(cg_ctx* ctx, cg_batch* b) {
+// Automatic mode first looks at a pseudo-random sample of the keys on the host: the
+// exact device count (which needs a host round trip) only runs when the sample holds
+// enough repeats for n / n_keys >= 8 to be plausible (half the birthday-bound
+// threshold, so a true reuse batch passes with a wide margin).
+bool key_sample_suggests_reuse(const uint8_t* pk, size_t pk_stride, const std::vector<uint32_t>& idx0, uint32_t ne) {
+  constexpr uint32_t kSample = 1024;
+  if (ne < 8 * kSample) return true;  // small batch: the exact count is cheap
+  std::vector<std::array<uint8_t, 32>> keys(kSample);
+  for (uint32_t j = 0; j < kSample; ++j) {
+    const uint64_t i = ((uint64_t)j * 0x9E3779B1u + 12345u) % ne;
+    const size_t e = idx0.size() == ne ? idx0[i] : i;
+    std::memcpy(keys[j].data(), pk + e * pk_stride, 32);
+  }
+  std::sort(keys.begin(), keys.end());
+  uint32_t repeats = 0;
+  for (uint32_t j = 1; j < kSample; ++j) repeats += keys[j] == keys[j - 1];
+  // n_keys ~ kSample^2 / (2 repeats); reuse needs n_keys <= ne / 8
+  return (uint64_t)repeats * ne >= (uint64_t)kSample * kSample * 2;
+}
+
+cg_status stage_key_dedupe(cg_ctx* ctx, cg_batch* b, const uint8_t* pk, size_t pk_stride,
+                           const std::vector<uint32_t>& idx0) {
   const uint32_t ne = b->n_ed;
   const int forced = key_reuse_forced();
   if (forced == 0 || (ne < 64 && forced != 1)) return CG_OK;
+  if (forced != 1 && !key_sample_suggests_reuse(pk, pk_stride, idx0, ne)) return CG_OK;
   uint32_t tsize = 1;
   while (tsize < 2 * ne) tsize <<= 1;
   uint32_t *table = nullptr, *slot_of = nullptr, *owner = nullptr, *counter = nullptr;
@@ -635,7 +717,13 @@ cg_status create_batch(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const ui
   }
   if (idx[0].size() != n) ed_identity = false;
   const size_t nwords = (n + 31) / 32;
-  if ((st = dalloc(ctx, &b->verdict, n, "alloc verdict")) != CG_OK) return bail(st);
+  const uint64_t fallbacks0 = ctx->pin_fallbacks;
+  if (m.verdict_dev) {
+    b->verdict = m.verdict_dev;
+    b->verdict_owned = false;
+  } else if ((st = dalloc(ctx, &b->verdict, n, "alloc verdict")) != CG_OK) {
+    return bail(st);
+  }
   if ((st = dalloc(ctx, &b->bitmap, nwords, "alloc bitmap")) != CG_OK) return bail(st);
   if (m.dev) {
     b->arena = m.dev;  // library-owned device arena (padded by its producer)
@@ -673,7 +761,7 @@ cg_status create_batch(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const ui
     const uint32_t ne = (uint32_t)idx[0].size();
     b->n_ed = ne;
     if (ne) {
-      if (!ed_identity && (st = upload(ctx, &b->ed_index, idx[0].data(), ne, "upload ed index")) != CG_OK)
+      if (!ed_identity && (st = upload_idx(ctx, &b->ed_index, idx[0].data(), ne, "upload ed index")) != CG_OK)
         return bail(st);
       if ((st = dalloc(ctx, &b->ed_pk, (size_t)8 * ne, "alloc ed pk")) != CG_OK ||
           (st = dalloc(ctx, &b->ed_sig, (size_t)16 * ne, "alloc ed sig")) != CG_OK ||
@@ -689,7 +777,7 @@ cg_status create_batch(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const ui
       if (e == hipSuccess) e = cg::launch_gather_u64(b->msg_off_all, b->ed_index, ne, b->ed_msg_off, ctx->stream);
       if (e == hipSuccess) e = cg::launch_gather_u32(b->msg_len_all, b->ed_index, ne, b->ed_msg_len, 0, ctx->stream);
       if (e != hipSuccess) return bail(hip_fail(ctx, e, "stage ed25519"));
-      if ((st = stage_key_dedupe(ctx, b)) != CG_OK) return bail(st);
+      if ((st = stage_key_dedupe(ctx, b, pk, pk_stride, idx[0])) != CG_OK) return bail(st);
     }
     for (int c = 0; c < 2; ++c) {
       const std::vector<uint32_t>& ix = idx[1 + c];
@@ -698,7 +786,7 @@ cg_status create_batch(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const ui
       const size_t ne_c = ix.size();
       eb.n = (uint32_t)ne_c;
       eb.scheme = c == 0 ? CG_SCHEME_ECDSA_SECP256K1_SHA256 : CG_SCHEME_ECDSA_SECP256R1_SHA256;
-      if ((st = upload(ctx, &eb.index, ix.data(), ne_c, "upload ecdsa index")) != CG_OK ||
+      if ((st = upload_idx(ctx, &eb.index, ix.data(), ne_c, "upload ecdsa index")) != CG_OK ||
           (st = dalloc(ctx, &eb.q, 16 * ne_c, "alloc ecdsa q")) != CG_OK ||
           (st = dalloc(ctx, &eb.rs, 16 * ne_c, "alloc ecdsa rs")) != CG_OK ||
           (st = dalloc(ctx, &eb.der, ne_c, "alloc ecdsa der")) != CG_OK ||
@@ -711,11 +799,12 @@ cg_status create_batch(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const ui
       if (e != hipSuccess) return bail(hip_fail(ctx, e, "stage ecdsa"));
     }
   }
-  // the host index vectors die here: wait for the copies that read them
-  hipError_t e = hipStreamSynchronize(ctx->stream);
+  // the host index vectors die here: wait for the copies that read them (unless every
+  // one went through the pinned staging area of an asynchronous tx-pipeline stage)
+  hipError_t e = (m.async && ctx->pin_fallbacks == fallbacks0) ? hipSuccess : hipStreamSynchronize(ctx->stream);
   free_raw();
   if (e != hipSuccess) return bail(hip_fail(ctx, e, "stage sync"));
-  collect_timings(ctx);
+  if (!m.async) collect_timings(ctx);  // (it waits on every pending span: the pipeline collects at its end)
   *out = b;
   return CG_OK;
 }
@@ -733,11 +822,23 @@ cg_status ecdsa_scratch_retry(cg_ctx* ctx, int scheme, uint32_t n, uint32_t* chu
   return e == hipSuccess ? CG_OK : hip_fail(ctx, e, "alloc ecdsa scratch");
 }
 
+// Orders ctx->stream after everything the ECDSA streams hold so far.
+cg_status join_ecdsa_streams(cg_ctx* ctx) {
+  for (int c = 0; c < 2; ++c) {
+    CG_TRY(ctx, hipEventRecord(ctx->ev_join[c], ctx->ec_stream[c]), "record ecdsa join");
+    CG_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_join[c], 0), "join ecdsa");
+  }
+  return CG_OK;
+}
+
 // Launches the verify kernels of a staged batch and the accept bitmap; no sync.
 // Every exit — success or error — leaves ctx->stream ordered after the ECDSA
 // streams it forked, so the caller's stream-ordered frees (batch_free, the block
 // cache) can never hand a buffer to new work while an ECDSA kernel still writes it.
-cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode) {
+// join_streams = false (the tx pipeline): a successful exit leaves the ECDSA work
+// running on its streams and skips the bitmap; the caller joins once after the last
+// batch and frees the batches only after its final sync.
+cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = true) {
   const size_t n = b->n;
   bool joins[2] = {false, false};
   cg_status st = CG_OK;
@@ -856,8 +957,8 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode) {
     return CG_OK;
   };
   st = run();
-  join();
-  if (st != CG_OK) return st;
+  if (st != CG_OK || join_streams) join();
+  if (st != CG_OK || !join_streams) return st;
   CG_TRY(ctx, cg::launch_verdict_bitmap(b->verdict, (uint32_t)n, b->bitmap, ctx->stream), "launch bitmap");
   return CG_OK;
 }
@@ -1085,19 +1186,21 @@ struct TxDev {
 // bounds are checked by the leaf kernel (error flag, read back by the caller).
 // Leaf hashes of the components of txs [t0, t1) and their Merkle roots (the arena
 // bytes of those components must be on the device, in stream order).
-cg_status hash_txs(cg_ctx* ctx, TxDev& d, size_t arena_bytes, const uint32_t* comp_start, size_t t0, size_t t1) {
+cg_status hash_txs(cg_ctx* ctx, TxDev& d, size_t arena_bytes, const uint32_t* comp_start, size_t t0, size_t t1,
+                   hipStream_t s = nullptr) {
+  if (!s) s = ctx->stream;
   const uint32_t c0 = comp_start[t0], c1 = comp_start[t1];
   {
-    Timed t(ctx, "merkle_leaf", c1 - c0);
+    Timed t(ctx, "merkle_leaf", c1 - c0, s);
     CG_TRY(ctx, cg::launch_merkle_leaf(d.arena, arena_bytes, d.comp_off, d.comp_len, d.comp_start, d.comp_tx, d.salts,
-                                       nullptr, c0, c1, d.leaves, ctx->err_flag, ctx->stream, d.order + c0,
+                                       nullptr, c0, c1, d.leaves, ctx->err_flag, s, d.order + c0,
                                        d.leaf_hist),
            "launch merkle_leaf");
   }
   {
-    Timed t(ctx, "merkle_tree", t1 - t0);
+    Timed t(ctx, "merkle_tree", t1 - t0, s);
     CG_TRY(ctx, cg::launch_merkle_tree(d.leaves, d.comp_start + t0, (uint32_t)(t1 - t0), (uint32_t*)d.ids + 8 * t0,
-                                       ctx->stream),
+                                       s),
            "launch merkle_tree");
   }
   return CG_OK;
@@ -1154,24 +1257,22 @@ cg_status compute_txids(cg_ctx* ctx, size_t n_tx, const uint8_t* arena, size_t a
 // arena overlaps the kernels and the host-side staging.  Any layout works; a
 // component-ordered arena (what the JVM producer writes) makes the prefixes grow
 // evenly.  Verdicts land in verdict_d at their absolute signature positions.
+cg_status hip_ok(cg_ctx* ctx, hipError_t e, const char* what);
+
 cg_status tx_pipeline(cg_ctx* ctx, int mode, size_t n_tx, const uint8_t* arena, size_t arena_bytes,
                       const uint64_t* comp_off, const uint32_t* comp_len, const uint32_t* comp_start,
                       const uint32_t* sig_start, const uint8_t* scheme_id, const uint8_t* pk, size_t pk_stride,
                       const uint8_t* sig, size_t sig_stride, const uint32_t* sig_len, TxDev& d, uint8_t* verdict_d,
-                      std::vector<hipEvent_t>& ev) {
-  // chunks: enough to overlap the upload, few enough that each chunk's signature
-  // subsets still fill the device
-  // (CORDA_AMD_TX_CHUNKS / CORDA_AMD_TX_MIN_CHUNK override, for tuning and tests)
-  size_t kmax = 4, min_chunk = 131072;
+                      std::vector<hipEvent_t>& ev, std::vector<cg_batch*>& batches) {
+  // chunks: enough that the upload of the last one (after which only its kernels
+  // remain) is short, few enough that each chunk's signature subsets still fill the
+  // device (CORDA_AMD_TX_CHUNKS / CORDA_AMD_TX_MIN_CHUNK override, for tuning and tests)
+  size_t kmax = 6, min_chunk = 65536;
   if (const char* e = std::getenv("CORDA_AMD_TX_CHUNKS")) kmax = std::max(1, std::atoi(e));
   if (const char* e = std::getenv("CORDA_AMD_TX_MIN_CHUNK")) min_chunk = std::max(1, std::atoi(e));
   const size_t K = std::max<size_t>(1, std::min<size_t>(kmax, n_tx / min_chunk));
   std::vector<size_t> tb(K + 1);
   for (size_t k = 0; k <= K; ++k) tb[k] = n_tx * k / K;
-  // Everything goes out on copy_stream before any host-side scanning, so the copy
-  // engine starts immediately: the arena in kB equal byte pieces (event ev[j] each)
-  // and, after the pieces of the arena share of chunk k, that chunk's signature rows
-  // (event ev[kB + k]).  The compute stream then never waits behind a host copy.
   // The row buffers come from the block cache: every block in it is idle here (the
   // API calls that freed them ended with a stream sync; compute_txids only enqueued
   // work on live blocks).
@@ -1181,19 +1282,26 @@ cg_status tx_pipeline(cg_ctx* ctx, int mode, size_t n_tx, const uint8_t* arena, 
                 (st = dalloc(ctx, &d.raw_sig, n_sig * sig_stride, "alloc sig rows")) != CG_OK ||
                 (sig_len && (st = dalloc(ctx, &d.raw_sl, n_sig, "alloc sig_len rows")) != CG_OK)))
     return st;
-  const size_t kB = 8, piece = (arena_bytes + kB - 1) / kB;
-  ev.assign(kB + K, nullptr);
+  ev.assign(2 * K + 1, nullptr);  // ev[k]: chunk k uploaded; ev[K + k]: its ids; ev[2K]: metadata staged
   for (hipEvent_t& e : ev) CG_TRY(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming), "tx pipeline event");
-  for (size_t k = 0; k < K; ++k) {
-    for (size_t j = kB * k / K; j < kB * (k + 1) / K; ++j) {
-      const size_t lo = std::min(arena_bytes, j * piece), hi = std::min(arena_bytes, (j + 1) * piece);
-      if (hi > lo)
-        CG_TRY(ctx, hipMemcpyAsync(d.arena + lo, arena + lo, hi - lo, hipMemcpyHostToDevice, ctx->copy_stream),
-               "upload tx arena");
-      CG_TRY(ctx, hipEventRecord(ev[j], ctx->copy_stream), "tx pipeline record");
+  // Chunk k's upload on copy_stream = the arena bytes its components reach beyond
+  // what earlier chunks uploaded (a prefix; a component-ordered arena — what the JVM
+  // producer writes — makes the pieces even), then its signature rows; event ev[k].
+  // Uploads are enqueued chunk by chunk as the host scans the components, so the
+  // copy engine starts at once and chunk k's kernels wait for exactly its own bytes.
+  uint64_t up_to = 0;
+  auto enqueue_upload = [&](size_t k) -> cg_status {
+    const uint64_t from = up_to;
+    for (uint32_t c = comp_start[tb[k]]; c < comp_start[tb[k + 1]]; ++c)
+      up_to = std::max<uint64_t>(up_to, std::min<uint64_t>(comp_off[c] + comp_len[c], arena_bytes));
+    if (up_to > from) {
+      Timed t(ctx, "h2d_arena", up_to - from, ctx->copy_stream);
+      CG_TRY(ctx, hipMemcpyAsync(d.arena + from, arena + from, up_to - from, hipMemcpyHostToDevice, ctx->copy_stream),
+             "upload tx arena");
     }
     const size_t s0 = sig_start[tb[k]], s1 = sig_start[tb[k + 1]];
     if (s1 > s0) {
+      Timed t(ctx, "h2d_rows", (s1 - s0) * (pk_stride + sig_stride), ctx->copy_stream);
       CG_TRY(ctx, hipMemcpyAsync(d.raw_pk + s0 * pk_stride, pk + s0 * pk_stride, (s1 - s0) * pk_stride,
                                  hipMemcpyHostToDevice, ctx->copy_stream), "upload pk rows");
       CG_TRY(ctx, hipMemcpyAsync(d.raw_sig + s0 * sig_stride, sig + s0 * sig_stride, (s1 - s0) * sig_stride,
@@ -1202,17 +1310,63 @@ cg_status tx_pipeline(cg_ctx* ctx, int mode, size_t n_tx, const uint8_t* arena, 
         CG_TRY(ctx, hipMemcpyAsync(d.raw_sl + s0, sig_len + s0, (s1 - s0) * 4, hipMemcpyHostToDevice, ctx->copy_stream),
                "upload sig_len rows");
     }
-    CG_TRY(ctx, hipEventRecord(ev[kB + k], ctx->copy_stream), "tx pipeline record");
-  }
-  uint64_t up_to = 0;
+    CG_TRY(ctx, hipEventRecord(ev[k], ctx->copy_stream), "tx pipeline record");
+    return CG_OK;
+  };
+  // Two chunks' uploads in flight before the first kernels are enqueued; chunk k + 2's
+  // upload is enqueued with chunk k's kernels, so the copy engine never waits for the
+  // host.
+  if ((st = enqueue_upload(0)) != CG_OK) return st;
+  if (K > 1 && (st = enqueue_upload(1)) != CG_OK) return st;
+  // No host sync until the end: each chunk's staging goes out without one (index
+  // vectors through pinned staging), its verdicts land in place, the ECDSA streams
+  // run on across chunks and are joined once, and the batches live until the
+  // caller's final sync.  The scratch buffers are sized for the largest chunk first,
+  // so no chunk regrows (and frees) one that earlier chunks' kernels still use.
+  uint32_t max_cnt[3] = {0, 0, 0};
   for (size_t k = 0; k < K; ++k) {
-    for (uint32_t c = comp_start[tb[k]]; c < comp_start[tb[k + 1]]; ++c)  // arena prefix chunk k reads
-      up_to = std::max<uint64_t>(up_to, std::min<uint64_t>(comp_off[c] + comp_len[c], arena_bytes));
-    if (up_to) {
-      const size_t j = std::min(kB - 1, (size_t)((up_to - 1) / (piece ? piece : 1)));
-      CG_TRY(ctx, hipStreamWaitEvent(ctx->stream, ev[j], 0), "tx pipeline wait");
+    uint32_t cnt[3] = {0, 0, 0};
+    for (size_t i = sig_start[tb[k]]; i < sig_start[tb[k + 1]]; ++i) {
+      const uint8_t sc = scheme_id ? scheme_id[i] : CG_SCHEME_EDDSA_ED25519_SHA512;
+      cnt[sc == CG_SCHEME_EDDSA_ED25519_SHA512 ? 0 : sc == CG_SCHEME_ECDSA_SECP256K1_SHA256 ? 1 : 2] +=
+          sc == CG_SCHEME_EDDSA_ED25519_SHA512 || sc == CG_SCHEME_ECDSA_SECP256K1_SHA256 ||
+          sc == CG_SCHEME_ECDSA_SECP256R1_SHA256;
     }
-    if ((st = hash_txs(ctx, d, arena_bytes, comp_start, tb[k], tb[k + 1])) != CG_OK) return st;
+    for (int c = 0; c < 3; ++c) max_cnt[c] = std::max(max_cnt[c], cnt[c]);
+  }
+  if (max_cnt[0] && (st = ensure_ed_scratch(ctx, max_cnt[0])) != CG_OK) return st;
+  for (int c = 0; c < 2; ++c) {
+    uint32_t chunk = 0;
+    if (max_cnt[1 + c] &&
+        (st = ecdsa_scratch_retry(ctx, c == 0 ? CG_SCHEME_ECDSA_SECP256K1_SHA256 : CG_SCHEME_ECDSA_SECP256R1_SHA256,
+                                  max_cnt[1 + c], &chunk)) != CG_OK)
+      return st;
+  }
+  const size_t pin_need = 4 * n_sig + 3 * 256 * K;
+  if (ctx->pin_cap < pin_need) {
+    if (ctx->pin) (void)hipHostFree(ctx->pin);  // idle: every earlier call ended with a sync
+    ctx->pin = nullptr;
+    ctx->pin_cap = 0;
+    if (hipHostMalloc((void**)&ctx->pin, pin_need, hipHostMallocDefault) == hipSuccess) ctx->pin_cap = pin_need;
+    else (void)hipGetLastError();  // no staging: the chunks sync instead
+  }
+  ctx->pin_used = 0;
+  ctx->pin_active = true;
+  struct PinOff {
+    cg_ctx* c;
+    ~PinOff() { c->pin_active = false; }
+  } pin_off{ctx};
+  // Merkle ids on hash_stream (after compute_txids' metadata uploads and tx_index on
+  // ctx->stream), so chunk k+1's hashing runs beside chunk k's signature kernels; the
+  // signature kernels of chunk k wait for its ids (the ECDSA fork inherits that).
+  CG_TRY(ctx, hipEventRecord(ev[2 * K], ctx->stream), "tx pipeline record");
+  CG_TRY(ctx, hipStreamWaitEvent(ctx->hash_stream, ev[2 * K], 0), "tx pipeline wait");
+  for (size_t k = 0; k < K; ++k) {
+    CG_TRY(ctx, hipStreamWaitEvent(ctx->hash_stream, ev[k], 0), "tx pipeline wait");
+    if ((st = hash_txs(ctx, d, arena_bytes, comp_start, tb[k], tb[k + 1], ctx->hash_stream)) != CG_OK) return st;
+    CG_TRY(ctx, hipEventRecord(ev[K + k], ctx->hash_stream), "tx pipeline record");
+    // (before the staging, which waits on the host when the key-reuse count runs)
+    if (k + 2 < K && (st = enqueue_upload(k + 2)) != CG_OK) return st;
     const size_t s0 = sig_start[tb[k]], s1 = sig_start[tb[k + 1]];
     if (s1 > s0) {
       MsgSrc m;
@@ -1223,21 +1377,22 @@ cg_status tx_pipeline(cg_ctx* ctx, int mode, size_t n_tx, const uint8_t* arena, 
       m.pk_dev = d.raw_pk + s0 * pk_stride;
       m.sig_dev = d.raw_sig + s0 * sig_stride;
       m.sl_dev = sig_len ? d.raw_sl + s0 : nullptr;
-      m.raw_ready = ev[kB + k];
+      m.raw_ready = ev[k];
+      m.verdict_dev = verdict_d + s0;
+      m.async = true;
       cg_batch* b = nullptr;
       st = create_batch(ctx, s1 - s0, scheme_id ? scheme_id + s0 : nullptr, pk + s0 * pk_stride, pk_stride,
                         sig + s0 * sig_stride, sig_stride, sig_len ? sig_len + s0 : nullptr, m, &b);
-      if (st == CG_OK) st = launch_verify(ctx, b, mode);
-      if (st == CG_OK) {
-        const hipError_t e =
-            hipMemcpyAsync(verdict_d + s0, b->verdict, s1 - s0, hipMemcpyDeviceToDevice, ctx->stream);
-        if (e != hipSuccess) st = hip_fail(ctx, e, "tx verdicts");
-      }
-      if (b) batch_free(ctx, b);  // blocks go back to the stream-ordered cache
+      if (b) batches.push_back(b);  // freed by the caller after its final sync
+      if (st == CG_OK) st = hip_ok(ctx, hipStreamWaitEvent(ctx->stream, ev[K + k], 0), "tx pipeline wait");
+      if (st == CG_OK) st = launch_verify(ctx, b, mode, /*join_streams=*/false);
       if (st != CG_OK) return st;
     }
   }
-  return CG_OK;
+  // ids of chunks without signatures, and the first_bad / ids readers, follow ctx->stream
+  CG_TRY(ctx, hipEventRecord(ev[2 * K], ctx->hash_stream), "tx pipeline record");
+  CG_TRY(ctx, hipStreamWaitEvent(ctx->stream, ev[2 * K], 0), "tx pipeline wait");
+  return join_ecdsa_streams(ctx);
 }
 
 cg_status hip_ok(cg_ctx* ctx, hipError_t e, const char* what) {
@@ -1261,11 +1416,14 @@ struct TxRun {
   uint8_t* verdict_d = nullptr;
   int32_t* fb_d = nullptr;
   std::vector<hipEvent_t> ev;
+  std::vector<cg_batch*> batches;  // the pipeline's chunk batches (verdicts are slices of verdict_d)
   bool any_empty = false;
   size_t n_sig = 0;
   void release(cg_ctx* ctx) {
-    (void)hipStreamSynchronize(ctx->copy_stream);
-    (void)hipStreamSynchronize(ctx->stream);
+    for (hipStream_t s : {ctx->copy_stream, ctx->hash_stream, ctx->ec_stream[0], ctx->ec_stream[1], ctx->stream})
+      (void)hipStreamSynchronize(s);
+    for (cg_batch* b : batches) batch_free(ctx, b);
+    batches.clear();
     for (hipEvent_t e : ev)
       if (e) (void)hipEventDestroy(e);
     ev.clear();
@@ -1287,7 +1445,7 @@ cg_status tx_run(cg_ctx* ctx, int mode, size_t n_tx, const uint8_t* arena, size_
   r.n_sig = sig_start[n_tx];
   if (r.n_sig && (st = dalloc(ctx, &r.verdict_d, r.n_sig, "alloc tx verdicts")) != CG_OK) return st;
   st = tx_pipeline(ctx, mode, n_tx, arena, arena_bytes, comp_off, comp_len, comp_start, sig_start, scheme_id, pk,
-                   pk_stride, sig, sig_stride, sig_len, r.d, r.verdict_d, r.ev);
+                   pk_stride, sig, sig_stride, sig_len, r.d, r.verdict_d, r.ev, r.batches);
   if (st != CG_OK) return st;
   if ((st = dalloc(ctx, &r.fb_d, n_tx, "alloc first_bad")) != CG_OK) return st;
   CG_TRY(ctx, cg::launch_first_bad(r.verdict_d, r.d.sig_start, (uint32_t)n_tx, r.fb_d, ctx->stream), "first_bad");

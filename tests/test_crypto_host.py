@@ -60,3 +60,64 @@ def test_host_schemes_need_a_host_verifier():
     with pytest.raises(crypto.IllegalArgumentException) as ei:
         crypto._verify_mixed(None, [4, 1], [b"\1" * 32, b"k"], [b"s" * 64, b"s"], [b"m", b"m"], 0, None)
     assert ei.value.index == 1
+
+
+def _fake_verifier(monkeypatch, codes):
+    """Replace the device batch with fixed verdict codes, to check the loop semantics of
+    corda_amd.signatures without a GPU."""
+    from corda_amd import signatures
+    calls = []
+
+    def fake(ctx, schemes, keys, sigs, data, mode, host_verify):
+        calls.append((list(schemes), list(keys), list(sigs), list(data), mode))
+        return np.array(codes[:len(sigs)], dtype=np.uint8)
+    monkeypatch.setattr(signatures, "_verify_mixed", fake)
+    monkeypatch.setattr(crypto, "_verify_mixed", fake)
+    return calls
+
+
+def test_public_key_is_valid_loop_semantics(monkeypatch):
+    """PublicKey.isValid (CryptoUtils.kt:63-67): bools for ACCEPT/REJECT, Crypto.isValid's exception
+    at the first throwing element, IllegalStateException at the first CompositeKey — whichever the
+    loop meets first; elements past a composite key are never verified."""
+    from corda_amd import signatures as S
+    ed = lambda b: S.PublicKey(crypto.EDDSA_ED25519_SHA512, bytes([b]) * 32)  # noqa: E731
+    comp = S.PublicKey(6, b"composite")
+    calls = _fake_verifier(monkeypatch, [ACCEPT, REJECT, ACCEPT])
+    got = S.public_key_is_valid_batch(None, [ed(1), ed(2), ed(3)], [b"a", b"b", b"c"], [b"s"] * 3)
+    assert got.tolist() == [True, False, True] and calls[-1][4] == crypto._lib.MODE_IS_VALID
+    with pytest.raises(S.IllegalStateException) as ei:
+        S.public_key_is_valid_batch(None, [ed(1), ed(2), comp, ed(3)], [b"a"] * 4, [b"s"] * 4)
+    assert ei.value.index == 2 and len(calls[-1][2]) == 2
+    _fake_verifier(monkeypatch, [ACCEPT, SIG_MALFORMED])
+    with pytest.raises(crypto.SignatureException) as ei:
+        S.public_key_is_valid_batch(None, [ed(1), ed(2), comp], [b"a"] * 3, [b"s"] * 3)
+    assert ei.value.index == 1
+    _fake_verifier(monkeypatch, [KEY_INVALID])
+    with pytest.raises(crypto.InvalidKeyException):
+        S.with_key_is_valid_batch(None, [S.WithKey(ed(1), b"s")], [b"a"])
+    _fake_verifier(monkeypatch, [ACCEPT, ARG_EMPTY])  # isValid has no empty-data rule of its own
+    with pytest.raises(crypto.IllegalArgumentException):
+        S.public_key_is_valid_batch(None, [ed(1), ed(2)], [b"a", b""], [b"s"] * 2)
+
+
+def test_transaction_signature_mirrors(monkeypatch):
+    """TransactionSignature.verify (TransactionSignature.kt:20) verifies under metaData.publicKey;
+    Crypto.doVerify(publicKey, txSig) (Crypto.kt:497-501) under the PASSED key, over
+    metaData.bytes(), and a key differing from metaData.publicKey is not an error by itself."""
+    from corda_amd import signatures as S
+    ka = S.PublicKey(crypto.EDDSA_ED25519_SHA512, b"A" * 32)
+    kb = S.PublicKey(crypto.ECDSA_SECP256R1_SHA256, b"B" * 64)
+    ts = S.TransactionSignature(b"sig", b"metadata-bytes", ka)
+    calls = _fake_verifier(monkeypatch, [ACCEPT])
+    assert S.transaction_signatures_verify(None, [ts])
+    assert calls[-1][:4] == ([4], [b"A" * 32], [b"sig"], [b"metadata-bytes"])
+    assert calls[-1][4] == crypto._lib.MODE_DO_VERIFY
+    assert S.do_verify_transaction_signatures(None, [kb], [ts])
+    assert calls[-1][:4] == ([3], [b"B" * 64], [b"sig"], [b"metadata-bytes"])
+    _fake_verifier(monkeypatch, [ACCEPT, REJECT])
+    with pytest.raises(crypto.SignatureException) as ei:
+        S.transaction_signatures_verify(None, [ts, ts])
+    assert ei.value.index == 1
+    with pytest.raises(ValueError):
+        S.do_verify_transaction_signatures(None, [ka], [ts, ts])

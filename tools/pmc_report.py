@@ -23,6 +23,7 @@ import csv
 import glob
 import json
 import os
+import re
 import shutil
 import statistics
 import sys
@@ -48,6 +49,10 @@ def occupancy(e, c, regs):
     cycles summed over the 8 XCDs (MI355X_MICROARCH.md, PMC units)."""
     k = e.get("kernel_short", "")
     r = regs.get(k) or next((v for n, v in regs.items() if n.startswith(k + "<")), {})
+    m = re.match(r"(.*?)(?:_([np]))?_([kr]1)$", k)  # prof_summary.short() names of the curve templates
+    if not r and m:
+        base, inv, curve = m.group(1), m.group(2), m.group(3).upper()
+        r = regs.get(f"{base}<Inv{inv.upper()}<{curve}> >" if inv else f"{base}<{curve}>", {})
     for key in ("vgpr", "agpr", "sgpr", "vgpr_spill", "scratch_bytes", "lds_bytes", "waves_per_simd_limit"):
         if key in r:
             e[key] = r[key]
