@@ -5,6 +5,18 @@
 #pragma once
 #include <stdint.h>
 
+// Wave issue priority (s_setprio 0..3) for the kernels that run beside the long
+// Ed25519 MSM waves in the tx pipeline: the SIMD arbiter issues a higher-priority
+// wave's instructions first, so the short, latency-bound kernels of a chunk (Merkle
+// hashing, staging, the ECDSA prep and inversion tree) are not stretched 3-5x by
+// sharing their SIMDs with MSM waves (measured in the tx timeline, r02o).  The MSM
+// keeps priority 0 and takes the cycles the others leave.  Scalar, no memory access.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define CG_WAVE_PRIO(p) __builtin_amdgcn_s_setprio(p)
+#else
+#define CG_WAVE_PRIO(p) ((void)0)
+#endif
+
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
 #define CG_HD __host__ __device__ __forceinline__

@@ -24,6 +24,7 @@ __global__ __launch_bounds__(256) void cg_composite_eval(const uint32_t* __restr
                                                          const uint32_t* __restrict__ sig_start,
                                                          const uint8_t* __restrict__ verdicts, uint32_t n,
                                                          uint32_t* __restrict__ stack, uint8_t* __restrict__ out) {
+  CG_WAVE_PRIO(2);
   const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= n) return;
   if (out[q] == cg::kCompositeInvalid) return;  // the host pass rejected the program
@@ -60,6 +61,7 @@ __global__ __launch_bounds__(256) void cg_tx_missing(int32_t* __restrict__ statu
                                                      const uint8_t* __restrict__ fulfilled,
                                                      const uint8_t* __restrict__ allowed, uint32_t n_tx,
                                                      uint8_t* __restrict__ missing) {
+  CG_WAVE_PRIO(2);
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n_tx) return;
   const int32_t st = status[t];

@@ -69,6 +69,7 @@ __global__ __launch_bounds__(256) void cg_der_parse(const uint8_t* __restrict__ 
                                                     const uint32_t* __restrict__ sig_len, uint32_t fill_len,
                                                     const uint32_t* __restrict__ idx, uint32_t n, uint32_t cap,
                                                     uint32_t* __restrict__ rs, uint32_t* __restrict__ der) {
+  CG_WAVE_PRIO(2);
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const size_t e = idx ? idx[i] : i;
@@ -165,6 +166,7 @@ CG_DEV void lds_put(uint32_t* h, uint32_t k, const uint32_t v[W]) {
 template <class F>
 __global__ __launch_bounds__(256) void cg_inv_up(const uint32_t* __restrict__ in, uint32_t n,
                                                  uint32_t* __restrict__ tree, uint32_t* __restrict__ out) {
+  CG_WAVE_PRIO(2);
   constexpr int W = F::W;
   __shared__ uint32_t h[512 * W];
   const uint32_t t = threadIdx.x, b = blockIdx.x, i = b * 256 + t;
@@ -190,6 +192,7 @@ __global__ __launch_bounds__(256) void cg_inv_up(const uint32_t* __restrict__ in
 // The two roots of a chunk (s mod n, Z mod p) in parallel: wave 0 and wave 1.
 template <class C>
 __global__ void cg_inv_roots(uint32_t* __restrict__ vn, uint32_t* __restrict__ vp) {
+  CG_WAVE_PRIO(2);
   if (threadIdx.x == 0) {
     uint32_t x[8];
     gl_get<8>(x, vn);
@@ -207,6 +210,7 @@ template <class F>
 __global__ __launch_bounds__(256) void cg_inv_down(uint32_t* __restrict__ in, uint32_t n,
                                                    const uint32_t* __restrict__ tree,
                                                    const uint32_t* __restrict__ out_inv) {
+  CG_WAVE_PRIO(2);
   constexpr int W = F::W;
   __shared__ uint32_t h[512 * W], g[256 * W];
   const uint32_t t = threadIdx.x, b = blockIdx.x, i = b * 256 + t;
@@ -256,6 +260,7 @@ __global__ __launch_bounds__(256) void cg_ecdsa_prep_a(const uint32_t* __restric
                                                        uint32_t scap, uint32_t mode, uint32_t* __restrict__ status,
                                                        uint32_t* __restrict__ ework, uint32_t* __restrict__ leaf_n,
                                                        uint32_t* __restrict__ leaf_p, uint32_t* __restrict__ qtab) {
+  CG_WAVE_PRIO(2);
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint32_t qw[16], qx[8], qy[8], s[8], e[8], a[8];
@@ -302,6 +307,7 @@ __global__ __launch_bounds__(256) void cg_ecdsa_prep_b(const uint32_t* __restric
                                                        const uint32_t* __restrict__ leaf_n,
                                                        const uint32_t* __restrict__ leaf_p,
                                                        uint32_t* __restrict__ digits, uint32_t* __restrict__ qtab) {
+  CG_WAVE_PRIO(2);
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n || status[i] != 0xff) return;
   uint32_t w[8], e[8], r[8], u1[8], u2[8], d1[9], d2[9], d3[9], aux = 0;
@@ -361,6 +367,7 @@ void cg_ecdsa_msm(const uint32_t* __restrict__ rs,
                                                     const uint32_t* __restrict__ gtab_g, uint32_t n, uint32_t cap,
                                                     uint32_t scap, const uint32_t* __restrict__ out_index,
                                                     uint8_t* __restrict__ verdict) {
+  CG_WAVE_PRIO(1);
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t st = i < n ? status[i] : 0u;
   const bool live = i < n && (st & 0xff) == 0xff;

@@ -47,6 +47,7 @@ __global__ __launch_bounds__(256) void cg_ed25519_hash(const uint32_t* __restric
                                                        uint32_t scap, uint32_t mode, uint32_t* __restrict__ status,
                                                        uint32_t* __restrict__ digits, uint32_t full_mod,
                                                        uint32_t index_base) {
+  CG_WAVE_PRIO(1);
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint32_t pkw[8], sw[16], dig[kDigitWords], ndig, rneg;
@@ -94,6 +95,7 @@ CG_DEV void load_cached(const int4* src, ge_cached& c) {
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_POINTS_WAVES, 8))) void cg_ed25519_points(const uint32_t* __restrict__ pk,
                                                          const uint32_t* __restrict__ sig, uint32_t n, uint32_t cap,
                                                          uint32_t* __restrict__ status, int32_t* __restrict__ table) {
+  CG_WAVE_PRIO(1);
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint32_t pkw[8], rw[8];
@@ -122,6 +124,7 @@ CG_DEV int4* key_table(int32_t* ktab, uint32_t j) {
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_POINTS_WAVES, 8))) void cg_ed25519_keyprep(
     const uint32_t* __restrict__ pk, uint32_t cap, const uint32_t* __restrict__ key_first, uint32_t n_keys,
     int32_t* __restrict__ ktab, uint32_t* __restrict__ kstat) {
+  CG_WAVE_PRIO(1);
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n_keys) return;
   const uint32_t e = key_first[j];
@@ -138,6 +141,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_POINTS_W
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_POINTS_WAVES, 8))) void cg_ed25519_points_r(
     const uint32_t* __restrict__ sig, uint32_t n, uint32_t cap, const uint32_t* __restrict__ key_index,
     const uint32_t* __restrict__ kstat, uint32_t* __restrict__ status, int32_t* __restrict__ table) {
+  CG_WAVE_PRIO(1);
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint32_t rw[8];
@@ -180,6 +184,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_MSM_WAVE
     const uint32_t* __restrict__ sig, const uint32_t* __restrict__ status, const uint32_t* __restrict__ digits,
     const int32_t* __restrict__ table, const int32_t* __restrict__ btab_g, uint32_t n, uint32_t cap, uint32_t scap,
     const uint32_t* __restrict__ out_index, uint8_t* __restrict__ verdict) {
+  CG_WAVE_PRIO(0);
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t st = i < n ? status[i] : 0u;
   const bool live = i < n && ed_status_verdict(st) == V_COMPUTE;
@@ -244,6 +249,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_MSM_WAVE
     const uint32_t* __restrict__ status, const uint32_t* __restrict__ digits, const int32_t* __restrict__ table,
     const int32_t* __restrict__ ktab, const uint32_t* __restrict__ key_index, const int32_t* __restrict__ btab_g,
     uint32_t n, uint32_t scap, const uint32_t* __restrict__ out_index, uint8_t* __restrict__ verdict) {
+  CG_WAVE_PRIO(0);
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t st = i < n ? status[i] : 0u;
   const bool live = i < n && ed_status_verdict(st) == V_COMPUTE;

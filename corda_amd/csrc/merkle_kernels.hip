@@ -33,6 +33,7 @@ __global__ __launch_bounds__(256) void k_tx_index(const uint32_t* __restrict__ c
                                                   const uint32_t* __restrict__ sig_start, uint32_t n_tx,
                                                   uint32_t* __restrict__ comp_tx, uint64_t* __restrict__ sig_moff,
                                                   uint32_t* __restrict__ sig_mlen) {
+  CG_WAVE_PRIO(2);
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n_tx) return;
   for (uint32_t c = comp_start[t]; c < comp_start[t + 1]; ++c) comp_tx[c] = t;
@@ -53,6 +54,7 @@ __global__ __launch_bounds__(256) void cg_merkle_leaf(const uint8_t* __restrict_
                                                       const uint32_t* __restrict__ nonces, uint32_t c_begin,
                                                       uint32_t c_end, const uint32_t* __restrict__ order,
                                                       uint32_t* __restrict__ leaves, uint32_t* __restrict__ err) {
+  CG_WAVE_PRIO(2);
   __shared__ uint32_t tails[256 * kTailWords];
   const uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (c_begin + idx >= c_end) return;
@@ -102,6 +104,7 @@ CG_DEV uint32_t leaf_bin(uint32_t len) {
 
 __global__ __launch_bounds__(256) void k_leaf_hist(const uint32_t* __restrict__ comp_len, uint32_t c_begin,
                                                    uint32_t c_end, uint32_t* __restrict__ hist) {
+  CG_WAVE_PRIO(2);
   __shared__ uint32_t h[kLeafBins];
   if (threadIdx.x < kLeafBins) h[threadIdx.x] = 0;
   __syncthreads();
@@ -114,6 +117,7 @@ __global__ __launch_bounds__(256) void k_leaf_hist(const uint32_t* __restrict__ 
 // hist -> exclusive bin offsets, in place (one lane; 32 bins, longest first so the
 // heaviest waves start earliest)
 __global__ void k_leaf_scan(uint32_t* __restrict__ hist) {
+  CG_WAVE_PRIO(2);
   if (threadIdx.x) return;
   uint32_t acc = 0;
   for (int b = kLeafBins - 1; b >= 0; --b) {
@@ -126,6 +130,7 @@ __global__ void k_leaf_scan(uint32_t* __restrict__ hist) {
 __global__ __launch_bounds__(256) void k_leaf_scatter(const uint32_t* __restrict__ comp_len, uint32_t c_begin,
                                                       uint32_t c_end, uint32_t* __restrict__ cursor,
                                                       uint32_t* __restrict__ order) {
+  CG_WAVE_PRIO(2);
   __shared__ uint32_t h[kLeafBins], base[kLeafBins];
   if (threadIdx.x < kLeafBins) h[threadIdx.x] = 0;
   __syncthreads();
@@ -147,6 +152,7 @@ __global__ __launch_bounds__(256) void k_leaf_scatter(const uint32_t* __restrict
 __global__ __launch_bounds__(256) void cg_merkle_tree(uint32_t* __restrict__ leaves,
                                                       const uint32_t* __restrict__ comp_start, uint32_t n_tx,
                                                       uint32_t* __restrict__ ids) {
+  CG_WAVE_PRIO(2);
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n_tx) return;
   const uint32_t c0 = comp_start[t];
@@ -174,6 +180,7 @@ __global__ __launch_bounds__(256) void cg_merkle_tree(uint32_t* __restrict__ lea
 __global__ __launch_bounds__(256) void cg_first_bad(const uint8_t* __restrict__ verdict,
                                                     const uint32_t* __restrict__ sig_start, uint32_t n_tx,
                                                     int32_t* __restrict__ out) {
+  CG_WAVE_PRIO(2);
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n_tx) return;
   const uint32_t a = sig_start[t], b = sig_start[t + 1];
@@ -200,6 +207,7 @@ __global__ __launch_bounds__(256) void cg_pmt_eval(const uint32_t* __restrict__ 
                                                    const uint32_t* __restrict__ leaves,
                                                    const uint32_t* __restrict__ roots, uint32_t n,
                                                    uint32_t* __restrict__ stack, uint8_t* __restrict__ status) {
+  CG_WAVE_PRIO(2);
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n) return;
   const uint32_t c0 = comp_start[t], k = comp_start[t + 1] - c0;

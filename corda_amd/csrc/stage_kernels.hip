@@ -10,6 +10,7 @@ namespace {
 __global__ __launch_bounds__(256) void k_gather_words(const uint8_t* __restrict__ src, size_t stride, size_t offset,
                                                       uint32_t nwords, const uint32_t* __restrict__ idx, uint32_t n,
                                                       uint32_t cap, uint32_t* __restrict__ dst) {
+  CG_WAVE_PRIO(2);
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const size_t e = idx ? idx[i] : i;
@@ -23,6 +24,7 @@ __global__ __launch_bounds__(256) void k_gather_words(const uint8_t* __restrict_
 
 __global__ __launch_bounds__(256) void k_gather_u32(const uint32_t* __restrict__ src, const uint32_t* __restrict__ idx,
                                                     uint32_t n, uint32_t* __restrict__ dst, uint32_t fill) {
+  CG_WAVE_PRIO(2);
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   dst[i] = src ? src[idx ? idx[i] : i] : fill;
@@ -30,6 +32,7 @@ __global__ __launch_bounds__(256) void k_gather_u32(const uint32_t* __restrict__
 
 __global__ __launch_bounds__(256) void k_gather_u64(const uint64_t* __restrict__ src, const uint32_t* __restrict__ idx,
                                                     uint32_t n, uint64_t* __restrict__ dst) {
+  CG_WAVE_PRIO(2);
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   dst[i] = src[idx ? idx[i] : i];
@@ -38,6 +41,7 @@ __global__ __launch_bounds__(256) void k_gather_u64(const uint64_t* __restrict__
 // accept bitmap: bit i%32 of word i/32 set iff verdict[i] == ACCEPT (0).
 __global__ __launch_bounds__(256) void k_verdict_bitmap(const uint8_t* __restrict__ verdict, uint32_t n,
                                                         uint32_t* __restrict__ bitmap) {
+  CG_WAVE_PRIO(2);
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const bool acc = i < n && verdict[i] == 0;
   const unsigned long long b = __ballot(acc);
@@ -71,6 +75,7 @@ __global__ __launch_bounds__(256) void k_key_insert(const uint32_t* __restrict__
                                                     uint32_t* __restrict__ table, uint32_t mask,
                                                     uint32_t* __restrict__ slot_of, uint32_t* __restrict__ owner_id,
                                                     uint32_t* __restrict__ counter, uint32_t* __restrict__ key_first) {
+  CG_WAVE_PRIO(2);
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint32_t k[8];
@@ -100,6 +105,7 @@ __global__ __launch_bounds__(256) void k_key_insert(const uint32_t* __restrict__
 __global__ __launch_bounds__(256) void k_key_lookup(const uint32_t* __restrict__ slot_of,
                                                     const uint32_t* __restrict__ owner_id, uint32_t n,
                                                     uint32_t* __restrict__ key_index) {
+  CG_WAVE_PRIO(2);
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint32_t s = slot_of[i];
