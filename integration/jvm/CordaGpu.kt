@@ -9,6 +9,7 @@ import net.corda.core.contracts.PrivacySalt
 import net.corda.core.crypto.Crypto
 import net.corda.core.crypto.DigitalSignature
 import net.corda.core.crypto.SignatureScheme
+import net.corda.core.crypto.TransactionSignature
 import net.corda.core.crypto.composite.CompositeKey
 import net.corda.core.serialization.SerializationDefaults.P2P_CONTEXT
 import net.corda.core.serialization.serialize
@@ -304,6 +305,40 @@ fun Crypto.doVerifyBatch(schemes: List<SignatureScheme>, keys: List<PublicKey>, 
     }
     return true
 }
+
+/**
+ * `keys[i].isValid(contents[i], sigs[i])` for every i (CryptoUtils.kt:63-67): a Boolean per element,
+ * or the first exception the loop would meet — IllegalStateException at the first CompositeKey, else
+ * Crypto.isValid's own (SignatureException / InvalidKeyException / IllegalArgumentException).
+ * Elements past a CompositeKey are never verified, as in the loop.
+ */
+fun isValidBatch(keys: List<PublicKey>, contents: List<ByteArray>, sigs: List<DigitalSignature>): BooleanArray {
+    val stop = keys.indexOfFirst { it is CompositeKey }.let { if (it < 0) keys.size else it }
+    val head = keys.subList(0, stop)
+    val v = verdicts(head.map { Crypto.findSignatureScheme(it) }, head, sigs.subList(0, stop).map { it.bytes },
+            contents.subList(0, stop), doVerifyMode = false)
+    for (i in v.indices) when (v[i]) {
+        Verdict.ACCEPT, Verdict.REJECT -> {}
+        Verdict.KEY_INVALID -> throw InvalidKeyException("public key cannot be decoded")
+        Verdict.SIG_MALFORMED -> throw SignatureException("error decoding signature bytes.")
+        else -> throw IllegalArgumentException("Unsupported key/algorithm for schemeCodeName: ${Crypto.findSignatureScheme(keys[i]).schemeCodeName}")
+    }
+    if (stop < keys.size) throw IllegalStateException("Verification of CompositeKey signatures currently not supported.")
+    return BooleanArray(v.size) { v[it] == Verdict.ACCEPT }
+}
+
+/** `for (s in sigs) s.verify()` (TransactionSignature.kt:20): each under metaData.publicKey over metaData.bytes(). */
+fun verifyTransactionSignaturesBatch(sigs: List<TransactionSignature>): Boolean =
+        Crypto.doVerifyBatch(sigs.map { Crypto.findSignatureScheme(it.metaData.publicKey) }, sigs.map { it.metaData.publicKey },
+                sigs.map { it.signatureData }, sigs.map { it.metaData.bytes() })
+
+/**
+ * `Crypto.doVerify(keys[i], sigs[i])` for every i (Crypto.kt:497-501): verification under the PASSED key
+ * over metaData.bytes(); the reference builds, but never throws, the key-mismatch exception (:499),
+ * so a mismatching key is not rejected by itself here either.
+ */
+fun Crypto.doVerifyBatch(keys: List<PublicKey>, sigs: List<TransactionSignature>): Boolean =
+        doVerifyBatch(keys.map { findSignatureScheme(it) }, keys, sigs.map { it.signatureData }, sigs.map { it.metaData.bytes() })
 
 /**
  * Batch form of TransactionWithSignatures.checkSignaturesAreValid (TransactionWithSignatures.kt:58-62)
