@@ -174,8 +174,8 @@ CG_HD uint32_t ed25519_points_stage(const uint32_t pk[8], const uint32_t r[8], u
   if (!ok[1] || !ge_strict_check(P[1], r)) return V_REJECT;
   R = P[1];
   negA = P[0];
-  fe_neg(negA.X, P[0].X);
-  fe_neg(negA.T, P[0].T);
+  fe_neg_p(negA.X, P[0].X);  // -A kept floor-shaped (cg_ge25519.h carry discipline)
+  fe_neg_p(negA.T, P[0].T);
   return V_COMPUTE;
 }
 
@@ -214,8 +214,8 @@ template <typename Put>
 CG_HD uint32_t ed25519_key_tables(const uint32_t pk[8], Put&& put) {
   ge_p3 P;
   if (!ge_frombytes_i2p(P, pk)) return 0;
-  fe_neg(P.X, P.X);
-  fe_neg(P.T, P.T);
+  fe_neg_p(P.X, P.X);
+  fe_neg_p(P.T, P.T);
   ge_p1p1 x;
   CG_NOUNROLL for (int t = 0; t < 4; ++t) {
     if (t) {
@@ -316,7 +316,10 @@ CG_HD uint32_t ed25519_msm(uint32_t ndig, const uint32_t dig[kDigitWords], uint3
   CG_NOUNROLL for (int pos = top; pos >= 0; --pos) {
     if (pos != top) {
       ge_p1p1_to_p2(r2, t);
-      ge_p2_dbl(t, r2);
+      if ((pos & 3) == 0)
+        ge_p2_dbl<true>(t, r2);  // the additions follow (ge_p1p1_to_p3)
+      else
+        ge_p2_dbl<false>(t, r2);
     }
     if ((pos & 3) == 0) {
       const uint32_t ea = da[7] >> 28, er = dr[7] >> 28;
@@ -345,10 +348,10 @@ CG_HD uint32_t ed25519_msm(uint32_t ndig, const uint32_t dig[kDigitWords], uint3
       bh[3] >>= kBWin;
       const uint32_t nl = el < kHalf, nh = eh < kHalf;
       getB(0, nl ? kHalf - el : el - kHalf, pb);
-      ge_p1p1_to_p3(r3, t);
+      ge_p1p1_to_p3<true>(r3, t);
       ge_madd(t, r3, pb, nl);
       getB(2, nh ? kHalf - eh : eh - kHalf, pb);
-      ge_p1p1_to_p3(r3, t);
+      ge_p1p1_to_p3<true>(r3, t);
       ge_madd(t, r3, pb, nh);
     }
   }
@@ -389,7 +392,10 @@ CG_HD uint32_t ed25519_msm_reuse(uint32_t c3w, uint32_t win17, const uint32_t di
   CG_NOUNROLL for (int pos = top; pos >= 0; --pos) {
     if (pos != top) {
       ge_p1p1_to_p2(r2, t);
-      ge_p2_dbl(t, r2);
+      if ((pos & 3) == 0)
+        ge_p2_dbl<true>(t, r2);
+      else
+        ge_p2_dbl<false>(t, r2);
     }
     if ((pos & 3) == 0) {
       const uint32_t j = (uint32_t)pos >> 2;
@@ -432,7 +438,7 @@ CG_HD uint32_t ed25519_msm_reuse(uint32_t c3w, uint32_t win17, const uint32_t di
         bt[3] = nx;
         const uint32_t n = e < kHalf;
         getB(c, n ? kHalf - e : e - kHalf, pb);
-        ge_p1p1_to_p3(r3, t);
+        ge_p1p1_to_p3<true>(r3, t);
         ge_madd(t, r3, pb, n);
       }
     }

@@ -20,51 +20,44 @@ struct fe {
   int32_t v[10];
 };
 
-// Host-only bound checking (tests/native, -DCG_CHECK_BOUNDS): recomputes every
-// column sum of a mul/sq in 128 bits, traps on int64 overflow and records the
-// largest input limb and column sum seen (cg_bounds_report).
+// Host-only bound checking (tests/native, -DCG_CHECK_BOUNDS): every product chain
+// recomputes its column sums in 128 bits and traps when a sum leaves int64 or a
+// prescaled operand (19 g, 2 f, 4 f, 8 f) leaves int32; records the largest g-side
+// limb (the operand scaled by 19), f-side limb and column sum (cgh_bounds_report).
 #if defined(CG_CHECK_BOUNDS) && !defined(__HIP_DEVICE_COMPILE__)
 struct CgBounds {
-  int64_t max_limb = 0;
+  int64_t max_limb = 0;    // g side (the limbs multiplied by 19)
+  int64_t max_flimb = 0;   // f side
   __int128 max_col = 0;
 };
 inline CgBounds& cg_bounds() {
   static CgBounds b;
   return b;
 }
-template <typename F, typename G>
-inline void cg_bounds_mul(const F& f, const G& g, const int64_t t[10], int dbl) {
+inline int32_t cg_bounds_scale(int64_t x, int64_t m, bool g_side) {
   CgBounds& b = cg_bounds();
-  __int128 col[10] = {0};
-  for (int i = 0; i < 10; ++i) {
-    const int64_t af = f.v[i] < 0 ? -(int64_t)f.v[i] : f.v[i], ag = g.v[i] < 0 ? -(int64_t)g.v[i] : g.v[i];
-    if (af > b.max_limb) b.max_limb = af;
-    if (ag > b.max_limb) b.max_limb = ag;
-    for (int j = 0; j < 10; ++j) {
-      const int k = i + j;
-      __int128 p = (__int128)f.v[i] * g.v[j] * (((i & 1) && (j & 1)) ? 2 : 1) * (k >= 10 ? 19 : 1);
-      col[k >= 10 ? k - 10 : k] += p;
-    }
+  const int64_t a = x < 0 ? -x : x;
+  if (g_side && a > b.max_limb) b.max_limb = a;
+  if (!g_side && a > b.max_flimb) b.max_flimb = a;
+  const int64_t y = x * m;
+  if (y != (int64_t)(int32_t)y) {
+    fprintf(stderr, "cg bounds: prescaled limb %lld * %lld leaves int32\n", (long long)x, (long long)m);
+    __builtin_trap();
   }
-  for (int k = 0; k < 10; ++k) {
-    const __int128 c = col[k] * (dbl ? 2 : 1);
-    const __int128 a = c < 0 ? -c : c;
-    if (a > b.max_col) b.max_col = a;
-    const int64_t tk = t[k];
-    if (a >= ((__int128)1 << 62) || (int64_t)c != tk) {
-      fprintf(stderr, "cg bounds: column %d = 2^%.2f (int64 %s)\n  f:", k, __builtin_log2((double)a),
-              (int64_t)c != tk ? "wrapped" : "ok");
-      for (int i = 0; i < 10; ++i) fprintf(stderr, " %d", f.v[i]);
-      fprintf(stderr, "\n  g:");
-      for (int i = 0; i < 10; ++i) fprintf(stderr, " %d", g.v[i]);
-      fprintf(stderr, "\n");
-      __builtin_trap();
-    }
+  return (int32_t)y;
+}
+inline void cg_bounds_col(__int128 c) {
+  CgBounds& b = cg_bounds();
+  const __int128 a = c < 0 ? -c : c;
+  if (a > b.max_col) b.max_col = a;
+  if (a >= ((__int128)1 << 63)) {
+    fprintf(stderr, "cg bounds: column sum 2^%.2f leaves int64\n", __builtin_log2((double)a));
+    __builtin_trap();
   }
 }
-#define CG_BOUNDS_MUL(f, g, t, dbl) cg_bounds_mul(f, g, t, dbl)
+#define CG_SCALE(x, m, gside) cg_bounds_scale((x), (m), (gside))
 #else
-#define CG_BOUNDS_MUL(f, g, t, dbl) ((void)0)
+#define CG_SCALE(x, m, gside) ((int32_t)((x) * (m)))
 #endif
 
 CG_HD void fe_0(fe& h) {
@@ -83,10 +76,32 @@ CG_HD void fe_sub(fe& h, const fe& f, const fe& g) {
 CG_HD void fe_neg(fe& h, const fe& f) {
   CG_UNROLL for (int i = 0; i < 10; ++i) h.v[i] = -f.v[i];
 }
+// h = f + g - p, limb by limb (p = 2^255 - 19 as limbs 2^26 - 19, 2^25 - 1, 2^26 - 1, ...):
+// the sum of two floor-reduced values (limbs in [0, 2^w)) brought back to
+// (-2^w, 2^w], so it may be the 19-scaled operand of a product.  Same field element.
+CG_HD void fe_add_p(fe& h, const fe& f, const fe& g) {
+  CG_UNROLL for (int i = 0; i < 10; ++i) {
+    const int32_t p = i == 0 ? (1 << 26) - 19 : (i & 1) ? (1 << 25) - 1 : (1 << 26) - 1;
+    h.v[i] = f.v[i] + g.v[i] - p;
+  }
+}
+// h = p - f, limb by limb: the negation of a floor-reduced value kept floor-shaped
+// (limbs in [0, 2^w) except limb 0 in [-18, 2^26)).
+CG_HD void fe_neg_p(fe& h, const fe& f) {
+  CG_UNROLL for (int i = 0; i < 10; ++i) {
+    const int32_t p = i == 0 ? (1 << 26) - 19 : (i & 1) ? (1 << 25) - 1 : (1 << 26) - 1;
+    h.v[i] = p - f.v[i];
+  }
+}
 // h = c ? g : f   (c is 0/1; branch-free so divergent lanes cost nothing extra)
 CG_HD void fe_select(fe& h, const fe& f, const fe& g, uint32_t c) {
   const int32_t m = -(int32_t)c;
   CG_UNROLL for (int i = 0; i < 10; ++i) h.v[i] = f.v[i] ^ ((f.v[i] ^ g.v[i]) & m);
+}
+// h = c ? -f : f   (c is 0/1, per lane): (f ^ m) - m with m = -c
+CG_HD void fe_cneg(fe& h, const fe& f, uint32_t c) {
+  const int32_t m = -(int32_t)c;
+  CG_UNROLL for (int i = 0; i < 10; ++i) h.v[i] = (f.v[i] ^ m) - m;
 }
 
 // Pins a scaled limb (19 g_j, 2 f_i, ...) as a 32-bit value.  Without it LLVM
@@ -99,25 +114,10 @@ CG_HD int32_t fe_pin(int32_t x) {
 #endif
   return x;
 }
-
-// 2x / 4x / 8x of a limb as pinned 32-bit values through v_add_u32 (x + x): gfx950
-// issues v_add_u32 at the 2-cycle rate (72 T lane-ops/s measured) but v_lshlrev_b32,
-// which LLVM would pick for 2 * x, at the 4-cycle rate (38 T;
-// profiles/r02a_isa_rates.json); 4x and 8x are chained doublings of the 2x / 4x
-// values a squaring needs anyway.
-#ifndef CG_FE_X2_ADD
-#define CG_FE_X2_ADD 0  // A/B r02: the asm add version measured 0.8 % slower (more s_nop between dependent mads)
-#endif
-CG_HD int32_t fe_pin(int32_t x);
-CG_HD int32_t fe_x2(int32_t x) {
-#if defined(__HIP_DEVICE_COMPILE__) && CG_FE_X2_ADD
-  int32_t r;
-  asm("v_add_u32 %0, %1, %1" : "=v"(r) : "v"(x));
-  return r;
-#else
-  return fe_pin((int32_t)((uint32_t)x * 2u));
-#endif
-}
+// m * x pinned as 32 bits (m = 2, 4, 8: v_lshlrev_b32; 19: v_mul_lo_u32).  A/B r02:
+// doublings through v_add_u32 x, x (a 2-cycle op, v_lshlrev_b32 takes 4) measured
+// 0.8 % slower as inline asm (it broke the interleaving of the mad chains).
+CG_HD int32_t fe_scale(int32_t x, int m, bool g_side = false) { return fe_pin(CG_SCALE(x, m, g_side)); }
 
 // Signed carry chain (round-to-nearest) on 64-bit column sums -> reduced limbs.
 // With rounding carries c = (t + 2^(w-1)) >> w, the residue t - c*2^w is exactly
@@ -130,31 +130,7 @@ CG_HD int32_t sext_low32(int32_t x, int bits) {
   return (int32_t)((uint32_t)x << (32 - bits)) >> (32 - bits);
 }
 
-CG_HD void fe_carry_wide(fe& h, int64_t t[10]) {
-  int64_t c;
-#define CG_C26(k)                      \
-  c = (t[k] + (1LL << 25)) >> 26;      \
-  t[(k) + 1] += c;                     \
-  t[k] = sext_low64(t[k], 26);
-#define CG_C25(k)                      \
-  c = (t[k] + (1LL << 24)) >> 25;      \
-  t[(k) + 1] += c;                     \
-  t[k] = sext_low64(t[k], 25);
-  CG_C26(0) CG_C26(4)
-  CG_C25(1) CG_C25(5)
-  CG_C26(2) CG_C26(6)
-  CG_C25(3) CG_C25(7)
-  CG_C26(4) CG_C26(8)
-  c = (t[9] + (1LL << 24)) >> 25;
-  t[0] += c * 19;
-  t[9] = sext_low64(t[9], 25);
-  CG_C26(0)
-#undef CG_C26
-#undef CG_C25
-  CG_UNROLL for (int i = 0; i < 10; ++i) h.v[i] = fe_pin((int32_t)t[i]);
-}
-
-// Same chain on 32-bit limbs (for values already within ~2^29 per limb).
+// Rounding chain on 32-bit limbs (for values already within ~2^29 per limb).
 CG_HD void fe_reduce(fe& h) {
   int32_t c;
 #define CG_C26(k)                      \
@@ -188,93 +164,156 @@ CG_HD int64_t fe_pin64(int64_t x) {
   return x;
 }
 
-#ifndef CG_FE_FOLD
-#define CG_FE_FOLD 1
-#endif
-
-// Product sources for the column chains: op(k, i, acc) returns acc + the i-th
-// product of column k (acc unchanged if column k has no i-th product).
-struct FeMulOp {
-  int32_t f[10], f2[10], g[10], g19[10];
-  CG_HDM FeMulOp(const fe& F, const fe& G) {
-    CG_UNROLL for (int j = 0; j < 10; ++j) {
-      f[j] = F.v[j];
-      g[j] = G.v[j];
-      g19[j] = fe_pin(19 * G.v[j]);
-      f2[j] = (j & 1) ? fe_x2(F.v[j]) : F.v[j];
-    }
-  }
-  CG_HDM int64_t operator()(int k, int i, int64_t acc) const {
-    const int j = (k - i + 10) % 10;
-    const int32_t a = (j & 1) ? f2[i] : f[i];
-    const int32_t b = (i + j >= 10) ? g19[j] : g[j];
-    return fe_pin64(acc + (int64_t)a * b);
-  }
-};
-// f^2 (DOUBLE: 2 f^2, by doubling the limb multipliers: 8 f_i <= 2^30.7 for the
-// odd limbs, within int32 like 19 f_j).
-template <bool DOUBLE>
-struct FeSqOp {
-  int32_t f[10], f2[10], f4[10], f8[10], f19[10];
-  CG_HDM explicit FeSqOp(const fe& F) {
-    CG_UNROLL for (int j = 0; j < 10; ++j) {
-      f[j] = F.v[j];
-      f19[j] = fe_pin(19 * F.v[j]);
-      f2[j] = fe_x2(F.v[j]);
-      f4[j] = fe_x2(f2[j]);
-      f8[j] = fe_x2(f4[j]);
-    }
-  }
-  // column k: products i <= j, i + j = k (mod 10), by rank n: i = n for
-  // n <= k/2 (j = k - i), then i = k + 1 ... (k + 10)/2 (j = k + 10 - i)
-  CG_HDM int64_t operator()(int k, int n, int64_t acc) const {
-    const int i = n <= k / 2 ? n : k + n - k / 2;
-    if (i > (k + 10) / 2) return acc;
-    const int j = (k - i + 10) % 10;
-    const int m = ((i == j) ? 1 : 2) * (((i & 1) && (j & 1)) ? 2 : 1) * (DOUBLE ? 2 : 1);
-    const int32_t a = m == 1 ? f[i] : m == 2 ? f2[i] : m == 4 ? f4[i] : f8[i];
-    const int32_t b = (i + j >= 10) ? f19[j] : f[j];
-    return fe_pin64(acc + (int64_t)a * b);
-  }
-};
-
-// Column-serial carry chain: column k's mad chain starts from column k-1's
-// carry (the mad's 64-bit addend, so the carry costs no add), then carry out
-// with round-to-nearest.  Columns 0..9 in order, the wrap 19*c9 into limb 0 and
-// one more carry 0 -> 1: 11 carries of 3 instructions instead of the 12 of 4 of
-// fe_carry_wide.  Output limb bounds match fe_carry_wide's (|h_k| <= 2^25 /
-// 2^24, limb 1 a few units more).  fe_fold_pair runs two independent chains in
-// lockstep so consecutive mads never depend on each other (a dependent
-// v_mad_i64_i32 needs a wait state).
+// ---------------------------------------------------------------------------
+// Products.  A product is ten column chains of v_mad_i64_i32 (column k collects
+// f_i g_j for i + j = k, and 19 f_i g_j for i + j = k + 10; products of two odd
+// limbs carry an extra factor 2 because the odd limbs are 25 bits wide), each chain
+// starting from the previous column's carry, then a carry out.  Two carry modes:
+//
+//   round  c = (t + 2^(w-1)) >> w, limb = sext_low(t, w): limbs in [-2^(w-1), 2^(w-1))
+//          — 3 four-cycle ops per carry (64-bit add, 64-bit shift, v_bfe_i32)
+//   floor  c = t >> w, limb = t & (2^w - 1): limbs in [0, 2^w) — one 64-bit shift and
+//          one 2-cycle v_and_b32 per carry (A/B r02s: msm -7.6 %, points -9 %)
+//
+// Floor-reduced limbs are twice as large in magnitude, so which carry each product
+// uses is chosen per product in cg_ge25519.h, together with fe_add_p corrections,
+// such that every 19-scaled operand stays within int32 (|g| <= 1.684 * 2^26) and every
+// column within int64 — proved for all inputs by tests/test_fe_intervals.py (an
+// interval analysis of the exact operation sequences) and checked on real data by
+// the -DCG_CHECK_BOUNDS host build.
+// ---------------------------------------------------------------------------
 struct FeFoldState {
   int64_t acc, c;
   int32_t r[10];
 };
+template <bool FLOOR>
 CG_HD void fe_fold_carry(FeFoldState& s, int k) {
   const int w = (k & 1) ? 25 : 26;
-  s.c = (s.acc + (1LL << (w - 1))) >> w;
-  s.r[k] = (int32_t)sext_low64(s.acc, w);
+  if (FLOOR) {
+    s.c = s.acc >> w;
+    s.r[k] = (int32_t)((uint32_t)s.acc & ((1u << w) - 1));
+  } else {
+    s.c = (s.acc + (1LL << (w - 1))) >> w;
+    s.r[k] = (int32_t)sext_low64(s.acc, w);
+  }
 }
+// Wrap of the top carry: limb 0 += 19 c, one more carry 0 -> 1 (limb 1 may end a
+// few units outside its range: |19 c / 2^26| < 2^16).
+template <bool FLOOR>
 CG_HD void fe_fold_finish(fe& h, FeFoldState& s) {
   const int64_t t0 = (int64_t)s.r[0] + s.c * 19;
-  const int64_t c = (t0 + (1LL << 25)) >> 26;
-  s.r[0] = (int32_t)sext_low64(t0, 26);
+  int64_t c;
+  if (FLOOR) {
+    c = t0 >> 26;
+    s.r[0] = (int32_t)((uint32_t)t0 & ((1u << 26) - 1));
+  } else {
+    c = (t0 + (1LL << 25)) >> 26;
+    s.r[0] = (int32_t)sext_low64(t0, 26);
+  }
   s.r[1] += (int32_t)c;
   CG_UNROLL for (int i = 0; i < 10; ++i) h.v[i] = fe_pin(s.r[i]);
 }
+
+// Product sources for the column chains: op(k, i, acc) returns acc + the i-th
+// product of column k (acc unchanged if column k has no i-th product); term(k, i)
+// the same product in 128 bits (bound checking).  SCALE = 2: the doubled product
+// 2 f g, by doubling the f-side multipliers (2 f_i, 4 f_i for odd i).
+template <bool FLOOR, int SCALE = 1>
+struct FeMulOp {
+  static constexpr bool kFloor = FLOOR;
+  int32_t f[10], f2[10], g[10], g19[10];
+  CG_HDM FeMulOp(const fe& F, const fe& G) {
+    CG_UNROLL for (int j = 0; j < 10; ++j) {
+      f[j] = SCALE == 1 ? F.v[j] : fe_scale(F.v[j], SCALE);
+      f2[j] = (j & 1) ? fe_scale(F.v[j], 2 * SCALE) : f[j];
+      g[j] = G.v[j];
+      g19[j] = fe_scale(G.v[j], 19, true);
+    }
+  }
+  CG_HDM int32_t a(int k, int i) const { return ((k - i + 10) % 10 & 1) ? f2[i] : f[i]; }
+  CG_HDM int32_t b(int k, int i) const {
+    const int j = (k - i + 10) % 10;
+    return (i + j >= 10) ? g19[j] : g[j];
+  }
+  CG_HDM bool has(int, int) const { return true; }
+  CG_HDM int64_t operator()(int k, int i, int64_t acc) const { return fe_pin64(acc + (int64_t)a(k, i) * b(k, i)); }
+};
+// f^2 (SCALE = 2: 2 f^2, by doubling the limb multipliers: 8 f_i for the odd limbs).
+template <bool FLOOR, int SCALE = 1>
+struct FeSqOp {
+  static constexpr bool kFloor = FLOOR;
+  int32_t f[10], f2[10], f4[10], f8[10], f19[10];
+  CG_HDM explicit FeSqOp(const fe& F) {
+    CG_UNROLL for (int j = 0; j < 10; ++j) {
+      f[j] = F.v[j];
+      f19[j] = j >= 5 ? fe_scale(F.v[j], 19, true) : 0;  // only j >= 5 wrap (i <= j, i + j >= 10)
+      f2[j] = fe_scale(F.v[j], 2);
+      f4[j] = (j & 1) || SCALE == 2 ? fe_scale(F.v[j], 4) : 0;
+      f8[j] = (j & 1) && SCALE == 2 ? fe_scale(F.v[j], 8) : 0;
+    }
+  }
+  // column k: products i <= j, i + j = k (mod 10), by rank n: i = n for
+  // n <= k/2 (j = k - i), then i = k + 1 ... (k + 10)/2 (j = k + 10 - i)
+  CG_HDM int idx(int k, int n) const { return n <= k / 2 ? n : k + n - k / 2; }
+  CG_HDM bool has(int k, int n) const { return idx(k, n) <= (k + 10) / 2; }
+  CG_HDM int32_t a(int k, int n) const {
+    const int i = idx(k, n), j = (k - i + 10) % 10;
+    const int m = ((i == j) ? 1 : 2) * (((i & 1) && (j & 1)) ? 2 : 1) * SCALE;
+    return m == 1 ? f[i] : m == 2 ? f2[i] : m == 4 ? f4[i] : f8[i];
+  }
+  CG_HDM int32_t b(int k, int n) const {
+    const int i = idx(k, n), j = (k - i + 10) % 10;
+    return (i + j >= 10) ? f19[j] : f[j];
+  }
+  CG_HDM int64_t operator()(int k, int n, int64_t acc) const {
+    if (!has(k, n)) return acc;
+    return fe_pin64(acc + (int64_t)a(k, n) * b(k, n));
+  }
+};
+
+#if defined(CG_CHECK_BOUNDS) && !defined(__HIP_DEVICE_COMPILE__)
+// The chain of one op in 128 bits: columns checked against int64 and the result
+// compared with the 64-bit chain's.
+template <typename Op>
+inline void cg_bounds_chain(const Op& op) {
+  __int128 c = 0;
+  for (int k = 0; k < 10; ++k) {
+    __int128 acc = c;
+    int64_t acc64 = (int64_t)c;
+    for (int i = 0; i < 10; ++i) {
+      if (!op.has(k, i)) continue;
+      acc += (__int128)op.a(k, i) * op.b(k, i);
+      cg_bounds_col(acc);
+      acc64 = op(k, i, acc64);
+    }
+    if ((__int128)acc64 != acc) __builtin_trap();
+    const int w = (k & 1) ? 25 : 26;
+    c = Op::kFloor ? (acc >> w) : ((acc + ((__int128)1 << (w - 1))) >> w);
+  }
+}
+#define CG_BOUNDS_CHAIN(op) cg_bounds_chain(op)
+#else
+#define CG_BOUNDS_CHAIN(op) ((void)0)
+#endif
+
 template <typename Op>
 CG_HD void fe_fold_chain(fe& h, const Op& op) {
+  CG_BOUNDS_CHAIN(op);
   FeFoldState s;
   s.c = 0;
   CG_UNROLL for (int k = 0; k < 10; ++k) {
     s.acc = s.c;
     CG_UNROLL for (int i = 0; i < 10; ++i) s.acc = op(k, i, s.acc);
-    fe_fold_carry(s, k);
+    fe_fold_carry<Op::kFloor>(s, k);
   }
-  fe_fold_finish(h, s);
+  fe_fold_finish<Op::kFloor>(h, s);
 }
+// Two / three independent chains in lockstep so consecutive mads never depend on
+// each other (a dependent v_mad_i64_i32 needs wait states).
 template <typename Op0, typename Op1>
 CG_HD void fe_fold_pair(fe& h0, const Op0& op0, fe& h1, const Op1& op1) {
+  CG_BOUNDS_CHAIN(op0);
+  CG_BOUNDS_CHAIN(op1);
   FeFoldState s0, s1;
   s0.c = s1.c = 0;
   CG_UNROLL for (int k = 0; k < 10; ++k) {
@@ -284,77 +323,17 @@ CG_HD void fe_fold_pair(fe& h0, const Op0& op0, fe& h1, const Op1& op1) {
       s0.acc = op0(k, i, s0.acc);
       s1.acc = op1(k, i, s1.acc);
     }
-    fe_fold_carry(s0, k);
-    fe_fold_carry(s1, k);
+    fe_fold_carry<Op0::kFloor>(s0, k);
+    fe_fold_carry<Op1::kFloor>(s1, k);
   }
-  fe_fold_finish(h0, s0);
-  fe_fold_finish(h1, s1);
+  fe_fold_finish<Op0::kFloor>(h0, s0);
+  fe_fold_finish<Op1::kFloor>(h1, s1);
 }
-
-// h = f * g.  Column k collects f_i g_j for i+j = k (and 19 f_i g_j for
-// i+j = k+10); products of two odd limbs carry an extra factor 2 because the
-// odd limbs are 25 bits wide.
-CG_HD void fe_mul(fe& h, const fe& f, const fe& g) {
-#if !CG_FE_FOLD || defined(CG_CHECK_BOUNDS)
-  int32_t g19[10], f2[10];
-  CG_UNROLL for (int j = 0; j < 10; ++j) g19[j] = fe_pin(19 * g.v[j]);
-  CG_UNROLL for (int i = 0; i < 10; ++i) f2[i] = (i & 1) ? fe_pin(2 * f.v[i]) : f.v[i];
-  int64_t t[10];
-  CG_UNROLL for (int k = 0; k < 10; ++k) t[k] = 0;
-  CG_UNROLL for (int i = 0; i < 10; ++i) {
-    CG_UNROLL for (int j = 0; j < 10; ++j) {
-      const int k = i + j;
-      const int32_t a = (j & 1) ? f2[i] : f.v[i];
-      const int32_t b = (k >= 10) ? g19[j] : g.v[j];
-      t[k >= 10 ? k - 10 : k] += (int64_t)a * b;
-    }
-  }
-  CG_BOUNDS_MUL(f, g, t, 0);
-#endif
-#if CG_FE_FOLD
-  fe_fold_chain(h, FeMulOp(f, g));
-#else
-  fe_carry_wide(h, t);
-#endif
-}
-
-// h = f^2 (DOUBLE ? 2 f^2 : f^2): 55 products using the symmetry f_i f_j = f_j f_i.
-template <bool DOUBLE>
-CG_HD void fe_sq_t(fe& h, const fe& f) {
-#if !CG_FE_FOLD || defined(CG_CHECK_BOUNDS)
-  int32_t f19[10], f2[10], f4[10];
-  CG_UNROLL for (int j = 0; j < 10; ++j) {
-    f19[j] = fe_pin(19 * f.v[j]);
-    f2[j] = fe_pin(2 * f.v[j]);
-    f4[j] = fe_pin(4 * f.v[j]);
-  }
-  int64_t t[10];
-  CG_UNROLL for (int k = 0; k < 10; ++k) t[k] = 0;
-  CG_UNROLL for (int i = 0; i < 10; ++i) {
-    CG_UNROLL for (int j = i; j < 10; ++j) {
-      const int k = i + j;
-      const int m = ((i == j) ? 1 : 2) * (((i & 1) && (j & 1)) ? 2 : 1);
-      const int32_t a = m == 1 ? f.v[i] : m == 2 ? f2[i] : f4[i];
-      const int32_t b = (k >= 10) ? f19[j] : f.v[j];
-      t[k >= 10 ? k - 10 : k] += (int64_t)a * b;
-    }
-  }
-  if (DOUBLE) {
-    CG_UNROLL for (int k = 0; k < 10; ++k) t[k] *= 2;
-  }
-  CG_BOUNDS_MUL(f, f, t, DOUBLE);
-#endif
-#if CG_FE_FOLD
-  fe_fold_chain(h, FeSqOp<DOUBLE>(f));
-#else
-  fe_carry_wide(h, t);
-#endif
-}
-CG_HD void fe_sq(fe& h, const fe& f) { fe_sq_t<false>(h, f); }
-CG_HD void fe_sq2(fe& h, const fe& f) { fe_sq_t<true>(h, f); }
-
 template <typename Op0, typename Op1, typename Op2>
 CG_HD void fe_fold_triple(fe& h0, const Op0& op0, fe& h1, const Op1& op1, fe& h2, const Op2& op2) {
+  CG_BOUNDS_CHAIN(op0);
+  CG_BOUNDS_CHAIN(op1);
+  CG_BOUNDS_CHAIN(op2);
   FeFoldState s0, s1, s2;
   s0.c = s1.c = s2.c = 0;
   CG_UNROLL for (int k = 0; k < 10; ++k) {
@@ -366,62 +345,65 @@ CG_HD void fe_fold_triple(fe& h0, const Op0& op0, fe& h1, const Op1& op1, fe& h2
       s1.acc = op1(k, i, s1.acc);
       s2.acc = op2(k, i, s2.acc);
     }
-    fe_fold_carry(s0, k);
-    fe_fold_carry(s1, k);
-    fe_fold_carry(s2, k);
+    fe_fold_carry<Op0::kFloor>(s0, k);
+    fe_fold_carry<Op1::kFloor>(s1, k);
+    fe_fold_carry<Op2::kFloor>(s2, k);
   }
-  fe_fold_finish(h0, s0);
-  fe_fold_finish(h1, s1);
-  fe_fold_finish(h2, s2);
+  fe_fold_finish<Op0::kFloor>(h0, s0);
+  fe_fold_finish<Op1::kFloor>(h1, s1);
+  fe_fold_finish<Op2::kFloor>(h2, s2);
 }
 
-// Two independent products interleaved (h0 = op0, h1 = op1); the ops copy their
-// inputs, so h0 / h1 may alias any source.
-struct FeMul {
+// Product descriptors (the op objects copy their inputs, so outputs may alias any
+// source).  Suffix F = floor carries; Mul2 / Sq2 = doubled product.
+template <bool FLOOR, int SCALE>
+struct FeMulT {
   const fe& f;
   const fe& g;
 };
-struct FeSq {
+template <bool FLOOR, int SCALE>
+struct FeSqT {
   const fe& f;
 };
-struct FeSq2 {
-  const fe& f;
-};
-CG_HD void fe_single(fe& h, const FeMul& o) { fe_mul(h, o.f, o.g); }
-CG_HD void fe_single(fe& h, const FeSq& o) { fe_sq(h, o.f); }
-CG_HD void fe_single(fe& h, const FeSq2& o) { fe_sq2(h, o.f); }
-CG_HD FeMulOp fe_op(const FeMul& o) { return FeMulOp(o.f, o.g); }
-CG_HD FeSqOp<false> fe_op(const FeSq& o) { return FeSqOp<false>(o.f); }
-CG_HD FeSqOp<true> fe_op(const FeSq2& o) { return FeSqOp<true>(o.f); }
+using FeMul = FeMulT<false, 1>;
+using FeMulF = FeMulT<true, 1>;
+using FeMul2F = FeMulT<true, 2>;
+using FeSq = FeSqT<false, 1>;
+using FeSqF = FeSqT<true, 1>;
+using FeSq2 = FeSqT<false, 2>;
+using FeSq2F = FeSqT<true, 2>;
+template <bool FL, int SC>
+CG_HD FeMulOp<FL, SC> fe_op(const FeMulT<FL, SC>& o) {
+  return FeMulOp<FL, SC>(o.f, o.g);
+}
+template <bool FL, int SC>
+CG_HD FeSqOp<FL, SC> fe_op(const FeSqT<FL, SC>& o) {
+  return FeSqOp<FL, SC>(o.f);
+}
+template <typename A>
+CG_HD void fe_one(fe& h, const A& a) {
+  fe_fold_chain(h, fe_op(a));
+}
 template <typename A, typename B>
 CG_HD void fe_pair(fe& h0, const A& a, fe& h1, const B& b) {
-#if CG_FE_FOLD && !defined(CG_CHECK_BOUNDS)
   fe_fold_pair(h0, fe_op(a), h1, fe_op(b));
-#else
-  fe t;
-  fe_single(t, a);
-  fe_single(h1, b);
-  h0 = t;
-#endif
 }
-
 template <typename A, typename B, typename C>
 CG_HD void fe_triple(fe& h0, const A& a, fe& h1, const B& b, fe& h2, const C& c) {
-#if CG_FE_FOLD && !defined(CG_CHECK_BOUNDS)
   fe_fold_triple(h0, fe_op(a), h1, fe_op(b), h2, fe_op(c));
-#else
-  fe t0, t1;
-  fe_single(t0, a);
-  fe_single(t1, b);
-  fe_single(h2, c);
-  h0 = t0;
-  h1 = t1;
-#endif
 }
 
+// h = f * g, f^2, 2 f^2 (rounding carries: limbs |h_k| <= 2^(w-1) + small)
+CG_HD void fe_mul(fe& h, const fe& f, const fe& g) { fe_one(h, FeMul{f, g}); }
+CG_HD void fe_sq(fe& h, const fe& f) { fe_one(h, FeSq{f}); }
+CG_HD void fe_sq2(fe& h, const fe& f) { fe_one(h, FeSq2{f}); }
+// floor-carry versions (limbs in [0, 2^w), limb 1 within 2^16 of it)
+CG_HD void fe_mul_f(fe& h, const fe& f, const fe& g) { fe_one(h, FeMulF{f, g}); }
+CG_HD void fe_sq_f(fe& h, const fe& f) { fe_one(h, FeSqF{f}); }
+
 CG_HD void fe_sqn(fe& h, const fe& f, int n) {
-  fe_sq(h, f);
-  CG_NOUNROLL for (int i = 1; i < n; ++i) fe_sq(h, h);
+  fe_sq_f(h, f);
+  CG_NOUNROLL for (int i = 1; i < n; ++i) fe_sq_f(h, h);
 }
 
 // 8 little-endian 32-bit words -> limbs.  Bit 255 is ignored and the value is NOT
@@ -479,53 +461,54 @@ CG_HD uint32_t fe_iszero(const fe& f) {
 }
 
 // z^(2^250 - 1) and z^11 (shared prefix of the inversion / square-root chains).
+// The exponentiations use floor carries throughout (every input is a reduced value).
 CG_HD void fe_pow2_250_1(fe& out, fe& z11, const fe& z) {
   fe z2, z9, t, a, b;
-  fe_sq(z2, z);
+  fe_sq_f(z2, z);
   fe_sqn(t, z2, 2);
-  fe_mul(z9, t, z);
-  fe_mul(z11, z9, z2);
-  fe_sq(t, z11);
-  fe_mul(a, t, z9);     // 2^5 - 1
+  fe_mul_f(z9, t, z);
+  fe_mul_f(z11, z9, z2);
+  fe_sq_f(t, z11);
+  fe_mul_f(a, t, z9);     // 2^5 - 1
   fe_sqn(t, a, 5);
-  fe_mul(a, t, a);      // 2^10 - 1
+  fe_mul_f(a, t, a);      // 2^10 - 1
   fe_sqn(t, a, 10);
-  fe_mul(b, t, a);      // 2^20 - 1
+  fe_mul_f(b, t, a);      // 2^20 - 1
   fe_sqn(t, b, 20);
-  fe_mul(t, t, b);      // 2^40 - 1
+  fe_mul_f(t, t, b);      // 2^40 - 1
   fe_sqn(t, t, 10);
-  fe_mul(a, t, a);      // 2^50 - 1
+  fe_mul_f(a, t, a);      // 2^50 - 1
   fe_sqn(t, a, 50);
-  fe_mul(b, t, a);      // 2^100 - 1
+  fe_mul_f(b, t, a);      // 2^100 - 1
   fe_sqn(t, b, 100);
-  fe_mul(t, t, b);      // 2^200 - 1
+  fe_mul_f(t, t, b);      // 2^200 - 1
   fe_sqn(t, t, 50);
-  fe_mul(out, t, a);    // 2^250 - 1
+  fe_mul_f(out, t, a);    // 2^250 - 1
 }
 
 CG_HD void fe_invert(fe& out, const fe& z) {
   fe t, z11;
   fe_pow2_250_1(t, z11, z);
   fe_sqn(t, t, 5);
-  fe_mul(out, t, z11);  // z^(2^255 - 21)
+  fe_mul_f(out, t, z11);  // z^(2^255 - 21)
 }
 
 CG_HD void fe_pow22523(fe& out, const fe& z) {
   fe t, z11;
   fe_pow2_250_1(t, z11, z);
   fe_sqn(t, t, 2);
-  fe_mul(out, t, z);    // z^(2^252 - 3)
+  fe_mul_f(out, t, z);    // z^(2^252 - 3)
 }
 
 // The same chains on two independent inputs in lockstep (the key and R decodes
 // of the points kernel): every step is an fe_pair, so the dependent squarings of
 // one chain interleave with the other's.
 CG_HD void fe_sqn_pair(fe& h0, const fe& f0, fe& h1, const fe& f1, int n) {
-  fe_pair(h0, FeSq{f0}, h1, FeSq{f1});
-  CG_NOUNROLL for (int i = 1; i < n; ++i) fe_pair(h0, FeSq{h0}, h1, FeSq{h1});
+  fe_pair(h0, FeSqF{f0}, h1, FeSqF{f1});
+  CG_NOUNROLL for (int i = 1; i < n; ++i) fe_pair(h0, FeSqF{h0}, h1, FeSqF{h1});
 }
 CG_HD void fe_mul_pair(fe& h0, const fe& f0, const fe& g0, fe& h1, const fe& f1, const fe& g1) {
-  fe_pair(h0, FeMul{f0, g0}, h1, FeMul{f1, g1});
+  fe_pair(h0, FeMulF{f0, g0}, h1, FeMulF{f1, g1});
 }
 CG_HD void fe_pow22523_pair(fe& out0, const fe& z0, fe& out1, const fe& z1) {
   fe z2[2], z9[2], z11[2], t[2], a[2], b[2];

@@ -1,11 +1,11 @@
 # A/B timing of library variants on the GPU box: bash tools/ab_bench.sh [name ...]
-# "new" is the in-tree corda_amd/libcordagpu.so, any other name variants/libcg_<name>.so.
+# "new" is the in-tree corda_amd/libcordagpu.so, any other name abvar/libcg_<name>.so.
 # Each variant runs twice, interleaved; results go to gpurun_out/ab.txt.
 set -e
 names=${*:-base new}
 for rep in 1 2; do
   for v in $names; do
-    if [ $v = new ]; then unset CORDA_AMD_LIB; else export CORDA_AMD_LIB=$PWD/variants/libcg_$v.so; fi
+    if [ $v = new ]; then unset CORDA_AMD_LIB; else export CORDA_AMD_LIB=$PWD/abvar/libcg_$v.so; fi
     timeout -k 10 200 python -u bench.py --steps 10 --warmup 2 --no-cpu-baseline --latency-runs 1 $AB_ARGS > gpurun_out/ab_$v.log 2>&1
     python -c "import json; d=json.loads(open('gpurun_out/ab_$v.log').read().splitlines()[-1]); print('$v', d['value'], {k:v['avg_launch_ms'] for k,v in d['kernels'].items()})" >> gpurun_out/ab.txt
   done
