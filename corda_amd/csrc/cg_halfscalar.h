@@ -21,6 +21,8 @@
 // unusually long chain (probability ~1e-8 for hash-derived h) fall back to
 // (c0, c1) = (h, 1), i.e. a full-length loop for that wave: same result, slower.
 #pragma once
+#include <math.h>
+
 #include "cg_sc25519.h"
 
 namespace cg {
@@ -166,38 +168,58 @@ CG_HD void mp9_lincomb(uint32_t out[9], const uint32_t x[9], const uint32_t y[9]
   }
 }
 
+CG_HD double hs_rcp(double y) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_rcp(y);
+#else
+  return 1.0 / y;
+#endif
+}
+
 // Lehmer's algorithm (Knuth TAOCP 4.5.2, Algorithm L) on 52-bit leading digits:
-// up to ~20 Euclid quotients emulated in 64-bit arithmetic (each verified by
+// up to ~20 Euclid quotients emulated on the leading digits (each verified by
 // Knuth's two-sided test, so the quotient sequence is exactly Euclid's), then
 // applied to (a, b, ta, tb) at once.  The emulation stops before a remainder
 // can get close to 2^128, so the exact single steps find the first remainder
 // below 2^128 — the same (a, b, ta, tb) the plain step-by-step loop reaches.
+// The emulation runs in fp64: every quantity is an integer of magnitude < 2^53
+// (leading digits < 2^52, cofactors < 2^31), so each v_fma_f64 below is exact
+// whenever its true result is below 2^53, and rounding is monotonic where it is
+// not (those cases only ever trip a bound check and end the emulation).  About
+// a third of the int64 version's instructions (64-bit multiplies and compares
+// are several ops each on the VALU).  The quotient estimate x1 * rcp(y1) (one
+// Newton step) is within one of floor(x1 / y1) and corrected on the remainder.
 // Returns 0 when no quotient was emulated (the caller takes an exact step).
 template <int TB = 128>
 CG_HD uint32_t hs_lehmer(uint32_t a[9], uint32_t b[9], uint32_t ta[9], uint32_t tb[9]) {
   const uint32_t s = mp9_bitlen(a) - 52;  // caller guarantees bitlen(a) > TB + 4
-  int64_t uh = (int64_t)mp9_shr64(a, s), vh = (int64_t)mp9_shr64(b, s);
+  double uh = (double)mp9_shr64(a, s), vh = (double)mp9_shr64(b, s);
   // An emulated remainder T stands for a true one in (T - |C| - |D|, T + |C| + |D|)
   // * 2^s with |C|, |D| < 2^31: T >= 2^(TB+1-s) + 2^33 keeps every emulated
   // remainder above 2^TB (s ranges over TB-47..204).
-  const int64_t thr = (s < (uint32_t)TB + 1 ? (int64_t)1 << (TB + 1 - s) : (int64_t)0) + ((int64_t)1 << 33);
-  int64_t A = 1, B = 0, C = 0, D = 1;
+  const double thr = (double)((s < (uint32_t)TB + 1 ? (int64_t)1 << (TB + 1 - s) : (int64_t)0) + ((int64_t)1 << 33));
+  const double lim = 2147483647.0;
+  double A = 1.0, B = 0.0, C = 0.0, D = 1.0;
   CG_NOUNROLL for (int it = 0; it < 48; ++it) {
-    const int64_t y1 = vh + C, y2 = vh + D, x1 = uh + A, x2 = uh + B;
-    if (y1 <= 0 || y2 <= 0 || x1 < 0 || x2 < 0) break;
-    // q = floor(x1 / y1): operands < 2^53 are exact doubles, the rounded quotient
-    // is within 1 of the floor
-    int64_t q = (int64_t)((double)x1 / (double)y1);
-    const int64_t r1 = x1 - q * y1;
-    q = r1 < 0 ? q - 1 : (r1 >= y1 ? q + 1 : q);
-    if (q < 1 || q >= ((int64_t)1 << 31)) break;
-    // Knuth's test: the other bound gives the same quotient (q y2 <= x2 < 2^53)
-    if ((double)q * (double)y2 > 9.0e15) break;
-    const int64_t r2 = x2 - q * y2;
-    if (r2 < 0 || r2 >= y2) break;
-    const int64_t T = uh - q * vh, nC = A - q * C, nD = B - q * D;
-    const int64_t lim = ((int64_t)1 << 31) - 1;
-    if (T < thr || nC > lim || nC < -lim || nD > lim || nD < -lim) break;
+    const double y1 = vh + C, y2 = vh + D, x1 = uh + A, x2 = uh + B;
+    if (y1 <= 0.0 || y2 <= 0.0 || x1 < 0.0 || x2 < 0.0) break;
+    double r = hs_rcp(y1);
+    r = fma(fma(-y1, r, 1.0), r, r);
+    double q = floor(x1 * r);
+    double r1 = fma(-q, y1, x1);
+    if (r1 < 0.0) {
+      q -= 1.0;
+      r1 += y1;
+    } else if (r1 >= y1) {
+      q += 1.0;
+      r1 -= y1;
+    }
+    if (r1 < 0.0 || r1 >= y1 || q < 1.0 || q > lim) break;
+    // Knuth's test: the other bound gives the same quotient
+    const double r2 = fma(-q, y2, x2);
+    if (r2 < 0.0 || r2 >= y2) break;
+    const double T = fma(-q, vh, uh), nC = fma(-q, C, A), nD = fma(-q, D, B);
+    if (T < thr || fabs(nC) > lim || fabs(nD) > lim) break;
     A = C;
     C = nC;
     B = D;
@@ -205,12 +227,13 @@ CG_HD uint32_t hs_lehmer(uint32_t a[9], uint32_t b[9], uint32_t ta[9], uint32_t 
     uh = vh;
     vh = T;
   }
-  if (B == 0) return 0;
+  if (B == 0.0) return 0;
   uint32_t na[9], nb[9], nta[9], ntb[9];
-  mp9_lincomb(na, a, b, A, B);
-  mp9_lincomb(nb, a, b, C, D);
-  mp9_lincomb(nta, ta, tb, A, B);
-  mp9_lincomb(ntb, ta, tb, C, D);
+  const int64_t iA = (int64_t)A, iB = (int64_t)B, iC = (int64_t)C, iD = (int64_t)D;
+  mp9_lincomb(na, a, b, iA, iB);
+  mp9_lincomb(nb, a, b, iC, iD);
+  mp9_lincomb(nta, ta, tb, iA, iB);
+  mp9_lincomb(ntb, ta, tb, iC, iD);
   CG_UNROLL for (int w = 0; w < 9; ++w) {
     a[w] = na[w];
     b[w] = nb[w];
