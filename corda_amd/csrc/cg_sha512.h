@@ -136,6 +136,29 @@ CG_HD uint32_t alignbyte(uint32_t hi, uint32_t lo, uint32_t sh) {
 #endif
 }
 
+// nw big-endian 64-bit words from message dwords m4[0 .. 2 nw] (byte shift sh):
+// 16-byte loads at 4-byte alignment (the arena is only dword-aligned), then a
+// funnel shift per dword.  Reads exactly 2 nw + 1 dwords.
+template <int NW>
+CG_HD void sha512_load_words(uint64_t* w, const uint32_t* m4, uint32_t sh) {
+  uint32_t x[2 * NW + 1];
+#if defined(__HIP_DEVICE_COMPILE__)
+  typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
+  CG_UNROLL for (int q = 0; q < NW / 2; ++q) {
+    const u32x4_a4 v = reinterpret_cast<const u32x4_a4*>(m4)[q];
+    x[4 * q] = v.x;
+    x[4 * q + 1] = v.y;
+    x[4 * q + 2] = v.z;
+    x[4 * q + 3] = v.w;
+  }
+#else
+  for (int q = 0; q < 2 * NW; ++q) x[q] = m4[q];
+#endif
+  x[2 * NW] = m4[2 * NW];
+  CG_UNROLL for (int j = 0; j < NW; ++j)
+    w[j] = be64_from_le32(alignbyte(x[2 * j + 1], x[2 * j], sh), alignbyte(x[2 * j + 2], x[2 * j + 1], sh));
+}
+
 // SHA-512(prefix64 || M) where prefix64 is given as 8 little-endian u32 words of
 // R followed by 8 of Abyte, M = msg[0..n).  The reader never touches bytes at or
 // beyond m + n rounded up to 4 (callers pad device arenas by 16 bytes anyway).
@@ -152,6 +175,18 @@ CG_HD void sha512_ed25519(uint32_t out[16], const uint32_t r[8], const uint32_t 
   // dword j of M (relative, may be partially before m when sh != 0) is m4[j]
   const int64_t ndw = ((int64_t)n + sh + 3) >> 2;  // dwords that hold message bytes
   CG_NOUNROLL for (uint32_t blk = 0; blk < nb; ++blk) {
+    // fast path: the block's message words lie inside M and the dword after them is
+    // readable (every block but the last one or two of a long message); lanes of a
+    // wave may differ here, the compression below is shared
+    const int64_t q0 = 128 * (int64_t)blk - 64;  // message byte offset of word 0
+    if (blk == 0 && (int64_t)n >= 64 && 16 < ndw) {
+      CG_UNROLL for (int j = 0; j < 8; ++j) {
+        w[j] = j < 4 ? be64_from_le32(r[2 * j], r[2 * j + 1]) : be64_from_le32(abyte[2 * (j - 4)], abyte[2 * (j - 4) + 1]);
+      }
+      sha512_load_words<8>(w + 8, m4, sh);
+    } else if (blk != 0 && q0 + 128 <= (int64_t)n && (q0 >> 2) + 32 < ndw) {
+      sha512_load_words<16>(w, m4 + (q0 >> 2), sh);
+    } else {
     CG_UNROLL for (int j = 0; j < 16; ++j) {
       const int64_t off = 128 * (int64_t)blk + 8 * j;  // stream byte offset
       uint64_t word;
@@ -181,6 +216,7 @@ CG_HD void sha512_ed25519(uint32_t out[16], const uint32_t r[8], const uint32_t 
       if (blk == nb - 1 && j == 14) word = 0;
       if (blk == nb - 1 && j == 15) word = total * 8;
       w[j] = word;
+    }
     }
     sha512_block(h, w);
   }
