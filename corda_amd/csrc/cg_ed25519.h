@@ -331,8 +331,12 @@ CG_HD uint32_t ed25519_msm(uint32_t ndig, const uint32_t dig[kDigitWords], uint3
       dr[0] <<= 4;
       const uint32_t na = ea < 8, nr = er < 8;
       getA(na ? 8 - ea : ea - 8, ca);
-      ge_p1p1_to_p3(r3, t);
-      ge_add_cached(t, r3, ca, na);
+      if (pos != top) {
+        ge_p1p1_to_p3(r3, t);
+        ge_add_cached(t, r3, ca, na);
+      } else {
+        ge_add_cached(t, ge_identity_p3(), ca, na);  // constant operand: mostly folded away
+      }
       getR(nr ? 8 - er : er - 8, ca);
       ge_p1p1_to_p3(r3, t);
       ge_add_cached(t, r3, ca, nr ^ rneg);
@@ -412,8 +416,12 @@ CG_HD uint32_t ed25519_msm_reuse(uint32_t c3w, uint32_t win17, const uint32_t di
           if (c < 3 || j < c3w) {  // wave-uniform
             const uint32_t n = e < 8;
             getA(c, n ? 8 - e : e - 8, ca);
-            ge_p1p1_to_p3(r3, t);
-            ge_add_cached(t, r3, ca, n);
+            if (pos != top || c != 0) {
+              ge_p1p1_to_p3(r3, t);
+              ge_add_cached(t, r3, ca, n);
+            } else {
+              ge_add_cached(t, ge_identity_p3(), ca, n);
+            }
           }
         }
       }
@@ -424,8 +432,12 @@ CG_HD uint32_t ed25519_msm_reuse(uint32_t c3w, uint32_t win17, const uint32_t di
       }
       const uint32_t nr = er < 8;
       getR(nr ? 8 - er : er - 8, ca);
-      ge_p1p1_to_p3(r3, t);
-      ge_add_cached(t, r3, ca, nr ^ rneg);
+      if (pos != top || j < 16) {
+        ge_p1p1_to_p3(r3, t);
+        ge_add_cached(t, r3, ca, nr ^ rneg);
+      } else {
+        ge_add_cached(t, ge_identity_p3(), ca, nr ^ rneg);  // a 17th window: R comes first
+      }
     }
     if ((pos & 15) == 0 && pos < 64) {
       constexpr uint32_t kHalf = 1u << 15;

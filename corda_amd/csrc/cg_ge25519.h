@@ -99,6 +99,17 @@ CG_HD void ge_p3_dbl(ge_p1p1& r, const ge_p3& p) {
   ge_p2_dbl<true>(r, q);
 }
 
+// The identity as a p3 constant (0 : 1 : 1 : 0): an addition to it folds to a few
+// products (the MSM's first window).
+CG_HD ge_p3 ge_identity_p3() {
+  ge_p3 r;
+  fe_0(r.X);
+  fe_1(r.Y);
+  fe_1(r.Z);
+  fe_0(r.T);
+  return r;
+}
+
 // P + Q (neg = 0) or P - Q (neg = 1) with Q cached; neg may differ per lane.
 // -Q = (Y-X, Y+X, Z, -2dT): the first two are swapped, 2dT negated.
 CG_HD void ge_add_cached(ge_p1p1& r, const ge_p3& p, const ge_cached& q, uint32_t neg) {

@@ -296,6 +296,7 @@ def negate_p3(p):
 
 
 IDENTITY_P1P1 = (ZERO, ONE, ONE, ONE)
+IDENTITY_P3 = (ZERO, ONE, ONE, ZERO)
 IDENTITY_CACHED = (ONE, ONE, ONE, ZERO)
 
 
@@ -372,7 +373,8 @@ def msm_states(C, tab_a, tab_r, btab, rounds=4):
             p2 = to_p2(C, src)
             new["DBL0"] = dbl(C, p2, False)
             new["DBL1"] = dbl(C, p2, True)
-        new["ADD"] = add_cached(C, to_p3(C, union_of(["ID", "DBL1", "ADD"])), tab)
+        new["ADD"] = p3_union(add_cached(C, to_p3(C, union_of(["ID", "DBL1", "ADD"])), tab),
+                              add_cached(C, IDENTITY_P3, tab))  # first window: the constant identity
         if "ADD" in st:
             new["MADD"] = madd(C, to_p3(C, union_of(["ADD", "MADD"]), z_round=True), btab)
         for k, v in new.items():
