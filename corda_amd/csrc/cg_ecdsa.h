@@ -102,30 +102,27 @@ struct jpt {
 template <class C>
 CG_HD void ec_dbl(jpt& r, const jpt& p) {
   f26 t0, t1, t2, t3, x3, y3, z3;
+  // independent products run in pairs (f26_pair: two column chains interleaved)
   if (C::kAMinus3) {
     // dbl-2001-b: delta = Z^2, gamma = Y^2, beta = X gamma, alpha = 3 (X - delta)(X + delta)
-    f26 delta, gamma, beta, alpha;
-    f26_sqr<C>(delta, p.Z);  // 3 x 3
-    f26_sqr<C>(gamma, p.Y);
-    f26_mul<C>(beta, p.X, gamma);
+    f26 delta, gamma, beta, alpha, yz;
+    f26_pair<C>(delta, F26Sqr{p.Z}, gamma, F26Sqr{p.Y});  // 3 x 3, 1 x 1
     f26_sub(t0, p.X, delta);
     f26_add(t1, p.X, delta);
-    f26_mul<C>(t2, t0, t1);  // 2 x 2
+    f26_pair<C>(beta, F26Mul{p.X, gamma}, t2, F26Mul{t0, t1});  // 1 x 1, 2 x 2
     f26_add(alpha, t2, t2);
     f26_add(alpha, alpha, t2);  // c 3
-    f26_sqr<C>(x3, alpha);      // 3 x 3
+    f26_add(yz, p.Y, p.Z);
+    f26_pair<C>(x3, F26Sqr{alpha}, z3, F26Sqr{yz});  // 3 x 3, 4 x 4
     f26_add(t0, beta, beta);
     f26_add(t0, t0, t0);  // 4 beta
     f26_add(t1, t0, t0);  // 8 beta
     f26_sub(x3, x3, t1);
     f26_norm<C>(x3);  // c 9
-    f26_add(t2, p.Y, p.Z);
-    f26_sqr<C>(z3, t2);  // 4 x 4
     f26_sub(z3, z3, gamma);
     f26_sub(z3, z3, delta);  // c 3, left unnormalised: Z feeds only products (<= 4 x 4)
     f26_sub(t0, t0, x3);  // 4 beta - X3: c 5
-    f26_mul<C>(y3, alpha, t0);  // 3 x 5
-    f26_sqr<C>(t3, gamma);
+    f26_pair<C>(y3, F26Mul{alpha, t0}, t3, F26Sqr{gamma});  // 3 x 5, 1 x 1
     f26_add(t3, t3, t3);
     f26_add(t3, t3, t3);
     f26_add(t3, t3, t3);  // 8 gamma^2
@@ -133,18 +130,17 @@ CG_HD void ec_dbl(jpt& r, const jpt& p) {
     f26_norm<C>(y3);  // c 9
   } else {
     // dbl-2009-l (a = 0)
-    f26 A, B, Cc, D, E, F;
-    f26_sqr<C>(A, p.X);
-    f26_sqr<C>(B, p.Y);
-    f26_sqr<C>(Cc, B);
+    f26 A, B, Cc, D, E, F, y2;
+    f26_pair<C>(A, F26Sqr{p.X}, B, F26Sqr{p.Y});
     f26_add(t0, p.X, B);
-    f26_sqr<C>(t1, t0);  // 2 x 2
+    f26_pair<C>(Cc, F26Sqr{B}, t1, F26Sqr{t0});  // 1 x 1, 2 x 2
     f26_sub(t1, t1, A);
     f26_sub(t1, t1, Cc);
     f26_add(D, t1, t1);  // c 6
     f26_add(E, A, A);
     f26_add(E, E, A);    // c 3
-    f26_sqr<C>(F, E);    // 3 x 3
+    f26_add(y2, p.Y, p.Y);
+    f26_pair<C>(F, F26Sqr{E}, z3, F26Mul{y2, p.Z});  // 3 x 3, 2 x 1
     f26_add(t2, D, D);
     f26_sub(x3, F, t2);
     f26_norm<C>(x3);      // c 13
@@ -155,8 +151,6 @@ CG_HD void ec_dbl(jpt& r, const jpt& p) {
     f26_add(t3, t3, t3);
     f26_sub(y3, y3, t3);
     f26_norm<C>(y3);  // c 9
-    f26_add(t0, p.Y, p.Y);
-    f26_mul<C>(z3, t0, p.Z);  // 2 x 1
   }
   r.X = x3;
   r.Y = y3;
@@ -180,30 +174,27 @@ CG_HD void ec_add(jpt& r, const jpt& p, const jpt& q, uint32_t q_skip) {
     f26_mul<C>(t, q.Z, z2z2);
     f26_mul<C>(s1, p.Y, t);
   }
-  f26_mul<C>(u2, q.X, z1z1);
-  f26_mul<C>(t, p.Z, z1z1);
-  f26_mul<C>(s2, q.Y, t);
+  // independent products in pairs (f26_pair)
+  f26_pair<C>(u2, F26Mul{q.X, z1z1}, t, F26Mul{p.Z, z1z1});
   f26_sub(h, u2, u1);    // c 2
+  f26_pair<C>(s2, F26Mul{q.Y, t}, hh, F26Sqr{h});  // 1 x 1, 2 x 2
   f26_sub(rr, s2, s1);   // c 2
-  f26_sqr<C>(hh, h);     // 2 x 2
-  f26_mul<C>(hhh, h, hh);  // 2 x 1
-  f26_mul<C>(v, u1, hh);
-  f26_sqr<C>(x3, rr);    // 2 x 2
+  if (AFFINE) {
+    f26_pair<C>(x3, F26Sqr{rr}, z3, F26Mul{p.Z, h});  // 2 x 2, 3 x 2
+  } else {
+    f26 zz;
+    f26_pair<C>(x3, F26Sqr{rr}, zz, F26Mul{p.Z, q.Z});
+    f26_mul<C>(z3, zz, h);  // 1 x 2
+  }
+  f26_pair<C>(hhh, F26Mul{h, hh}, v, F26Mul{u1, hh});  // 2 x 1, 1 x 1
   f26_sub(x3, x3, hhh);
   f26_sub(x3, x3, v);
   f26_sub(x3, x3, v);
   f26_norm<C>(x3);       // c 4
   f26_sub(t, v, x3);     // c 2
-  f26_mul<C>(y3, rr, t);   // 2 x 2
-  f26_mul<C>(t, s1, hhh);
+  f26_pair<C>(y3, F26Mul{rr, t}, t, F26Mul{s1, hhh});  // 2 x 2, 1 x 1
   f26_sub(y3, y3, t);
   f26_norm<C>(y3);       // c 2
-  if (AFFINE) {
-    f26_mul<C>(z3, p.Z, h);  // 3 x 2
-  } else {
-    f26_mul<C>(t, p.Z, q.Z);
-    f26_mul<C>(z3, t, h);    // 1 x 2
-  }
   const uint32_t hz = f26_iszero<C>(h);
   jpt out;
   out.X = x3;

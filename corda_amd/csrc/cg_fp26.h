@@ -98,6 +98,15 @@ CG_HD int32_t f26_kpin(int32_t x) {
   return x;
 }
 
+// 64-bit column accumulator barrier (see fe_pin64 in cg_fe25519.h): keeps a column
+// chain in source order, the carry as the first mad's addend.
+CG_HD int64_t f26_pin64(int64_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm("" : "+v"(x));
+#endif
+  return x;
+}
+
 // Constants (p, R mod p, ...) as SGPR values: uniform, so they neither take VGPRs
 // nor get hoisted out of the hot loops into VGPRs.
 CG_HD void f26_load(f26& h, const int32_t (&c)[10]) {
@@ -110,15 +119,20 @@ struct F26;
 
 template <>
 struct F26<CurveR1> {
-  // one Montgomery step: t[k] + m p == 0 mod 2^26 with m = t[k] mod 2^26; the
-  // exact quotient (t[k] - m) / 2^26 = t[k] >> 26 carries into t[k+1]
-  CG_HDM static void step(int64_t t[19], int k) {
-    const int32_t m = (int32_t)((uint32_t)t[k] & (uint32_t)kF26Mask);
-    t[k + 1] += t[k] >> 26;
-    t[k + 3] += (int64_t)m * f26_kpin(1 << 18);
-    t[k + 7] += (int64_t)m * f26_kpin(1 << 10);
-    t[k + 8] += (int64_t)m * f26_kpin(-(1 << 16));
-    t[k + 9] += (int64_t)m * f26_kpin(1 << 22);
+  // Montgomery step k of the column-serial product (f26_chain): the reduction
+  // terms m_s p_(k-s) of the earlier steps land in column k (p_3 = 2^18, p_7 =
+  // 2^10, p_8 = -2^16, p_9 = 2^22); then m_k = t_k mod 2^26 (-p^-1 = 1), and with
+  // p_0 = -1 the exact quotient (t_k - m_k) / 2^26 = t_k >> 26 is the carry.
+  CG_HDM static int64_t red_terms(int k, const int32_t m[10], int64_t acc) {
+    if (k >= 3 && k - 3 <= 9) acc = f26_pin64(acc + (int64_t)m[k - 3] * f26_kpin(1 << 18));
+    if (k >= 7 && k - 7 <= 9) acc = f26_pin64(acc + (int64_t)m[k - 7] * f26_kpin(1 << 10));
+    if (k >= 8 && k - 8 <= 9) acc = f26_pin64(acc + (int64_t)m[k - 8] * f26_kpin(-(1 << 16)));
+    if (k >= 9 && k - 9 <= 9) acc = f26_pin64(acc + (int64_t)m[k - 9] * f26_kpin(1 << 22));
+    return acc;
+  }
+  CG_HDM static int64_t step(int64_t acc, int32_t& m) {
+    m = (int32_t)((uint32_t)acc & (uint32_t)kF26Mask);
+    return acc >> 26;
   }
   // h - top p with top = h.v[9] >> 22: -top 2^256 + top (2^224 - 2^192 - 2^96 + 1)
   CG_HDM static void fold(f26& h) {
@@ -155,11 +169,15 @@ struct F26<CurveR1> {
 template <>
 struct F26<CurveK1> {
   static constexpr uint32_t kPinv = 0x2253531u;  // 977^-1 = -p^-1 mod 2^26
-  CG_HDM static void step(int64_t t[19], int k) {
-    const int32_t m = (int32_t)(((uint32_t)t[k] * kPinv) & (uint32_t)kF26Mask);
-    t[k + 1] += (t[k] + (int64_t)m * f26_kpin(-977)) >> 26;
-    t[k + 1] += (int64_t)m * f26_kpin(-(1 << 6));
-    t[k + 9] += (int64_t)m * f26_kpin(1 << 22);
+  // p_1 = -2^6, p_9 = 2^22; m_k = t_k (-p^-1) mod 2^26, carry (t_k - 977 m_k) / 2^26
+  CG_HDM static int64_t red_terms(int k, const int32_t m[10], int64_t acc) {
+    if (k >= 1 && k - 1 <= 9) acc = f26_pin64(acc + (int64_t)m[k - 1] * f26_kpin(-(1 << 6)));
+    if (k >= 9 && k - 9 <= 9) acc = f26_pin64(acc + (int64_t)m[k - 9] * f26_kpin(1 << 22));
+    return acc;
+  }
+  CG_HDM static int64_t step(int64_t acc, int32_t& m) {
+    m = (int32_t)(((uint32_t)acc * kPinv) & (uint32_t)kF26Mask);
+    return (acc + (int64_t)m * f26_kpin(-977)) >> 26;
   }
   // h - top p = h - top 2^256 + top (2^32 + 977)
   CG_HDM static void fold(f26& h) {
@@ -224,54 +242,131 @@ CG_HD void f26_norm(f26& h) {
 }
 
 // ------------------------------------------------------------ Montgomery product
-// 64-bit column sums t[0..18] -> t R^-1 mod p as a unit value.
-template <class C>
-CG_HD void f26_redc(f26& h, int64_t t[19]) {
-  CG_UNROLL for (int k = 0; k < 10; ++k) F26<C>::step(t, k);
-  CG_UNROLL for (int k = 10; k < 18; ++k) {
-    t[k + 1] += t[k] >> 26;
-    h.v[k - 10] = (int32_t)((uint32_t)t[k] & (uint32_t)kF26Mask);
+// Column-serial: column k (0..18) is one chain of v_mad_i64_i32 starting from
+// column k-1's carry as its addend — the limb products f_i g_(k-i), then the
+// reduction terms of the Montgomery steps s < k that reach it — followed by step k
+// (k <= 9: m_k and the exact quotient) or an output limb (k >= 10).  No separate
+// 64-bit carry additions (the parallel-columns form spent 18 v_lshl_add_u64 per
+// product on them).  Two or three independent products run interleaved
+// (f26_pair / f26_triple) so consecutive mads never depend on each other.
+struct F26MulOp {
+  int32_t f[10], g[10];
+  CG_HDM F26MulOp(const f26& F, const f26& G) {
+    CG_UNROLL for (int i = 0; i < 10; ++i) {
+      f[i] = F.v[i];
+      g[i] = G.v[i];
+    }
   }
-  h.v[8] = (int32_t)((uint32_t)t[18] & (uint32_t)kF26Mask);
-  h.v[9] = (int32_t)(t[18] >> 26);
+  // n-th product of column k: i = max(0, k - 9) + n
+  CG_HDM bool has(int k, int n) const {
+    const int i = (k > 9 ? k - 9 : 0) + n;
+    return i <= 9 && i <= k;
+  }
+  CG_HDM int32_t a(int k, int n) const { return f[(k > 9 ? k - 9 : 0) + n]; }
+  CG_HDM int32_t b(int k, int n) const { return g[k - ((k > 9 ? k - 9 : 0) + n)]; }
+};
+// f^2: 45 cross products against pre-doubled limbs + 10 squares
+struct F26SqrOp {
+  int32_t f[10], f2[10];
+  CG_HDM explicit F26SqrOp(const f26& F) {
+    CG_UNROLL for (int i = 0; i < 10; ++i) {
+      f[i] = F.v[i];
+      f2[i] = f26_pin(2 * F.v[i]);
+    }
+  }
+  // n-th product of column k: i = max(0, k - 9) + n, up to i = k / 2 (j = k - i >= i)
+  CG_HDM bool has(int k, int n) const {
+    const int i = (k > 9 ? k - 9 : 0) + n;
+    return 2 * i <= k;
+  }
+  CG_HDM int32_t a(int k, int n) const {
+    const int i = (k > 9 ? k - 9 : 0) + n;
+    return 2 * i == k ? f[i] : f2[i];
+  }
+  CG_HDM int32_t b(int k, int n) const { return f[k - ((k > 9 ? k - 9 : 0) + n)]; }
+};
+
+template <class C>
+struct F26Chain {
+  int32_t m[10];
+  int64_t c;
+  CG_HDM F26Chain() : c(0) {}
+  template <typename Op>
+  CG_HDM void column(f26& h, const Op& op, int k) {
+    int64_t acc = c;
+    CG_UNROLL for (int n = 0; n < 10; ++n) {
+      if (op.has(k, n)) acc = f26_pin64(acc + (int64_t)op.a(k, n) * op.b(k, n));
+    }
+    acc = F26<C>::red_terms(k, m, acc);
+    if (k <= 9) {
+      c = F26<C>::step(acc, m[k]);
+    } else if (k < 18) {
+      h.v[k - 10] = (int32_t)((uint32_t)acc & (uint32_t)kF26Mask);
+      c = acc >> 26;
+    } else {
+      h.v[8] = (int32_t)((uint32_t)acc & (uint32_t)kF26Mask);
+      h.v[9] = (int32_t)(acc >> 26);
+    }
+  }
+};
+
+template <class C, typename Op>
+CG_HD void f26_chain(f26& h, const Op& op) {
+  F26Chain<C> s;
+  CG_UNROLL for (int k = 0; k < 19; ++k) s.column(h, op, k);
   F26<C>::fold(h);
+}
+template <class C, typename Op0, typename Op1>
+CG_HD void f26_chain_pair(f26& h0, const Op0& op0, f26& h1, const Op1& op1) {
+  F26Chain<C> s0, s1;
+  f26 r0, r1;
+  CG_UNROLL for (int k = 0; k < 19; ++k) {
+    s0.column(r0, op0, k);
+    s1.column(r1, op1, k);
+  }
+  F26<C>::fold(r0);
+  F26<C>::fold(r1);
+  h0 = r0;
+  h1 = r1;
 }
 
 // h = f g R^-1 mod p
 template <class C>
 CG_HD void f26_mul(f26& h, const f26& f, const f26& g) {
   CG_BOUNDS26_MUL(f, g);
-  int64_t t[19];
-  CG_UNROLL for (int k = 0; k < 19; ++k) t[k] = 0;
-  CG_UNROLL for (int i = 0; i < 10; ++i) {
-    CG_UNROLL for (int j = 0; j < 10; ++j) t[i + j] += (int64_t)f.v[i] * g.v[j];
-  }
-  f26_redc<C>(h, t);
+  f26_chain<C>(h, F26MulOp(f, g));
 }
 
-// h = f^2 R^-1 mod p: 45 cross products against pre-doubled limbs + 10 squares
+// h = f^2 R^-1 mod p
 template <class C>
 CG_HD void f26_sqr(f26& h, const f26& f) {
   CG_BOUNDS26_MUL(f, f);
-  int32_t f2[10];
-  CG_UNROLL for (int i = 0; i < 10; ++i) f2[i] = f26_pin(2 * f.v[i]);
-  int64_t t[19];
-  CG_UNROLL for (int k = 0; k < 19; ++k) t[k] = 0;
-  CG_UNROLL for (int i = 0; i < 10; ++i) {
-    t[2 * i] += (int64_t)f.v[i] * f.v[i];
-    CG_UNROLL for (int j = i + 1; j < 10; ++j) t[i + j] += (int64_t)f2[i] * f.v[j];
-  }
-  f26_redc<C>(h, t);
+  f26_chain<C>(h, F26SqrOp(f));
 }
 
-// Two independent products interleaved (the scheduler overlaps their reductions).
+// Two independent products interleaved (outputs may alias inputs).
+struct F26Mul {
+  const f26& f;
+  const f26& g;
+};
+struct F26Sqr {
+  const f26& f;
+};
+CG_HD F26MulOp f26_op(const F26Mul& o) {
+  CG_BOUNDS26_MUL(o.f, o.g);
+  return F26MulOp(o.f, o.g);
+}
+CG_HD F26SqrOp f26_op(const F26Sqr& o) {
+  CG_BOUNDS26_MUL(o.f, o.f);
+  return F26SqrOp(o.f);
+}
+template <class C, typename A, typename B>
+CG_HD void f26_pair(f26& h0, const A& a, f26& h1, const B& b) {
+  f26_chain_pair<C>(h0, f26_op(a), h1, f26_op(b));
+}
 template <class C>
 CG_HD void f26_mul2(f26& h0, const f26& f0, const f26& g0, f26& h1, const f26& f1, const f26& g1) {
-  f26 a, b;
-  f26_mul<C>(a, f0, g0);
-  f26_mul<C>(b, f1, g1);
-  h0 = a;
-  h1 = b;
+  f26_pair<C>(h0, F26Mul{f0, g0}, h1, F26Mul{f1, g1});
 }
 
 // ------------------------------------------------------------ predicates, conversion
