@@ -354,7 +354,10 @@ __global__ __launch_bounds__(256) void cg_ecdsa_prep_b(const uint32_t* __restric
 // Two waves per SIMD (<= 256 VGPRs); the GLV loop keeps one add site per formula
 // (rolled slot loops) so it fits without scratch spills.
 template <class C>
-constexpr int ecdsa_msm_waves_min() { return 2; }
+#ifndef CG_ECDSA_MSM_WAVES
+#define CG_ECDSA_MSM_WAVES 2
+#endif
+constexpr int ecdsa_msm_waves_min() { return CG_ECDSA_MSM_WAVES; }
 template <class C>
 constexpr int ecdsa_msm_waves_max() { return 8; }
 
