@@ -27,6 +27,12 @@
 
 namespace cg {
 
+// Instrumentation hook (tools/ubench/hs_stats.hip counts rounds / emulated
+// quotients / exact steps per lane); empty in the library.
+#ifndef CG_HS_STAT
+#define CG_HS_STAT(kind) ((void)0)
+#endif
+
 #define CG_8L_WORDS {0xe7ae9f68u, 0xc09318d2u, 0x17bce6b2u, 0xa6f7cef5u, 0u, 0u, 0u, 0x80000000u, 0u}
 
 // ---------------------------------------------------------------- 9-word integers
@@ -112,6 +118,7 @@ CG_HD uint32_t mp9_abs(uint32_t out[9], const uint32_t t[9]) {
 // quotient estimated in fp64 and corrected exactly.  Returns 0 when q >= 2^31
 // (the caller falls back).
 CG_HD uint32_t hs_exact_step(uint32_t a[9], uint32_t b[9], uint32_t ta[9], uint32_t tb[9]) {
+  CG_HS_STAT(2);
   const double qd = mp9_to_double(a) / mp9_to_double(b);
   if (!(qd < 2147483648.0)) return 0;
   const uint32_t q = (uint32_t)qd;
@@ -194,32 +201,35 @@ template <int TB = 128>
 CG_HD uint32_t hs_lehmer(uint32_t a[9], uint32_t b[9], uint32_t ta[9], uint32_t tb[9]) {
   const uint32_t s = mp9_bitlen(a) - 52;  // caller guarantees bitlen(a) > TB + 4
   double uh = (double)mp9_shr64(a, s), vh = (double)mp9_shr64(b, s);
-  // An emulated remainder T stands for a true one in (T - |C| - |D|, T + |C| + |D|)
-  // * 2^s with |C|, |D| < 2^31: T >= 2^(TB+1-s) + 2^33 keeps every emulated
-  // remainder above 2^TB (s ranges over TB-47..204).
-  const double thr = (double)((s < (uint32_t)TB + 1 ? (int64_t)1 << (TB + 1 - s) : (int64_t)0) + ((int64_t)1 << 33));
+  // An emulated remainder T with cofactors (C, D) stands for the true one
+  // R = C a + D b = T 2^s + C a_low + D b_low, so R > (T - |C| - |D|) 2^s:
+  // T >= |C| + |D| + 2^(TB+1-s) (or + 1 when s > TB) keeps every committed remainder
+  // above 2^TB (s ranges over TB-47..204).  A fixed margin of 2^33 (for the largest
+  // cofactors) instead capped a round at 19 of the 52 digit bits: 8.9 rounds per
+  // reduction, measured (tools/ubench/hs_stats.hip).
+  const double thr = (double)(s < (uint32_t)TB + 1 ? (int64_t)1 << (TB + 1 - s) : (int64_t)1);
   const double lim = 2147483647.0;
   double A = 1.0, B = 0.0, C = 0.0, D = 1.0;
+  // branch-free body (one exit test per iteration instead of six nested exec-mask
+  // branches): every check folds into `ok`; a failed step leaves the state as is
+  CG_HS_STAT(0);
   CG_NOUNROLL for (int it = 0; it < 48; ++it) {
+    CG_HS_STAT(1);
     const double y1 = vh + C, y2 = vh + D, x1 = uh + A, x2 = uh + B;
-    if (y1 <= 0.0 || y2 <= 0.0 || x1 < 0.0 || x2 < 0.0) break;
     double r = hs_rcp(y1);
     r = fma(fma(-y1, r, 1.0), r, r);
     double q = floor(x1 * r);
-    double r1 = fma(-q, y1, x1);
-    if (r1 < 0.0) {
-      q -= 1.0;
-      r1 += y1;
-    } else if (r1 >= y1) {
-      q += 1.0;
-      r1 -= y1;
-    }
-    if (r1 < 0.0 || r1 >= y1 || q < 1.0 || q > lim) break;
+    // the estimate is within one of floor(x1 / y1): r1 in [-y1, 2 y1) and one correction
+    const double r1 = fma(-q, y1, x1);
+    q = r1 < 0.0 ? q - 1.0 : (r1 >= y1 ? q + 1.0 : q);
     // Knuth's test: the other bound gives the same quotient
     const double r2 = fma(-q, y2, x2);
-    if (r2 < 0.0 || r2 >= y2) break;
     const double T = fma(-q, vh, uh), nC = fma(-q, C, A), nD = fma(-q, D, B);
-    if (T < thr || fabs(nC) > lim || fabs(nD) > lim) break;
+    const uint32_t ok = (uint32_t)(y1 > 0.0) & (uint32_t)(y2 > 0.0) & (uint32_t)(x1 >= 0.0) & (uint32_t)(x2 >= 0.0) &
+                        (uint32_t)(r1 >= -y1) & (uint32_t)(r1 < y1 + y1) & (uint32_t)(q >= 1.0) & (uint32_t)(q <= lim) &
+                        (uint32_t)(r2 >= 0.0) & (uint32_t)(r2 < y2) & (uint32_t)(T >= fabs(nC) + fabs(nD) + thr) &
+                        (uint32_t)(fabs(nC) <= lim) & (uint32_t)(fabs(nD) <= lim);
+    if (!ok) break;
     A = C;
     C = nC;
     B = D;
