@@ -45,10 +45,11 @@ CG_HD double mp9_to_double(const uint32_t a[9]) {
 }
 
 // r = a - q b (mod 2^288); returns 1 when the true result is negative (a, b unsigned).
-CG_HD uint32_t mp9_submul(uint32_t r[9], const uint32_t a[9], const uint32_t b[9], uint32_t q) {
+template <int N = 9>
+CG_HD uint32_t mp9_submul(uint32_t r[N], const uint32_t a[N], const uint32_t b[N], uint32_t q) {
   uint64_t mc = 0;     // carry of q*b
   uint32_t bw = 0;     // borrow of a - q*b
-  CG_UNROLL for (int w = 0; w < 9; ++w) {
+  CG_UNROLL for (int w = 0; w < N; ++w) {
     const uint64_t p = (uint64_t)q * b[w] + mc;
     mc = p >> 32;
     const uint64_t d = (uint64_t)a[w] - (uint32_t)p - bw;
@@ -59,9 +60,10 @@ CG_HD uint32_t mp9_submul(uint32_t r[9], const uint32_t a[9], const uint32_t b[9
 }
 
 // r += b; returns the carry out of bit 288.
-CG_HD uint32_t mp9_add(uint32_t r[9], const uint32_t b[9]) {
+template <int N = 9>
+CG_HD uint32_t mp9_add(uint32_t r[N], const uint32_t b[N]) {
   uint64_t c = 0;
-  CG_UNROLL for (int w = 0; w < 9; ++w) {
+  CG_UNROLL for (int w = 0; w < N; ++w) {
     const uint64_t s = (uint64_t)r[w] + b[w] + c;
     r[w] = (uint32_t)s;
     c = s >> 32;
@@ -69,9 +71,10 @@ CG_HD uint32_t mp9_add(uint32_t r[9], const uint32_t b[9]) {
   return (uint32_t)c;
 }
 
-CG_HD void mp9_sub(uint32_t r[9], const uint32_t b[9]) {
+template <int N = 9>
+CG_HD void mp9_sub(uint32_t r[N], const uint32_t b[N]) {
   uint32_t bw = 0;
-  CG_UNROLL for (int w = 0; w < 9; ++w) {
+  CG_UNROLL for (int w = 0; w < N; ++w) {
     const uint64_t d = (uint64_t)r[w] - b[w] - bw;
     r[w] = (uint32_t)d;
     bw = (uint32_t)(d >> 63);
@@ -95,17 +98,19 @@ CG_HD uint32_t clz32_(uint32_t x) {
 #endif
 }
 
-CG_HD uint32_t mp9_bitlen(const uint32_t a[9]) {
+template <int N = 9>
+CG_HD uint32_t mp9_bitlen(const uint32_t a[N]) {
   uint32_t bl = 0;
-  CG_UNROLL for (int w = 0; w < 9; ++w) bl = a[w] ? 32u * (w + 1) - clz32_(a[w]) : bl;
+  CG_UNROLL for (int w = 0; w < N; ++w) bl = a[w] ? 32u * (w + 1) - clz32_(a[w]) : bl;
   return bl;
 }
 
 // |t| of a two's-complement value; returns the sign.
-CG_HD uint32_t mp9_abs(uint32_t out[9], const uint32_t t[9]) {
-  const uint32_t neg = t[8] >> 31;
+template <int N = 9>
+CG_HD uint32_t mp9_abs(uint32_t out[N], const uint32_t t[N]) {
+  const uint32_t neg = t[N - 1] >> 31;
   uint64_t c = neg;
-  CG_UNROLL for (int w = 0; w < 9; ++w) {
+  CG_UNROLL for (int w = 0; w < N; ++w) {
     const uint64_t s = (uint64_t)(t[w] ^ (0u - neg)) + c;
     out[w] = (uint32_t)s;
     c = s >> 32;
@@ -117,27 +122,30 @@ CG_HD uint32_t mp9_abs(uint32_t out[9], const uint32_t t[9]) {
 // One exact Euclid step (a, b, ta, tb) -> (b, a mod b, tb, ta - q tb) with the
 // quotient estimated in fp64 and corrected exactly.  Returns 0 when q >= 2^31
 // (the caller falls back).
-CG_HD uint32_t hs_exact_step(uint32_t a[9], uint32_t b[9], uint32_t ta[9], uint32_t tb[9]) {
+template <int CW>
+CG_HD uint32_t hs_exact_step(uint32_t a[9], uint32_t b[9], uint32_t ta[CW], uint32_t tb[CW]) {
   CG_HS_STAT(2);
   const double qd = mp9_to_double(a) / mp9_to_double(b);
   if (!(qd < 2147483648.0)) return 0;
   const uint32_t q = (uint32_t)qd;
-  uint32_t r[9], tn[9];
+  uint32_t r[9], tn[CW];
   uint32_t neg = mp9_submul(r, a, b, q);
-  mp9_submul(tn, ta, tb, q);
+  mp9_submul<CW>(tn, ta, tb, q);
   // the fp64 estimate is within +-1 of floor(a/b) here; correct it exactly
   CG_NOUNROLL for (int k = 0; k < 2 && neg; ++k) {
     neg = mp9_add(r, b) ? 0u : 1u;
-    mp9_add(tn, tb);
+    mp9_add<CW>(tn, tb);
   }
   CG_NOUNROLL for (int k = 0; k < 2 && !neg && mp9_ge(r, b); ++k) {
     mp9_sub(r, b);
-    mp9_sub(tn, tb);
+    mp9_sub<CW>(tn, tb);
   }
   if (neg || mp9_ge(r, b)) return 0;
   CG_UNROLL for (int w = 0; w < 9; ++w) {
     a[w] = b[w];
     b[w] = r[w];
+  }
+  CG_UNROLL for (int w = 0; w < CW; ++w) {
     ta[w] = tb[w];
     tb[w] = tn[w];
   }
@@ -145,27 +153,30 @@ CG_HD uint32_t hs_exact_step(uint32_t a[9], uint32_t b[9], uint32_t ta[9], uint3
 }
 
 // floor(x / 2^s) & (2^64 - 1) for a 9-word x; s is per lane (select chain, no
-// dynamically indexed registers).
+// dynamically indexed registers) with s >> 5 in [WLO, 6] (the caller's range:
+// bitlen in (TB + 4, 256], s = bitlen - 52).
+template <int WLO = 0>
 CG_HD uint64_t mp9_shr64(const uint32_t x[9], uint32_t s) {
   const uint32_t ws = s >> 5, bs = s & 31;
-  uint32_t w0 = 0, w1 = 0, w2 = 0;
-  CG_UNROLL for (int w = 0; w < 9; ++w) {
+  uint32_t w0 = x[WLO], w1 = x[WLO + 1], w2 = x[WLO + 2];
+  CG_UNROLL for (int w = WLO + 1; w <= 6; ++w) {
     w0 = (uint32_t)w == ws ? x[w] : w0;
-    w1 = (uint32_t)w == ws + 1 ? x[w] : w1;
-    w2 = (uint32_t)w == ws + 2 ? x[w] : w2;
+    w1 = (uint32_t)w == ws ? x[w + 1] : w1;
+    w2 = (uint32_t)w == ws ? x[w + 2] : w2;
   }
   const uint64_t lo = bs ? ((uint64_t)w0 >> bs | (uint64_t)w1 << (32 - bs)) : w0;
   const uint64_t hi = bs ? ((uint64_t)w1 >> bs | (uint64_t)w2 << (32 - bs)) : w1;
   return (lo & 0xffffffffull) | hi << 32;
 }
 
-// out = (A x + B y) mod 2^288 for signed 32-bit A, B (two's complement words).
-CG_HD void mp9_lincomb(uint32_t out[9], const uint32_t x[9], const uint32_t y[9], int64_t A, int64_t B) {
+// out = (A x + B y) mod 2^(32 N) for signed 32-bit A, B (two's complement words).
+template <int N = 9>
+CG_HD void mp9_lincomb(uint32_t out[N], const uint32_t x[N], const uint32_t y[N], int64_t A, int64_t B) {
   const uint32_t ma = (uint32_t)(A < 0 ? -A : A), mb = (uint32_t)(B < 0 ? -B : B);
   const uint32_t na = A < 0 ? 0xffffffffu : 0u, nb = B < 0 ? 0xffffffffu : 0u;
   // (+-ma x) = (ma x) ^ na + (na & 1), likewise for y; both folded into one carry chain
   uint64_t cx = 0, cy = 0, c = (uint64_t)(na & 1u) + (nb & 1u);
-  CG_UNROLL for (int w = 0; w < 9; ++w) {
+  CG_UNROLL for (int w = 0; w < N; ++w) {
     const uint64_t px = (uint64_t)ma * x[w] + cx, py = (uint64_t)mb * y[w] + cy;
     cx = px >> 32;
     cy = py >> 32;
@@ -197,10 +208,11 @@ CG_HD double hs_rcp(double y) {
 // are several ops each on the VALU).  The quotient estimate x1 * rcp(y1) (one
 // Newton step) is within one of floor(x1 / y1) and corrected on the remainder.
 // Returns 0 when no quotient was emulated (the caller takes an exact step).
-template <int TB = 128>
-CG_HD uint32_t hs_lehmer(uint32_t a[9], uint32_t b[9], uint32_t ta[9], uint32_t tb[9]) {
+template <int TB = 128, int CW = 9>
+CG_HD uint32_t hs_lehmer(uint32_t a[9], uint32_t b[9], uint32_t ta[CW], uint32_t tb[CW]) {
   const uint32_t s = mp9_bitlen(a) - 52;  // caller guarantees bitlen(a) > TB + 4
-  double uh = (double)mp9_shr64(a, s), vh = (double)mp9_shr64(b, s);
+  constexpr int kWLo = (TB + 5 - 52) / 32;
+  double uh = (double)mp9_shr64<kWLo>(a, s), vh = (double)mp9_shr64<kWLo>(b, s);
   // An emulated remainder T with cofactors (C, D) stands for the true one
   // R = C a + D b = T 2^s + C a_low + D b_low, so R > (T - |C| - |D|) 2^s:
   // T >= |C| + |D| + 2^(TB+1-s) (or + 1 when s > TB) keeps every committed remainder
@@ -238,15 +250,17 @@ CG_HD uint32_t hs_lehmer(uint32_t a[9], uint32_t b[9], uint32_t ta[9], uint32_t 
     vh = T;
   }
   if (B == 0.0) return 0;
-  uint32_t na[9], nb[9], nta[9], ntb[9];
+  uint32_t na[9], nb[9], nta[CW], ntb[CW];
   const int64_t iA = (int64_t)A, iB = (int64_t)B, iC = (int64_t)C, iD = (int64_t)D;
   mp9_lincomb(na, a, b, iA, iB);
   mp9_lincomb(nb, a, b, iC, iD);
-  mp9_lincomb(nta, ta, tb, iA, iB);
-  mp9_lincomb(ntb, ta, tb, iC, iD);
+  mp9_lincomb<CW>(nta, ta, tb, iA, iB);
+  mp9_lincomb<CW>(ntb, ta, tb, iC, iD);
   CG_UNROLL for (int w = 0; w < 9; ++w) {
     a[w] = na[w];
     b[w] = nb[w];
+  }
+  CG_UNROLL for (int w = 0; w < CW; ++w) {
     ta[w] = nta[w];
     tb[w] = ntb[w];
   }
@@ -268,9 +282,11 @@ CG_HD uint32_t mp9_ge_pow2(const uint32_t b[9]) {
 // (252 / 66).  Returns 0 when the caller must fall back to (h, 1).
 template <int TB = 128, int C1BITS = 252>
 CG_HD uint32_t ed25519_half_scalars(const uint32_t h[8], uint32_t c0[8], uint32_t c1[8], uint32_t& c1neg) {
-  uint32_t a[9] = CG_8L_WORDS, b[9], ta[9], tb[9];
-  CG_UNROLL for (int w = 0; w < 9; ++w) {
-    b[w] = w < 8 ? h[w] : 0u;
+  // cofactors: |t| <= 8L / (a remainder >= 2^TB) < 2^(257 - TB) in CW two's-complement words
+  constexpr int CW = (257 - TB) / 32 + 1;
+  uint32_t a[9] = CG_8L_WORDS, b[9], ta[CW], tb[CW];
+  CG_UNROLL for (int w = 0; w < 9; ++w) b[w] = w < 8 ? h[w] : 0u;
+  CG_UNROLL for (int w = 0; w < CW; ++w) {
     ta[w] = 0;
     tb[w] = w == 0;
   }
@@ -280,8 +296,8 @@ CG_HD uint32_t ed25519_half_scalars(const uint32_t h[8], uint32_t c0[8], uint32_
       ok = 0;
       break;
     }
-    if (mp9_bitlen(a) > TB + 4 && hs_lehmer<TB>(a, b, ta, tb)) continue;
-    if (!hs_exact_step(a, b, ta, tb)) {
+    if (mp9_bitlen(a) > TB + 4 && hs_lehmer<TB, CW>(a, b, ta, tb)) continue;
+    if (!hs_exact_step<CW>(a, b, ta, tb)) {
       ok = 0;
       break;
     }
@@ -290,35 +306,42 @@ CG_HD uint32_t ed25519_half_scalars(const uint32_t h[8], uint32_t c0[8], uint32_
   // since consecutive cofactors are coprime) — keep the shorter one (balanced
   // split: the longer of the two scalars; key-reuse split: the shorter c0 among the
   // candidates whose |c1| fits C1BITS)
+  // (the extra step may leave the cofactor bound: q tb can reach 2^160, so the
+  // candidate stage runs on 9-word cofactors)
+  uint32_t ta9[9], tb9[9];
+  CG_UNROLL for (int w = 0; w < 9; ++w) {
+    ta9[w] = w < CW ? ta[w] : 0u - (ta[CW - 1] >> 31);
+    tb9[w] = w < CW ? tb[w] : 0u - (tb[CW - 1] >> 31);
+  }
   uint32_t x0[9], x1[9], s1 = 0;
   CG_UNROLL for (int w = 0; w < 9; ++w) {
     x0[w] = b[w];
-    x1[w] = tb[w];
+    x1[w] = tb9[w];
   }
   auto cost = [](uint32_t l0, uint32_t l1) CG_LINLINE -> uint32_t {
     return TB == 128 ? (l0 > l1 ? l0 : l1) : (l1 > (uint32_t)C1BITS ? 1000u : l0);
   };
-  if (ok && !(tb[0] & 1)) {
+  if (ok && !(tb9[0] & 1)) {
     uint32_t ua[9], un[9], r[9], tn[9];
-    mp9_abs(ua, ta);
+    mp9_abs(ua, ta9);
     uint32_t best = cost(mp9_bitlen(a), mp9_bitlen(ua));
     CG_UNROLL for (int w = 0; w < 9; ++w) {
       x0[w] = a[w];
-      x1[w] = ta[w];
+      x1[w] = ta9[w];
     }
     const uint32_t bnz = b[0] | b[1] | b[2] | b[3];
     const double qd = bnz ? mp9_to_double(a) / mp9_to_double(b) : 0.0;
     if (bnz && qd < 2147483648.0) {
       const uint32_t q = (uint32_t)qd;
       uint32_t neg = mp9_submul(r, a, b, q);
-      mp9_submul(tn, ta, tb, q);
+      mp9_submul(tn, ta9, tb9, q);
       CG_NOUNROLL for (int k = 0; k < 2 && neg; ++k) {
         neg = mp9_add(r, b) ? 0u : 1u;
-        mp9_add(tn, tb);
+        mp9_add(tn, tb9);
       }
       CG_NOUNROLL for (int k = 0; k < 2 && !neg && mp9_ge(r, b); ++k) {
         mp9_sub(r, b);
-        mp9_sub(tn, tb);
+        mp9_sub(tn, tb9);
       }
       if (!neg && !mp9_ge(r, b)) {
         mp9_abs(un, tn);
