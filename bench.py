@@ -447,14 +447,18 @@ def run_ed25519(args, dist):
 
     value = n * world * args.steps / elapsed
     model = OP_MODEL["ed25519_1kb" if msg_bytes > 32 else "ed25519_32b"]
-    pmc = pmc_view("pmc_ed25519.json")
+    # the key-reuse path runs other kernels under the same timing names (points_r, msm_r),
+    # profiled in their own PMC pass (profiles/pmc_ed25519_reuse.json)
+    reuse = args.key_reuse > 0
+    pmc = pmc_view("pmc_ed25519_reuse.json" if reuse else "pmc_ed25519.json")
+    kname = {k: f"cg_{k}_r" if reuse and k != "ed25519_hash" else f"cg_{k}" for k in ED_KERNELS}
     msm = ks.get("ed25519_msm", {})
-    roof = valu_roofline(pmc, "cg_ed25519_msm", msm.get("units_per_launch", 0), msm.get("avg_launch_ms", 0) / 1e3,
-                         model["msm"])
-    prep = {k: valu_roofline(pmc, f"cg_{k}", ks.get(k, {}).get("units_per_launch", 0),
+    roof = valu_roofline(pmc, kname["ed25519_msm"], msm.get("units_per_launch", 0),
+                         msm.get("avg_launch_ms", 0) / 1e3, model["msm"])
+    prep = {k: valu_roofline(pmc, kname[k], ks.get(k, {}).get("units_per_launch", 0),
                              ks.get(k, {}).get("avg_launch_ms", 0) / 1e3) for k in ED_PREP_KERNELS}
     # whole path: VALU lane-instructions of the three kernels per verify x verifies/s
-    path_instr = sum((pmc.get("kernels", {}).get(f"cg_{k}", {}).get("valu_instr_per_unit") or 0) for k in ED_KERNELS)
+    path_instr = sum((pmc.get("kernels", {}).get(kname[k], {}).get("valu_instr_per_unit") or 0) for k in ED_KERNELS)
     path = {"valu_instr_per_verify": path_instr or None,
             "achieved": round(path_instr * value / world / 1e12, 3) if path_instr else None,
             "frac": round(path_instr * value / world / 1e12 / PEAK, 4) if path_instr else None,
@@ -873,7 +877,9 @@ def run_backlog(args, dist):
     value = total * args.steps / elapsed
     model = OP_MODEL["ed25519_32b" if msg_bytes <= 32 else "ed25519_1kb"]
     msm = ks.get("ed25519_msm", {})
-    roof = valu_roofline(pmc_view("pmc_ed25519.json"), "cg_ed25519_msm", msm.get("units_per_launch", 0),
+    reuse = args.key_reuse > 0
+    roof = valu_roofline(pmc_view("pmc_ed25519_reuse.json" if reuse else "pmc_ed25519.json"),
+                         "cg_ed25519_msm_r" if reuse else "cg_ed25519_msm", msm.get("units_per_launch", 0),
                          msm.get("avg_launch_ms", 0) / 1e3, model["msm"])
     roof["pmc_note"] = "instruction counts from the config-2 (1 KB message) PMC pass; the msm kernel does not " \
                        "read messages, so its count per verify is the same for 32 B ids"
