@@ -31,7 +31,7 @@ COMPOSITE_LEAF, COMPOSITE_NODE, COMPOSITE_INVALID = 0, 1, 0x80
 # per-tx codes of cg_tx_verify_batch / cg_tx_verify_signatures_except (>= 0: first bad signature)
 TX_OK, TX_NO_SIGNATURES, TX_NO_COMPONENTS, TX_SIGNATURES_MISSING = -1, -2, -3, -4
 # cg_set_debug options (test hooks)
-DEBUG_FORCE_FULL_LENGTH, DEBUG_FAIL_ALLOC, DEBUG_THROW = 1, 2, 3
+DEBUG_FORCE_FULL_LENGTH, DEBUG_FAIL_ALLOC, DEBUG_THROW, DEBUG_FORCE_GLV_FALLBACK = 1, 2, 3, 4
 ABI_VERSION = 2
 
 # exported symbols and their prototypes: (restype, argtypes)

@@ -491,7 +491,10 @@ CG_HD uint32_t mp_bitlen256(const uint32_t a[8]) {
 // u2 -> (|k1|, |k2|, signs) with u2 == k1 + k2 lambda (mod n); returns the number of
 // signed radix-16 digits the joint loop needs (>= 33: the 2^128 G table's top digit
 // sits at bit 128).
-CG_HD uint32_t glv_split(const uint32_t u2[8], uint32_t k1[8], uint32_t k2[8], uint32_t& neg1, uint32_t& neg2) {
+// force_fallback (test hook, cg_set_debug CG_DEBUG_FORCE_GLV_FALLBACK) takes the
+// (|u2|, 0) full-length pair whatever the split.
+CG_HD uint32_t glv_split(const uint32_t u2[8], uint32_t k1[8], uint32_t k2[8], uint32_t& neg1, uint32_t& neg2,
+                         bool force_fallback = false) {
   uint32_t nn[8], g[8], c1[8], c2[8], t1[8], t2[8], r1[8], r2[8], lam[8];
   CurveK1::n(nn);
   GlvK1::g1(g);
@@ -513,7 +516,7 @@ CG_HD uint32_t glv_split(const uint32_t u2[8], uint32_t k1[8], uint32_t k2[8], u
   uint32_t bl = mp_bitlen256(k1);
   const uint32_t b2 = mp_bitlen256(k2);
   bl = b2 > bl ? b2 : bl;
-  if (bl > 129) {  // fallback: u2 Q on its own, full length
+  if (bl > 129 || force_fallback) {  // fallback: u2 Q on its own, full length
     neg1 = glv_abs(k1, u2, nn);
     neg2 = 0;
     CG_UNROLL for (int i = 0; i < 8; ++i) k2[i] = 0;
@@ -525,9 +528,9 @@ CG_HD uint32_t glv_split(const uint32_t u2[8], uint32_t k1[8], uint32_t k2[8], u
 
 // secp256k1 digits from (u1, u2) with the GLV split; returns aux (below).
 CG_HD uint32_t ecdsa_k1_digits(const uint32_t u1[8], const uint32_t u2[8], uint32_t dg[9], uint32_t dk1[9],
-                               uint32_t dk2[9]) {
+                               uint32_t dk2[9], bool force_fallback = false) {
   uint32_t k1[8], k2[8], neg1, neg2;
-  const uint32_t nd = glv_split(u2, k1, k2, neg1, neg2);
+  const uint32_t nd = glv_split(u2, k1, k2, neg1, neg2, force_fallback);
   recode_g(dg, u1);
   recode16_65(dk1, k1);
   recode16_65(dk2, k2);

@@ -22,6 +22,9 @@ struct EcdsaBatch {
 };
 
 hipError_t ecdsa_consts_create(EcdsaConsts** out, hipStream_t s);
+// test hook: secp256k1 elements whose index in the curve's subset is a multiple of m take
+// the GLV split's full-length fallback (0: off)
+void ecdsa_set_debug_glv(EcdsaConsts* c, uint32_t m);
 void ecdsa_consts_free(EcdsaConsts* c);
 // Stages one curve's subset into the SoA buffers of b (allocated by the caller:
 // index[n] already uploaded, q[16n], rs[16n], der/sig_len/msg_len[n], msg_off[n]).

@@ -1149,6 +1149,10 @@ cg_status cg_set_debug(cg_ctx* ctx, int option, int64_t value) {
     case CG_DEBUG_THROW:
       ctx->debug_throw = value != 0;
       return CG_OK;
+    case CG_DEBUG_FORCE_GLV_FALLBACK:
+      if (value < 0 || value > 0xffffffffll) return fail(ctx, CG_E_INVALID_ARGUMENT, "bad modulus");
+      cg::ecdsa_set_debug_glv(ctx->ec, (uint32_t)value);
+      return CG_OK;
     default:
       return fail(ctx, CG_E_INVALID_ARGUMENT, "unknown debug option");
   }

@@ -45,7 +45,10 @@ struct EcScratch {
 struct EcdsaConsts {
   uint32_t* gtab[2] = {nullptr, nullptr};  // affine k*G [kGTabEntries][kGStride]; K1 also k*2^128 G after it
   EcScratch sc[2];                         // secp256k1, secp256r1
+  uint32_t glv_full_mod = 0;               // test hook: K1 elements (index % m == 0) take the GLV fallback
 };
+
+void ecdsa_set_debug_glv(EcdsaConsts* c, uint32_t m) { c->glv_full_mod = m; }
 
 }  // namespace cg
 
@@ -306,7 +309,8 @@ __global__ __launch_bounds__(256) void cg_ecdsa_prep_b(const uint32_t* __restric
                                                        const uint32_t* __restrict__ ework,
                                                        const uint32_t* __restrict__ leaf_n,
                                                        const uint32_t* __restrict__ leaf_p,
-                                                       uint32_t* __restrict__ digits, uint32_t* __restrict__ qtab) {
+                                                       uint32_t* __restrict__ digits, uint32_t* __restrict__ qtab,
+                                                       uint32_t glv_full_mod, uint32_t index_base) {
   CG_WAVE_PRIO(2);
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n || status[i] != 0xff) return;
@@ -319,7 +323,7 @@ __global__ __launch_bounds__(256) void cg_ecdsa_prep_b(const uint32_t* __restric
   mn_mul<C>(u1, e, w);
   mn_mul<C>(u2, r, w);
   if constexpr (C::kScheme == 2) {
-    aux = ecdsa_k1_digits(u1, u2, d1, d2, d3);
+    aux = ecdsa_k1_digits(u1, u2, d1, d2, d3, glv_full_mod != 0 && (index_base + i) % glv_full_mod == 0);
   } else {
     recode_g(d1, u1);
     recode16_65(d2, u2);
@@ -535,7 +539,7 @@ hipError_t launch_prep(const EcdsaBatch& b, EcdsaConsts* cc, uint32_t base, uint
   launch_inv_down<InvN<C>>(c->inv, vn, tn, mn, ln, s);
   launch_inv_down<InvP<C>>(c->invp, vp, tp, mp, lp, s);
   hipLaunchKernelGGL(cg_ecdsa_prep_b<C>, grid_for(cnt), dim3(256), 0, s, b.rs + base, cnt, b.n, c->scap, c->status,
-                     c->ework, c->inv + vn[0], c->invp + vp[0], c->digits, c->qtab);
+                     c->ework, c->inv + vn[0], c->invp + vp[0], c->digits, c->qtab, cc->glv_full_mod, base);
   return hipGetLastError();
 }
 

@@ -298,8 +298,12 @@ cg_status cg_reset_stats(cg_ctx* ctx);
  *       out of memory (CG_E_OUT_OF_MEMORY must come back, nothing may crash).
  *   CG_DEBUG_THROW  value 1: the next batch staging throws std::bad_alloc inside the
  *       library (it must come back as CG_E_OUT_OF_MEMORY, not unwind).
+ *   CG_DEBUG_FORCE_GLV_FALLBACK  value m > 0: secp256k1 elements whose index in the
+ *       batch's secp256k1 subset is a multiple of m take the GLV split's full-length
+ *       fallback (|u2|, 0) (taken for real when a split half exceeds 129 bits, never
+ *       observed); 0 turns it off.  Verdicts must not change.
  */
-enum { CG_DEBUG_FORCE_FULL_LENGTH = 1, CG_DEBUG_FAIL_ALLOC = 2, CG_DEBUG_THROW = 3 };
+enum { CG_DEBUG_FORCE_FULL_LENGTH = 1, CG_DEBUG_FAIL_ALLOC = 2, CG_DEBUG_THROW = 3, CG_DEBUG_FORCE_GLV_FALLBACK = 4 };
 cg_status cg_set_debug(cg_ctx* ctx, int option, int64_t value);
 
 #ifdef __cplusplus

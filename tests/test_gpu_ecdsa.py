@@ -122,3 +122,32 @@ def test_config3_full_size_mixed_batch(gpu_ctx, oracle):
     idx = np.flatnonzero(adv)
     assert np.array_equal(got[idx], oracle_verdicts(oracle, w.subset(idx), MODE_IS_VALID))
     assert idx.size > 15000 and (w.scheme[idx] == 2).any() and (w.scheme[idx] == 3).any()
+
+
+@pytest.mark.parametrize("mod", [3, 1])
+def test_forced_glv_fallback_vs_oracle(gpu_ctx, oracle, golden_ecdsa, mod):
+    """secp256k1's GLV split falls back to the full-length pair (|u2|, 0) when a half
+    exceeds 129 bits (cg_ecdsa.h glv_split; never observed on real scalars).  Forced on
+    the device through cg_set_debug for every mod-th K1 element — the golden D1-D8 and
+    B.4 rows plus a mutated random K1 batch — the verdicts must stay the oracle's (the
+    waves holding a forced lane run 65 digits instead of ~33)."""
+    from corda_amd._lib import DEBUG_FORCE_GLV_FALLBACK
+    g = [e for e in golden_ecdsa if e["scheme"] == 2]
+    w = datagen.add_ecdsa_adversarial(datagen.make_batch(3000, msg_bytes=77, scheme=2, seed=31, key_base=90_000),
+                                      frac=0.3, seed=5)
+    gpu_ctx.set_debug(DEBUG_FORCE_GLV_FALLBACK, mod)
+    try:
+        for mode, key in ((MODE_IS_VALID, "is_valid"), (MODE_DO_VERIFY, "do_verify")):
+            b = crypto.pack([e["scheme"] for e in g], [bytes.fromhex(e["q"]) for e in g],
+                            [bytes.fromhex(e["sig"]) for e in g], [bytes.fromhex(e["msg"]) for e in g])
+            v = crypto.verify_packed(gpu_ctx, b, mode)
+            exp = np.array([e[key] for e in g], dtype=np.uint8)
+            bad = np.flatnonzero(v != exp)
+            assert bad.size == 0, [(g[i]["cls"], int(v[i]), int(exp[i])) for i in bad[:10]]
+            got = gpu_verdicts(gpu_ctx, w, mode)
+            exp = oracle_verdicts(oracle, w, mode)
+            bad = np.flatnonzero(got != exp)
+            assert bad.size == 0, [(w.classes[i], int(got[i]), int(exp[i])) for i in bad[:10]]
+        assert (got == ACCEPT).sum() > 1500
+    finally:
+        gpu_ctx.set_debug(DEBUG_FORCE_GLV_FALLBACK, 0)
