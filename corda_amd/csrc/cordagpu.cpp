@@ -1275,8 +1275,14 @@ cg_status tx_pipeline(cg_ctx* ctx, int mode, size_t n_tx, const uint8_t* arena, 
   if (const char* e = std::getenv("CORDA_AMD_TX_CHUNKS")) kmax = std::max(1, std::atoi(e));
   if (const char* e = std::getenv("CORDA_AMD_TX_MIN_CHUNK")) min_chunk = std::max(1, std::atoi(e));
   const size_t K = std::max<size_t>(1, std::min<size_t>(kmax, n_tx / min_chunk));
+  // The last chunk's kernels run after the last upload, unhidden: it gets `tail` of
+  // a regular chunk's transactions (CORDA_AMD_TX_TAIL, default 1 = even split).
+  double tail = 1.0;
+  if (const char* e = std::getenv("CORDA_AMD_TX_TAIL")) tail = std::min(1.0, std::max(0.1, std::atof(e)));
   std::vector<size_t> tb(K + 1);
-  for (size_t k = 0; k <= K; ++k) tb[k] = n_tx * k / K;
+  const double wsum = (double)(K - 1) + tail;
+  for (size_t k = 0; k <= K; ++k)
+    tb[k] = k == K ? n_tx : (size_t)((double)n_tx * (double)k / wsum);
   // The row buffers come from the block cache: every block in it is idle here (the
   // API calls that freed them ended with a stream sync; compute_txids only enqueued
   // work on live blocks).
@@ -1360,6 +1366,20 @@ cg_status tx_pipeline(cg_ctx* ctx, int mode, size_t n_tx, const uint8_t* arena, 
     cg_ctx* c;
     ~PinOff() { c->pin_active = false; }
   } pin_off{ctx};
+  // With four hardware queues both curves would share ec_stream[0], and the ECDSA
+  // stream (~37 ms of kernels per 1 M transactions) became the step's critical path
+  // once the Ed25519 kernels got faster (timeline r02x).  The second curve then runs
+  // on hash_stream: chunk k's R1 work queues behind chunk k's Merkle ids and ahead of
+  // chunk k+1's, which only start after chunk k+1's upload (~6 ms later) anyway.
+  struct CurveStream {
+    cg_ctx* c;
+    hipStream_t saved;
+    ~CurveStream() { c->ec_stream[1] = saved; }
+  } curve_stream{ctx, ctx->ec_stream[1]};
+  {
+    const char* e = std::getenv("CORDA_AMD_TX_CURVE_ON_HASH");
+    if (ctx->ec_stream[1] == ctx->ec_stream[0] && (!e || std::atoi(e) != 0)) ctx->ec_stream[1] = ctx->hash_stream;
+  }
   // Merkle ids on hash_stream (after compute_txids' metadata uploads and tx_index on
   // ctx->stream), so chunk k+1's hashing runs beside chunk k's signature kernels; the
   // signature kernels of chunk k wait for its ids (the ECDSA fork inherits that).
