@@ -554,7 +554,7 @@ def run_ecdsa(args, dist):
             dist.d.all_gather_into_tensor(gathered, bitmap_dev)
 
     elapsed = timed(dist, ctx, step, args.steps, args.warmup)
-    names = ["ecdsa_k1_prep", "ecdsa_k1_msm", "ecdsa_r1_prep", "ecdsa_r1_msm"]
+    names = ["ecdsa_k1_der", "ecdsa_k1_prep", "ecdsa_k1_msm", "ecdsa_r1_der", "ecdsa_r1_prep", "ecdsa_r1_msm"]
     ks_mixed = kstats(ctx, names)
     verdict = pb.verify(MODE_IS_VALID)
     adv = np.array([c != "valid" for c in w.classes])
@@ -613,7 +613,7 @@ def run_ecdsa(args, dist):
         "workload": f"BASELINE config 3: {n} ECDSA_SECP256K1_SHA256 + {n} ECDSA_SECP256R1_SHA256 per GPU, "
                     f"{msg_bytes} B messages, {args.adversarial:.0%} adversarial (D1-D8); "
                     + ("distinct keys" if pool == n else f"{pool} distinct signed tuples per curve tiled to size")
-                    + "; K4 DER pre-pass staged once with the batch (cg_batch_create), not in the step",
+                    + "; every step re-parses the DER signatures (K4) from the device-resident raw rows",
         "batch_per_gpu": w.n, "global_batch": w.n * world, "msg_bytes": msg_bytes,
         "parallelism": f"dp{world} (signature-index shards)"})
     line.update({

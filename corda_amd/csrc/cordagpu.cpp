@@ -326,6 +326,12 @@ struct cg_batch {
   uint32_t* ed_key_first = nullptr;
   // ECDSA subsets (K1, R1)
   cg::EcdsaBatch ec[2];
+  // raw signature rows kept for the K4 DER parse that opens every verify of the ECDSA
+  // subsets (BC decodes the DER inside each engineVerify call); null in tx-pipeline
+  // batches, whose staging parse already sits inside the pipeline's own timed run
+  uint8_t* ec_sig_raw = nullptr;       // [n][ec_sig_stride]
+  uint32_t* ec_sig_len_raw = nullptr;  // [n], or null: every row is ec_sig_stride long
+  size_t ec_sig_stride = 0;
 };
 
 namespace {
@@ -351,6 +357,8 @@ void batch_free(cg_ctx* ctx, cg_batch* b) {
     for (const void* p : {(const void*)e.index, (const void*)e.q, (const void*)e.rs, (const void*)e.der,
                           (const void*)e.sig_len, (const void*)e.msg_off, (const void*)e.msg_len})
       dfree(ctx, p);
+  dfree(ctx, b->ec_sig_raw);
+  dfree(ctx, b->ec_sig_len_raw);
   delete b;
 }
 
@@ -798,6 +806,13 @@ cg_status create_batch(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const ui
                                                  b->msg_len_all, ctx->stream);
       if (e != hipSuccess) return bail(hip_fail(ctx, e, "stage ecdsa"));
     }
+    if (raw_owned && (b->ec[0].n || b->ec[1].n)) {  // the batch keeps the rows for its per-verify DER parse
+      b->ec_sig_raw = sig_raw;
+      b->ec_sig_len_raw = sl_raw;
+      b->ec_sig_stride = sig_stride;
+      sig_raw = nullptr;
+      sl_raw = nullptr;
+    }
   }
   // the host index vectors die here: wait for the copies that read them (unless every
   // one went through the pinned staging area of an asynchronous tx-pipeline stage)
@@ -896,6 +911,13 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = 
       if (s2 != CG_OK) return s2;
       CG_TRY(ctx, hipStreamWaitEvent(es, ctx->ev_fork, 0), "fork ecdsa");
       joins[c] = true;  // from here on this curve's stream may hold work: the exit path joins it
+      if (b->ec_sig_raw) {  // K4: strict DER -> r, s + status, from the kept raw rows
+        Timed t(ctx, eb.scheme == 2 ? "ecdsa_k1_der" : "ecdsa_r1_der", eb.n, es);
+        CG_TRY(ctx,
+               cg::launch_der_parse(eb.scheme, b->ec_sig_raw, b->ec_sig_stride, b->ec_sig_len_raw,
+                                    (uint32_t)b->ec_sig_stride, eb.index, eb.n, eb.n, eb.rs, eb.der, es),
+               "launch ecdsa der parse");
+      }
       for (uint32_t base = 0; base < eb.n; base += chunk) {
         const uint32_t cnt = std::min(chunk, eb.n - base);
         {
