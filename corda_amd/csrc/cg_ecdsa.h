@@ -60,12 +60,9 @@ CG_HD int der_int(Byte&& b, uint32_t end, uint32_t& i, const uint32_t order[8], 
     if (mag == 0 || mag > 32) {
       range_bad = 1;
     } else {
-      for (uint32_t m = 0; m < mag; ++m) {  // big-endian bytes -> LE words
-        const uint32_t pos = mag - 1 - m;    // byte significance
-        const uint32_t byte = b(i + k + m);
-        for (int wi = 0; wi < 8; ++wi)
-          if ((uint32_t)wi == (pos >> 2)) out[wi] |= byte << (8 * (pos & 3));
-      }
+      const uint32_t lsb = i + k + mag - 1;  // big-endian bytes -> LE words, by significance:
+      CG_UNROLL for (uint32_t pos = 0; pos < 32; ++pos)  // static word/shift, no per-byte word select
+        if (pos < mag) out[pos >> 2] |= b(lsb - pos) << (8 * (pos & 3));
       if (!mp_lt(out, order)) range_bad = 1;
     }
   }

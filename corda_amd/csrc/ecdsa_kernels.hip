@@ -1,7 +1,7 @@
 // K2 (secp256r1 / P-256) + K3 (secp256k1) ECDSA verification and K4 DER pre-pass
 // for gfx950, BouncyCastle 1.57 semantics (cg_ecdsa.h).
 //
-//   cg_der_parse<C>   staging-time pre-pass: strict DER -> r, s limbs + status
+//   cg_der_parse<C>   first launch of every verify: strict DER -> r, s limbs + status
 //   cg_ecdsa_prep_a<C> key check, SHA-256(M) mod n, k*Q table, s into the batched
 //                     inversion (cg_inv_up / cg_inv_root / cg_inv_down: a product
 //                     tree over the chunk, ~3 multiplications per s^-1 mod n)
@@ -67,21 +67,45 @@ CG_DEV uint32_t wave_max_u32(uint32_t v) {
   return v;
 }
 
+// One lane per signature.  A block whose 256 rows are one contiguous run of the raw
+// array (the usual case: each curve's subset is a run of the batch) first copies the
+// run into LDS with coalesced dword loads — a lane-per-row byte walk strides 72 B
+// between lanes and spends its time in the address path — and parses from there; a
+// lane whose row lies outside the run (scattered subsets) reads its row from HBM.
+constexpr uint32_t kDerTileStride = 128;  // longest row staged through LDS (DER max is 72)
 template <class C>
 __global__ __launch_bounds__(256) void cg_der_parse(const uint8_t* __restrict__ sig, size_t stride,
                                                     const uint32_t* __restrict__ sig_len, uint32_t fill_len,
                                                     const uint32_t* __restrict__ idx, uint32_t n, uint32_t cap,
                                                     uint32_t* __restrict__ rs, uint32_t* __restrict__ der) {
   CG_WAVE_PRIO(2);
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  __shared__ uint32_t tile[256 * kDerTileStride / 4];
+  const uint32_t i0 = blockIdx.x * blockDim.x;
+  const uint32_t cnt = min((uint32_t)blockDim.x, n - i0);
+  const size_t e0 = idx ? idx[i0] : i0;
+  const bool staged = stride % 4 == 0 && stride <= kDerTileStride && ((uintptr_t)sig & 3) == 0 &&
+                      (idx ? (size_t)idx[i0 + cnt - 1] - e0 == cnt - 1 : true);  // block-uniform
+  if (staged) {
+    const uint32_t words = cnt * (uint32_t)(stride / 4);
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(sig + e0 * stride);
+    for (uint32_t w = threadIdx.x; w < words; w += blockDim.x) tile[w] = src[w];
+    __syncthreads();
+  }
+  const uint32_t i = i0 + threadIdx.x;
   if (i >= n) return;
   const size_t e = idx ? idx[i] : i;
-  const uint8_t* p = sig + e * stride;
   uint32_t len = sig_len ? sig_len[e] : fill_len;
   if (len > stride) len = (uint32_t)stride;  // host rejects this case; never read past the slot
   uint32_t nn[8], r[8], s[8];
   C::n(nn);
-  const uint32_t st = der_parse([&](uint32_t j) { return (uint32_t)p[j]; }, len, nn, r, s);
+  uint32_t st;
+  if (staged && e >= e0 && e - e0 < cnt) {
+    const uint8_t* p = reinterpret_cast<const uint8_t*>(tile) + (e - e0) * stride;
+    st = der_parse([&](uint32_t j) { return (uint32_t)p[j]; }, len, nn, r, s);
+  } else {
+    const uint8_t* p = sig + e * stride;
+    st = der_parse([&](uint32_t j) { return (uint32_t)p[j]; }, len, nn, r, s);
+  }
   CG_UNROLL for (int w = 0; w < 8; ++w) {
     rs[(size_t)w * cap + i] = r[w];
     rs[(size_t)(8 + w) * cap + i] = s[w];

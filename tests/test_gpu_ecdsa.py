@@ -151,3 +151,32 @@ def test_forced_glv_fallback_vs_oracle(gpu_ctx, oracle, golden_ecdsa, mod):
         assert (got == ACCEPT).sum() > 1500
     finally:
         gpu_ctx.set_debug(DEBUG_FORCE_GLV_FALLBACK, 0)
+
+
+def test_prepared_batch_reparses_der_every_verify(gpu_ctx, oracle, golden_ecdsa):
+    """A staged batch keeps its raw DER rows and every cg_batch_verify re-runs the K4
+    parse before the ECDSA kernels (BC decodes inside each engineVerify).  The same
+    staged mixed batch — golden D1-D8 rows (malformed and out-of-range DER among
+    them), mutated random K1/R1 and Ed25519 elements — verified repeatedly in both
+    modes must give the oracle's verdicts every time."""
+    g = golden_ecdsa
+    gold = crypto.pack([e["scheme"] for e in g], [bytes.fromhex(e["q"]) for e in g],
+                       [bytes.fromhex(e["sig"]) for e in g], [bytes.fromhex(e["msg"]) for e in g])
+    sch = np.random.default_rng(9).choice(np.array([2, 3, 4], np.uint8), size=3000)
+    w = datagen.add_ecdsa_adversarial(datagen.make_batch(len(sch), msg_bytes=41, scheme=sch, seed=19,
+                                                         key_base=310_000), frac=0.3, seed=11)
+    rand = crypto.PackedBatch(w.n, w.scheme, w.pk, w.pk_stride, w.sig, w.sig_stride, w.sig_len, w.msg, w.msg_off,
+                              w.msg_len)
+    for b, exp_of in ((gold, lambda mode: np.array([e["is_valid" if mode == MODE_IS_VALID else "do_verify"]
+                                                    for e in g], np.uint8)),
+                      (rand, lambda mode: oracle_verdicts(oracle, w, mode))):
+        pb = crypto.PreparedBatch(gpu_ctx, b)
+        try:
+            for mode in (MODE_IS_VALID, MODE_DO_VERIFY, MODE_IS_VALID):
+                got, exp = pb.verify(mode), exp_of(mode)
+                if b.key_invalid is not None:  # host-side key-length rule, as verify_packed applies it
+                    got[b.key_invalid] = crypto.KEY_INVALID
+                bad = np.flatnonzero(got != exp)
+                assert bad.size == 0, [(int(i), int(got[i]), int(exp[i])) for i in bad[:10]]
+        finally:
+            pb.close()
