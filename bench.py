@@ -840,6 +840,8 @@ def run_backlog(args, dist):
     p = datagen.make_batch(pool, msg_bytes=msg_bytes, seed=42 + rank, key_base=(2 << 32) + rank * pool,
                            threads=cpu_threads(), key_reuse=args.key_reuse)
     t_gen = time.perf_counter() - t_gen
+    if not args.key_reuse:  # config 5 has distinct keys: the tiling's repeats must not reach the key-reuse path
+        os.environ["CORDA_AMD_KEY_REUSE"] = "0"
     ctx = Context(dist.local_rank)
     adv_ok = [True]
     t_stage = time.perf_counter()
@@ -888,7 +890,9 @@ def run_backlog(args, dist):
                          "workload": f"BASELINE config 5: {total} EDDSA_ED25519_SHA512 signatures over {msg_bytes} B "
                                      f"tx ids split by index over {world} GPU(s), staged in 2^24 chunks, "
                                      f"{args.adversarial:.0%} adversarial; {pool} distinct signed tuples per rank "
-                                     "tiled to size",
+                                     "tiled to size" + ("" if args.key_reuse else
+                                                        " (balanced per-signature path forced, "
+                                                        "CORDA_AMD_KEY_REUSE=0: no key dedupe of the tiling)"),
                          "batch_per_gpu": n, "global_batch": total,
                          "parallelism": f"dp{world} (index shards" + (", RCCL all-gather)" if world > 1 else ")")},
                      scaling="strong")
