@@ -342,23 +342,43 @@ def pcie_h2d_peak_GBps(device=0, mb=512, reps=5):
 
 
 # ------------------------------------------------------------------ --dry-run
+def _dry_words(lo: int, hi: int) -> np.ndarray:
+    """Accept-bitmap words of the synthetic dry-run verdicts (element i accepts iff
+    i % 7 != 3) for indices [lo, hi), lo a multiple of 32; built in 2^22 pieces."""
+    from corda_amd import dist as D
+    step = 1 << 22
+    parts = [D.pack_bits((np.arange(a, min(hi, a + step), dtype=np.int64) % 7) != 3) for a in range(lo, hi, step)]
+    return np.concatenate(parts).view(np.int32) if parts else np.zeros(0, np.int32)
+
+
 def run_dry(args, dist):
     """The multi-rank plumbing without a GPU: every rank owns a synthetic index
     shard, a step packs a verdict bitmap and all-gathers it (gloo), timing is the
-    max over ranks between barriers — what the real workloads do over RCCL."""
+    max over ranks between barriers — what the real workloads do over RCCL.
+    ``--workload backlog`` uses config 5's shapes: ``--batch`` (default 100 M) is the
+    TOTAL, split by ``shard_bounds`` (uneven for world 3, 6, 7 ...), gathered with
+    ``gather_ordered`` as ShardBacklog.allgather does; otherwise ``--batch`` per rank."""
     import torch
     from corda_amd import dist as D
     if os.environ.get("CORDA_AMD_DRY_FAIL_RANK") == str(dist.rank):
         sys.exit(3)  # tests: a failing rank must fail the launcher
-    n = args.batch or 4096
-    bounds = D.shard_bounds(n * dist.world, dist.world)
+    backlog = args.workload == "backlog"
+    total = (args.batch or 100_000_000) if backlog else (args.batch or 4096) * dist.world
+    bounds = D.shard_bounds(total, dist.world)
     lo, hi = bounds[dist.rank], bounds[dist.rank + 1]
-    accept = (np.arange(lo, hi) % 7) != 3
-    words = torch.from_numpy(D.pack_bits(accept).view(np.int32).copy())
+    wmax = max((bounds[r + 1] - bounds[r] + 31) // 32 for r in range(dist.world))
+    words = torch.zeros(max(wmax, 1), dtype=torch.int32)
+    mine = _dry_words(lo, hi)
+    words[:len(mine)] = torch.from_numpy(mine.copy())
     got = [None]
 
     def step():
-        got[0] = D.allgather_bitmap(words, bounds, dist.rank) if dist.d is not None else words
+        if dist.d is None:
+            got[0] = words[:len(mine)]
+        elif backlog:
+            got[0] = D.gather_ordered(words, bounds)
+        else:
+            got[0] = D.allgather_bitmap(words[:len(mine)], bounds, dist.rank)
 
     for _ in range(args.warmup):
         step()
@@ -368,12 +388,15 @@ def run_dry(args, dist):
         step()
     dist.sync()
     elapsed = dist.max(time.perf_counter() - t0)
-    exp = D.pack_bits((np.arange(n * dist.world) % 7) != 3).view(np.int32)
+    ok = bool(np.array_equal(got[0].numpy(), _dry_words(0, total))) if dist.rank == 0 else None
     line = base_line(args, dist, "dry-run bitmap all-gathers/sec", "steps/s", args.steps / max(elapsed, 1e-9),
-                     elapsed * 1e3 / args.steps, {"workload": "dry run (gloo, CPU)", "batch_per_gpu": n,
-                                                  "global_batch": n * dist.world,
+                     elapsed * 1e3 / args.steps, {"workload": "dry run (gloo, CPU)" + (", config-5 shards" if backlog
+                                                                                        else ""),
+                                                  "batch_per_gpu": hi - lo, "global_batch": total,
+                                                  "shard_elements": [bounds[r + 1] - bounds[r]
+                                                                     for r in range(dist.world)],
                                                   "parallelism": f"dp{dist.world}"})
-    line["checks"] = {"bitmap_matches": bool(np.array_equal(got[0].numpy(), exp)), "rank_pid_world": dist.world}
+    line["checks"] = {"bitmap_matches": ok, "rank_pid_world": dist.world}
     line["dry_run"] = True
     return line
 
@@ -832,7 +855,6 @@ def run_backlog(args, dist):
     bounds = D.shard_bounds(total, world)  # 32-aligned index shards: bitmap words concatenate
     lo, hi = bounds[rank], bounds[rank + 1]
     n = hi - lo
-    n_max = max(bounds[r + 1] - bounds[r] for r in range(world))
     chunk = 1 << 24
     pool = min(args.pool * 8, n)
     msg_bytes = args.msg_bytes or 32
@@ -861,18 +883,19 @@ def run_backlog(args, dist):
             yield pb
 
     # the rank's shard staged as 2^24-element chunks verified into one device bitmap (C1 input)
-    backlog = D.ShardBacklog(ctx, chunks(), words=(n_max + 31) // 32)
+    backlog = D.ShardBacklog(ctx, chunks(), bounds=bounds)
     t_stage = time.perf_counter() - t_stage
     sizes = backlog.sizes
     gathered = None
     if dist.d is not None:
         import torch
         gathered = torch.zeros(backlog.words * world, dtype=torch.int32, device="cuda")
+        ordered = torch.zeros((total + 31) // 32, dtype=torch.int32, device="cuda")
 
     def step():
         backlog.verify(MODE_IS_VALID)
         if dist.d is not None:
-            backlog.allgather(gathered)  # C1 over the whole shard's bitmap
+            backlog.allgather(gathered, ordered)  # C1: the index-ordered global bitmap
 
     elapsed = timed(dist, ctx, step, args.steps, args.warmup)
     ks = kstats(ctx, ED_KERNELS + ED_REUSE_KERNELS)

@@ -32,7 +32,7 @@ COMPOSITE_LEAF, COMPOSITE_NODE, COMPOSITE_INVALID = 0, 1, 0x80
 TX_OK, TX_NO_SIGNATURES, TX_NO_COMPONENTS, TX_SIGNATURES_MISSING = -1, -2, -3, -4
 # cg_set_debug options (test hooks)
 DEBUG_FORCE_FULL_LENGTH, DEBUG_FAIL_ALLOC, DEBUG_THROW, DEBUG_FORCE_GLV_FALLBACK = 1, 2, 3, 4
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 # exported symbols and their prototypes: (restype, argtypes)
 _u8p, _u32p, _u64p, _i32p = POINTER(c_uint8), POINTER(c_uint32), POINTER(c_uint64), POINTER(ctypes.c_int32)

@@ -89,10 +89,26 @@ def key_length_ok(scheme_id: int, key) -> bool:
     return want is None or len(bytes(key)) == want
 
 
-def _check_key_length(scheme_id: int, key, index: int | None = None):
-    if not key_length_ok(scheme_id, key):
-        raise InvalidKeyException(f"public key of scheme {scheme_id} must be {KEY_BYTES[scheme_id]} bytes, "
-                                  f"got {len(bytes(key))}", index)
+# OR-ed into the scheme id of an element whose key bytes are not the scheme's wire form
+# (include/cordagpu.h CG_SCHEME_FLAG_KEY_INVALID): the key object cannot be constructed,
+# so the library reports KEY_INVALID for it on every path (verify, prepared batches and
+# their device bitmaps, shards, transactions) and never reads its rows.
+SCHEME_FLAG_KEY_INVALID = 0x80
+
+
+def pack_key_row(pk: np.ndarray, scheme: np.ndarray, i: int, key) -> bool:
+    """Writes element i's key row (device schemes only — the rows of host-verified schemes
+    such as RSA are never read by the device and may be any length).  A key of the wrong
+    length flags the element KEY_INVALID and leaves its row zero.  Returns False for it."""
+    sid = int(scheme[i])
+    if sid not in KEY_BYTES:
+        return True
+    kb = bytes(key)
+    if not key_length_ok(sid, kb):
+        scheme[i] = sid | SCHEME_FLAG_KEY_INVALID
+        return False
+    pk[i, :len(kb)] = np.frombuffer(kb, dtype=np.uint8)
+    return True
 
 
 @dataclass
@@ -109,8 +125,8 @@ class PackedBatch:
     msg: np.ndarray
     msg_off: np.ndarray
     msg_len: np.ndarray
-    # elements whose key bytes are not the scheme's wire form: the key object cannot
-    # be constructed, so their verdict is KEY_INVALID whatever the device computes
+    # elements whose key bytes are not the scheme's wire form (flagged in `scheme` with
+    # SCHEME_FLAG_KEY_INVALID: the library gives them KEY_INVALID); informational
     key_invalid: np.ndarray | None = None
 
 
@@ -127,13 +143,7 @@ def pack(schemes, public_keys: Sequence[bytes], signatures: Sequence[bytes], cle
         scheme = np.array([_scheme_id(s) for s in schemes], dtype=np.uint8)
     pk_stride = 64
     pk = np.zeros((max(n, 1), pk_stride), dtype=np.uint8)
-    bad_keys = []
-    for i, k in enumerate(public_keys):
-        kb = bytes(k)
-        if not key_length_ok(int(scheme[i]), kb):
-            bad_keys.append(i)
-            continue  # the row stays zero; the verdict is overridden
-        pk[i, :len(kb)] = np.frombuffer(kb, dtype=np.uint8)
+    bad_keys = [i for i, k in enumerate(public_keys) if not pack_key_row(pk, scheme, i, k)]
     maxlen = max([len(s) for s in signatures] + [64])
     sig_stride = (maxlen + 3) // 4 * 4
     sig = np.zeros((max(n, 1), sig_stride), dtype=np.uint8)
@@ -158,10 +168,6 @@ def verify_packed(ctx: _lib.Context, b: PackedBatch, mode: int, bitmap: bool = F
                                       _lib.ptr(b.sig), b.sig_stride, _lib.ptr(b.sig_len), _lib.ptr(b.msg),
                                       len(b.msg), _lib.ptr(b.msg_off), _lib.ptr(b.msg_len), _lib.ptr(verdict),
                                       _lib.ptr(bm)))
-    if b.key_invalid is not None:  # KEY_INVALID outranks every other outcome (JVM order)
-        verdict[b.key_invalid] = KEY_INVALID
-        if bm is not None:
-            bm[b.key_invalid // 32] &= ~(np.uint32(1) << (b.key_invalid % 32).astype(np.uint32))
     return (verdict[:b.n], bm) if bitmap else verdict[:b.n]
 
 

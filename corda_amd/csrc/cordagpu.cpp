@@ -324,6 +324,9 @@ struct cg_batch {
   uint32_t n_keys = 0;
   uint32_t* ed_key_index = nullptr;
   uint32_t* ed_key_first = nullptr;
+  // elements flagged CG_SCHEME_FLAG_KEY_INVALID: their verdict is CG_KEY_INVALID
+  uint32_t n_bad = 0;
+  uint32_t* bad_index = nullptr;
   // ECDSA subsets (K1, R1)
   cg::EcdsaBatch ec[2];
   // raw signature rows kept for the K4 DER parse that opens every verify of the ECDSA
@@ -353,6 +356,7 @@ void batch_free(cg_ctx* ctx, cg_batch* b) {
   dfree(ctx, b->ed_msg_len);
   dfree(ctx, b->ed_key_index);
   dfree(ctx, b->ed_key_first);
+  dfree(ctx, b->bad_index);
   for (auto& e : b->ec)
     for (const void* p : {(const void*)e.index, (const void*)e.q, (const void*)e.rs, (const void*)e.der,
                           (const void*)e.sig_len, (const void*)e.msg_off, (const void*)e.msg_len})
@@ -396,6 +400,9 @@ cg_status check_inputs(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const ui
   bool has_ed = false, has_ec = false;
   for (size_t i = 0; i < n; ++i) {
     const uint8_t s = scheme_id ? scheme_id[i] : CG_SCHEME_EDDSA_ED25519_SHA512;
+    if (m.off_host && (uint64_t)m.off_host[i] + m.len_host[i] > m.bytes)
+      return fail(ctx, CG_E_INVALID_ARGUMENT, "message out of arena bounds at element " + std::to_string(i));
+    if (s & CG_SCHEME_FLAG_KEY_INVALID) continue;  // never read beyond its verdict
     if (s == CG_SCHEME_EDDSA_ED25519_SHA512) has_ed = true;
     if (s == CG_SCHEME_ECDSA_SECP256K1_SHA256 || s == CG_SCHEME_ECDSA_SECP256R1_SHA256) {
       has_ec = true;
@@ -403,8 +410,6 @@ cg_status check_inputs(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const ui
       if (l > sig_stride)
         return fail(ctx, CG_E_INVALID_ARGUMENT, "ECDSA signature longer than sig_stride at element " + std::to_string(i));
     }
-    if (m.off_host && (uint64_t)m.off_host[i] + m.len_host[i] > m.bytes)
-      return fail(ctx, CG_E_INVALID_ARGUMENT, "message out of arena bounds at element " + std::to_string(i));
   }
   if (has_ed && (pk_stride < 32 || sig_stride < 64))
     return fail(ctx, CG_E_INVALID_ARGUMENT, "Ed25519 needs pk_stride >= 32 and sig_stride >= 64");
@@ -710,11 +715,14 @@ cg_status create_batch(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const ui
   };
   // host-side partition by scheme
   std::vector<uint32_t> idx[3];  // 0: ed25519, 1: K1, 2: R1
+  std::vector<uint32_t> bad;     // flagged CG_SCHEME_FLAG_KEY_INVALID
   debug_throw_point(ctx);
   bool ed_identity = true;
   for (size_t i = 0; i < n; ++i) {
     const uint8_t s = scheme_id ? scheme_id[i] : CG_SCHEME_EDDSA_ED25519_SHA512;
-    if (s == CG_SCHEME_EDDSA_ED25519_SHA512) {
+    if (s & CG_SCHEME_FLAG_KEY_INVALID) {
+      bad.push_back((uint32_t)i);
+    } else if (s == CG_SCHEME_EDDSA_ED25519_SHA512) {
       if (idx[0].size() != i) ed_identity = false;
       idx[0].push_back((uint32_t)i);
     } else if (s == CG_SCHEME_ECDSA_SECP256K1_SHA256) {
@@ -762,6 +770,11 @@ cg_status create_batch(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const ui
     if ((st = upload(ctx, &pk_raw, pk, n * pk_stride, "upload pk")) != CG_OK) return bail(st);
     if ((st = upload(ctx, &sig_raw, sig, n * sig_stride, "upload sig")) != CG_OK) return bail(st);
     if (sig_len && (st = upload(ctx, &sl_raw, sig_len, n, "upload sig_len")) != CG_OK) return bail(st);
+  }
+  if (!bad.empty()) {
+    b->n_bad = (uint32_t)bad.size();
+    if ((st = upload_idx(ctx, &b->bad_index, bad.data(), bad.size(), "upload key-invalid index")) != CG_OK)
+      return bail(st);
   }
   {
     Timed t(ctx, "stage", n);
@@ -873,6 +886,9 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = 
   auto run = [&]() -> cg_status {
     // elements of unsupported schemes keep this value
     CG_TRY(ctx, hipMemsetAsync(b->verdict, CG_UNSUPPORTED, n, ctx->stream), "init verdict");
+    // keys the caller could not construct: KEY_INVALID (no verify kernel touches them)
+    CG_TRY(ctx, cg::launch_fill_index(b->bad_index, b->n_bad, b->verdict, CG_KEY_INVALID, ctx->stream),
+           "launch key-invalid fill");
     CG_TRY(ctx, hipEventRecord(ctx->ev_fork, ctx->stream), "fork ecdsa");
     bool keys_pending = false;
     if (b->n_ed && b->ed_key_index) {
@@ -985,6 +1001,171 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = 
   return CG_OK;
 }
 
+// ------------------------------------------------------------ host-buffer verify
+// cg_verify_batch is what a JVM caller hits (Crypto.isValid / doVerify in a loop,
+// Crypto.kt:534-541): host buffers in, verdicts out.  Uploading the whole batch and
+// then verifying it leaves the GPU idle for the PCIe transfer (~20 ns per 1 KB
+// signature at ~57 GB/s, twice the kernels' ~10 ns).  The pipeline cuts the batch
+// into index-range chunks: chunk k's rows and the arena prefix its messages reach
+// are copied on copy_stream while chunk k-1's kernels run on the compute streams, so
+// the call costs the transfer plus the last chunk's kernels.  The last chunk is the
+// smallest (`tail` of a regular chunk): only its kernels run after the last byte.
+struct VerifyRun {
+  uint8_t* arena = nullptr;
+  uint64_t* off = nullptr;
+  uint32_t* len = nullptr;
+  uint8_t* pk = nullptr;
+  uint8_t* sig = nullptr;
+  uint32_t* sl = nullptr;
+  uint8_t* verdict = nullptr;
+  uint32_t* bitmap = nullptr;
+  std::vector<hipEvent_t> ev;
+  std::vector<cg_batch*> batches;  // chunk batches (verdicts are slices of `verdict`)
+  void release(cg_ctx* ctx) {
+    for (hipStream_t s : {ctx->copy_stream, ctx->ec_stream[0], ctx->ec_stream[1], ctx->stream})
+      (void)hipStreamSynchronize(s);
+    for (cg_batch* b : batches) batch_free(ctx, b);
+    batches.clear();
+    for (hipEvent_t e : ev)
+      if (e) (void)hipEventDestroy(e);
+    ev.clear();
+    for (const void* p : {(const void*)arena, (const void*)off, (const void*)len, (const void*)pk, (const void*)sig,
+                          (const void*)sl, (const void*)verdict, (const void*)bitmap})
+      dfree(ctx, p);
+    arena = pk = sig = verdict = nullptr;
+    off = nullptr;
+    len = sl = bitmap = nullptr;
+  }
+};
+
+// Chunk boundaries of an n-element host batch: K = n / min_chunk chunks (at most
+// kmax), 64-aligned (whole waves), the last one `tail` times a regular one.
+// CORDA_AMD_VERIFY_CHUNKS / _MIN_CHUNK / _TAIL override (tuning, tests).
+std::vector<size_t> verify_chunk_bounds(size_t n) {
+  size_t kmax = 8, min_chunk = 16384;
+  double tail = 0.5;
+  if (const char* e = std::getenv("CORDA_AMD_VERIFY_CHUNKS")) kmax = std::max(1, std::atoi(e));
+  if (const char* e = std::getenv("CORDA_AMD_VERIFY_MIN_CHUNK")) min_chunk = std::max(1, std::atoi(e));
+  if (const char* e = std::getenv("CORDA_AMD_VERIFY_TAIL")) tail = std::min(1.0, std::max(0.05, std::atof(e)));
+  const size_t K = std::max<size_t>(1, std::min<size_t>(kmax, n / min_chunk));
+  std::vector<size_t> b(K + 1, 0);
+  const double wsum = (double)(K - 1) + tail;
+  for (size_t k = 1; k < K; ++k) b[k] = std::min(n, (size_t)((double)n * (double)k / wsum) / 64 * 64);
+  b[K] = n;
+  for (size_t k = 1; k <= K; ++k) b[k] = std::max(b[k], b[k - 1]);
+  return b;
+}
+
+cg_status verify_pipeline(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme_id, const uint8_t* pk,
+                          size_t pk_stride, const uint8_t* sig, size_t sig_stride, const uint32_t* sig_len,
+                          const uint8_t* msg, size_t msg_bytes, const uint64_t* msg_off, const uint32_t* msg_len,
+                          const std::vector<size_t>& cb, VerifyRun& r) {
+  const size_t K = cb.size() - 1;
+  cg_status st;
+  if ((st = dalloc(ctx, &r.arena, msg_bytes + 16, "alloc arena")) != CG_OK ||
+      (st = dalloc(ctx, &r.off, n, "alloc msg_off")) != CG_OK || (st = dalloc(ctx, &r.len, n, "alloc msg_len")) != CG_OK ||
+      (st = dalloc(ctx, &r.pk, n * pk_stride, "alloc pk rows")) != CG_OK ||
+      (st = dalloc(ctx, &r.sig, n * sig_stride, "alloc sig rows")) != CG_OK ||
+      (sig_len && (st = dalloc(ctx, &r.sl, n, "alloc sig_len rows")) != CG_OK) ||
+      (st = dalloc(ctx, &r.verdict, n, "alloc verdict")) != CG_OK ||
+      (st = dalloc(ctx, &r.bitmap, (n + 31) / 32, "alloc bitmap")) != CG_OK)
+    return st;
+  r.ev.assign(K, nullptr);
+  for (hipEvent_t& e : r.ev) CG_TRY(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming), "verify pipeline event");
+  // the arena's 16-byte tail pad (kernels' vector loads may run past a message end)
+  CG_TRY(ctx, hipMemsetAsync(r.arena + msg_bytes, 0, 16, ctx->copy_stream), "pad arena");
+  // Chunk k's upload: the arena bytes its messages reach beyond what earlier chunks
+  // uploaded (a prefix: an element-ordered arena, what a caller packs, gives even
+  // pieces; any layout is correct), then its metadata and rows; event ev[k].
+  uint64_t up_to = 0;
+  auto enqueue_upload = [&](size_t k) -> cg_status {
+    const size_t lo = cb[k], hi = cb[k + 1];
+    const uint64_t from = up_to;
+    for (size_t i = lo; i < hi; ++i) up_to = std::max<uint64_t>(up_to, msg_off[i] + msg_len[i]);
+    hipStream_t cs = ctx->copy_stream;
+    {
+      Timed t(ctx, "h2d_verify", (up_to - from) + (hi - lo) * (pk_stride + sig_stride + 16), cs);
+      if (up_to > from)
+        CG_TRY(ctx, hipMemcpyAsync(r.arena + from, msg + from, up_to - from, hipMemcpyHostToDevice, cs), "upload arena");
+      CG_TRY(ctx, hipMemcpyAsync(r.off + lo, msg_off + lo, (hi - lo) * 8, hipMemcpyHostToDevice, cs), "upload msg_off");
+      CG_TRY(ctx, hipMemcpyAsync(r.len + lo, msg_len + lo, (hi - lo) * 4, hipMemcpyHostToDevice, cs), "upload msg_len");
+      CG_TRY(ctx, hipMemcpyAsync(r.pk + lo * pk_stride, pk + lo * pk_stride, (hi - lo) * pk_stride,
+                                 hipMemcpyHostToDevice, cs), "upload pk rows");
+      CG_TRY(ctx, hipMemcpyAsync(r.sig + lo * sig_stride, sig + lo * sig_stride, (hi - lo) * sig_stride,
+                                 hipMemcpyHostToDevice, cs), "upload sig rows");
+      if (sig_len)
+        CG_TRY(ctx, hipMemcpyAsync(r.sl + lo, sig_len + lo, (hi - lo) * 4, hipMemcpyHostToDevice, cs), "upload sig_len");
+    }
+    CG_TRY(ctx, hipEventRecord(r.ev[k], cs), "verify pipeline record");
+    return CG_OK;
+  };
+  if ((st = enqueue_upload(0)) != CG_OK) return st;
+  // Scratch sized for the largest chunk first, so no chunk regrows (frees) a buffer
+  // an earlier chunk's kernels still use.
+  uint32_t max_cnt[3] = {0, 0, 0};
+  for (size_t k = 0; k < K; ++k) {
+    uint32_t cnt[3] = {0, 0, 0};
+    for (size_t i = cb[k]; i < cb[k + 1]; ++i) {
+      const uint8_t sc = scheme_id ? scheme_id[i] : CG_SCHEME_EDDSA_ED25519_SHA512;
+      if (sc == CG_SCHEME_EDDSA_ED25519_SHA512) ++cnt[0];
+      else if (sc == CG_SCHEME_ECDSA_SECP256K1_SHA256) ++cnt[1];
+      else if (sc == CG_SCHEME_ECDSA_SECP256R1_SHA256) ++cnt[2];
+    }
+    for (int c = 0; c < 3; ++c) max_cnt[c] = std::max(max_cnt[c], cnt[c]);
+  }
+  if (max_cnt[0] && (st = ensure_ed_scratch(ctx, max_cnt[0])) != CG_OK) return st;
+  for (int c = 0; c < 2; ++c) {
+    uint32_t chunk = 0;
+    if (max_cnt[1 + c] &&
+        (st = ecdsa_scratch_retry(ctx, c == 0 ? CG_SCHEME_ECDSA_SECP256K1_SHA256 : CG_SCHEME_ECDSA_SECP256R1_SHA256,
+                                  max_cnt[1 + c], &chunk)) != CG_OK)
+      return st;
+  }
+  // the staging's host index vectors go out through page-locked memory, so no chunk
+  // waits on the host for its own copies
+  const size_t pin_need = 4 * n + 4 * 256 * K;
+  if (ctx->pin_cap < pin_need) {
+    if (ctx->pin) (void)hipHostFree(ctx->pin);  // idle: every earlier call ended with a sync
+    ctx->pin = nullptr;
+    ctx->pin_cap = 0;
+    if (hipHostMalloc((void**)&ctx->pin, pin_need, hipHostMallocDefault) == hipSuccess) ctx->pin_cap = pin_need;
+    else (void)hipGetLastError();  // no staging: the chunks sync instead
+  }
+  ctx->pin_used = 0;
+  ctx->pin_active = true;
+  struct PinOff {
+    cg_ctx* c;
+    ~PinOff() { c->pin_active = false; }
+  } pin_off{ctx};
+  for (size_t k = 0; k < K; ++k) {
+    // the next chunk's copy is enqueued first (a pageable copy may hold the host until
+    // it is done: chunk k's kernels, enqueued below, then start right after it)
+    if (k + 1 < K && (st = enqueue_upload(k + 1)) != CG_OK) return st;
+    const size_t lo = cb[k], hi = cb[k + 1];
+    if (hi == lo) continue;
+    MsgSrc m;
+    m.dev = r.arena;
+    m.bytes = msg_bytes;
+    m.off_dev = r.off + lo;
+    m.len_dev = r.len + lo;
+    m.pk_dev = r.pk + lo * pk_stride;
+    m.sig_dev = r.sig + lo * sig_stride;
+    m.sl_dev = sig_len ? r.sl + lo : nullptr;
+    m.raw_ready = r.ev[k];
+    m.verdict_dev = r.verdict + lo;
+    m.async = true;
+    cg_batch* b = nullptr;
+    st = create_batch(ctx, hi - lo, scheme_id ? scheme_id + lo : nullptr, pk + lo * pk_stride, pk_stride,
+                      sig + lo * sig_stride, sig_stride, sig_len ? sig_len + lo : nullptr, m, &b);
+    if (b) r.batches.push_back(b);  // freed after the final sync
+    if (st == CG_OK) st = launch_verify(ctx, b, mode, /*join_streams=*/false);
+    if (st != CG_OK) return st;
+  }
+  if ((st = join_ecdsa_streams(ctx)) != CG_OK) return st;
+  CG_TRY(ctx, cg::launch_verdict_bitmap(r.verdict, (uint32_t)n, r.bitmap, ctx->stream), "launch bitmap");
+  return CG_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1048,12 +1229,41 @@ cg_status cg_verify_batch(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
   if (!ctx) return CG_E_INVALID_ARGUMENT;
   if (n && !verdict_out) return fail(ctx, CG_E_INVALID_ARGUMENT, "null verdict_out");
   if (n == 0) return CG_OK;
-  cg_batch* b = nullptr;
-  cg_status st = cg_batch_create(ctx, n, scheme_id, pk, pk_stride, sig, sig_stride, sig_len, msg, msg_bytes, msg_off,
-                                 msg_len, &b);
+  const std::vector<size_t> cb = verify_chunk_bounds(n);
+  if (cb.size() == 2) {  // one chunk: stage, then verify
+    cg_batch* b = nullptr;
+    cg_status st = cg_batch_create(ctx, n, scheme_id, pk, pk_stride, sig, sig_stride, sig_len, msg, msg_bytes,
+                                   msg_off, msg_len, &b);
+    if (st != CG_OK) return st;
+    st = cg_batch_verify(ctx, b, mode, verdict_out, accept_bitmap_out, nullptr);
+    cg_batch_destroy(ctx, b);
+    return st;
+  }
+  if (mode != CG_MODE_IS_VALID && mode != CG_MODE_DO_VERIFY) return fail(ctx, CG_E_INVALID_ARGUMENT, "bad mode");
+  MsgSrc m;
+  m.host = msg;
+  m.bytes = msg_bytes;
+  m.off_host = msg_off;
+  m.len_host = msg_len;
+  cg_status st = check_inputs(ctx, n, scheme_id, pk, pk_stride, sig, sig_stride, sig_len, m);
   if (st != CG_OK) return st;
-  st = cg_batch_verify(ctx, b, mode, verdict_out, accept_bitmap_out, nullptr);
-  cg_batch_destroy(ctx, b);
+  if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, CG_E_DEVICE, "hipSetDevice");
+  VerifyRun r;
+  struct RunGuard {  // also on an exception caught by CG_API_END (release is idempotent)
+    VerifyRun& r;
+    cg_ctx* c;
+    ~RunGuard() { r.release(c); }
+  } guard{r, ctx};
+  st = verify_pipeline(ctx, n, mode, scheme_id, pk, pk_stride, sig, sig_stride, sig_len, msg, msg_bytes, msg_off,
+                       msg_len, cb, r);
+  hipError_t e = hipSuccess;
+  if (st == CG_OK) e = hipMemcpyAsync(verdict_out, r.verdict, n, hipMemcpyDeviceToHost, ctx->stream);
+  if (st == CG_OK && e == hipSuccess && accept_bitmap_out)
+    e = hipMemcpyAsync(accept_bitmap_out, r.bitmap, (n + 31) / 32 * 4, hipMemcpyDeviceToHost, ctx->stream);
+  if (st == CG_OK && e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  if (st == CG_OK && e != hipSuccess) st = hip_fail(ctx, e, "download verdicts");
+  r.release(ctx);
+  collect_timings(ctx);
   return st;
   CG_API_END(ctx)
 }
@@ -1070,7 +1280,7 @@ cg_status cg_der_parse_batch(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, co
   if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, CG_E_DEVICE, "hipSetDevice");
   std::vector<uint32_t> idx[2];
   for (size_t i = 0; i < n; ++i)
-    idx[(scheme_id && scheme_id[i] == CG_SCHEME_ECDSA_SECP256K1_SHA256) ? 0 : 1].push_back((uint32_t)i);
+    idx[(scheme_id && (scheme_id[i] & 0x7F) == CG_SCHEME_ECDSA_SECP256K1_SHA256) ? 0 : 1].push_back((uint32_t)i);
   uint8_t* sig_d = nullptr;
   uint32_t *sl_d = nullptr, *rs_d = nullptr, *st_d = nullptr, *ix_d = nullptr;
   cg_status st = CG_OK;

@@ -38,6 +38,15 @@ __global__ __launch_bounds__(256) void k_gather_u64(const uint64_t* __restrict__
   dst[i] = src[idx ? idx[i] : i];
 }
 
+// verdict[idx[i]] = value for i < n (elements whose key the caller could not construct:
+// CG_KEY_INVALID, which outranks every verdict the verify kernels write later).
+__global__ __launch_bounds__(256) void k_fill_index(const uint32_t* __restrict__ idx, uint32_t n,
+                                                    uint8_t* __restrict__ verdict, uint8_t value) {
+  CG_WAVE_PRIO(2);
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) verdict[idx[i]] = value;
+}
+
 // accept bitmap: bit i%32 of word i/32 set iff verdict[i] == ACCEPT (0).
 __global__ __launch_bounds__(256) void k_verdict_bitmap(const uint8_t* __restrict__ verdict, uint32_t n,
                                                         uint32_t* __restrict__ bitmap) {
@@ -146,6 +155,12 @@ hipError_t launch_key_dedupe(const uint32_t* pk, uint32_t n, uint32_t cap, uint3
   hipLaunchKernelGGL(k_key_insert, grid_for(n), dim3(256), 0, s, pk, n, cap, table, tsize - 1, slot_of, owner_id,
                      counter, key_first);
   hipLaunchKernelGGL(k_key_lookup, grid_for(n), dim3(256), 0, s, slot_of, owner_id, n, key_index);
+  return hipGetLastError();
+}
+
+hipError_t launch_fill_index(const uint32_t* idx, uint32_t n, uint8_t* verdict, uint8_t value, hipStream_t s) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(k_fill_index, grid_for(n), dim3(256), 0, s, idx, n, verdict, value);
   return hipGetLastError();
 }
 

@@ -94,6 +94,38 @@ def allgather_bitmap(local_words, bounds: list[int], rank: int, group=None):
     return torch.cat([out[r][:words[r]] for r in range(world)])
 
 
+def gather_ordered(local_words, bounds: list[int], out=None, ordered=None, group=None):
+    """C1 for shards of any sizes in ONE collective: every rank contributes
+    ``words_max`` = the largest shard's word count (its own words zero-padded, as
+    ``all_gather_into_tensor`` needs equal pieces), then rank r's
+    ``ceil((b[r+1] - b[r]) / 32)`` words move to word ``b[r] / 32`` of the index-ordered
+    global bitmap (shards are 32-aligned, so words never straddle ranks).  When every
+    shard has ``words_max`` words the gathered buffer is already in index order and no
+    copy runs.  ``local_words``: int32 tensor of at least ``words_max`` words (the tail
+    past the rank's own words must be zero); ``out`` / ``ordered``: optional preallocated
+    buffers of ``world * words_max`` / ``ceil(n / 32)`` words.  Returns the global bitmap."""
+    import torch
+    import torch.distributed as dist
+    world = len(bounds) - 1
+    if any(x % 32 for x in bounds[1:-1]):
+        raise ValueError("shard boundaries must be multiples of 32")
+    words = [(bounds[r + 1] - bounds[r] + 31) // 32 for r in range(world)]
+    wmax = max(max(words), 1)
+    if local_words.numel() < wmax:
+        raise ValueError(f"local bitmap has {local_words.numel()} words, the largest shard needs {wmax}")
+    if out is None:
+        out = torch.empty(world * wmax, dtype=torch.int32, device=local_words.device)
+    dist.all_gather_into_tensor(out, local_words[:wmax].contiguous(), group=group)
+    total = (bounds[-1] + 31) // 32
+    if all(w == wmax for w in words[:-1]):
+        return out[:total]  # rank r's words already sit at r * wmax = b[r] / 32
+    if ordered is None:
+        ordered = torch.empty(total, dtype=torch.int32, device=local_words.device)
+    for r in range(world):
+        ordered[bounds[r] // 32:bounds[r] // 32 + words[r]] = out[r * wmax:r * wmax + words[r]]
+    return ordered
+
+
 def verify_sharded(ctx: _lib.Context, batch: PackedBatch, rank: int, world: int, mode: int = _lib.MODE_IS_VALID,
                    group=None):
     """Each rank verifies its shard of `batch` on its device and all ranks
@@ -123,9 +155,14 @@ class ShardBacklog:
     all-gather over RCCL.  Chunks bound the library's scratch (SURVEY 8d config 5:
     streamed in 2^24 pieces); the bitmap never leaves the device."""
 
-    def __init__(self, ctx: _lib.Context, chunks, words: int | None = None):
+    def __init__(self, ctx: _lib.Context, chunks, words: int | None = None, bounds: list[int] | None = None):
+        """``bounds``: the global 32-aligned shard boundaries (``shard_bounds``), so that
+        allgather returns the index-ordered global bitmap for any world size; ``words``
+        (default: the largest shard's word count from ``bounds``) sizes the local bitmap."""
         import torch
-        self.ctx = ctx
+        self.ctx, self.bounds = ctx, bounds
+        if bounds is not None:
+            words = max(words or 0, max((bounds[r + 1] - bounds[r] + 31) // 32 for r in range(len(bounds) - 1)))
         self.batches, self.sizes = [], []
         for b in chunks:
             if self.sizes and self.sizes[-1] % 32:
@@ -145,11 +182,14 @@ class ShardBacklog:
             off += (m + 31) // 32
         return self.bitmap
 
-    def allgather(self, out=None, group=None):
-        """C1: the ranks' bitmaps concatenated (equal word counts per rank: pass
-        `words` = the largest shard's word count when shards differ)."""
+    def allgather(self, out=None, ordered=None, group=None):
+        """C1: the global accept bitmap in index order (``gather_ordered`` over the
+        backlog's ``bounds``; without bounds, equal shards of ``words`` words each are
+        assumed and the gathered words are returned as they are)."""
         import torch
         import torch.distributed as dist
+        if self.bounds is not None:
+            return gather_ordered(self.bitmap, self.bounds, out, ordered, group)
         world = dist.get_world_size(group)
         if out is None:
             out = torch.zeros(self.words * world, dtype=torch.int32, device=self.bitmap.device)

@@ -24,7 +24,7 @@ from typing import Sequence
 import numpy as np
 
 from . import _lib
-from .crypto import IllegalArgumentException, SignatureException, _check_key_length, _scheme_id, raise_for_verdict
+from .crypto import IllegalArgumentException, SignatureException, _scheme_id, pack_key_row, raise_for_verdict
 
 
 class MerkleTreeException(Exception):
@@ -82,8 +82,9 @@ def _pack_sigs(stxs: Sequence[SignedTx]):
     sig = np.zeros((max(n_sig, 1), sig_stride), dtype=np.uint8)
     sig_len = np.zeros(max(n_sig, 1), dtype=np.uint32)
     for i, (sch, k, s) in enumerate(flat):
-        _check_key_length(_scheme_id(sch), k)
-        pk[i, :len(k)] = np.frombuffer(bytes(k)[:64], dtype=np.uint8)
+        # a wrong-length key is KEY_INVALID for that signature alone (flagged in its scheme
+        # id), so the first failing signature in tx order still decides the exception
+        pack_key_row(pk, scheme, i, k)
         sig[i, :len(s)] = np.frombuffer(bytes(s), dtype=np.uint8)
         sig_len[i] = len(s)
     return sig_start, scheme, pk, sig, sig_stride, sig_len, n_sig

@@ -73,7 +73,7 @@
 extern "C" {
 #endif
 
-#define CG_ABI_VERSION 2
+#define CG_ABI_VERSION 3
 
 typedef int32_t cg_status;
 enum {
@@ -102,6 +102,12 @@ enum {
   CG_SCHEME_ECDSA_SECP256R1_SHA256 = 3,
   CG_SCHEME_EDDSA_ED25519_SHA512 = 4,
 };
+/* OR-ed into an element's scheme id by a caller that could not construct the element's
+ * PublicKey from its wire bytes (wrong length, undecodable X.509 SubjectPublicKeyInfo:
+ * Crypto.decodePublicKey throws, Crypto.kt:320-355, before any verify call).  The
+ * element's verdict is CG_KEY_INVALID on every path (verify, prepared batch, tx) and
+ * its key / signature rows are never read.  Scheme id 0x80 | s for any s. */
+enum { CG_SCHEME_FLAG_KEY_INVALID = 0x80 };
 
 typedef struct cg_ctx cg_ctx;
 typedef struct cg_batch cg_batch;
@@ -118,7 +124,8 @@ const char* cg_last_error(const cg_ctx* ctx);
 
 /*
  * Signature batch input (host memory, element-major; caller-owned):
- *   scheme_id  n bytes (NULL: every element is CG_SCHEME_EDDSA_ED25519_SHA512)
+ *   scheme_id  n bytes (NULL: every element is CG_SCHEME_EDDSA_ED25519_SHA512); a scheme id
+ *              with CG_SCHEME_FLAG_KEY_INVALID set gives that element CG_KEY_INVALID
  *   pk         n * pk_stride bytes.  Ed25519: the 32-byte key A as carried on the wire
  *              (Kryo Ed25519PublicKeySerializer, Kryo.kt:330-340).  ECDSA: 64 bytes X||Y,
  *              big-endian affine coordinates decoded from the X.509 SubjectPublicKeyInfo by the

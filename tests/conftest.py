@@ -77,3 +77,45 @@ def gpu_ctx():
     ctx = Context(int(os.environ.get("LOCAL_RANK", "0")))
     yield ctx
     ctx.close()
+
+
+def _der_with(r: int, s: int, pad_r: bool = False) -> bytes:
+    def integer(v, pad=False):
+        b = v.to_bytes(max(1, (v.bit_length() + 8) // 8), "big")  # minimal two's complement (v >= 0)
+        if pad:
+            b = b"\0" + b
+        return b"\x02" + bytes([len(b)]) + b
+    body = integer(r, pad_r) + integer(s)
+    return b"\x30" + bytes([len(body)]) + body
+
+
+@pytest.fixture(scope="session")
+def ref_cert_cases():
+    """The reference's own BC-signed certificate signatures (tests/golden/ref_cert_vectors.json,
+    extracted by make_ref_cert_vectors.py) plus mutants derived from each: TBS bit flip, sig[0]++
+    (CryptoUtilsTest.kt's corruption), high-S (n - s, BC has no low-S rule), r + n, a non-minimal
+    r INTEGER, an empty message and the key presented under the other curve's scheme.  Each case:
+    dict(cls, scheme, q (hex X||Y), sig, msg)."""
+    import ecdsa_bc as EC
+    rows = load_golden("ref_cert_vectors.json")["rows"]
+    out = []
+    for r in rows:
+        sig, msg = bytes.fromhex(r["sig"]), bytes.fromhex(r["msg"])
+        base = dict(scheme=r["scheme"], q=r["q"])
+        out.append(dict(base, cls=r["cls"], sig=sig, msg=msg))
+        if r["cls"] != "ref_cert":
+            continue
+        n = EC.CURVES[r["scheme"]].n
+        rr, ss = EC.der_decode(sig)
+        flip = bytearray(msg)
+        flip[len(flip) // 2] ^= 0x10
+        bump = bytearray(sig)
+        bump[0] = (bump[0] + 1) & 0xFF
+        out += [dict(base, cls="ref_tbs_flip", sig=sig, msg=bytes(flip)),
+                dict(base, cls="ref_sig0_inc", sig=bytes(bump), msg=msg),
+                dict(base, cls="ref_high_s", sig=_der_with(rr, n - ss), msg=msg),
+                dict(base, cls="ref_r_plus_n", sig=_der_with(rr + n, ss), msg=msg),
+                dict(base, cls="ref_nonminimal_r", sig=_der_with(rr, ss, pad_r=True), msg=msg),
+                dict(base, cls="ref_empty_msg", sig=sig, msg=b""),
+                dict(base, cls="ref_other_curve", scheme=5 - r["scheme"], sig=sig, msg=msg)]
+    return out

@@ -79,3 +79,22 @@ def test_pmc_report_hash_matches_bench_hash():
     import bench
     import pmc_report
     assert pmc_report.src_identity()[1] == bench.kernel_src_hash()
+
+
+@pytest.mark.parametrize("n,batch", [(8, None), (3, 1000003), (7, None)])
+def test_backlog_dry_run_config5_shards(n, batch):
+    """Config 5's C1 at the driver's rank counts: 100 M signatures (default) split into
+    32-aligned shards — even at 8 ranks, uneven at 3 and 7 — each rank's bitmap gathered
+    with corda_amd.dist.gather_ordered (ShardBacklog.allgather's collective) over gloo; rank
+    0 checks the global bitmap is in index order, bit for bit."""
+    args = ["--gpus", str(n), "--dry-run", "--workload", "backlog", "--steps", "2", "--warmup", "1"]
+    if batch:
+        args += ["--batch", str(batch)]
+    r = _run(args, _env(), timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")][-1]
+    assert line["n_gpus"] == n and line["config"]["global_batch"] == (batch or 100_000_000)
+    assert sum(line["config"]["shard_elements"]) == (batch or 100_000_000)
+    if n != 8:
+        assert len(set(line["config"]["shard_elements"])) > 1  # really uneven
+    assert line["checks"]["bitmap_matches"] is True

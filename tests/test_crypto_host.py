@@ -39,7 +39,8 @@ def test_exception_mapping(code, exc):
 
 
 def test_mixed_scheme_pack():
-    b = crypto.pack([2, 3, 4], [b"\0" * 64] * 3, [b"\x30\x06\x02\x01\x01\x02\x01\x01", b"", b"\0" * 64], [b"a"] * 3)
+    b = crypto.pack([2, 3, 4], [b"\0" * 64] * 2 + [b"\0" * 32], [b"\x30\x06\x02\x01\x01\x02\x01\x01", b"", b"\0" * 64],
+                    [b"a"] * 3)
     assert list(b.scheme) == [2, 3, 4]
     assert np.array_equal(b.sig_len, [8, 0, 64])
 
@@ -49,7 +50,13 @@ def test_wrong_length_keys_are_key_invalid_not_truncated():
     verdict is KEY_INVALID (never verified as a truncated / zero-padded key)."""
     b = crypto.pack([4, 4, 4, 3], [b"\1" * 31, b"\1" * 33, b"\1" * 32, b"\2" * 65], [b"\3" * 64] * 4, [b"m"] * 4)
     assert list(b.key_invalid) == [0, 1, 3]
+    # flagged in the scheme id, so the library reports KEY_INVALID on every path
+    # (verify, prepared batches and their device bitmaps, shards, transactions)
+    assert list(b.scheme) == [4 | 0x80, 4 | 0x80, 4, 3 | 0x80]
     assert not b.pk[0].any() and not b.pk[1].any() and not b.pk[3].any()
+    from corda_amd import dist as D
+    sh = D.slice_batch(b, 1, 4)
+    assert list(sh.scheme) == [4 | 0x80, 4, 3 | 0x80]
     assert crypto.key_length_ok(4, b"x" * 32) and not crypto.key_length_ok(2, b"x" * 32)
 
 
@@ -121,3 +128,29 @@ def test_transaction_signature_mirrors(monkeypatch):
     assert ei.value.index == 1
     with pytest.raises(ValueError):
         S.do_verify_transaction_signatures(None, [ka], [ts, ts])
+
+
+def test_host_scheme_keys_of_any_length(monkeypatch):
+    """RSA / SPHINCS keys are long (X.509 SPKI of a 2048-bit RSA key ~294 B, SPHINCS-256
+    ~1 KB): the device never reads their rows, so pack() leaves them empty instead of
+    failing to fit them into the 64-byte row, and host_verify gets the full key bytes."""
+    rsa, sphincs = b"R" * 294, b"S" * 1056
+    b = crypto.pack([1, 5, 4], [rsa, sphincs, b"\1" * 32], [b"s"] * 3, [b"m"] * 3)
+    assert b.key_invalid is None and list(b.scheme) == [1, 5, 4] and not b.pk[:2].any()
+    monkeypatch.setattr(crypto, "verify_packed", lambda ctx, bb, mode: np.full(bb.n, UNSUPPORTED, np.uint8))
+    seen = []
+
+    def host_verify(sid, key, sig, data, mode):
+        seen.append((sid, len(key)))
+        return ACCEPT
+    v = crypto._verify_mixed(None, [1, 5, 4], [rsa, sphincs, b"\1" * 32], [b"s"] * 3, [b"m"] * 3, 0, host_verify)
+    assert seen == [(1, 294), (5, 1056)] and v.tolist() == [ACCEPT, ACCEPT, UNSUPPORTED]
+
+
+def test_tx_pack_flags_wrong_length_keys_per_signature():
+    """A wrong-length key makes only its own signature KEY_INVALID (no batch-wide raise),
+    so the first failing signature in tx order still decides the exception."""
+    from corda_amd import transactions as T
+    stx = T.SignedTx(T.WireTx([b"c"], bytes(32)), [(4, b"\1" * 32, b"s" * 64), (4, b"\1" * 31, b"s" * 64)])
+    sig_start, scheme, pk, sig, sig_stride, sig_len, n_sig = T._pack_sigs([stx])
+    assert n_sig == 2 and list(scheme) == [4, 4 | 0x80] and not pk[1].any()

@@ -115,3 +115,45 @@ def test_cost_weighted_shards_balance_mixed_batches():
         assert counts[-1] < counts[0]  # the ECDSA-heavy tail gets fewer elements
     same = np.full(10_000, 4, np.uint8)
     assert D.shard_bounds_weighted(same, 4) == D.shard_bounds(10_000, 4)
+
+
+def _gather_worker(rank, world, port, total, q):
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, ROOT)
+    from corda_amd import dist as D
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        rng = np.random.default_rng(11)
+        accept = rng.random(total) < 0.9  # the same global verdicts on every rank
+        bounds = D.shard_bounds(total, world)
+        lo, hi = bounds[rank], bounds[rank + 1]
+        wmax = max((bounds[r + 1] - bounds[r] + 31) // 32 for r in range(world))
+        local = torch.zeros(wmax + 3, dtype=torch.int32)  # longer than needed, like a padded device bitmap
+        mine = D.pack_bits(accept[lo:hi]).view(np.int32)
+        local[:len(mine)] = torch.from_numpy(mine.copy())
+        glob = D.gather_ordered(local, bounds)
+        q.put((rank, bool(np.array_equal(glob.numpy(), D.pack_bits(accept).view(np.int32)))))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,total", [(3, 100_003), (3, 96), (2, 33)])
+def test_gather_ordered_uneven_shards(world, total):
+    """ShardBacklog.allgather's collective (dist.gather_ordered) at world 3 with uneven
+    32-aligned shards: one all_gather_into_tensor of equal padded pieces, then every rank's
+    words moved to word bounds[r]/32 — the global bitmap equals pack_bits of the global
+    verdicts on every rank."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_worker, args=(r, world, port, total, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(180)
+    assert all(p.exitcode == 0 for p in procs)
+    res = sorted(q.get(timeout=5) for _ in range(world))
+    assert res == [(r, True) for r in range(world)]

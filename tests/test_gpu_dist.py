@@ -71,3 +71,49 @@ def test_backlog_chunks_into_one_device_bitmap_world1(gpu_ctx, oracle):
         bl.close()
     finally:
         dist.destroy_process_group()
+
+
+def test_wrong_length_keys_stay_key_invalid_on_every_path(gpu_ctx, oracle):
+    """Keys of the wrong length (31 / 33 bytes) cannot be PublicKey objects: pack() flags
+    them in the scheme id (CG_SCHEME_FLAG_KEY_INVALID) and the library reports KEY_INVALID
+    for them on every path — verify_packed and its bitmap, a PreparedBatch (host verdicts
+    and the device bitmap), and verify_sharded over RCCL — with several of them in one
+    32-element bitmap word, and never verifies them against a zero key."""
+    import torch
+    import torch.distributed as dist
+    import datagen
+    from corda_amd import crypto
+    from corda_amd import dist as D
+    from corda_amd._lib import KEY_INVALID, MODE_DO_VERIFY, MODE_IS_VALID
+    from test_gpu_ed25519 import oracle_verdicts
+    w = datagen.add_ed25519_adversarial(datagen.make_batch(300, msg_bytes=50, seed=91, key_base=9100), 0.1, seed=3)
+    keys = [bytes(w.pk[i, :32]) for i in range(w.n)]
+    bad = [0, 1, 3, 31, 40, 299]
+    for j, i in enumerate(bad):
+        keys[i] = keys[i][:31] if j % 2 == 0 else keys[i] + b"\0"
+    sigs = [bytes(w.sig[i, :w.sig_len[i]]) for i in range(w.n)]
+    msgs = [bytes(w.msg[w.msg_off[i]:w.msg_off[i] + w.msg_len[i]]) for i in range(w.n)]
+    b = crypto.pack(crypto.EDDSA_ED25519_SHA512, keys, sigs, msgs)
+    for mode in (MODE_IS_VALID, MODE_DO_VERIFY):
+        exp = oracle_verdicts(oracle, w, mode)
+        exp[bad] = KEY_INVALID
+        v, bm = crypto.verify_packed(gpu_ctx, b, mode, bitmap=True)
+        assert np.array_equal(v, exp)
+        assert np.array_equal(bm.view(np.int32), D.pack_bits(exp == 0).view(np.int32))
+        pb = crypto.PreparedBatch(gpu_ctx, b)
+        dev = torch.zeros((w.n + 31) // 32, dtype=torch.int32, device=f"cuda:{gpu_ctx.device}")
+        assert np.array_equal(pb.verify(mode, device_bitmap_ptr=dev.data_ptr()), exp)
+        assert np.array_equal(dev.cpu().numpy(), D.pack_bits(exp == 0).view(np.int32))
+        pb.close()
+    s = socket.socket(); s.bind(("127.0.0.1", 0)); port = s.getsockname()[1]; s.close()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(gpu_ctx.device)
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    try:
+        exp = oracle_verdicts(oracle, w, MODE_IS_VALID)
+        exp[bad] = KEY_INVALID
+        v, glob, _ = D.verify_sharded(gpu_ctx, b, 0, 1)
+        assert np.array_equal(v, exp)
+        assert np.array_equal(glob.cpu().numpy(), D.pack_bits(exp == 0).view(np.int32))
+    finally:
+        dist.destroy_process_group()

@@ -174,9 +174,71 @@ def test_prepared_batch_reparses_der_every_verify(gpu_ctx, oracle, golden_ecdsa)
         try:
             for mode in (MODE_IS_VALID, MODE_DO_VERIFY, MODE_IS_VALID):
                 got, exp = pb.verify(mode), exp_of(mode)
-                if b.key_invalid is not None:  # host-side key-length rule, as verify_packed applies it
-                    got[b.key_invalid] = crypto.KEY_INVALID
                 bad = np.flatnonzero(got != exp)
                 assert bad.size == 0, [(int(i), int(got[i]), int(exp[i])) for i in bad[:10]]
         finally:
             pb.close()
+
+
+def test_reference_certificate_signatures(gpu_ctx, oracle, ref_cert_cases):
+    """The reference's own BC-signed ecdsa-with-SHA256 certificates (dev CA / sample
+    keystores; tests/golden/ref_cert_vectors.json) and their mutants through
+    cg_verify_batch in both modes, and the K4 DER pre-pass on their signature rows:
+    the device gives the verdicts the structure implies (test_oracle.REF_EXPECT), which
+    the oracle and OpenSSL also give.  The rows are also tiled 300× into one batch with
+    mutated random K1/R1 signatures, so they sit in every lane position of a wave."""
+    from test_oracle import REF_EXPECT
+    cases = ref_cert_cases
+    b = crypto.pack([c["scheme"] for c in cases], [bytes.fromhex(c["q"]) for c in cases], [c["sig"] for c in cases],
+                    [c["msg"] for c in cases])
+    for mode in (MODE_IS_VALID, MODE_DO_VERIFY):
+        v = crypto.verify_packed(gpu_ctx, b, mode)
+        exp = np.array([REF_EXPECT[c["cls"]][mode] for c in cases], np.uint8)
+        bad = np.flatnonzero(v != exp)
+        assert bad.size == 0, [(cases[i]["cls"], cases[i]["scheme"], int(v[i]), int(exp[i])) for i in bad]
+    # K4 alone: the reference rows parse to the oracle's (r, s); the malformed mutants fail
+    sigs = [c["sig"] for c in cases]
+    stride = (max(len(s) for s in sigs) + 3) // 4 * 4
+    buf = np.zeros((len(sigs), stride), np.uint8)
+    sl = np.array([len(s) for s in sigs], np.uint32)
+    for i, s in enumerate(sigs):
+        buf[i, :len(s)] = np.frombuffer(s, np.uint8)
+    sch = np.array([c["scheme"] for c in cases], np.uint8)
+    rs, st = np.zeros((len(sigs), 64), np.uint8), np.zeros(len(sigs), np.uint8)
+    gpu_ctx.check(gpu_ctx.lib.cg_der_parse_batch(gpu_ctx.h, len(sigs), ptr(sch), ptr(buf), stride, ptr(sl), ptr(rs),
+                                                 ptr(st)))
+    oracle.oracle_der_decode.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p,
+                                         ctypes.c_char_p, ctypes.POINTER(ctypes.c_int)]
+    for i, s in enumerate(sigs):
+        r, ss, fl = ctypes.create_string_buffer(32), ctypes.create_string_buffer(32), ctypes.c_int()
+        rc = oracle.oracle_der_decode(int(sch[i]), s, len(s), r, ss, ctypes.byref(fl))
+        assert (st[i] == 2) == (rc != 0) == (cases[i]["cls"] in ("ref_sig0_inc", "ref_nonminimal_r")), cases[i]["cls"]
+        if rc == 0:
+            assert st[i] == (1 if fl.value else 0), cases[i]["cls"]
+            if not fl.value:
+                assert bytes(rs[i]) == r.raw + ss.raw, cases[i]["cls"]
+    # tiled among random mutated ECDSA signatures
+    rep = 300
+    w = datagen.add_ecdsa_adversarial(datagen.make_batch(4000, msg_bytes=300, scheme=np.array([2, 3] * 2000, np.uint8),
+                                                         seed=41, key_base=410_000), frac=0.3, seed=17)
+    pos = np.random.default_rng(5).permutation(w.n + rep * len(cases))
+    all_s, all_q, all_sig, all_m = [], [], [], []
+    for j in range(w.n):
+        all_s.append(int(w.scheme[j]))
+        all_q.append(bytes(w.pk[j, :64]))
+        all_sig.append(bytes(w.sig[j, :w.sig_len[j]]))
+        all_m.append(bytes(w.msg[w.msg_off[j]:w.msg_off[j] + w.msg_len[j]]))
+    for _ in range(rep):
+        for c in cases:
+            all_s.append(c["scheme"])
+            all_q.append(bytes.fromhex(c["q"]))
+            all_sig.append(c["sig"])
+            all_m.append(c["msg"])
+    order = np.argsort(pos)
+    bt = crypto.pack([all_s[i] for i in order], [all_q[i] for i in order], [all_sig[i] for i in order],
+                     [all_m[i] for i in order])
+    for mode in (MODE_IS_VALID, MODE_DO_VERIFY):
+        got = crypto.verify_packed(gpu_ctx, bt, mode)
+        exp_r = oracle_verdicts(oracle, w, mode)
+        exp = np.concatenate([exp_r, np.tile(np.array([REF_EXPECT[c["cls"]][mode] for c in cases], np.uint8), rep)])
+        assert np.array_equal(got, exp[order])

@@ -130,17 +130,23 @@ def test_do_verify_batch_raises_like_loop(gpu_ctx, golden_ed25519):
 
 
 def test_config2_scale_properties(gpu_ctx, oracle):
-    """1M Ed25519, 1 KB messages, 1% adversarial: untouched elements all accept and
-    the adversarial subset matches the oracle element-wise."""
+    """BASELINE config 2 exactly as bench.py builds it on rank 0 (1M Ed25519, 1 KB
+    messages, distinct keys with every 4,096th one a reference test key
+    entropyToKeyPair(20..110), 1% adversarial over E1-E12), verified from host buffers
+    (cg_verify_batch's chunked upload pipeline): untouched elements all accept; the
+    adversarial subset and every reference-test-key element match the oracle
+    element-wise."""
     n = 1 << 20
-    w = datagen.make_batch(n, msg_bytes=1024, seed=42, key_base=0)
+    w = datagen.make_batch(n, msg_bytes=1024, seed=42, key_base=0, ref_seed_stride=4096)
     w = datagen.add_ed25519_adversarial(w, frac=0.01, seed=1)
     got = gpu_verdicts(gpu_ctx, w, MODE_IS_VALID)
     adv = np.array([c != "valid" for c in w.classes])
     assert (got[~adv] == ACCEPT).all()
-    sub = w.subset(np.flatnonzero(adv))
-    exp = oracle_verdicts(oracle, sub, MODE_IS_VALID)
-    assert np.array_equal(got[adv], exp)
+    ref = np.arange(0, n, 4096)
+    check = np.union1d(np.flatnonzero(adv), ref)
+    exp = oracle_verdicts(oracle, w.subset(check), MODE_IS_VALID)
+    assert np.array_equal(got[check], exp)
+    assert ref.size == 256 and (got[ref] == ACCEPT).sum() >= 250
 
 
 def test_reference_message_shapes_all_schemes(gpu_ctx, oracle):
@@ -279,3 +285,62 @@ def test_key_reuse_prepared_batch_bitmap(gpu_ctx, oracle, key_reuse):
     assert (gpu_verdicts(gpu_ctx, d, MODE_IS_VALID) == ACCEPT).all()
     assert np.array_equal(pb.verify(MODE_IS_VALID), exp)
     pb.close()
+
+
+@pytest.mark.parametrize("chunks,min_chunk,tail", [("9", "700", "0.3"), ("3", "1", "1.0")])
+def test_host_verify_pipeline_small_chunks_vs_oracle(gpu_ctx, oracle, monkeypatch, chunks, min_chunk, tail):
+    """cg_verify_batch's pipeline (chunk k's upload on the copy stream beside chunk k-1's
+    kernels) forced onto small, ragged chunks: a mixed batch — Ed25519 from distinct and
+    from 12 repeated signers (the key-reuse path inside a chunk), secp256k1, P-256, an
+    unsupported scheme id and wrong-length keys — whose arena is packed in REVERSE element
+    order (the first chunk's messages sit at the end, so its prefix is the whole arena),
+    in both modes, verdicts and accept bitmap against the oracle."""
+    from corda_amd import dist as D
+    from corda_amd._lib import KEY_INVALID, UNSUPPORTED
+    monkeypatch.setenv("CORDA_AMD_VERIFY_CHUNKS", chunks)
+    monkeypatch.setenv("CORDA_AMD_VERIFY_MIN_CHUNK", min_chunk)
+    monkeypatch.setenv("CORDA_AMD_VERIFY_TAIL", tail)
+    sch = np.random.default_rng(12).choice(np.array([2, 3, 4, 4, 4], np.uint8), size=5200)
+    w = datagen.make_batch(len(sch), msg_bytes=70, scheme=sch, seed=23, key_base=620_000)
+    w = datagen.add_ecdsa_adversarial(w, frac=0.2, seed=4)
+    reuse = datagen.add_ed25519_adversarial(datagen.make_batch(1400, msg_bytes=33, seed=29, key_base=640_000,
+                                                               key_reuse=12), frac=0.2, seed=6)
+    ed = datagen.add_ed25519_adversarial(datagen.make_batch(1500, msg_bytes=120, seed=31, key_base=650_000),
+                                         frac=0.2, seed=8)
+    parts = [w, reuse, ed]
+    keys, sigs, msgs, schemes = [], [], [], []
+    for p in parts:
+        for i in range(p.n):
+            s = int(p.scheme[i])
+            keys.append(bytes(p.pk[i, :64 if s in (2, 3) else 32]))
+            sigs.append(bytes(p.sig[i, :p.sig_len[i]]))
+            msgs.append(bytes(p.msg[p.msg_off[i]:p.msg_off[i] + p.msg_len[i]]))
+            schemes.append(s)
+    n = len(keys)
+    bad_key = list(range(5, n, 997))
+    for i in bad_key:
+        keys[i] = keys[i][:-1]
+    unsup = list(range(11, n, 1301))
+    for i in unsup:
+        schemes[i] = 9
+    b = crypto.pack(schemes, keys, sigs, msgs)
+    # reverse the arena: element i's message moves to the mirrored position
+    ln = b.msg_len[:n].astype(np.uint64)
+    new_off = np.zeros(n, np.uint64)
+    new_off[::-1] = np.concatenate([[0], np.cumsum(ln[::-1])[:-1]]).astype(np.uint64)
+    arena = np.zeros(len(b.msg) + 1, np.uint8)
+    for i in range(n):
+        arena[int(new_off[i]):int(new_off[i] + ln[i])] = b.msg[int(b.msg_off[i]):int(b.msg_off[i] + ln[i])]
+    b2 = crypto.PackedBatch(n, b.scheme, b.pk, b.pk_stride, b.sig, b.sig_stride, b.sig_len, arena, new_off,
+                            b.msg_len)
+    oracle_w = datagen.Workload(n, b.scheme & 0x7F, b.pk, b.pk_stride, b.sig, b.sig_stride, b.sig_len, arena,
+                                new_off, b.msg_len)
+    for mode in (MODE_IS_VALID, MODE_DO_VERIFY):
+        exp = oracle_verdicts(oracle, oracle_w, mode)
+        exp[bad_key] = KEY_INVALID
+        exp[unsup] = UNSUPPORTED
+        got, bm = crypto.verify_packed(gpu_ctx, b2, mode, bitmap=True)
+        bad = np.flatnonzero(got != exp)
+        assert bad.size == 0, [(int(i), int(schemes[i]), int(got[i]), int(exp[i])) for i in bad[:10]]
+        assert np.array_equal(bm.view(np.int32), D.pack_bits(exp == ACCEPT).view(np.int32))
+    assert (exp == ACCEPT).sum() > 0.6 * n

@@ -222,3 +222,29 @@ def test_partial_merkle_build_like_reference():
     # the post-order program round-trips through the oracle's decoder
     t = MK.pmt_build(mt, [hashed[1], hashed[4]])
     assert MK.pmt_postorder(MK.pmt_from_postorder(MK.pmt_postorder(t))) == MK.pmt_postorder(t)
+
+
+REF_EXPECT = {"ref_cert": (0, 0), "ref_cert_wrong_issuer": (1, 1), "ref_tbs_flip": (1, 1), "ref_sig0_inc": (2, 2),
+              "ref_high_s": (0, 0), "ref_r_plus_n": (1, 1), "ref_nonminimal_r": (2, 2), "ref_empty_msg": (1, 4),
+              "ref_other_curve": (3, 3)}
+
+
+def test_ecdsa_reference_certificates(oracle, ref_cert_cases):
+    """The ECDSA oracle pinned by the reference's own signatures: the BC-signed dev CA /
+    sample certificates (Crypto.isValid(scheme, issuerKey, sig, tbs), Crypto.kt:534-541)
+    accept in the C restatement and the Python twin; every mutant gets the verdict its
+    structure implies (is_valid, do_verify), and OpenSSL agrees wherever it has an opinion
+    (everything except the malformed-DER and empty-message rows)."""
+    rows = [c for c in ref_cert_cases if c["cls"] == "ref_cert"]
+    assert len(rows) >= 6 and {c["scheme"] for c in rows} == {2, 3}
+    for c in ref_cert_cases:
+        q = bytes.fromhex(c["q"])
+        exp = REF_EXPECT[c["cls"]]
+        got_c = tuple(oracle.oracle_ecdsa_verify(c["scheme"], q, c["sig"], len(c["sig"]), c["msg"], len(c["msg"]), m)
+                      for m in (0, 1))
+        qi = (int.from_bytes(q[:32], "big"), int.from_bytes(q[32:], "big"))
+        got_py = (EC.is_valid(c["scheme"], qi, c["sig"], c["msg"]), EC.do_verify(c["scheme"], qi, c["sig"], c["msg"]))
+        assert got_c == exp and got_py == exp, (c["cls"], got_c, got_py)
+        if c["cls"] not in ("ref_sig0_inc", "ref_nonminimal_r", "ref_empty_msg"):
+            assert OSSL.ecdsa_verify(c["scheme"], q, c["sig"], hashlib.sha256(c["msg"]).digest()) == (exp[0] == 0), \
+                c["cls"]
