@@ -13,6 +13,7 @@
 // host and checks it against the oracle.
 #pragma once
 #include "cg_common.h"
+#include "cg_fe_asm.h"
 
 namespace cg {
 
@@ -164,6 +165,61 @@ CG_HD int64_t fe_pin64(int64_t x) {
   return x;
 }
 
+// acc + a * b as one v_mad_i64_i32 kept in the chain's order.
+CG_HD int64_t fe_mad(int64_t acc, int32_t a, int32_t b) { return fe_pin64(acc + (int64_t)a * b); }
+
+// CG_FE_ASM_COL = 1: every column of a product (or of 2 / 3 interleaved products) is one
+// inline-asm statement of v_mad_i64_i32 (cg_fe_asm.h, generated by tools/gen_fe_asm.py).
+// With the per-mad barrier above, LLVM pads each read of a barrier-defined register by
+// the very next VALU instruction with an s_nop (an asm might be a transcendental op):
+// ~500 s_nops in the MSM kernel, none inside a column statement.
+#ifndef CG_FE_ASM_COL
+#define CG_FE_ASM_COL 1
+#endif
+
+template <typename Op>
+CG_HD FeColOps fe_col_ops(const Op& op, int k) {
+  FeColOps x;
+  x.n = 0;
+  CG_UNROLL for (int i = 0; i < 10; ++i) {
+    if (op.has(k, i)) {
+      x.a[x.n] = op.a(k, i);
+      x.b[x.n] = op.b(k, i);
+      ++x.n;
+    }
+  }
+  return x;
+}
+// One column of 1 / 2 / 3 chains as one asm statement; false when no generated shape
+// fits (the caller then runs the C chain).  n is a compile-time constant here.
+CG_HD bool fe_col_asm(int64_t& c0, const FeColOps& x0) {
+#if defined(__HIP_DEVICE_COMPILE__) && CG_FE_ASM_COL
+  if (x0.n == 10) return fe_asm_col1_10(c0, x0), true;
+  if (x0.n == 6) return fe_asm_col1_6(c0, x0), true;
+  if (x0.n == 5) return fe_asm_col1_5(c0, x0), true;
+#endif
+  (void)c0;
+  (void)x0;
+  return false;
+}
+CG_HD bool fe_col_asm(int64_t& c0, const FeColOps& x0, int64_t& c1, const FeColOps& x1) {
+#if defined(__HIP_DEVICE_COMPILE__) && CG_FE_ASM_COL
+  if (x0.n == 10 && x1.n == 10) return fe_asm_col2_10(c0, c1, x0, x1), true;
+  if (x0.n == 6 && x1.n == 6) return fe_asm_col2_6(c0, c1, x0, x1), true;
+  if (x0.n == 5 && x1.n == 5) return fe_asm_col2_5(c0, c1, x0, x1), true;
+#endif
+  (void)c0, (void)x0, (void)c1, (void)x1;
+  return false;
+}
+CG_HD bool fe_col_asm(int64_t& c0, const FeColOps& x0, int64_t& c1, const FeColOps& x1, int64_t& c2,
+                      const FeColOps& x2) {
+#if defined(__HIP_DEVICE_COMPILE__) && CG_FE_ASM_COL
+  if (x0.n == 10 && x1.n == 10 && x2.n == 10) return fe_asm_col3_10(c0, c1, c2, x0, x1, x2), true;
+#endif
+  (void)c0, (void)x0, (void)c1, (void)x1, (void)c2, (void)x2;
+  return false;
+}
+
 // ---------------------------------------------------------------------------
 // Products.  A product is ten column chains of v_mad_i64_i32 (column k collects
 // f_i g_j for i + j = k, and 19 f_i g_j for i + j = k + 10; products of two odd
@@ -236,7 +292,7 @@ struct FeMulOp {
     return (i + j >= 10) ? g19[j] : g[j];
   }
   CG_HDM bool has(int, int) const { return true; }
-  CG_HDM int64_t operator()(int k, int i, int64_t acc) const { return fe_pin64(acc + (int64_t)a(k, i) * b(k, i)); }
+  CG_HDM int64_t operator()(int k, int i, int64_t acc) const { return fe_mad(acc, a(k, i), b(k, i)); }
 };
 // f^2 (SCALE = 2: 2 f^2, by doubling the limb multipliers: 8 f_i for the odd limbs).
 template <bool FLOOR, int SCALE = 1>
@@ -267,7 +323,7 @@ struct FeSqOp {
   }
   CG_HDM int64_t operator()(int k, int n, int64_t acc) const {
     if (!has(k, n)) return acc;
-    return fe_pin64(acc + (int64_t)a(k, n) * b(k, n));
+    return fe_mad(acc, a(k, n), b(k, n));
   }
 };
 
@@ -303,7 +359,9 @@ CG_HD void fe_fold_chain(fe& h, const Op& op) {
   s.c = 0;
   CG_UNROLL for (int k = 0; k < 10; ++k) {
     s.acc = s.c;
-    CG_UNROLL for (int i = 0; i < 10; ++i) s.acc = op(k, i, s.acc);
+    if (!fe_col_asm(s.acc, fe_col_ops(op, k))) {
+      CG_UNROLL for (int i = 0; i < 10; ++i) s.acc = op(k, i, s.acc);
+    }
     fe_fold_carry<Op::kFloor>(s, k);
   }
   fe_fold_finish<Op::kFloor>(h, s);
@@ -319,9 +377,11 @@ CG_HD void fe_fold_pair(fe& h0, const Op0& op0, fe& h1, const Op1& op1) {
   CG_UNROLL for (int k = 0; k < 10; ++k) {
     s0.acc = s0.c;
     s1.acc = s1.c;
-    CG_UNROLL for (int i = 0; i < 10; ++i) {
-      s0.acc = op0(k, i, s0.acc);
-      s1.acc = op1(k, i, s1.acc);
+    if (!fe_col_asm(s0.acc, fe_col_ops(op0, k), s1.acc, fe_col_ops(op1, k))) {
+      CG_UNROLL for (int i = 0; i < 10; ++i) {
+        s0.acc = op0(k, i, s0.acc);
+        s1.acc = op1(k, i, s1.acc);
+      }
     }
     fe_fold_carry<Op0::kFloor>(s0, k);
     fe_fold_carry<Op1::kFloor>(s1, k);
@@ -340,10 +400,12 @@ CG_HD void fe_fold_triple(fe& h0, const Op0& op0, fe& h1, const Op1& op1, fe& h2
     s0.acc = s0.c;
     s1.acc = s1.c;
     s2.acc = s2.c;
-    CG_UNROLL for (int i = 0; i < 10; ++i) {
-      s0.acc = op0(k, i, s0.acc);
-      s1.acc = op1(k, i, s1.acc);
-      s2.acc = op2(k, i, s2.acc);
+    if (!fe_col_asm(s0.acc, fe_col_ops(op0, k), s1.acc, fe_col_ops(op1, k), s2.acc, fe_col_ops(op2, k))) {
+      CG_UNROLL for (int i = 0; i < 10; ++i) {
+        s0.acc = op0(k, i, s0.acc);
+        s1.acc = op1(k, i, s1.acc);
+        s2.acc = op2(k, i, s2.acc);
+      }
     }
     fe_fold_carry<Op0::kFloor>(s0, k);
     fe_fold_carry<Op1::kFloor>(s1, k);

@@ -278,10 +278,11 @@ cg_status upload_idx(cg_ctx* ctx, uint32_t** dst, const uint32_t* src, size_t co
   return CG_OK;
 }
 
-cg_status ensure_ed_scratch(cg_ctx* ctx, uint32_t need) {
-  const uint32_t want = std::min(need, kEdChunk);
+cg_status ensure_ed_scratch(cg_ctx* ctx, uint32_t need, uint32_t limit = kEdChunk) {
+  const uint32_t want = std::min(need, limit);
   if (ctx->ed_scap >= want) return CG_OK;
   (void)hipStreamSynchronize(ctx->stream);
+  (void)hipStreamSynchronize(ctx->hash_stream);  // (the verify pipeline's second compute stream)
   dfree(ctx, ctx->ed_status);
   dfree(ctx, ctx->ed_digits);
   dfree(ctx, ctx->ed_table);
@@ -669,6 +670,7 @@ cg_status stage_key_dedupe(cg_ctx* ctx, cg_batch* b, const uint8_t* pk, size_t p
 cg_status ensure_key_scratch(cg_ctx* ctx, uint32_t n_keys) {
   if (ctx->ed_kcap >= n_keys) return CG_OK;
   (void)hipStreamSynchronize(ctx->stream);
+  (void)hipStreamSynchronize(ctx->hash_stream);  // (the verify pipeline's second compute stream)
   dfree(ctx, ctx->ed_ktab);
   dfree(ctx, ctx->ed_kstat);
   ctx->ed_ktab = nullptr;
@@ -866,7 +868,9 @@ cg_status join_ecdsa_streams(cg_ctx* ctx) {
 // join_streams = false (the tx pipeline): a successful exit leaves the ECDSA work
 // running on its streams and skips the bitmap; the caller joins once after the last
 // batch and frees the batches only after its final sync.
-cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = true) {
+// scratch_off: the batch's Ed25519 lanes use scratch lanes [scratch_off, scratch_off + n_ed)
+// (the verify pipeline runs two chunks at once on disjoint halves); 0 otherwise.
+cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = true, uint32_t scratch_off = 0) {
   const size_t n = b->n;
   bool joins[2] = {false, false};
   cg_status st = CG_OK;
@@ -949,8 +953,9 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = 
     if (b->n_ed) {
       cg_status s2 = ensure_ed_scratch(ctx, b->n_ed);
       if (s2 != CG_OK) return s2;
-      for (uint32_t base = 0; base < b->n_ed; base += ctx->ed_scap) {
-        const uint32_t cnt = std::min(ctx->ed_scap, b->n_ed - base);
+      const uint32_t span = ctx->ed_scap - scratch_off;  // scratch lanes this batch may use
+      for (uint32_t base = 0; base < b->n_ed; base += span) {
+        const uint32_t cnt = std::min(span, b->n_ed - base);
         cg::Ed25519Dev d;
         d.cap = b->n_ed;
         d.scap = ctx->ed_scap;
@@ -960,9 +965,9 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = 
         d.arena = b->arena;
         d.msg_off = b->ed_msg_off + base;
         d.msg_len = b->ed_msg_len + base;
-        d.status = ctx->ed_status;
-        d.digits = ctx->ed_digits;
-        d.table = ctx->ed_table;
+        d.status = ctx->ed_status + scratch_off;
+        d.digits = ctx->ed_digits + scratch_off;  // rows keep their stride scap
+        d.table = ctx->ed_table + cg::ed25519_table_bytes(scratch_off) / sizeof(int32_t);
         d.btab = ctx->btab;
         d.full_mod = ctx->debug_full_mod;
         d.index_base = base;
@@ -1010,6 +1015,10 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = 
 // are copied on copy_stream while chunk k-1's kernels run on the compute streams, so
 // the call costs the transfer plus the last chunk's kernels.  The last chunk is the
 // smallest (`tail` of a regular chunk): only its kernels run after the last byte.
+// Consecutive chunks alternate between two compute streams (ctx->stream and
+// hash_stream) over disjoint halves of the Ed25519 scratch, so a chunk's kernels
+// start as soon as its bytes land instead of queueing behind the previous chunk's
+// (each chunk's three kernels are a serial ~1 ms chain per lane, whatever its size).
 struct VerifyRun {
   uint8_t* arena = nullptr;
   uint64_t* off = nullptr;
@@ -1022,7 +1031,7 @@ struct VerifyRun {
   std::vector<hipEvent_t> ev;
   std::vector<cg_batch*> batches;  // chunk batches (verdicts are slices of `verdict`)
   void release(cg_ctx* ctx) {
-    for (hipStream_t s : {ctx->copy_stream, ctx->ec_stream[0], ctx->ec_stream[1], ctx->stream})
+    for (hipStream_t s : {ctx->copy_stream, ctx->hash_stream, ctx->ec_stream[0], ctx->ec_stream[1], ctx->stream})
       (void)hipStreamSynchronize(s);
     for (cg_batch* b : batches) batch_free(ctx, b);
     batches.clear();
@@ -1039,21 +1048,46 @@ struct VerifyRun {
 };
 
 // Chunk boundaries of an n-element host batch: K = n / min_chunk chunks (at most
-// kmax), 64-aligned (whole waves), the last one `tail` times a regular one.
-// CORDA_AMD_VERIFY_CHUNKS / _MIN_CHUNK / _TAIL override (tuning, tests).
+// kmax), 64-aligned (whole waves); the first is `head` and the last `tail` times a
+// regular one (a small first chunk starts the kernels early, a small last one
+// shortens what runs after the last byte).  CORDA_AMD_VERIFY_CHUNKS / _MIN_CHUNK /
+// _HEAD / _TAIL override (tuning, tests).
 std::vector<size_t> verify_chunk_bounds(size_t n) {
-  size_t kmax = 8, min_chunk = 16384;
-  double tail = 0.5;
+  size_t kmax = 8, min_chunk = 32768;
+  double head = 0.5, tail = 0.5;
   if (const char* e = std::getenv("CORDA_AMD_VERIFY_CHUNKS")) kmax = std::max(1, std::atoi(e));
   if (const char* e = std::getenv("CORDA_AMD_VERIFY_MIN_CHUNK")) min_chunk = std::max(1, std::atoi(e));
-  if (const char* e = std::getenv("CORDA_AMD_VERIFY_TAIL")) tail = std::min(1.0, std::max(0.05, std::atof(e)));
+  if (const char* e = std::getenv("CORDA_AMD_VERIFY_HEAD")) head = std::min(2.0, std::max(0.05, std::atof(e)));
+  if (const char* e = std::getenv("CORDA_AMD_VERIFY_TAIL")) tail = std::min(2.0, std::max(0.05, std::atof(e)));
   const size_t K = std::max<size_t>(1, std::min<size_t>(kmax, n / min_chunk));
   std::vector<size_t> b(K + 1, 0);
-  const double wsum = (double)(K - 1) + tail;
-  for (size_t k = 1; k < K; ++k) b[k] = std::min(n, (size_t)((double)n * (double)k / wsum) / 64 * 64);
+  std::vector<double> w(K, 1.0);
+  if (K > 1) {
+    w[0] = head;
+    w[K - 1] = tail;
+  }
+  double wsum = 0;
+  for (double x : w) wsum += x;
+  double acc = 0;
+  for (size_t k = 1; k < K; ++k) {
+    acc += w[k - 1];
+    b[k] = std::min(n, (size_t)((double)n * acc / wsum) / 64 * 64);
+  }
   b[K] = n;
   for (size_t k = 1; k <= K; ++k) b[k] = std::max(b[k], b[k - 1]);
   return b;
+}
+
+// Page-locked host memory (cg_register_host, hipHostMalloc): a copy from it is truly
+// asynchronous.  A pageable copy is staged by the runtime and holds the calling thread.
+bool host_is_pinned(const void* p) {
+  if (!p) return true;
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return a.type == hipMemoryTypeHost;
 }
 
 cg_status verify_pipeline(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme_id, const uint8_t* pk,
@@ -1080,6 +1114,16 @@ cg_status verify_pipeline(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
   uint64_t up_to = 0;
   auto enqueue_upload = [&](size_t k) -> cg_status {
     const size_t lo = cb[k], hi = cb[k + 1];
+    // the chunk's inputs are checked just before they go out (the host scan then
+    // overlaps the earlier chunks' copies and kernels); an error ends the call
+    MsgSrc mc;
+    mc.host = msg;
+    mc.bytes = msg_bytes;
+    mc.off_host = msg_off + lo;
+    mc.len_host = msg_len + lo;
+    cg_status cst = check_inputs(ctx, hi - lo, scheme_id ? scheme_id + lo : nullptr, pk + lo * pk_stride, pk_stride,
+                                 sig + lo * sig_stride, sig_stride, sig_len ? sig_len + lo : nullptr, mc);
+    if (cst != CG_OK) return cst;
     const uint64_t from = up_to;
     for (size_t i = lo; i < hi; ++i) up_to = std::max<uint64_t>(up_to, msg_off[i] + msg_len[i]);
     hipStream_t cs = ctx->copy_stream;
@@ -1099,7 +1143,21 @@ cg_status verify_pipeline(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
     CG_TRY(ctx, hipEventRecord(r.ev[k], cs), "verify pipeline record");
     return CG_OK;
   };
-  if ((st = enqueue_upload(0)) != CG_OK) return st;
+  // Pinned inputs: the copies are asynchronous, so they are enqueued one chunk ahead of
+  // the kernels and the copy engine never waits for the host.  Pageable inputs: each
+  // copy holds the host, so chunk k's kernels are enqueued before chunk k+1's copy.
+  const bool pinned = host_is_pinned(msg) && host_is_pinned(pk) && host_is_pinned(sig) &&
+                      host_is_pinned(msg_off) && host_is_pinned(msg_len) && host_is_pinned(sig_len);
+  const size_t ahead = pinned ? 2 : 1;
+  size_t uploaded = 0;  // chunks whose copies are enqueued
+  auto upload_through = [&](size_t k) -> cg_status {  // enqueue copies of chunks < min(k, K)
+    for (; uploaded < std::min(k, K); ++uploaded) {
+      cg_status s2 = enqueue_upload(uploaded);
+      if (s2 != CG_OK) return s2;
+    }
+    return CG_OK;
+  };
+  if ((st = upload_through(ahead)) != CG_OK) return st;
   // Scratch sized for the largest chunk first, so no chunk regrows (frees) a buffer
   // an earlier chunk's kernels still use.
   uint32_t max_cnt[3] = {0, 0, 0};
@@ -1113,7 +1171,12 @@ cg_status verify_pipeline(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
     }
     for (int c = 0; c < 3; ++c) max_cnt[c] = std::max(max_cnt[c], cnt[c]);
   }
-  if (max_cnt[0] && (st = ensure_ed_scratch(ctx, max_cnt[0])) != CG_OK) return st;
+  // two chunks in flight need two disjoint scratch halves; chunks too large for that
+  // (> kEdChunk Ed25519 lanes each) run one after the other on ctx->stream
+  const bool dual = K > 1 && max_cnt[0] <= kEdChunk && !(std::getenv("CORDA_AMD_VERIFY_SERIAL"));
+  if (max_cnt[0] &&
+      (st = ensure_ed_scratch(ctx, dual ? 2 * max_cnt[0] : max_cnt[0], dual ? 2 * kEdChunk : kEdChunk)) != CG_OK)
+    return st;
   for (int c = 0; c < 2; ++c) {
     uint32_t chunk = 0;
     if (max_cnt[1 + c] &&
@@ -1137,12 +1200,29 @@ cg_status verify_pipeline(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
     cg_ctx* c;
     ~PinOff() { c->pin_active = false; }
   } pin_off{ctx};
+  // chunk k runs on lane[k % 2]; ctx->stream is swapped for the chunk's staging and
+  // launches (every helper enqueues on ctx->stream) and restored on every exit
+  hipStream_t lane[2] = {ctx->stream, dual ? ctx->hash_stream : ctx->stream};
+  struct StreamRestore {
+    cg_ctx* c;
+    hipStream_t main;
+    ~StreamRestore() { c->stream = main; }
+  } restore{ctx, ctx->stream};
+  hipEvent_t done[2] = {nullptr, nullptr};  // the latest chunk's end on each lane
+  struct EvFree {
+    hipEvent_t* e;
+    ~EvFree() {
+      for (int i = 0; i < 2; ++i)
+        if (e[i]) (void)hipEventDestroy(e[i]);
+    }
+  } ev_free{done};
+  for (hipEvent_t& e : done) CG_TRY(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming), "verify pipeline event");
   for (size_t k = 0; k < K; ++k) {
-    // the next chunk's copy is enqueued first (a pageable copy may hold the host until
-    // it is done: chunk k's kernels, enqueued below, then start right after it)
-    if (k + 1 < K && (st = enqueue_upload(k + 1)) != CG_OK) return st;
     const size_t lo = cb[k], hi = cb[k + 1];
+    if ((st = upload_through(k + 1)) != CG_OK) return st;  // (chunk k's own copy, if not yet)
     if (hi == lo) continue;
+    const int L = dual ? (int)(k & 1) : 0;
+    ctx->stream = lane[L];
     MsgSrc m;
     m.dev = r.arena;
     m.bytes = msg_bytes;
@@ -1158,9 +1238,18 @@ cg_status verify_pipeline(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
     st = create_batch(ctx, hi - lo, scheme_id ? scheme_id + lo : nullptr, pk + lo * pk_stride, pk_stride,
                       sig + lo * sig_stride, sig_stride, sig_len ? sig_len + lo : nullptr, m, &b);
     if (b) r.batches.push_back(b);  // freed after the final sync
-    if (st == CG_OK) st = launch_verify(ctx, b, mode, /*join_streams=*/false);
     if (st != CG_OK) return st;
+    // the key-reuse path's per-key tables are one context-wide buffer: a chunk that
+    // builds them waits for the other lane's chunk, which may still read them
+    if (dual && b->ed_key_index)
+      CG_TRY(ctx, hipStreamWaitEvent(ctx->stream, done[L ^ 1], 0), "verify pipeline wait");
+    st = launch_verify(ctx, b, mode, /*join_streams=*/false, dual ? (uint32_t)(L * max_cnt[0]) : 0);
+    if (st != CG_OK) return st;
+    CG_TRY(ctx, hipEventRecord(done[L], ctx->stream), "verify pipeline record");
+    if ((st = upload_through(k + 1 + ahead)) != CG_OK) return st;
   }
+  ctx->stream = restore.main;
+  if (dual) CG_TRY(ctx, hipStreamWaitEvent(ctx->stream, done[1], 0), "verify pipeline join");
   if ((st = join_ecdsa_streams(ctx)) != CG_OK) return st;
   CG_TRY(ctx, cg::launch_verdict_bitmap(r.verdict, (uint32_t)n, r.bitmap, ctx->stream), "launch bitmap");
   return CG_OK;
@@ -1240,13 +1329,10 @@ cg_status cg_verify_batch(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
     return st;
   }
   if (mode != CG_MODE_IS_VALID && mode != CG_MODE_DO_VERIFY) return fail(ctx, CG_E_INVALID_ARGUMENT, "bad mode");
-  MsgSrc m;
-  m.host = msg;
-  m.bytes = msg_bytes;
-  m.off_host = msg_off;
-  m.len_host = msg_len;
-  cg_status st = check_inputs(ctx, n, scheme_id, pk, pk_stride, sig, sig_stride, sig_len, m);
-  if (st != CG_OK) return st;
+  if (n > 0xFFFFFFF0ull) return fail(ctx, CG_E_INVALID_ARGUMENT, "batch larger than 2^32 - 16 elements");
+  if (!pk || !sig || !msg_off || !msg_len || (msg_bytes > 0 && !msg))
+    return fail(ctx, CG_E_INVALID_ARGUMENT, "null input pointer");
+  cg_status st = CG_OK;
   if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, CG_E_DEVICE, "hipSetDevice");
   VerifyRun r;
   struct RunGuard {  // also on an exception caught by CG_API_END (release is idempotent)

@@ -1,0 +1,107 @@
+"""End-to-end (host buffers in, verdicts out) latency of cg_verify_batch over its
+pipeline settings, on the GPU box:
+
+    python tools/e2e_sweep.py [--out gpurun_out/e2e_sweep.json]
+
+For each batch size (config-2 elements: Ed25519, 1 KB messages, distinct keys) and
+each setting of CORDA_AMD_VERIFY_CHUNKS / _MIN_CHUNK / _TAIL / _SERIAL (read by the
+library on every call), the p50 of 15 calls after 3 warm-ups; also the same with the
+input buffers page-locked (cg_register_host) and the raw pageable / pinned H2D rates,
+so every p50 can be put against the PCIe bound of its bytes.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools", "datagen"))
+
+SETTINGS = [
+    {"CORDA_AMD_VERIFY_CHUNKS": "1"},
+    {},  # library defaults
+    {"CORDA_AMD_VERIFY_SERIAL": "1"},
+] + [{"CORDA_AMD_VERIFY_CHUNKS": str(k), "CORDA_AMD_VERIFY_MIN_CHUNK": "1024", "CORDA_AMD_VERIFY_HEAD": str(h),
+      "CORDA_AMD_VERIFY_TAIL": str(t)}
+     for k, h, t in ((2, 0.5, 0.5), (2, 1, 0.5), (3, 0.5, 0.5), (4, 0.5, 0.5), (4, 1, 1), (6, 0.5, 0.5),
+                     (6, 0.25, 0.25), (8, 0.3, 0.3), (8, 0.5, 0.5))]
+KEYS = ("CORDA_AMD_VERIFY_CHUNKS", "CORDA_AMD_VERIFY_MIN_CHUNK", "CORDA_AMD_VERIFY_HEAD", "CORDA_AMD_VERIFY_TAIL",
+        "CORDA_AMD_VERIFY_SERIAL")
+
+
+def h2d_rates(mb=256):
+    import torch
+    src = np.random.default_rng(1).integers(0, 255, mb << 20, dtype=np.uint8)
+    dst = torch.empty(mb << 20, dtype=torch.uint8, device="cuda")
+    out = {}
+    for name, t in (("pageable", torch.from_numpy(src)), ("pinned", torch.from_numpy(src).pin_memory())):
+        dst.copy_(t)
+        torch.cuda.synchronize()
+        best = 0.0
+        for _ in range(5):
+            t0 = time.perf_counter()
+            dst.copy_(t)
+            torch.cuda.synchronize()
+            best = max(best, (mb << 20) / (time.perf_counter() - t0) / 1e9)
+        out[name] = round(best, 2)
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "e2e_sweep.json"))
+    ap.add_argument("--sizes", default="4096,16384,65536,262144")
+    ap.add_argument("--runs", type=int, default=15)
+    a = ap.parse_args()
+    import datagen
+    from corda_amd import Context, crypto
+    from corda_amd._lib import ACCEPT, MODE_IS_VALID
+    sizes = [int(x) for x in a.sizes.split(",")]
+    w = datagen.make_batch(max(sizes), msg_bytes=1024, seed=42, key_base=0, ref_seed_stride=4096)
+    res = {"h2d_GBps": h2d_rates(), "runs": a.runs, "rows": []}
+    with Context(0) as ctx:
+        for n in sizes:
+            s = w.subset(np.arange(n))
+            b = crypto.PackedBatch(s.n, s.scheme, s.pk, s.pk_stride, s.sig, s.sig_stride, s.sig_len, s.msg, s.msg_off,
+                                   s.msg_len)
+            nbytes = sum(x.nbytes for x in (b.scheme, b.pk, b.sig, b.sig_len, b.msg, b.msg_off, b.msg_len))
+            for pinned in (False, True):
+                if pinned:
+                    ctx.register_host(b.scheme, b.pk, b.sig, b.sig_len, b.msg, b.msg_off, b.msg_len)
+                for st in SETTINGS:
+                    for k in KEYS:
+                        os.environ.pop(k, None)
+                    os.environ.update(st)
+                    for _ in range(3):
+                        v = crypto.verify_packed(ctx, b, MODE_IS_VALID)
+                    ok = bool((v == ACCEPT).all())
+                    ts = []
+                    for _ in range(a.runs):
+                        t0 = time.perf_counter()
+                        crypto.verify_packed(ctx, b, MODE_IS_VALID)
+                        ts.append(time.perf_counter() - t0)
+                    p50 = statistics.median(ts) * 1e3
+                    row = {"n": n, "pinned": pinned, "setting": st, "p50_ms": round(p50, 3),
+                           "min_ms": round(min(ts) * 1e3, 3), "bytes": nbytes, "all_accept": ok,
+                           "GBps": round(nbytes / (p50 / 1e3) / 1e9, 2)}
+                    res["rows"].append(row)
+                    print(json.dumps(row), flush=True)
+                if pinned:
+                    ctx.unregister_host(b.scheme, b.pk, b.sig, b.sig_len, b.msg, b.msg_off, b.msg_len)
+    for k in KEYS:
+        os.environ.pop(k, None)
+    os.makedirs(os.path.dirname(a.out), exist_ok=True)
+    with open(a.out, "w") as f:
+        json.dump(res, f, indent=1)
+    print(json.dumps(res["h2d_GBps"]))
+
+
+if __name__ == "__main__":
+    main()
