@@ -69,6 +69,7 @@ sys.path.insert(0, os.path.join(ROOT, "tools", "datagen"))
 with open(os.path.join(ROOT, "bench", "roofline_model.json")) as _f:
     OP_MODEL = json.load(_f)
 PEAK = OP_MODEL["peak_int32_tops"]
+SIMDS = 1024  # 256 CUs x 4 SIMDs (MI355X); a wave64 VALU instruction holds one SIMD 2 or 4 cycles
 
 
 def kernel_src_hash() -> str:
@@ -307,6 +308,17 @@ def valu_roofline(pmc, kernel, units_per_launch, avg_launch_s, model_ops=None):
         ach = instr * units_per_launch / avg_launch_s / 1e12
         out["achieved"] = round(ach, 3)
         out["frac"] = round(ach / PEAK, 4)
+        # issue utilisation: a 64-bit VALU op (v_mad_i64_i32, 64-bit shifts: SQ_INSTS_VALU_INT64) holds the
+        # SIMD for 4 cycles, a 32-bit one for 2 (profiles/r02a_isa_rates.json; 32-bit multiplies, v_lshlrev
+        # and a few more take 4 too, so this is a lower bound); cycles the mix needs / cycles available at 2.4
+        # GHz and at the PMC pass's measured clock
+        i64 = e.get("int64_instr_per_unit")
+        if i64 is not None:
+            need = (2.0 * (instr - i64) + 4.0 * i64) * units_per_launch / (SIMDS * 64)  # cycles per SIMD
+            out["issue_util"] = round(need / (avg_launch_s * 2.4e9), 4)
+            clk = e.get("effective_clock_GHz")
+            if clk:
+                out["issue_util_at_pmc_clock"] = round(need / (avg_launch_s * clk * 1e9), 4)
     if model_ops and avg_launch_s > 0:
         m = model_ops * units_per_launch / avg_launch_s / 1e12
         out["model_ops_per_unit"] = model_ops
@@ -445,16 +457,21 @@ def run_ed25519(args, dist):
 
     # p50 batch latency: device-only (resident batch) and end-to-end (H2D + kernels + D2H)
     lat_dev, lat_e2e, lat_small = [], [], {}
+    e2e_bytes, e2e_ok, h2d_peak = 0, None, None
     e2e_n = min(n, 1 << 18)
     if rank == 0:
         for _ in range(args.latency_runs):
             t1 = time.perf_counter(); pb.verify(MODE_IS_VALID, want_verdicts=False); lat_dev.append(time.perf_counter() - t1)
+        # end to end from pageable host buffers in the layout an Ed25519-only caller packs
+        # (32-byte keys, 64-byte R||S rows, no scheme / sig_len arrays)
         sub = w.subset(np.arange(e2e_n))
-        sb = crypto.PackedBatch(sub.n, sub.scheme, sub.pk, sub.pk_stride, sub.sig, sub.sig_stride, sub.sig_len,
-                                sub.msg, sub.msg_off, sub.msg_len)
-        crypto.verify_packed(ctx, sb, MODE_IS_VALID)
+        sb = crypto.PackedBatch(sub.n, None, np.ascontiguousarray(sub.pk[:, :32]), 32,
+                                np.ascontiguousarray(sub.sig[:, :64]), 64, None, sub.msg, sub.msg_off, sub.msg_len)
+        e2e_bytes = sum(x.nbytes for x in (sb.pk, sb.sig, sb.msg_off, sb.msg_len)) + int(sb.msg_len.sum())
+        e2e_ok = bool(np.array_equal(crypto.verify_packed(ctx, sb, MODE_IS_VALID), verdict[:e2e_n]))
         for _ in range(args.latency_runs):
             t1 = time.perf_counter(); crypto.verify_packed(ctx, sb, MODE_IS_VALID); lat_e2e.append(time.perf_counter() - t1)
+        h2d_peak = pcie_h2d_peak_GBps(dist.local_rank)
         # serving-size batches (a notary's request queue): end-to-end p50 from host buffers
         for bn in (4096, 65536):
             if bn > n:
@@ -519,6 +536,13 @@ def run_ed25519(args, dist):
         "latency": {"p50_device_ms": round(statistics.median(lat_dev) * 1e3, 3) if lat_dev else None,
                     "p50_e2e_ms": round(statistics.median(lat_e2e) * 1e3, 3) if lat_e2e else None,
                     "e2e_batch": e2e_n, "runs": args.latency_runs,
+                    "e2e_bytes": e2e_bytes if lat_e2e else None,
+                    "e2e_layout": "Ed25519-only host rows: pk_stride 32, sig_stride 64, scheme_id / sig_len NULL; "
+                                  "pageable numpy buffers",
+                    "e2e_verdicts_match": e2e_ok if lat_e2e else None,
+                    "h2d_peak_GBps": h2d_peak if lat_e2e else None,
+                    "e2e_pcie_frac": round(e2e_bytes / statistics.median(lat_e2e) / 1e9 / h2d_peak, 4)
+                    if lat_e2e else None,
                     "p50_e2e_ms_by_batch": lat_small},
         "cpu_baseline": cpu,
         "checks": {"accepts": accepts, "untouched_all_accept": untouched_ok, "datagen_s": round(t_gen, 1)},

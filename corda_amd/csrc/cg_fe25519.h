@@ -118,7 +118,32 @@ CG_HD int32_t fe_pin(int32_t x) {
 // m * x pinned as 32 bits (m = 2, 4, 8: v_lshlrev_b32; 19: v_mul_lo_u32).  A/B r02:
 // doublings through v_add_u32 x, x (a 2-cycle op, v_lshlrev_b32 takes 4) measured
 // 0.8 % slower as inline asm (it broke the interleaving of the mad chains).
-CG_HD int32_t fe_scale(int32_t x, int m, bool g_side = false) { return fe_pin(CG_SCALE(x, m, g_side)); }
+// CG_FE_ADD_SCALE = 1: the power-of-two scalings as chains of v_add_u32 x, x (2 cycles
+// each; v_lshlrev_b32 takes 4), emitted as asm so LLVM does not fold them back into a
+// shift.
+#ifndef CG_FE_ADD_SCALE
+#define CG_FE_ADD_SCALE 0
+#endif
+CG_HD int32_t fe_scale(int32_t x, int m, bool g_side = false) {
+#if defined(__HIP_DEVICE_COMPILE__) && CG_FE_ADD_SCALE
+  if (m == 2) {
+    int32_t r;
+    asm("v_add_u32 %0, %1, %1" : "=v"(r) : "v"(x));
+    return r;
+  }
+  if (m == 4) {
+    int32_t r;
+    asm("v_add_u32 %0, %1, %1\n\tv_add_u32 %0, %0, %0" : "=&v"(r) : "v"(x));
+    return r;
+  }
+  if (m == 8) {
+    int32_t r;
+    asm("v_add_u32 %0, %1, %1\n\tv_add_u32 %0, %0, %0\n\tv_add_u32 %0, %0, %0" : "=&v"(r) : "v"(x));
+    return r;
+  }
+#endif
+  return fe_pin(CG_SCALE(x, m, g_side));
+}
 
 // Signed carry chain (round-to-nearest) on 64-bit column sums -> reduced limbs.
 // With rounding carries c = (t + 2^(w-1)) >> w, the residue t - c*2^w is exactly

@@ -55,6 +55,8 @@ hipError_t launch_gather_u32(const uint32_t* src, const uint32_t* idx, uint32_t 
                              hipStream_t s);
 hipError_t launch_gather_u64(const uint64_t* src, const uint32_t* idx, uint32_t n, uint64_t* dst, hipStream_t s);
 hipError_t launch_verdict_bitmap(const uint8_t* verdict, uint32_t n, uint32_t* bitmap, hipStream_t s);
+hipError_t launch_gather_rows(const uint8_t* src, size_t stride, const uint32_t* idx, uint32_t n, uint8_t* dst,
+                              hipStream_t s);
 hipError_t launch_fill_index(const uint32_t* idx, uint32_t n, uint8_t* verdict, uint8_t value, hipStream_t s);
 
 }  // namespace cg

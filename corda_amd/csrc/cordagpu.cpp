@@ -21,6 +21,7 @@
 
 #include <algorithm>
 #include <array>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -28,6 +29,7 @@
 #include <mutex>
 #include <new>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -44,6 +46,72 @@ struct Stat {
   double ms = 0;
   uint64_t launches = 0;
   uint64_t items = 0;
+};
+
+// Host copy workers for staging pageable caller buffers into page-locked memory
+// (cg_verify_batch's ring): one memcpy job split over the workers and the caller's
+// thread.  A single core copies ~10-20 GB/s; PCIe takes ~57 GB/s.
+class CopyPool {
+ public:
+  struct Piece {
+    void* dst;
+    const void* src;
+    size_t bytes;
+  };
+  explicit CopyPool(int workers) {
+    for (int t = 0; t < workers; ++t) th_.emplace_back([this] { loop(); });
+  }
+  ~CopyPool() {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  // Copies every piece (split into ~1 MB tasks); returns when all are done.
+  void run(const std::vector<Piece>& pieces) {
+    std::unique_lock<std::mutex> g(m_);
+    tasks_.clear();
+    constexpr size_t kTask = 1u << 20;
+    for (const Piece& p : pieces)
+      for (size_t o = 0; o < p.bytes; o += kTask)
+        tasks_.push_back({(char*)p.dst + o, (const char*)p.src + o, std::min(kTask, p.bytes - o)});
+    next_ = 0;
+    left_ = tasks_.size();
+    ++gen_;
+    cv_.notify_all();
+    work(g);  // the caller copies too
+    done_.wait(g, [this] { return left_ == 0; });
+  }
+
+ private:
+  void work(std::unique_lock<std::mutex>& g) {
+    while (next_ < tasks_.size()) {
+      const Piece t = tasks_[next_++];
+      g.unlock();
+      std::memcpy(t.dst, t.src, t.bytes);
+      g.lock();
+      if (--left_ == 0) done_.notify_all();
+    }
+  }
+  void loop() {
+    std::unique_lock<std::mutex> g(m_);
+    uint64_t seen = 0;
+    for (;;) {
+      cv_.wait(g, [&] { return stop_ || gen_ != seen; });
+      if (stop_) return;
+      seen = gen_;
+      work(g);
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex m_;
+  std::condition_variable cv_, done_;
+  std::vector<Piece> tasks_;
+  size_t next_ = 0, left_ = 0;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
 };
 
 }  // namespace
@@ -82,6 +150,11 @@ struct cg_ctx {
   size_t pin_cap = 0, pin_used = 0;
   bool pin_active = false;
   uint64_t pin_fallbacks = 0;  // uploads that found the staging area full
+  // cg_verify_batch's staging ring for pageable inputs: two page-locked slots (grow-only)
+  // filled by the copy workers while the other slot's DMA runs
+  uint8_t* ring[2] = {nullptr, nullptr};
+  size_t ring_cap = 0;
+  CopyPool* pool = nullptr;
   bool profiling = false;
   std::map<std::string, Stat> stats;
   std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending;
@@ -330,11 +403,12 @@ struct cg_batch {
   uint32_t* bad_index = nullptr;
   // ECDSA subsets (K1, R1)
   cg::EcdsaBatch ec[2];
-  // raw signature rows kept for the K4 DER parse that opens every verify of the ECDSA
-  // subsets (BC decodes the DER inside each engineVerify call); null in tx-pipeline
-  // batches, whose staging parse already sits inside the pipeline's own timed run
-  uint8_t* ec_sig_raw = nullptr;       // [n][ec_sig_stride]
-  uint32_t* ec_sig_len_raw = nullptr;  // [n], or null: every row is ec_sig_stride long
+  // the ECDSA subsets' raw signature rows, compacted per curve (subset order), kept for
+  // the K4 DER parse that opens every verify (BC decodes the DER inside each
+  // engineVerify call); null in tx-pipeline batches, whose staging parse already sits
+  // inside the pipeline's own timed run
+  uint8_t* ec_rows[2] = {nullptr, nullptr};     // [ec[c].n][ec_sig_stride]
+  uint32_t* ec_row_len[2] = {nullptr, nullptr};  // [ec[c].n], or null: every row is ec_sig_stride long
   size_t ec_sig_stride = 0;
 };
 
@@ -362,8 +436,10 @@ void batch_free(cg_ctx* ctx, cg_batch* b) {
     for (const void* p : {(const void*)e.index, (const void*)e.q, (const void*)e.rs, (const void*)e.der,
                           (const void*)e.sig_len, (const void*)e.msg_off, (const void*)e.msg_len})
       dfree(ctx, p);
-  dfree(ctx, b->ec_sig_raw);
-  dfree(ctx, b->ec_sig_len_raw);
+  for (int c = 0; c < 2; ++c) {
+    dfree(ctx, b->ec_rows[c]);
+    dfree(ctx, b->ec_row_len[c]);
+  }
   delete b;
 }
 
@@ -548,6 +624,9 @@ void cg_close(cg_ctx* ctx) {
     for (hipEvent_t e : {ctx->ev_fork, ctx->ev_join[0], ctx->ev_join[1], ctx->ev_keys})
       if (e) (void)hipEventDestroy(e);
     if (ctx->pin) (void)hipHostFree(ctx->pin);
+    for (uint8_t* r : ctx->ring)
+      if (r) (void)hipHostFree(r);
+    delete ctx->pool;
     delete ctx;
   } catch (...) {
     // nothing to report from a destructor-like call; never unwind into the caller
@@ -817,16 +896,19 @@ cg_status create_batch(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const ui
           (st = dalloc(ctx, &eb.msg_off, ne_c, "alloc ecdsa msg_off")) != CG_OK ||
           (st = dalloc(ctx, &eb.msg_len, ne_c, "alloc ecdsa msg_len")) != CG_OK)
         return bail(st);
-      const hipError_t e = cg::ecdsa_batch_stage(eb, pk_raw, pk_stride, sig_raw, sig_stride, sl_raw, b->msg_off_all,
-                                                 b->msg_len_all, ctx->stream);
+      hipError_t e = cg::ecdsa_batch_stage(eb, pk_raw, pk_stride, sig_raw, sig_stride, sl_raw, b->msg_off_all,
+                                           b->msg_len_all, ctx->stream);
       if (e != hipSuccess) return bail(hip_fail(ctx, e, "stage ecdsa"));
-    }
-    if (raw_owned && (b->ec[0].n || b->ec[1].n)) {  // the batch keeps the rows for its per-verify DER parse
-      b->ec_sig_raw = sig_raw;
-      b->ec_sig_len_raw = sl_raw;
-      b->ec_sig_stride = sig_stride;
-      sig_raw = nullptr;
-      sl_raw = nullptr;
+      if (raw_owned) {  // the batch keeps this subset's rows (only) for its per-verify DER parse
+        if ((st = dalloc(ctx, &b->ec_rows[c], ne_c * sig_stride, "alloc ecdsa rows")) != CG_OK ||
+            (sl_raw && (st = dalloc(ctx, &b->ec_row_len[c], ne_c, "alloc ecdsa row lengths")) != CG_OK))
+          return bail(st);
+        b->ec_sig_stride = sig_stride;
+        e = cg::launch_gather_rows(sig_raw, sig_stride, eb.index, (uint32_t)ne_c, b->ec_rows[c], ctx->stream);
+        if (e == hipSuccess && sl_raw)
+          e = cg::launch_gather_u32(sl_raw, eb.index, (uint32_t)ne_c, b->ec_row_len[c], 0, ctx->stream);
+        if (e != hipSuccess) return bail(hip_fail(ctx, e, "keep ecdsa rows"));
+      }
     }
   }
   // the host index vectors die here: wait for the copies that read them (unless every
@@ -931,11 +1013,11 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = 
       if (s2 != CG_OK) return s2;
       CG_TRY(ctx, hipStreamWaitEvent(es, ctx->ev_fork, 0), "fork ecdsa");
       joins[c] = true;  // from here on this curve's stream may hold work: the exit path joins it
-      if (b->ec_sig_raw) {  // K4: strict DER -> r, s + status, from the kept raw rows
+      if (b->ec_rows[c]) {  // K4: strict DER -> r, s + status, from the kept (compacted) raw rows
         Timed t(ctx, eb.scheme == 2 ? "ecdsa_k1_der" : "ecdsa_r1_der", eb.n, es);
         CG_TRY(ctx,
-               cg::launch_der_parse(eb.scheme, b->ec_sig_raw, b->ec_sig_stride, b->ec_sig_len_raw,
-                                    (uint32_t)b->ec_sig_stride, eb.index, eb.n, eb.n, eb.rs, eb.der, es),
+               cg::launch_der_parse(eb.scheme, b->ec_rows[c], b->ec_sig_stride, b->ec_row_len[c],
+                                    (uint32_t)b->ec_sig_stride, nullptr, eb.n, eb.n, eb.rs, eb.der, es),
                "launch ecdsa der parse");
       }
       for (uint32_t base = 0; base < eb.n; base += chunk) {
@@ -1111,7 +1193,51 @@ cg_status verify_pipeline(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
   // Chunk k's upload: the arena bytes its messages reach beyond what earlier chunks
   // uploaded (a prefix: an element-ordered arena, what a caller packs, gives even
   // pieces; any layout is correct), then its metadata and rows; event ev[k].
-  uint64_t up_to = 0;
+  // End of the arena prefix each chunk's messages reach (clamped: a chunk's offsets are
+  // checked against the arena before its copy goes out).
+  std::vector<uint64_t> aend(K + 1, 0);
+  for (size_t k = 0, u = 0; k < K; ++k) {
+    for (size_t i = cb[k]; i < cb[k + 1]; ++i) u = std::max<uint64_t>(u, msg_off[i] + msg_len[i]);
+    aend[k + 1] = u = std::min<uint64_t>(u, msg_bytes);
+  }
+  // Pinned inputs: the copies are asynchronous.  Pageable inputs go through the
+  // context's two page-locked ring slots, filled by the copy workers (chunk k+1's
+  // slot while chunk k's DMA runs; a slot is reused once chunk k-2's copies are done);
+  // without the ring (CORDA_AMD_VERIFY_RING=0, or no page-locked memory) a pageable
+  // copy holds the calling thread for its duration.
+  const bool pinned = host_is_pinned(msg) && host_is_pinned(pk) && host_is_pinned(sig) &&
+                      host_is_pinned(msg_off) && host_is_pinned(msg_len) && host_is_pinned(sig_len);
+  bool ring = !pinned && K > 1;
+  if (const char* e = std::getenv("CORDA_AMD_VERIFY_RING")) ring = ring && std::atoi(e) != 0;
+  const size_t row_bytes = 12 + pk_stride + sig_stride + (sig_len ? 4 : 0);
+  if (ring) {
+    size_t slot = 0;
+    for (size_t k = 0; k < K; ++k)
+      slot = std::max(slot, (size_t)(aend[k + 1] - aend[k]) + (cb[k + 1] - cb[k]) * row_bytes + 6 * 256);
+    if (ctx->ring_cap < slot) {
+      for (uint8_t*& rb : ctx->ring) {
+        if (rb) (void)hipHostFree(rb);  // idle: every earlier call ended with a sync
+        rb = nullptr;
+      }
+      ctx->ring_cap = 0;
+      if (hipHostMalloc((void**)&ctx->ring[0], slot, hipHostMallocDefault) == hipSuccess &&
+          hipHostMalloc((void**)&ctx->ring[1], slot, hipHostMallocDefault) == hipSuccess) {
+        ctx->ring_cap = slot;
+      } else {
+        (void)hipGetLastError();
+        for (uint8_t*& rb : ctx->ring) {
+          if (rb) (void)hipHostFree(rb);
+          rb = nullptr;
+        }
+      }
+    }
+    ring = ctx->ring_cap >= slot;
+    if (ring && !ctx->pool) {
+      int workers = 7;
+      if (const char* e = std::getenv("CORDA_AMD_COPY_THREADS")) workers = std::max(0, std::atoi(e) - 1);
+      ctx->pool = new CopyPool(workers);
+    }
+  }
   auto enqueue_upload = [&](size_t k) -> cg_status {
     const size_t lo = cb[k], hi = cb[k + 1];
     // the chunk's inputs are checked just before they go out (the host scan then
@@ -1124,31 +1250,39 @@ cg_status verify_pipeline(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
     cg_status cst = check_inputs(ctx, hi - lo, scheme_id ? scheme_id + lo : nullptr, pk + lo * pk_stride, pk_stride,
                                  sig + lo * sig_stride, sig_stride, sig_len ? sig_len + lo : nullptr, mc);
     if (cst != CG_OK) return cst;
-    const uint64_t from = up_to;
-    for (size_t i = lo; i < hi; ++i) up_to = std::max<uint64_t>(up_to, msg_off[i] + msg_len[i]);
+    // (device destination, host source, bytes) of the chunk: its arena piece and rows
+    std::vector<CopyPool::Piece> pieces = {
+        {r.arena + aend[k], msg + aend[k], (size_t)(aend[k + 1] - aend[k])},
+        {r.off + lo, msg_off + lo, (hi - lo) * 8},
+        {r.len + lo, msg_len + lo, (hi - lo) * 4},
+        {r.pk + lo * pk_stride, pk + lo * pk_stride, (hi - lo) * pk_stride},
+        {r.sig + lo * sig_stride, sig + lo * sig_stride, (hi - lo) * sig_stride}};
+    if (sig_len) pieces.push_back({r.sl + lo, sig_len + lo, (hi - lo) * 4});
     hipStream_t cs = ctx->copy_stream;
+    if (ring) {  // stage into slot k % 2 (free once chunk k-2's copies are done)
+      uint8_t* slot = ctx->ring[k & 1];
+      if (k >= 2) CG_TRY(ctx, hipEventSynchronize(r.ev[k - 2]), "verify ring wait");
+      std::vector<CopyPool::Piece> staged;
+      size_t o = 0;
+      for (CopyPool::Piece& p : pieces) {
+        staged.push_back({slot + o, p.src, p.bytes});
+        p.src = slot + o;  // the DMA now reads the slot
+        o += (p.bytes + 255) & ~(size_t)255;
+      }
+      ctx->pool->run(staged);
+    }
     {
-      Timed t(ctx, "h2d_verify", (up_to - from) + (hi - lo) * (pk_stride + sig_stride + 16), cs);
-      if (up_to > from)
-        CG_TRY(ctx, hipMemcpyAsync(r.arena + from, msg + from, up_to - from, hipMemcpyHostToDevice, cs), "upload arena");
-      CG_TRY(ctx, hipMemcpyAsync(r.off + lo, msg_off + lo, (hi - lo) * 8, hipMemcpyHostToDevice, cs), "upload msg_off");
-      CG_TRY(ctx, hipMemcpyAsync(r.len + lo, msg_len + lo, (hi - lo) * 4, hipMemcpyHostToDevice, cs), "upload msg_len");
-      CG_TRY(ctx, hipMemcpyAsync(r.pk + lo * pk_stride, pk + lo * pk_stride, (hi - lo) * pk_stride,
-                                 hipMemcpyHostToDevice, cs), "upload pk rows");
-      CG_TRY(ctx, hipMemcpyAsync(r.sig + lo * sig_stride, sig + lo * sig_stride, (hi - lo) * sig_stride,
-                                 hipMemcpyHostToDevice, cs), "upload sig rows");
-      if (sig_len)
-        CG_TRY(ctx, hipMemcpyAsync(r.sl + lo, sig_len + lo, (hi - lo) * 4, hipMemcpyHostToDevice, cs), "upload sig_len");
+      Timed t(ctx, "h2d_verify", (aend[k + 1] - aend[k]) + (hi - lo) * row_bytes, cs);
+      for (const CopyPool::Piece& p : pieces)
+        if (p.bytes) CG_TRY(ctx, hipMemcpyAsync(p.dst, p.src, p.bytes, hipMemcpyHostToDevice, cs), "upload chunk");
     }
     CG_TRY(ctx, hipEventRecord(r.ev[k], cs), "verify pipeline record");
     return CG_OK;
   };
-  // Pinned inputs: the copies are asynchronous, so they are enqueued one chunk ahead of
-  // the kernels and the copy engine never waits for the host.  Pageable inputs: each
-  // copy holds the host, so chunk k's kernels are enqueued before chunk k+1's copy.
-  const bool pinned = host_is_pinned(msg) && host_is_pinned(pk) && host_is_pinned(sig) &&
-                      host_is_pinned(msg_off) && host_is_pinned(msg_len) && host_is_pinned(sig_len);
-  const size_t ahead = pinned ? 2 : 1;
+  // Asynchronous copies (pinned or staged) run one chunk ahead of the kernels, so the
+  // copy engine never waits for the host; a copy that holds the host goes after the
+  // previous chunk's kernels are enqueued, so they run beside it.
+  const size_t ahead = (pinned || ring) ? 2 : 1;
   size_t uploaded = 0;  // chunks whose copies are enqueued
   auto upload_through = [&](size_t k) -> cg_status {  // enqueue copies of chunks < min(k, K)
     for (; uploaded < std::min(k, K); ++uploaded) {

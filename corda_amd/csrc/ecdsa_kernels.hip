@@ -17,8 +17,11 @@
 //   words), rs[w*cap+i] (16 LE limbs: r then s), der[i], sig_len[i], msg_off[i],
 //   msg_len[i]; scratch status[i] (verdict | digit count << 8 | signs << 16 for
 //   secp256k1), digits[w*scap+i] (27 words: u1 G digits, then k1 / k2 or u2
-//   nibbles), qtab[(e*20+w)*scap+i] (e = k-1 for affine k*Q, k = 1..8, x|y as 10
-//   radix-2^26 Montgomery limbs each, cg_fp26.h).
+//   nibbles), qtab: per lane 8 entries of one 128-byte line each (lane-contiguous,
+//   q_entry: affine k*Q, k = 1..8, x | y as 10 radix-2^26 Montgomery limbs each,
+//   cg_fp26.h; words 20..31 unused).  A lookup is then one line per lane; the old
+//   word-major layout qtab[(e*20+w)*scap+i] spread a wave's 20 loads of one entry over
+//   up to 8 rows (k differs per lane): ~38 KB of HBM traffic per P-256 verify.
 #include <vector>
 
 #include "cg_ecdsa.h"
@@ -36,6 +39,7 @@ struct EcScratch {
   uint32_t* status = nullptr;
   uint32_t* digits = nullptr;
   uint32_t* qtab = nullptr;
+  uint32_t* qjac = nullptr;   // prep_a -> prep_b: Jacobian X | Y of k*Q, word-major [8 * 20][scap] (coalesced)
   uint32_t* ework = nullptr;  // e mod n [8][scap]
   uint32_t* inv = nullptr;    // batched inversion mod n: leaves, tree levels, trees (element-major)
   uint32_t* invp = nullptr;   // batched inversion mod p (Z of the k*Q tables, 7 per lane)
@@ -55,8 +59,38 @@ void ecdsa_set_debug_glv(EcdsaConsts* c, uint32_t m) { c->glv_full_mod = m; }
 namespace {
 
 constexpr uint32_t kEcChunk = 1u << 20;
-constexpr int kQWords = 20;  // affine k*Q: X then Y, 10 Montgomery limbs each
-constexpr int kGStride = 20;  // affine table entry: x then y, 10 Montgomery limbs each (80 bytes)
+constexpr int kQWords = 32;   // affine k*Q entry: X then Y, 10 Montgomery limbs each, padded to a 128-byte line
+constexpr int kGStride = 32;  // shared table entry: x then y (20 words), padded to one 128-byte line
+
+// Entry k (1..8) of lane i's k*Q table (lane-contiguous, one line per entry).
+CG_DEV uint32_t* q_entry(uint32_t* qtab, uint32_t i, uint32_t k) {
+  return qtab + ((size_t)i * 8 + (k - 1)) * kQWords;
+}
+CG_DEV void q_store(uint32_t* e, const f26& X, const f26& Y) {
+  int4* p = reinterpret_cast<int4*>(e);
+  CG_UNROLL for (int q = 0; q < 5; ++q) {
+    int32_t v[4];
+    CG_UNROLL for (int j = 0; j < 4; ++j) {
+      const int w = 4 * q + j;
+      v[j] = w < 10 ? X.v[w] : Y.v[w - 10];
+    }
+    p[q] = make_int4(v[0], v[1], v[2], v[3]);
+  }
+}
+CG_DEV void q_load(const uint32_t* e, f26& X, f26& Y) {
+  const int4* p = reinterpret_cast<const int4*>(e);
+  CG_UNROLL for (int q = 0; q < 5; ++q) {
+    const int4 x = p[q];
+    const int32_t v[4] = {x.x, x.y, x.z, x.w};
+    CG_UNROLL for (int j = 0; j < 4; ++j) {
+      const int w = 4 * q + j;
+      if (w < 10)
+        X.v[w] = v[j];
+      else
+        Y.v[w - 10] = v[j];
+    }
+  }
+}
 constexpr int kDigitWordsEc = 27;
 
 CG_DEV uint32_t wave_max_u32(uint32_t v) {
@@ -286,7 +320,7 @@ __global__ __launch_bounds__(256) void cg_ecdsa_prep_a(const uint32_t* __restric
                                                        const uint32_t* __restrict__ msg_len, uint32_t n, uint32_t cap,
                                                        uint32_t scap, uint32_t mode, uint32_t* __restrict__ status,
                                                        uint32_t* __restrict__ ework, uint32_t* __restrict__ leaf_n,
-                                                       uint32_t* __restrict__ leaf_p, uint32_t* __restrict__ qtab) {
+                                                       uint32_t* __restrict__ leaf_p, uint32_t* __restrict__ qjac) {
   CG_WAVE_PRIO(2);
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -311,7 +345,7 @@ __global__ __launch_bounds__(256) void cg_ecdsa_prep_a(const uint32_t* __restric
   gl_put<8>(leaf_n + (size_t)i * 8, a);
   CG_UNROLL for (int w = 0; w < 8; ++w) ework[(size_t)w * scap + i] = e[w];
   ecdsa_q_table<C>(qx, qy, [&](int k, const jpt& p) {
-    uint32_t* base = qtab + (size_t)(k - 1) * kQWords * scap + i;
+    uint32_t* base = qjac + (size_t)(k - 1) * 20 * scap + i;
     CG_UNROLL for (int w = 0; w < 10; ++w) {
       base[(size_t)w * scap] = (uint32_t)p.X.v[w];
       base[(size_t)(10 + w) * scap] = (uint32_t)p.Y.v[w];
@@ -333,8 +367,9 @@ __global__ __launch_bounds__(256) void cg_ecdsa_prep_b(const uint32_t* __restric
                                                        const uint32_t* __restrict__ ework,
                                                        const uint32_t* __restrict__ leaf_n,
                                                        const uint32_t* __restrict__ leaf_p,
-                                                       uint32_t* __restrict__ digits, uint32_t* __restrict__ qtab,
-                                                       uint32_t glv_full_mod, uint32_t index_base) {
+                                                       uint32_t* __restrict__ digits, const uint32_t* __restrict__ qjac,
+                                                       uint32_t* __restrict__ qtab, uint32_t glv_full_mod,
+                                                       uint32_t index_base) {
   CG_WAVE_PRIO(2);
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n || status[i] != 0xff) return;
@@ -358,24 +393,28 @@ __global__ __launch_bounds__(256) void cg_ecdsa_prep_b(const uint32_t* __restric
     digits[(size_t)(9 + k) * scap + i] = d2[k];
     if constexpr (C::kScheme == 2) digits[(size_t)(18 + k) * scap + i] = d3[k];
   }
-  CG_NOUNROLL for (int k = 2; k <= 8; ++k) {
-    uint32_t zw[10];
+  // the table to affine, from the Jacobian prep_a wrote word-major into the per-lane
+  // lines the MSM reads (x = X / Z^2, y = Y / Z^3; k*Q for k = 1 is affine already)
+  CG_NOUNROLL for (int k = 1; k <= 8; ++k) {
     f26 zi, zi2, zi3, X, Y;
-    gl_get<10>(zw, leaf_p + ((size_t)(k - 2) * n + i) * 10);
-    uint32_t* base = qtab + (size_t)(k - 1) * kQWords * scap + i;
+    const uint32_t* jb = qjac + (size_t)(k - 1) * 20 * scap + i;
     CG_UNROLL for (int v = 0; v < 10; ++v) {
-      zi.v[v] = (int32_t)zw[v];
-      X.v[v] = (int32_t)base[(size_t)v * scap];
-      Y.v[v] = (int32_t)base[(size_t)(10 + v) * scap];
+      X.v[v] = (int32_t)jb[(size_t)v * scap];
+      Y.v[v] = (int32_t)jb[(size_t)(10 + v) * scap];
     }
+    uint32_t* base = q_entry(qtab, i, k);
+    if (k == 1) {
+      q_store(base, X, Y);
+      continue;
+    }
+    uint32_t zw[10];
+    gl_get<10>(zw, leaf_p + ((size_t)(k - 2) * n + i) * 10);
+    CG_UNROLL for (int v = 0; v < 10; ++v) zi.v[v] = (int32_t)zw[v];
     f26_sqr<C>(zi2, zi);
     f26_mul<C>(zi3, zi2, zi);
     f26_mul<C>(X, X, zi2);
     f26_mul<C>(Y, Y, zi3);
-    CG_UNROLL for (int v = 0; v < 10; ++v) {
-      base[(size_t)v * scap] = (uint32_t)X.v[v];
-      base[(size_t)(10 + v) * scap] = (uint32_t)Y.v[v];
-    }
+    q_store(base, X, Y);
   }
 }
 
@@ -418,19 +457,16 @@ void cg_ecdsa_msm(const uint32_t* __restrict__ rs,
   }
   CG_UNROLL for (int w = 0; w < 8; ++w) r[w] = rs[(size_t)w * cap + i];
   auto getQ = [&](uint32_t k, jpt& p) CG_LINLINE {
-        const uint32_t* base = qtab + (size_t)(k - 1) * kQWords * scap + i;
-        CG_UNROLL for (int w = 0; w < 10; ++w) {  // affine (cg_ecdsa_prep_b): Z is implied
-          p.X.v[w] = (int32_t)base[(size_t)w * scap];
-          p.Y.v[w] = (int32_t)base[(size_t)(10 + w) * scap];
-        }
+        q_load(q_entry(const_cast<uint32_t*>(qtab), i, k), p.X, p.Y);  // affine (cg_ecdsa_prep_b): Z implied
         p.inf = 0;
       };
   auto getG = [&](uint32_t t, uint32_t k, jpt& p) CG_LINLINE {
-        // affine k*G (t = 0) or k*2^128 G (t = 1): 80 bytes, five 16-byte loads from the
-        // L2-resident shared table (Z is implied; ec_add<C, true> never reads it)
+        // affine k*G (t = 0) or k*2^128 G (t = 1): 80 bytes of one 128-byte line, five
+        // 16-byte loads from the L2-resident shared table (Z is implied; ec_add<C, true>
+        // never reads it)
         const int4* g = reinterpret_cast<const int4*>(gtab_g + ((size_t)t * kGTabEntries + k) * kGStride);
-        int32_t v[kGStride];
-        CG_UNROLL for (int q = 0; q < kGStride / 4; ++q) {
+        int32_t v[20];
+        CG_UNROLL for (int q = 0; q < 5; ++q) {
           const int4 x = g[q];
           v[4 * q] = x.x;
           v[4 * q + 1] = x.y;
@@ -496,7 +532,7 @@ size_t inv_layout(uint32_t n, int words, size_t* val, size_t* tree, int* levels)
 }
 
 void free_scratch(EcScratch* c) {
-  for (auto* p : {c->status, c->digits, c->qtab, c->ework, c->inv, c->invp})
+  for (auto* p : {c->status, c->digits, c->qtab, c->qjac, c->ework, c->inv, c->invp})
     if (p) (void)hipFree(p);
   *c = EcScratch();
 }
@@ -507,14 +543,16 @@ hipError_t ensure_scratch(EcScratch* c, uint32_t need) {
   if (c->status) (void)hipFree(c->status);
   if (c->digits) (void)hipFree(c->digits);
   if (c->qtab) (void)hipFree(c->qtab);
+  if (c->qjac) (void)hipFree(c->qjac);
   if (c->ework) (void)hipFree(c->ework);
   if (c->inv) (void)hipFree(c->inv);
   if (c->invp) (void)hipFree(c->invp);
-  c->status = c->digits = c->qtab = c->ework = c->inv = c->invp = nullptr;
+  c->status = c->digits = c->qtab = c->qjac = c->ework = c->inv = c->invp = nullptr;
   c->scap = 0;
   hipError_t e = hipMalloc((void**)&c->status, (size_t)want * 4);
   if (e == hipSuccess) e = hipMalloc((void**)&c->digits, (size_t)kDigitWordsEc * want * 4);
   if (e == hipSuccess) e = hipMalloc((void**)&c->qtab, (size_t)8 * kQWords * want * 4);
+  if (e == hipSuccess) e = hipMalloc((void**)&c->qjac, (size_t)8 * 20 * want * 4);
   if (e == hipSuccess) e = hipMalloc((void**)&c->ework, (size_t)8 * want * 4);
   c->inv_words = inv_layout(want, 8, nullptr, nullptr, nullptr);
   c->invp_words = inv_layout(7 * want, 10, nullptr, nullptr, nullptr);
@@ -556,14 +594,15 @@ hipError_t launch_prep(const EcdsaBatch& b, EcdsaConsts* cc, uint32_t base, uint
   for (int l = 0; l < lp; ++l) mp[l + 1] = (mp[l] + 255) / 256;
   hipLaunchKernelGGL(cg_ecdsa_prep_a<C>, grid_for(cnt), dim3(256), 0, s, b.q + base, b.rs + base, b.der + base,
                      b.sig_len + base, arena, b.msg_off + base, b.msg_len + base, cnt, b.n, c->scap, mode, c->status,
-                     c->ework, c->inv + vn[0], c->invp + vp[0], c->qtab);
+                     c->ework, c->inv + vn[0], c->invp + vp[0], c->qjac);
   launch_inv_up<InvN<C>>(c->inv, vn, tn, mn, ln, s);
   launch_inv_up<InvP<C>>(c->invp, vp, tp, mp, lp, s);
   hipLaunchKernelGGL(cg_inv_roots<C>, dim3(1), dim3(128), 0, s, c->inv + vn[ln], c->invp + vp[lp]);
   launch_inv_down<InvN<C>>(c->inv, vn, tn, mn, ln, s);
   launch_inv_down<InvP<C>>(c->invp, vp, tp, mp, lp, s);
   hipLaunchKernelGGL(cg_ecdsa_prep_b<C>, grid_for(cnt), dim3(256), 0, s, b.rs + base, cnt, b.n, c->scap, c->status,
-                     c->ework, c->inv + vn[0], c->invp + vp[0], c->digits, c->qtab, cc->glv_full_mod, base);
+                     c->ework, c->inv + vn[0], c->invp + vp[0], c->digits, c->qjac, c->qtab, cc->glv_full_mod,
+                     base);
   return hipGetLastError();
 }
 

@@ -38,6 +38,19 @@ __global__ __launch_bounds__(256) void k_gather_u64(const uint64_t* __restrict__
   dst[i] = src[idx ? idx[i] : i];
 }
 
+// dst row i = src row idx[i] (stride bytes each): the ECDSA subsets' raw signature rows
+// compacted for the per-verify DER parse of a prepared batch.
+__global__ __launch_bounds__(256) void k_gather_rows(const uint8_t* __restrict__ src, size_t stride,
+                                                     const uint32_t* __restrict__ idx, uint32_t n,
+                                                     uint8_t* __restrict__ dst) {
+  CG_WAVE_PRIO(2);
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint8_t* s = src + (size_t)idx[i] * stride;
+  uint8_t* d = dst + (size_t)i * stride;
+  for (size_t b = 0; b < stride; ++b) d[b] = s[b];
+}
+
 // verdict[idx[i]] = value for i < n (elements whose key the caller could not construct:
 // CG_KEY_INVALID, which outranks every verdict the verify kernels write later).
 __global__ __launch_bounds__(256) void k_fill_index(const uint32_t* __restrict__ idx, uint32_t n,
@@ -155,6 +168,13 @@ hipError_t launch_key_dedupe(const uint32_t* pk, uint32_t n, uint32_t cap, uint3
   hipLaunchKernelGGL(k_key_insert, grid_for(n), dim3(256), 0, s, pk, n, cap, table, tsize - 1, slot_of, owner_id,
                      counter, key_first);
   hipLaunchKernelGGL(k_key_lookup, grid_for(n), dim3(256), 0, s, slot_of, owner_id, n, key_index);
+  return hipGetLastError();
+}
+
+hipError_t launch_gather_rows(const uint8_t* src, size_t stride, const uint32_t* idx, uint32_t n, uint8_t* dst,
+                              hipStream_t s) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(k_gather_rows, grid_for(n), dim3(256), 0, s, src, stride, idx, n, dst);
   return hipGetLastError();
 }
 

@@ -146,9 +146,9 @@ cg_status cg_verify_batch(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
  * Prepared batch: the same inputs staged once into device memory (HBM) in the
  * library's internal layout, then verified any number of times.  This is how a
  * notary backlog is fed, and what the benchmark times (inputs resident in HBM).
- * A batch holding ECDSA elements also keeps the raw signature rows (n * sig_stride
- * bytes, plus sig_len) in HBM: every cg_batch_verify re-parses their DER first, as
- * BC decodes the encoding inside each engineVerify.
+ * A batch holding ECDSA elements also keeps those elements' raw signature rows
+ * (n_ecdsa * sig_stride bytes, plus their sig_len) in HBM: every cg_batch_verify
+ * re-parses their DER first, as BC decodes the encoding inside each engineVerify.
  */
 cg_status cg_batch_create(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const uint8_t* pk, size_t pk_stride,
                           const uint8_t* sig, size_t sig_stride, const uint32_t* sig_len, const uint8_t* msg,

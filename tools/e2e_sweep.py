@@ -4,7 +4,7 @@ pipeline settings, on the GPU box:
     python tools/e2e_sweep.py [--out gpurun_out/e2e_sweep.json]
 
 For each batch size (config-2 elements: Ed25519, 1 KB messages, distinct keys) and
-each setting of CORDA_AMD_VERIFY_CHUNKS / _MIN_CHUNK / _TAIL / _SERIAL (read by the
+each setting of CORDA_AMD_VERIFY_CHUNKS / _MIN_CHUNK / _HEAD / _TAIL / _RING (read by the
 library on every call), the p50 of 15 calls after 3 warm-ups; also the same with the
 input buffers page-locked (cg_register_host) and the raw pageable / pinned H2D rates,
 so every p50 can be put against the PCIe bound of its bytes.
@@ -27,13 +27,14 @@ sys.path.insert(0, os.path.join(ROOT, "tools", "datagen"))
 SETTINGS = [
     {"CORDA_AMD_VERIFY_CHUNKS": "1"},
     {},  # library defaults
-    {"CORDA_AMD_VERIFY_SERIAL": "1"},
-] + [{"CORDA_AMD_VERIFY_CHUNKS": str(k), "CORDA_AMD_VERIFY_MIN_CHUNK": "1024", "CORDA_AMD_VERIFY_HEAD": str(h),
-      "CORDA_AMD_VERIFY_TAIL": str(t)}
-     for k, h, t in ((2, 0.5, 0.5), (2, 1, 0.5), (3, 0.5, 0.5), (4, 0.5, 0.5), (4, 1, 1), (6, 0.5, 0.5),
-                     (6, 0.25, 0.25), (8, 0.3, 0.3), (8, 0.5, 0.5))]
+    {"CORDA_AMD_VERIFY_RING": "0"},
+] + [dict({"CORDA_AMD_VERIFY_CHUNKS": str(k), "CORDA_AMD_VERIFY_MIN_CHUNK": "1024", "CORDA_AMD_VERIFY_HEAD": str(h),
+           "CORDA_AMD_VERIFY_TAIL": str(t)}, **extra)
+     for k, h, t in ((2, 0.5, 0.5), (3, 0.5, 0.5), (4, 0.5, 0.5), (4, 1, 0.5), (6, 0.5, 0.5), (6, 1, 0.5),
+                     (8, 0.5, 0.5))
+     for extra in ({}, {"CORDA_AMD_VERIFY_RING": "0"})]
 KEYS = ("CORDA_AMD_VERIFY_CHUNKS", "CORDA_AMD_VERIFY_MIN_CHUNK", "CORDA_AMD_VERIFY_HEAD", "CORDA_AMD_VERIFY_TAIL",
-        "CORDA_AMD_VERIFY_SERIAL")
+        "CORDA_AMD_VERIFY_SERIAL", "CORDA_AMD_VERIFY_RING")
 
 
 def h2d_rates(mb=256):
@@ -69,12 +70,12 @@ def main():
     with Context(0) as ctx:
         for n in sizes:
             s = w.subset(np.arange(n))
-            b = crypto.PackedBatch(s.n, s.scheme, s.pk, s.pk_stride, s.sig, s.sig_stride, s.sig_len, s.msg, s.msg_off,
-                                   s.msg_len)
-            nbytes = sum(x.nbytes for x in (b.scheme, b.pk, b.sig, b.sig_len, b.msg, b.msg_off, b.msg_len))
+            b = crypto.PackedBatch(s.n, None, np.ascontiguousarray(s.pk[:, :32]), 32,
+                                   np.ascontiguousarray(s.sig[:, :64]), 64, None, s.msg, s.msg_off, s.msg_len)
+            nbytes = sum(x.nbytes for x in (b.pk, b.sig, b.msg, b.msg_off, b.msg_len))
             for pinned in (False, True):
                 if pinned:
-                    ctx.register_host(b.scheme, b.pk, b.sig, b.sig_len, b.msg, b.msg_off, b.msg_len)
+                    ctx.register_host(b.pk, b.sig, b.msg, b.msg_off, b.msg_len)
                 for st in SETTINGS:
                     for k in KEYS:
                         os.environ.pop(k, None)
@@ -94,7 +95,7 @@ def main():
                     res["rows"].append(row)
                     print(json.dumps(row), flush=True)
                 if pinned:
-                    ctx.unregister_host(b.scheme, b.pk, b.sig, b.sig_len, b.msg, b.msg_off, b.msg_len)
+                    ctx.unregister_host(b.pk, b.sig, b.msg, b.msg_off, b.msg_len)
     for k in KEYS:
         os.environ.pop(k, None)
     os.makedirs(os.path.dirname(a.out), exist_ok=True)

@@ -13,7 +13,8 @@
 #                             config 3, config 4, ftx, config 5)                bench_<workload>.json
 #   profile=<name>[:<args>]   rocprofv3 trace + PMC passes of bench.py <args>   prof_<name>/
 #   parity=<n>[:<n_ec>]       tests/test_gpu_parity_mix.py at n Ed25519 / n_ec ECDSA  parity.log
-#   ab=<variants>             tools/ab_bench.sh over abvar/ variants (':' separated)  ab.txt
+#   ab=<variants>[@<args>]    tools/ab_bench.sh over abvar/ variants (':' separated), bench args
+#                             after '@' (':' separated)                           ab_<tag>.txt
 # Example:
 #   gpurun --timeout 1200 -- 'bash tools/gpu_run.sh r03a tests smoke bench=ed25519 profile=ed:'
 set -o pipefail
@@ -56,8 +57,10 @@ run_step() {
       CORDA_AMD_PARITY_N=$ne CORDA_AMD_PARITY_EC_N=$nc timeout -k 10 1000 python -u -m pytest \
         tests/test_gpu_parity_mix.py -x -v -s --timeout 900 --timeout-method thread > "$O/parity.log" 2>&1 ;;
     ab)
-      AB_NAMES="$(args_of "$val")" bash -c 'rm -f gpurun_out/ab.txt && bash tools/ab_bench.sh $AB_NAMES' \
-        > "$O/ab.log" 2>&1 && cp gpurun_out/ab.txt "$O/ab.txt" ;;
+      local an=${val%%@*} aa= tag=${val//[:@ ]/_}
+      [[ $val == *@* ]] && aa=$(args_of "${val#*@}")
+      AB_NAMES="$(args_of "$an")" AB_ARGS="$aa" bash -c 'rm -f gpurun_out/ab.txt && bash tools/ab_bench.sh $AB_NAMES' \
+        > "$O/ab_$tag.log" 2>&1 && cp gpurun_out/ab.txt "$O/ab_$tag.txt" ;;
     *)
       echo "unknown step $step" >&2; return 2 ;;
   esac
