@@ -42,6 +42,9 @@ constexpr int kATabEntries = 9;                          // per-lane tables, 4-b
 constexpr int kBTabEntries = (1 << (kBWin - 1)) + 1;     // shared tables, |d| <= 2^(kBWin-1)
 constexpr int kDigitWords = 24;    // A nibbles (8) | R nibbles (8) | B digits (8 words, 256 bits)
 constexpr int kMinDigits = 32;     // the loop always covers bit positions 0..127 (B tables)
+#ifndef CG_MSM_PREFETCH
+#define CG_MSM_PREFETCH 0
+#endif
 
 // Status word of the hash/points phases: verdict (bits 0-7; V_COMPUTE while the
 // MSM must decide), radix-16 digit count (bits 8-15), R sign flag (bit 16).
@@ -306,8 +309,8 @@ CG_HD uint32_t ed25519_msm(uint32_t ndig, const uint32_t dig[kDigitWords], uint3
   ge_p2 r2;
   ge_p3 r3;
   ge_p1p1 t;  // identity: x = X/Z = 0, y = Y/T = 1
-  ge_cached ca;
-  ge_precomp pb;
+  ge_cached ca, cr;
+  ge_precomp pb, pb2;
   fe_0(t.X);
   fe_1(t.Y);
   fe_1(t.Z);
@@ -316,6 +319,8 @@ CG_HD uint32_t ed25519_msm(uint32_t ndig, const uint32_t dig[kDigitWords], uint3
   // digit is added to the identity (no doublings).  The A entry of a window is
   // loaded before its four doublings (40 VGPRs held across them), so the load's
   // latency hides under ~3,600 VALU instructions instead of stalling the addition.
+  // CG_MSM_PREFETCH: 1 also loads the R entry, 2 also the first B entry of a B window,
+  // before the doublings (their latency hidden like the A entry's; +40 / +70 VGPRs)
   const int nwin = (int)ndig;
   CG_NOUNROLL for (int j = nwin - 1; j >= 0; --j) {
     const uint32_t ea = da[7] >> 28, er = dr[7] >> 28;
@@ -326,7 +331,27 @@ CG_HD uint32_t ed25519_msm(uint32_t ndig, const uint32_t dig[kDigitWords], uint3
     da[0] <<= 4;
     dr[0] <<= 4;
     const uint32_t na = ea < 8, nr = er < 8;
+    const bool bwin = ((4 * j) & (kBWin - 1)) == 0 && 4 * j < 128;
+    constexpr uint32_t kMask = (1u << kBWin) - 1, kHalf = 1u << (kBWin - 1);
+    uint32_t el = 0, eh = 0;
+    if (bwin) {
+      el = bl[0] & kMask;
+      eh = bh[0] & kMask;
+      CG_UNROLL for (int w = 0; w < 3; ++w) {
+        bl[w] = bl[w] >> kBWin | bl[w + 1] << (32 - kBWin);
+        bh[w] = bh[w] >> kBWin | bh[w + 1] << (32 - kBWin);
+      }
+      bl[3] >>= kBWin;
+      bh[3] >>= kBWin;
+    }
+    const uint32_t nl = el < kHalf, nh = eh < kHalf;
     getA(na ? 8 - ea : ea - 8, ca);
+#if CG_MSM_PREFETCH >= 1
+    getR(nr ? 8 - er : er - 8, cr);
+#endif
+#if CG_MSM_PREFETCH >= 2
+    if (bwin) getB(0, nl ? kHalf - el : el - kHalf, pb);
+#endif
     if (j != nwin - 1) {
       CG_NOUNROLL for (int k = 0; k < 3; ++k) {
         ge_p1p1_to_p2(r2, t);
@@ -339,25 +364,20 @@ CG_HD uint32_t ed25519_msm(uint32_t ndig, const uint32_t dig[kDigitWords], uint3
     } else {
       ge_add_cached(t, ge_identity_p3(), ca, na);  // constant operand: mostly folded away
     }
-    getR(nr ? 8 - er : er - 8, ca);
+#if CG_MSM_PREFETCH < 1
+    getR(nr ? 8 - er : er - 8, cr);
+#endif
     ge_p1p1_to_p3(r3, t);
-    ge_add_cached(t, r3, ca, nr ^ rneg);
-    if (((4 * j) & (kBWin - 1)) == 0 && 4 * j < 128) {
-      constexpr uint32_t kMask = (1u << kBWin) - 1, kHalf = 1u << (kBWin - 1);
-      const uint32_t el = bl[0] & kMask, eh = bh[0] & kMask;
-      CG_UNROLL for (int w = 0; w < 3; ++w) {
-        bl[w] = bl[w] >> kBWin | bl[w + 1] << (32 - kBWin);
-        bh[w] = bh[w] >> kBWin | bh[w + 1] << (32 - kBWin);
-      }
-      bl[3] >>= kBWin;
-      bh[3] >>= kBWin;
-      const uint32_t nl = el < kHalf, nh = eh < kHalf;
+    ge_add_cached(t, r3, cr, nr ^ rneg);
+    if (bwin) {
+#if CG_MSM_PREFETCH < 2
       getB(0, nl ? kHalf - el : el - kHalf, pb);
+#endif
+      getB(2, nh ? kHalf - eh : eh - kHalf, pb2);  // in flight during the first madd
       ge_p1p1_to_p3<true>(r3, t);
       ge_madd(t, r3, pb, nl);
-      getB(2, nh ? kHalf - eh : eh - kHalf, pb);
       ge_p1p1_to_p3<true>(r3, t);
-      ge_madd(t, r3, pb, nh);
+      ge_madd(t, r3, pb2, nh);
     }
   }
   // identity <=> x = X/Z = 0 and y = Y/T = 1

@@ -17,9 +17,10 @@ struct Ed25519Dev {
   const uint8_t* arena = nullptr;
   const uint64_t* msg_off = nullptr;
   const uint32_t* msg_len = nullptr;
-  uint32_t* status = nullptr;    // [scap]
+  uint32_t* status = nullptr;    // [scap] hash phase: verdict | digit count << 8 | R sign << 16
+  uint32_t* pstat = nullptr;     // [scap] points phase: KEY_INVALID / REJECT (R) / COMPUTE
   uint32_t* digits = nullptr;    // [24][scap]
-  int32_t* table = nullptr;      // [scap][18][40] lane-contiguous k*(-A), k*R
+  int32_t* table = nullptr;      // [scap][18][40] lane-contiguous k*(-A), k*R (ed25519_kernels.hip)
   const int32_t* btab = nullptr; // [2][kBTabEntries][30] shared k*B, k*2^128 B tables
   // key-reuse path (null key_index: the balanced path): per-signature index of the
   // signer's distinct-key slot, the per-key tables k * 2^(64 t) (-A) and key status
@@ -32,6 +33,7 @@ struct Ed25519Dev {
 
 size_t ed25519_btab_words();
 size_t ed25519_table_bytes(uint32_t cap);
+size_t ed25519_table_offset(uint32_t lanes);  // int32 offset of a scratch sub-range starting at lane `lanes`
 size_t ed25519_digit_words();
 hipError_t launch_ed25519_btab_build(int32_t* btab, hipStream_t s);
 hipError_t launch_ed25519_hash(const Ed25519Dev& d, uint32_t n, uint32_t mode, hipStream_t s);

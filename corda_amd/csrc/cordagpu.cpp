@@ -41,6 +41,10 @@
 namespace {
 
 constexpr uint32_t kEdChunk = 1u << 21;  // Ed25519 scratch chunk (elements)
+// cg_batch_verify of a large Ed25519 subset: pieces on two streams (launch_verify);
+// CORDA_AMD_ED_SPLIT overrides the count, pieces stay >= kEdSplitMin elements
+constexpr uint32_t kEdSplitMin = 65536;
+constexpr uint32_t kEdSplitDefault = 4;
 
 struct Stat {
   double ms = 0;
@@ -131,6 +135,8 @@ struct cg_ctx {
   hipStream_t ec_stream[2] = {nullptr, nullptr};
   hipEvent_t ev_fork = nullptr, ev_join[2] = {nullptr, nullptr};
   hipEvent_t ev_keys = nullptr;  // key-reuse path: per-key tables ready (keyprep runs on ec_stream[0])
+  hipEvent_t ev_split = nullptr;  // prepared-batch verify: the Ed25519 pieces on hash_stream are done
+  hipEvent_t ev_pts_in = nullptr, ev_pts_done = nullptr;  // Ed25519 points kernel beside the hash kernel
   std::string err;
   int32_t* btab = nullptr;
   // Ed25519 chunk scratch
@@ -356,6 +362,8 @@ cg_status ensure_ed_scratch(cg_ctx* ctx, uint32_t need, uint32_t limit = kEdChun
   if (ctx->ed_scap >= want) return CG_OK;
   (void)hipStreamSynchronize(ctx->stream);
   (void)hipStreamSynchronize(ctx->hash_stream);  // (the verify pipeline's second compute stream)
+  (void)hipStreamSynchronize(ctx->copy_stream);  // (points kernels beside the hash kernels)
+  (void)hipStreamSynchronize(ctx->ec_stream[0]);
   dfree(ctx, ctx->ed_status);
   dfree(ctx, ctx->ed_digits);
   dfree(ctx, ctx->ed_table);
@@ -364,7 +372,8 @@ cg_status ensure_ed_scratch(cg_ctx* ctx, uint32_t need, uint32_t limit = kEdChun
   ctx->ed_table = nullptr;
   ctx->ed_scap = 0;
   cg_status st;
-  if ((st = dalloc(ctx, &ctx->ed_status, want, "alloc ed25519 status")) != CG_OK) return st;
+  // status words of the hash phase [0, want) and of the points phase [want, 2 want)
+  if ((st = dalloc(ctx, &ctx->ed_status, 2 * (size_t)want, "alloc ed25519 status")) != CG_OK) return st;
   if ((st = dalloc(ctx, &ctx->ed_digits, cg::ed25519_digit_words() * want, "alloc ed25519 digits")) != CG_OK) return st;
   if ((st = dalloc(ctx, (uint8_t**)&ctx->ed_table, cg::ed25519_table_bytes(want), "alloc ed25519 table")) != CG_OK)
     return st;
@@ -576,7 +585,10 @@ cg_status cg_open(int device, cg_ctx** out) {
       hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_join[0], hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_join[1], hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&ctx->ev_keys, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&ctx->ev_keys, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->ev_split, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->ev_pts_in, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->ev_pts_done, hipEventDisableTiming) != hipSuccess) {
     cg_close(ctx);
     return CG_E_DEVICE;
   }
@@ -621,7 +633,8 @@ void cg_close(cg_ctx* ctx) {
     if (ctx->hash_stream) (void)hipStreamDestroy(ctx->hash_stream);
     if (ctx->ec_stream[1] && ctx->ec_stream[1] != ctx->ec_stream[0]) (void)hipStreamDestroy(ctx->ec_stream[1]);
     if (ctx->ec_stream[0]) (void)hipStreamDestroy(ctx->ec_stream[0]);
-    for (hipEvent_t e : {ctx->ev_fork, ctx->ev_join[0], ctx->ev_join[1], ctx->ev_keys})
+    for (hipEvent_t e : {ctx->ev_fork, ctx->ev_join[0], ctx->ev_join[1], ctx->ev_keys, ctx->ev_split, ctx->ev_pts_in,
+                         ctx->ev_pts_done})
       if (e) (void)hipEventDestroy(e);
     if (ctx->pin) (void)hipHostFree(ctx->pin);
     for (uint8_t* r : ctx->ring)
@@ -952,7 +965,15 @@ cg_status join_ecdsa_streams(cg_ctx* ctx) {
 // batch and frees the batches only after its final sync.
 // scratch_off: the batch's Ed25519 lanes use scratch lanes [scratch_off, scratch_off + n_ed)
 // (the verify pipeline runs two chunks at once on disjoint halves); 0 otherwise.
-cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = true, uint32_t scratch_off = 0) {
+// Ed25519 points kernels beside the hash kernels on `pts_stream` (null: after them on
+// the same stream); CORDA_AMD_ED_OVERLAP=0 turns it off.
+bool ed_overlap_enabled() {
+  const char* e = std::getenv("CORDA_AMD_ED_OVERLAP");
+  return !e || std::atoi(e) != 0;
+}
+
+cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = true, uint32_t scratch_off = 0,
+                        hipStream_t pts_stream = nullptr) {
   const size_t n = b->n;
   bool joins[2] = {false, false};
   cg_status st = CG_OK;
@@ -1036,8 +1057,33 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = 
       cg_status s2 = ensure_ed_scratch(ctx, b->n_ed);
       if (s2 != CG_OK) return s2;
       const uint32_t span = ctx->ed_scap - scratch_off;  // scratch lanes this batch may use
-      for (uint32_t base = 0; base < b->n_ed; base += span) {
-        const uint32_t cnt = std::min(span, b->n_ed - base);
+      // Large batches run as `split` index pieces alternating between ctx->stream and
+      // hash_stream (each piece on its own scratch lanes), so one piece's kernels fill
+      // the SIMDs another piece's kernel leaves idle while its last waves drain.  Only
+      // when this call owns the streams (join_streams: not inside verify_pipeline).
+      uint32_t split = 1;
+      if (join_streams && b->n_ed >= 2 * kEdSplitMin && b->n_ed <= span) {
+        split = kEdSplitDefault;
+        if (const char* e = std::getenv("CORDA_AMD_ED_SPLIT")) split = (uint32_t)std::max(1, std::atoi(e));
+        split = std::min<uint32_t>(split, b->n_ed / kEdSplitMin);
+      }
+      hipStream_t ed_lane[2] = {ctx->stream, ctx->hash_stream};
+      // prepared-batch verify (this call owns the streams): points beside hash on the idle copy stream
+      hipStream_t pts = pts_stream ? pts_stream : (join_streams && ed_overlap_enabled() ? ctx->copy_stream : nullptr);
+      if (split > 1) {
+        CG_TRY(ctx, hipStreamWaitEvent(ctx->hash_stream, ctx->ev_fork, 0), "fork ed25519 split");
+      }
+      struct StreamBack {  // ctx->stream is the piece's lane inside the loop; restored on every exit
+        cg_ctx* c;
+        hipStream_t main;
+        ~StreamBack() { c->stream = main; }
+      } back{ctx, ctx->stream};
+      for (uint32_t base = 0, piece = 0; base < b->n_ed; ++piece) {
+        uint32_t cnt = std::min(span, b->n_ed - base);
+        if (split > 1)  // piece sizes: whole 256-lane blocks, the last one takes the rest
+          cnt = piece + 1 == split ? b->n_ed - base : (uint32_t)(((uint64_t)b->n_ed / split + 255) / 256 * 256);
+        ctx->stream = ed_lane[piece & 1 & (split > 1)];
+        const uint32_t soff = scratch_off + (split > 1 ? base : 0);  // scratch lanes of this piece
         cg::Ed25519Dev d;
         d.cap = b->n_ed;
         d.scap = ctx->ed_scap;
@@ -1047,9 +1093,10 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = 
         d.arena = b->arena;
         d.msg_off = b->ed_msg_off + base;
         d.msg_len = b->ed_msg_len + base;
-        d.status = ctx->ed_status + scratch_off;
-        d.digits = ctx->ed_digits + scratch_off;  // rows keep their stride scap
-        d.table = ctx->ed_table + cg::ed25519_table_bytes(scratch_off) / sizeof(int32_t);
+        d.status = ctx->ed_status + soff;
+        d.pstat = ctx->ed_status + ctx->ed_scap + soff;
+        d.digits = ctx->ed_digits + soff;  // rows keep their stride scap
+        d.table = ctx->ed_table + cg::ed25519_table_offset(soff);
         d.btab = ctx->btab;
         d.full_mod = ctx->debug_full_mod;
         d.index_base = base;
@@ -1058,17 +1105,33 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = 
           d.ktab = ctx->ed_ktab;
           d.kstat = ctx->ed_kstat;
         }
-        {
-          Timed t(ctx, "ed25519_hash", cnt);
-          CG_TRY(ctx, cg::launch_ed25519_hash(d, cnt, (uint32_t)mode, ctx->stream), "launch ed25519_hash");
-        }
-        if (keys_pending) {
-          CG_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_keys, 0), "wait keyprep");
-          keys_pending = false;
-        }
-        {
-          Timed t(ctx, "ed25519_points", cnt);
-          CG_TRY(ctx, cg::launch_ed25519_points(d, cnt, ctx->stream), "launch ed25519_points");
+        if (pts) {
+          // the points kernel needs only the rows (ready where this lane stands now):
+          // it runs on pts beside the hash kernel, and the MSM waits for both
+          CG_TRY(ctx, hipEventRecord(ctx->ev_pts_in, ctx->stream), "fork points");
+          CG_TRY(ctx, hipStreamWaitEvent(pts, ctx->ev_pts_in, 0), "fork points");
+          if (keys_pending && piece == 0) CG_TRY(ctx, hipStreamWaitEvent(pts, ctx->ev_keys, 0), "wait keyprep");
+          {
+            Timed t(ctx, "ed25519_points", cnt, pts);
+            CG_TRY(ctx, cg::launch_ed25519_points(d, cnt, pts), "launch ed25519_points");
+          }
+          CG_TRY(ctx, hipEventRecord(ctx->ev_pts_done, pts), "points done");
+          {
+            Timed t(ctx, "ed25519_hash", cnt);
+            CG_TRY(ctx, cg::launch_ed25519_hash(d, cnt, (uint32_t)mode, ctx->stream), "launch ed25519_hash");
+          }
+          CG_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_pts_done, 0), "join points");
+        } else {
+          {
+            Timed t(ctx, "ed25519_hash", cnt);
+            CG_TRY(ctx, cg::launch_ed25519_hash(d, cnt, (uint32_t)mode, ctx->stream), "launch ed25519_hash");
+          }
+          if (keys_pending && piece < std::min<uint32_t>(split, 2))  // each lane's first points kernel
+            CG_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_keys, 0), "wait keyprep");
+          {
+            Timed t(ctx, "ed25519_points", cnt);
+            CG_TRY(ctx, cg::launch_ed25519_points(d, cnt, ctx->stream), "launch ed25519_points");
+          }
         }
         {
           Timed t(ctx, "ed25519_msm", cnt);
@@ -1077,11 +1140,22 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = 
                                         b->ed_index ? b->verdict : b->verdict + base, ctx->stream),
                  "launch ed25519_msm");
         }
+        base += cnt;
+      }
+      ctx->stream = back.main;
+      if (split > 1) {  // the main stream continues once the other lane's pieces are done
+        CG_TRY(ctx, hipEventRecord(ctx->ev_split, ctx->hash_stream), "split join");
+        CG_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_split, 0), "split join");
       }
     }
     return CG_OK;
   };
   st = run();
+  if (st != CG_OK) {  // a split's other lane or the points stream may hold work
+    (void)hipStreamSynchronize(ctx->hash_stream);
+    (void)hipStreamSynchronize(ctx->copy_stream);
+    if (pts_stream) (void)hipStreamSynchronize(pts_stream);
+  }
   if (st != CG_OK || join_streams) join();
   if (st != CG_OK || !join_streams) return st;
   CG_TRY(ctx, cg::launch_verdict_bitmap(b->verdict, (uint32_t)n, b->bitmap, ctx->stream), "launch bitmap");
@@ -1337,6 +1411,9 @@ cg_status verify_pipeline(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
   // chunk k runs on lane[k % 2]; ctx->stream is swapped for the chunk's staging and
   // launches (every helper enqueues on ctx->stream) and restored on every exit
   hipStream_t lane[2] = {ctx->stream, dual ? ctx->hash_stream : ctx->stream};
+  // Ed25519 points kernels beside the hash kernels on the first ECDSA stream when no
+  // chunk has ECDSA elements (it is idle then)
+  hipStream_t pts = (!max_cnt[1] && !max_cnt[2] && ed_overlap_enabled()) ? ctx->ec_stream[0] : nullptr;
   struct StreamRestore {
     cg_ctx* c;
     hipStream_t main;
@@ -1377,7 +1454,7 @@ cg_status verify_pipeline(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
     // builds them waits for the other lane's chunk, which may still read them
     if (dual && b->ed_key_index)
       CG_TRY(ctx, hipStreamWaitEvent(ctx->stream, done[L ^ 1], 0), "verify pipeline wait");
-    st = launch_verify(ctx, b, mode, /*join_streams=*/false, dual ? (uint32_t)(L * max_cnt[0]) : 0);
+    st = launch_verify(ctx, b, mode, /*join_streams=*/false, dual ? (uint32_t)(L * max_cnt[0]) : 0, pts);
     if (st != CG_OK) return st;
     CG_TRY(ctx, hipEventRecord(done[L], ctx->stream), "verify pipeline record");
     if ((st = upload_through(k + 1 + ahead)) != CG_OK) return st;

@@ -4,7 +4,9 @@
 //   cg_ed25519_hash     SHA-512 challenge, scalars, half-size reduction, digits —
 //                       integer/hash work, no field arithmetic beyond Abyte
 //   cg_ed25519_points   decode A and R (two square roots), tables k*(-A) and k*R
-//                       (k = 0..8) written to HBM scratch
+//                       (k = 0..8) written to HBM scratch; independent of the hash
+//                       kernel (its own verdict word pstat), so the two may run side
+//                       by side
 //   cg_ed25519_msm      [b]B + [c0](-A) + [c1](+-R) over ~132 shared bit positions
 //                       (4-bit windows for A/R, kBWin-bit windows over the shared
 //                       tables B and 2^128 B in HBM), identity test -> verdict
@@ -15,9 +17,14 @@
 //   pk[w*cap+i] (8 words), sig[w*cap+i] (16 words: R then S), sig_len[i],
 //   msg_off[i] (u64, into the arena), msg_len[i]; scratch (`scap` = chunk):
 //   status[i] (verdict | digit count << 8 | R sign << 16), digits[w*scap+i]
-//   (24 words), and the per-signature tables lane-contiguous (AoS):
-//   table[(i*18 + e)*40 + l], entries 0..8 = k*(-A), 9..17 = k*R, so an entry is
-//   ten 16-byte loads from two to three 128-byte lines of that lane.
+//   (24 words), and the per-signature tables entries 0..8 = k*(-A), 9..17 = k*R
+//   (cached points, 40 limbs = ten int4 quads) lane-contiguous: table[(i*18 + e)*40 + l],
+//   so an entry is ten 16-byte loads from two to three 128-byte lines of its lane.
+//   CG_ED_TAB_SOA=1 lays them quad-major across lanes instead (int4
+//   table[(e*10 + q)*scap + i]: each of a wave's ten loads one contiguous 1 KB run, no
+//   over-fetch) — measured slower (r03c, one box: msm 7.11 -> 8.35 ms, points 2.47 ->
+//   3.9 ms per 1 M; an entry's ten quads sit scap * 16 B = 16 MB apart, ten pages per
+//   entry instead of one), so the lane-contiguous layout stays.
 #include "cg_ed25519.h"
 #include "cg_kernels.h"
 
@@ -34,8 +41,23 @@ constexpr int kTabLimbs = 40;  // cached point: 4 fe x 10 limbs
 constexpr int kLaneEntries = 2 * kATabEntries;
 constexpr int kBStride = 32;   // shared-table entry (precomputed point, 3 fe x 10 limbs) padded to one 128-byte line
 
-CG_DEV int4* lane_table(int32_t* table, uint32_t i) {
-  return reinterpret_cast<int4*>(table + (size_t)i * (kLaneEntries * kTabLimbs));
+#ifndef CG_ED_TAB_SOA
+#define CG_ED_TAB_SOA 0
+#endif
+// A lane's view of the per-signature tables: entry k's quad q sits at
+// base[k * kstride + q * qstride].
+struct LaneTab {
+  int4* base;
+  size_t kstride, qstride;
+  CG_DEV int4* entry(uint32_t k) const { return base + (size_t)k * kstride; }
+};
+CG_DEV LaneTab lane_table(int32_t* table, uint32_t i, uint32_t scap) {
+#if CG_ED_TAB_SOA
+  return {reinterpret_cast<int4*>(table) + i, (size_t)(kTabLimbs / 4) * scap, scap};
+#else
+  (void)scap;
+  return {reinterpret_cast<int4*>(table + (size_t)i * (kLaneEntries * kTabLimbs)), kTabLimbs / 4, 1};
+#endif
 }
 
 template <bool REUSE>
@@ -61,7 +83,7 @@ __global__ __launch_bounds__(256) void cg_ed25519_hash(const uint32_t* __restric
   CG_UNROLL for (int w = 0; w < kDigitWords; ++w) digits[(size_t)w * scap + i] = dig[w];
 }
 
-CG_DEV void store_cached(int4* dst, const ge_cached& c) {
+CG_DEV void store_cached(int4* dst, size_t qs, const ge_cached& c) {
   int32_t v[kTabLimbs];
   CG_UNROLL for (int l = 0; l < 10; ++l) {
     v[l] = c.YplusX.v[l];
@@ -69,13 +91,14 @@ CG_DEV void store_cached(int4* dst, const ge_cached& c) {
     v[20 + l] = c.Z.v[l];
     v[30 + l] = c.T2d.v[l];
   }
-  CG_UNROLL for (int q = 0; q < kTabLimbs / 4; ++q) dst[q] = make_int4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+  CG_UNROLL for (int q = 0; q < kTabLimbs / 4; ++q)
+    dst[q * qs] = make_int4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
 }
 
-CG_DEV void load_cached(const int4* src, ge_cached& c) {
+CG_DEV void load_cached(const int4* src, size_t qs, ge_cached& c) {
   int32_t v[kTabLimbs];
   CG_UNROLL for (int q = 0; q < kTabLimbs / 4; ++q) {
-    const int4 x = src[q];
+    const int4 x = src[q * qs];
     v[4 * q] = x.x;
     v[4 * q + 1] = x.y;
     v[4 * q + 2] = x.z;
@@ -94,7 +117,8 @@ CG_DEV void load_cached(const int4* src, ge_cached& c) {
 #endif
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_POINTS_WAVES, 8))) void cg_ed25519_points(const uint32_t* __restrict__ pk,
                                                          const uint32_t* __restrict__ sig, uint32_t n, uint32_t cap,
-                                                         uint32_t* __restrict__ status, int32_t* __restrict__ table) {
+                                                         uint32_t scap, uint32_t* __restrict__ pstat,
+                                                         int32_t* __restrict__ table) {
   CG_WAVE_PRIO(1);
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -103,16 +127,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_POINTS_W
     pkw[w] = pk[(size_t)w * cap + i];
     rw[w] = sig[(size_t)w * cap + i];
   }
-  const uint32_t st = status[i];
+  // independent of the hash kernel (it may run beside it): the points verdict alone
+  // (KEY_INVALID / REJECT for a bad R / COMPUTE); the MSM merges it with the hash's
   ge_p3 negA, R;
-  const uint32_t v = ed25519_points_stage(pkw, rw, ed_status_verdict(st), negA, R);
-  if (v != ed_status_verdict(st)) status[i] = (st & ~0xffu) | v;
+  const uint32_t v = ed25519_points_stage(pkw, rw, V_COMPUTE, negA, R);
+  pstat[i] = v;
   if (v != V_COMPUTE) return;
-  int4* lt = lane_table(table, i);
-  ed25519_build_table(negA, [&](int k, const ge_cached& c) { store_cached(lt + k * (kTabLimbs / 4), c); });
-  ed25519_build_table(R, [&](int k, const ge_cached& c) {
-    store_cached(lt + (kATabEntries + k) * (kTabLimbs / 4), c);
-  });
+  const LaneTab lt = lane_table(table, i, scap);
+  ed25519_build_table(negA, [&](int k, const ge_cached& c) { store_cached(lt.entry(k), lt.qstride, c); });
+  ed25519_build_table(R, [&](int k, const ge_cached& c) { store_cached(lt.entry(kATabEntries + k), lt.qstride, c); });
 }
 
 // Key-reuse path, once per distinct key and verify call: decode A and build its
@@ -132,27 +155,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_POINTS_W
   CG_UNROLL for (int w = 0; w < 8; ++w) pkw[w] = pk[(size_t)w * cap + e];
   int4* kt = key_table(ktab, j);
   kstat[j] = ed25519_key_tables(pkw, [&](int t, int k, const ge_cached& c) CG_LINLINE {
-    store_cached(kt + (t * kATabEntries + k) * (kTabLimbs / 4), c);
+    store_cached(kt + (t * kATabEntries + k) * (kTabLimbs / 4), 1, c);
   });
 }
 
 // Key-reuse path, per signature: decode R only (the key's verdict comes from its
 // distinct-key slot) and build k*R in the lane table.
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_POINTS_WAVES, 8))) void cg_ed25519_points_r(
-    const uint32_t* __restrict__ sig, uint32_t n, uint32_t cap, const uint32_t* __restrict__ key_index,
-    const uint32_t* __restrict__ kstat, uint32_t* __restrict__ status, int32_t* __restrict__ table) {
+    const uint32_t* __restrict__ sig, uint32_t n, uint32_t cap, uint32_t scap, const uint32_t* __restrict__ key_index,
+    const uint32_t* __restrict__ kstat, uint32_t* __restrict__ pstat, int32_t* __restrict__ table) {
   CG_WAVE_PRIO(1);
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint32_t rw[8];
   CG_UNROLL for (int w = 0; w < 8; ++w) rw[w] = sig[(size_t)w * cap + i];
-  const uint32_t st = status[i];
   ge_p3 R;
-  const uint32_t v = ed25519_points_stage_r(rw, ed_status_verdict(st), kstat[key_index[i]], R);
-  if (v != ed_status_verdict(st)) status[i] = (st & ~0xffu) | v;
+  const uint32_t v = ed25519_points_stage_r(rw, V_COMPUTE, kstat[key_index[i]], R);
+  pstat[i] = v;
   if (v != V_COMPUTE) return;
-  int4* lt = lane_table(table, i);
-  ed25519_build_table(R, [&](int k, const ge_cached& c) { store_cached(lt + k * (kTabLimbs / 4), c); });
+  const LaneTab lt = lane_table(table, i, scap);
+  ed25519_build_table(R, [&](int k, const ge_cached& c) { store_cached(lt.entry(k), lt.qstride, c); });
 }
 
 // The shared B tables: entry k of table t = k * 2^(64 t) B in affine form, t = 0..3,
@@ -172,6 +194,14 @@ __global__ __launch_bounds__(256) void cg_ed25519_btab_build(int32_t* __restrict
   o[30] = o[31] = 0;
 }
 
+// The element's verdict from the hash phase's status word and the points phase's
+// verdict (ed25519_points_stage precedence: KEY_INVALID first, then the hash phase's
+// pre-verdict, then a bad R); V_COMPUTE: the MSM decides.
+CG_DEV uint32_t ed_merge_verdict(uint32_t st, uint32_t pv) {
+  const uint32_t vh = ed_status_verdict(st);
+  return pv == V_KEY_INVALID ? pv : vh != V_COMPUTE ? vh : pv;
+}
+
 CG_DEV uint32_t wave_max(uint32_t v) {
   CG_UNROLL for (int o = 32; o >= 1; o >>= 1) {
     const uint32_t u = (uint32_t)__shfl_xor((int)v, o, 64);
@@ -181,28 +211,29 @@ CG_DEV uint32_t wave_max(uint32_t v) {
 }
 
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_MSM_WAVES, CG_MSM_WAVES))) void cg_ed25519_msm(
-    const uint32_t* __restrict__ sig, const uint32_t* __restrict__ status, const uint32_t* __restrict__ digits,
-    const int32_t* __restrict__ table, const int32_t* __restrict__ btab_g, uint32_t n, uint32_t cap, uint32_t scap,
-    const uint32_t* __restrict__ out_index, uint8_t* __restrict__ verdict) {
+    const uint32_t* __restrict__ sig, const uint32_t* __restrict__ status, const uint32_t* __restrict__ pstat,
+    const uint32_t* __restrict__ digits, const int32_t* __restrict__ table, const int32_t* __restrict__ btab_g,
+    uint32_t n, uint32_t cap, uint32_t scap, const uint32_t* __restrict__ out_index, uint8_t* __restrict__ verdict) {
   CG_WAVE_PRIO(0);
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t st = i < n ? status[i] : 0u;
-  const bool live = i < n && ed_status_verdict(st) == V_COMPUTE;
+  const uint32_t v = i < n ? ed_merge_verdict(st, pstat[i]) : 0u;
+  const bool live = i < n && v == V_COMPUTE;
   // every lane of the wave walks the same bit positions: the longest scalar sets the length
   const uint32_t ndig = wave_max(live ? ed_status_ndig(st) : 0u);
   if (i >= n) return;
   const uint32_t dst = out_index ? out_index[i] : i;
   if (!live) {
-    verdict[dst] = (uint8_t)ed_status_verdict(st);
+    verdict[dst] = (uint8_t)v;
     return;
   }
   uint32_t dig[kDigitWords];
   CG_UNROLL for (int w = 0; w < kDigitWords; ++w) dig[w] = digits[(size_t)w * scap + i];
-  const int4* lt = lane_table(const_cast<int32_t*>(table), i);
+  const LaneTab lt = lane_table(const_cast<int32_t*>(table), i, scap);
   const uint32_t ok = ed25519_msm(
       ndig, dig, ed_status_rneg(st),
-      [&](uint32_t k, ge_cached& c) { load_cached(lt + k * (kTabLimbs / 4), c); },
-      [&](uint32_t k, ge_cached& c) { load_cached(lt + (kATabEntries + k) * (kTabLimbs / 4), c); },
+      [&](uint32_t k, ge_cached& c) { load_cached(lt.entry(k), lt.qstride, c); },
+      [&](uint32_t k, ge_cached& c) { load_cached(lt.entry(kATabEntries + k), lt.qstride, c); },
       [&](uint32_t t, uint32_t k, ge_precomp& p) {
         // one 128-byte line per entry: eight 16-byte loads (L2 / MALL resident table)
         const int4* b = reinterpret_cast<const int4*>(btab_g + ((size_t)t * kBTabEntries + k) * kBStride);
@@ -246,32 +277,34 @@ CG_DEV uint32_t wave_or(uint32_t v) { return __ballot(v != 0) != 0ull; }
 // MSM of the key-reuse split (cg_ed25519.h ed25519_msm_reuse): per-key A tables,
 // per-lane R table, four shared B tables; 60 doublings.
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_MSM_WAVES, CG_MSM_WAVES))) void cg_ed25519_msm_r(
-    const uint32_t* __restrict__ status, const uint32_t* __restrict__ digits, const int32_t* __restrict__ table,
-    const int32_t* __restrict__ ktab, const uint32_t* __restrict__ key_index, const int32_t* __restrict__ btab_g,
-    uint32_t n, uint32_t scap, const uint32_t* __restrict__ out_index, uint8_t* __restrict__ verdict) {
+    const uint32_t* __restrict__ status, const uint32_t* __restrict__ pstat, const uint32_t* __restrict__ digits,
+    const int32_t* __restrict__ table, const int32_t* __restrict__ ktab, const uint32_t* __restrict__ key_index,
+    const int32_t* __restrict__ btab_g, uint32_t n, uint32_t scap, const uint32_t* __restrict__ out_index,
+    uint8_t* __restrict__ verdict) {
   CG_WAVE_PRIO(0);
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t st = i < n ? status[i] : 0u;
-  const bool live = i < n && ed_status_verdict(st) == V_COMPUTE;
+  const uint32_t v = i < n ? ed_merge_verdict(st, pstat[i]) : 0u;
+  const bool live = i < n && v == V_COMPUTE;
   // wave-uniform loop shape: the most chunk-3 windows and a 17th c1 digit in any lane
   const uint32_t shape = live ? ed_status_ndig(st) : 0u;
   const uint32_t c3w = wave_max(shape & 31u), win17 = wave_or(shape >> 5);
   if (i >= n) return;
   const uint32_t dst = out_index ? out_index[i] : i;
   if (!live) {
-    verdict[dst] = (uint8_t)ed_status_verdict(st);
+    verdict[dst] = (uint8_t)v;
     return;
   }
   uint32_t dig[kDigitWords];
   CG_UNROLL for (int w = 0; w < kDigitWords; ++w) dig[w] = digits[(size_t)w * scap + i];
-  const int4* lt = lane_table(const_cast<int32_t*>(table), i);
+  const LaneTab lt = lane_table(const_cast<int32_t*>(table), i, scap);
   const int4* kt = key_table(const_cast<int32_t*>(ktab), key_index[i]);
   const uint32_t ok = ed25519_msm_reuse(
       c3w, win17, dig, ed_status_rneg(st),
       [&](uint32_t t, uint32_t k, ge_cached& c) CG_LINLINE {
-        load_cached(kt + (t * kATabEntries + k) * (kTabLimbs / 4), c);
+        load_cached(kt + (t * kATabEntries + k) * (kTabLimbs / 4), 1, c);
       },
-      [&](uint32_t k, ge_cached& c) CG_LINLINE { load_cached(lt + k * (kTabLimbs / 4), c); },
+      [&](uint32_t k, ge_cached& c) CG_LINLINE { load_cached(lt.entry(k), lt.qstride, c); },
       [&](uint32_t t, uint32_t k, ge_precomp& p) CG_LINLINE { load_bentry(btab_g, t, k, p); });
   verdict[dst] = ok ? (uint8_t)V_ACCEPT : (uint8_t)V_REJECT;
 }
@@ -281,6 +314,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_MSM_WAVE
 namespace cg {
 
 size_t ed25519_table_bytes(uint32_t scap) { return (size_t)kLaneEntries * kTabLimbs * scap * sizeof(int32_t); }
+size_t ed25519_table_offset(uint32_t lanes) {  // int32 offset of lane `lanes` (the base of a sub-range's view)
+  return CG_ED_TAB_SOA ? (size_t)lanes * 4 : (size_t)kLaneEntries * kTabLimbs * lanes;
+}
 size_t ed25519_digit_words() { return kDigitWords; }
 size_t ed25519_btab_words() { return (size_t)kBTables * kBTabEntries * kBStride; }
 size_t ed25519_key_table_bytes(uint32_t n_keys) { return (size_t)kKeyEntries * kTabLimbs * n_keys * sizeof(int32_t); }
@@ -313,11 +349,11 @@ hipError_t launch_ed25519_keyprep(const Ed25519Dev& d, const uint32_t* key_first
 hipError_t launch_ed25519_points(const Ed25519Dev& d, uint32_t n, hipStream_t s) {
   if (n == 0) return hipSuccess;
   if (d.key_index)
-    hipLaunchKernelGGL(cg_ed25519_points_r, dim3((n + 255) / 256), dim3(256), 0, s, d.sig, n, d.cap, d.key_index,
-                       d.kstat, d.status, d.table);
+    hipLaunchKernelGGL(cg_ed25519_points_r, dim3((n + 255) / 256), dim3(256), 0, s, d.sig, n, d.cap, d.scap,
+                       d.key_index, d.kstat, d.pstat, d.table);
   else
-    hipLaunchKernelGGL(cg_ed25519_points, dim3((n + 255) / 256), dim3(256), 0, s, d.pk, d.sig, n, d.cap, d.status,
-                       d.table);
+    hipLaunchKernelGGL(cg_ed25519_points, dim3((n + 255) / 256), dim3(256), 0, s, d.pk, d.sig, n, d.cap, d.scap,
+                       d.pstat, d.table);
   return hipGetLastError();
 }
 
@@ -325,11 +361,11 @@ hipError_t launch_ed25519_msm(const Ed25519Dev& d, uint32_t n, const uint32_t* o
                               hipStream_t s) {
   if (n == 0) return hipSuccess;
   if (d.key_index)
-    hipLaunchKernelGGL(cg_ed25519_msm_r, dim3((n + 255) / 256), dim3(256), 0, s, d.status, d.digits, d.table, d.ktab,
-                       d.key_index, d.btab, n, d.scap, out_index, verdict);
+    hipLaunchKernelGGL(cg_ed25519_msm_r, dim3((n + 255) / 256), dim3(256), 0, s, d.status, d.pstat, d.digits, d.table,
+                       d.ktab, d.key_index, d.btab, n, d.scap, out_index, verdict);
   else
-    hipLaunchKernelGGL(cg_ed25519_msm, dim3((n + 255) / 256), dim3(256), 0, s, d.sig, d.status, d.digits, d.table,
-                       d.btab, n, d.cap, d.scap, out_index, verdict);
+    hipLaunchKernelGGL(cg_ed25519_msm, dim3((n + 255) / 256), dim3(256), 0, s, d.sig, d.status, d.pstat, d.digits,
+                       d.table, d.btab, n, d.cap, d.scap, out_index, verdict);
   return hipGetLastError();
 }
 

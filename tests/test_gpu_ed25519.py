@@ -344,3 +344,35 @@ def test_host_verify_pipeline_small_chunks_vs_oracle(gpu_ctx, oracle, monkeypatc
         assert bad.size == 0, [(int(i), int(schemes[i]), int(got[i]), int(exp[i])) for i in bad[:10]]
         assert np.array_equal(bm.view(np.int32), D.pack_bits(exp == ACCEPT).view(np.int32))
     assert (exp == ACCEPT).sum() > 0.6 * n
+
+
+@pytest.mark.parametrize("chunks", [None, "5"])
+def test_compact_ed25519_layout_vs_oracle(gpu_ctx, oracle, monkeypatch, chunks):
+    """The layout an Ed25519-only JVM caller packs (and bench.py's end-to-end line times):
+    scheme_id NULL, 32-byte key rows, 64-byte R||S rows and sig_len NULL — and the same
+    with sig_len given when some rows are ragged (E12: 0 / 63 / 65 bytes, sig_stride 68).
+    Verdicts in both modes against the oracle on the full-layout rows."""
+    if chunks:
+        monkeypatch.setenv("CORDA_AMD_VERIFY_CHUNKS", chunks)
+        monkeypatch.setenv("CORDA_AMD_VERIFY_MIN_CHUNK", "300")
+    w = datagen.add_ed25519_adversarial(datagen.make_batch(4000, msg_bytes=200, seed=41, key_base=700_000),
+                                        frac=0.2, seed=13)
+    sl = w.sig_len[:w.n].astype(np.uint32)
+    ragged = sl != 64
+    assert ragged.any()
+    for mode in (MODE_IS_VALID, MODE_DO_VERIFY):
+        exp = oracle_verdicts(oracle, w, mode)
+        # every row 64 bytes: the ragged rows leave, so the layout with sig_len NULL is exact
+        keep = np.flatnonzero(~ragged)
+        s = w.subset(keep)
+        b = crypto.PackedBatch(s.n, None, np.ascontiguousarray(s.pk[:, :32]), 32,
+                               np.ascontiguousarray(s.sig[:, :64]), 64, None, s.msg, s.msg_off, s.msg_len)
+        got = crypto.verify_packed(gpu_ctx, b, mode)
+        assert np.array_equal(got, exp[keep]), np.flatnonzero(got != exp[keep])[:10]
+        # ragged rows with their lengths (65-byte rows need a wider stride)
+        sg = np.zeros((w.n, 68), np.uint8)
+        sg[:, :min(68, w.sig_stride)] = w.sig[:w.n, :min(68, w.sig_stride)]
+        b = crypto.PackedBatch(w.n, None, np.ascontiguousarray(w.pk[:w.n, :32]), 32, sg, 68, sl, w.msg, w.msg_off,
+                               w.msg_len)
+        got = crypto.verify_packed(gpu_ctx, b, mode)
+        assert np.array_equal(got, exp), np.flatnonzero(got != exp)[:10]
