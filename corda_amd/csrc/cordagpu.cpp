@@ -44,7 +44,7 @@ constexpr uint32_t kEdChunk = 1u << 21;  // Ed25519 scratch chunk (elements)
 // cg_batch_verify of a large Ed25519 subset: pieces on two streams (launch_verify);
 // CORDA_AMD_ED_SPLIT overrides the count, pieces stay >= kEdSplitMin elements
 constexpr uint32_t kEdSplitMin = 65536;
-constexpr uint32_t kEdSplitDefault = 4;
+constexpr uint32_t kEdSplitDefault = 1;  // r03d A/B: 2 or 4 pieces measured no faster (95-96 M/s either way)
 
 struct Stat {
   double ms = 0;
@@ -1215,7 +1215,11 @@ std::vector<size_t> verify_chunk_bounds(size_t n) {
   if (const char* e = std::getenv("CORDA_AMD_VERIFY_MIN_CHUNK")) min_chunk = std::max(1, std::atoi(e));
   if (const char* e = std::getenv("CORDA_AMD_VERIFY_HEAD")) head = std::min(2.0, std::max(0.05, std::atof(e)));
   if (const char* e = std::getenv("CORDA_AMD_VERIFY_TAIL")) tail = std::min(2.0, std::max(0.05, std::atof(e)));
-  const size_t K = std::max<size_t>(1, std::min<size_t>(kmax, n / min_chunk));
+  // below 2^17 elements one chunk is fastest (r03b sweep, 65,536 x 1 KB pageable: 2.38 ms
+  // as one chunk, 2.70 ms as two: every chunk adds a serial ~0.7 ms kernel chain)
+  const bool tuned = std::getenv("CORDA_AMD_VERIFY_MIN_CHUNK") || std::getenv("CORDA_AMD_VERIFY_CHUNKS");
+  const size_t whole = tuned ? 0 : (size_t)1 << 17;
+  const size_t K = n < whole ? 1 : std::max<size_t>(1, std::min<size_t>(kmax, n / min_chunk));
   std::vector<size_t> b(K + 1, 0);
   std::vector<double> w(K, 1.0);
   if (K > 1) {
