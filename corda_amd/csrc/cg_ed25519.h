@@ -162,8 +162,12 @@ CG_HD uint32_t ed25519_points_stage(const uint32_t pk[8], const uint32_t r[8], u
                                     ge_p3& R) {
   ge_p3 P[2];
   uint32_t ok[2];
+// CG_ED_PAIR_DECODE = 1 interleaves the two square roots (fe_pow22523_pair): more ILP
+// but 256 VGPRs with ~31 spilled; the two decodes one after the other need 234 and
+// spill nothing, and measured as fast or ~1 % faster with the points kernel running
+// beside the hash kernel (r03f A/B: 97.8 / 96.1 vs 96.8 / 95.2 M verifies/s).
 #ifndef CG_ED_PAIR_DECODE
-#define CG_ED_PAIR_DECODE 1
+#define CG_ED_PAIR_DECODE 0
 #endif
 #if CG_ED_PAIR_DECODE
   const uint32_t* const w[2] = {pk, r};

@@ -250,6 +250,7 @@ CG_HD void f26_norm(f26& h) {
 // product on them).  Two or three independent products run interleaved
 // (f26_pair / f26_triple) so consecutive mads never depend on each other.
 struct F26MulOp {
+  static constexpr int kTerms = 10;  // products per column at most
   int32_t f[10], g[10];
   CG_HDM F26MulOp(const f26& F, const f26& G) {
     CG_UNROLL for (int i = 0; i < 10; ++i) {
@@ -267,11 +268,14 @@ struct F26MulOp {
 };
 // f^2: 45 cross products against pre-doubled limbs + 10 squares
 struct F26SqrOp {
-  int32_t f[10], f2[10];
-  CG_HDM explicit F26SqrOp(const f26& F) {
+  static constexpr int kTerms = 10;
+  int32_t f[10], f2[10];  // a side (f = s F, f2 = 2 s F), b side fb = F
+  int32_t fb[10];
+  CG_HDM explicit F26SqrOp(const f26& F, int32_t scale = 1) {
     CG_UNROLL for (int i = 0; i < 10; ++i) {
-      f[i] = F.v[i];
-      f2[i] = f26_pin(2 * F.v[i]);
+      f[i] = scale == 1 ? F.v[i] : f26_pin(scale * F.v[i]);
+      f2[i] = f26_pin(2 * scale * F.v[i]);
+      fb[i] = F.v[i];
     }
   }
   // n-th product of column k: i = max(0, k - 9) + n, up to i = k / 2 (j = k - i >= i)
@@ -283,7 +287,19 @@ struct F26SqrOp {
     const int i = (k > 9 ? k - 9 : 0) + n;
     return 2 * i == k ? f[i] : f2[i];
   }
-  CG_HDM int32_t b(int k, int n) const { return f[k - ((k > 9 ? k - 9 : 0) + n)]; }
+  CG_HDM int32_t b(int k, int n) const { return fb[k - ((k > 9 ? k - 9 : 0) + n)]; }
+};
+// The column products of two ops in one chain: op0's, then op1's — a sum of two
+// products that takes ONE Montgomery reduction (the point formulas' "P0 - P1" outputs).
+template <typename Op0, typename Op1>
+struct F26SumOp {
+  static constexpr int kTerms = Op0::kTerms + Op1::kTerms;
+  Op0 o0;
+  Op1 o1;
+  CG_HDM F26SumOp(const Op0& a, const Op1& b) : o0(a), o1(b) {}
+  CG_HDM bool has(int k, int n) const { return n < Op0::kTerms ? o0.has(k, n) : o1.has(k, n - Op0::kTerms); }
+  CG_HDM int32_t a(int k, int n) const { return n < Op0::kTerms ? o0.a(k, n) : o1.a(k, n - Op0::kTerms); }
+  CG_HDM int32_t b(int k, int n) const { return n < Op0::kTerms ? o0.b(k, n) : o1.b(k, n - Op0::kTerms); }
 };
 
 template <class C>
@@ -294,7 +310,7 @@ struct F26Chain {
   template <typename Op>
   CG_HDM void column(f26& h, const Op& op, int k) {
     int64_t acc = c;
-    CG_UNROLL for (int n = 0; n < 10; ++n) {
+    CG_UNROLL for (int n = 0; n < Op::kTerms; ++n) {
       if (op.has(k, n)) acc = f26_pin64(acc + (int64_t)op.a(k, n) * op.b(k, n));
     }
     acc = F26<C>::red_terms(k, m, acc);
@@ -342,6 +358,42 @@ template <class C>
 CG_HD void f26_sqr(f26& h, const f26& f) {
   CG_BOUNDS26_MUL(f, f);
   f26_chain<C>(h, F26SqrOp(f));
+}
+
+// h = (f g - s q^2) R^-1 (one reduction; s a small scale, e.g. 8) and
+// h = (f g - u v) R^-1.  Inputs' c products summed must stay within the 80 budget.
+#if defined(CG_CHECK_BOUNDS) && !defined(__HIP_DEVICE_COMPILE__)
+inline void cg_bounds26_sum(const f26& f, const f26& g, const f26& u, const f26& v, int64_t su) {
+  CgBounds26& b = cg_bounds26();
+  __int128 col[19] = {0};
+  for (int i = 0; i < 10; ++i)
+    for (int j = 0; j < 10; ++j) col[i + j] += (__int128)f.v[i] * g.v[j] + (__int128)su * u.v[i] * v.v[j];
+  for (int k = 0; k < 19; ++k) {
+    const __int128 a = col[k] < 0 ? -col[k] : col[k];
+    if (a > b.max_col) b.max_col = a;
+    if (a >= ((__int128)1 << 62)) {
+      fprintf(stderr, "cg bounds (f26 sum): column %d = 2^%.2f\n", k, __builtin_log2((double)a));
+      __builtin_trap();
+    }
+  }
+}
+#define CG_BOUNDS26_SUM(f, g, u, v, su) cg_bounds26_sum(f, g, u, v, su)
+#else
+#define CG_BOUNDS26_SUM(f, g, u, v, su) ((void)0)
+#endif
+template <class C>
+CG_HD void f26_mul_sub_sq(f26& h, const f26& f, const f26& g, const f26& q, int32_t s) {
+  CG_BOUNDS26_MUL(f, g);
+  CG_BOUNDS26_SUM(f, g, q, q, -(int64_t)s);
+  f26_chain<C>(h, F26SumOp<F26MulOp, F26SqrOp>(F26MulOp(f, g), F26SqrOp(q, -s)));
+}
+template <class C>
+CG_HD void f26_mul_sub_mul(f26& h, const f26& f, const f26& g, const f26& u, const f26& v) {
+  CG_BOUNDS26_MUL(f, g);
+  CG_BOUNDS26_SUM(f, g, u, v, -1);
+  f26 nu;
+  f26_neg(nu, u);
+  f26_chain<C>(h, F26SumOp<F26MulOp, F26MulOp>(F26MulOp(f, g), F26MulOp(nu, v)));
 }
 
 // Two independent products interleaved (outputs may alias inputs).
