@@ -245,6 +245,18 @@ CG_HD bool fe_col_asm(int64_t& c0, const FeColOps& x0, int64_t& c1, const FeColO
   return false;
 }
 
+CG_HD bool fe_col_asm(int64_t& c0, const FeColOps& x0, int64_t& c1, const FeColOps& x1, int64_t& c2,
+                      const FeColOps& x2, int64_t& c3, const FeColOps& x3) {
+#if defined(__HIP_DEVICE_COMPILE__) && CG_FE_ASM_COL
+  if (x0.n == 10 && x1.n == 10 && x2.n == 10 && x3.n == 10)
+    return fe_asm_col4_10(c0, c1, c2, c3, x0, x1, x2, x3), true;
+  if (x0.n == 6 && x1.n == 6 && x2.n == 6 && x3.n == 6) return fe_asm_col4_6(c0, c1, c2, c3, x0, x1, x2, x3), true;
+  if (x0.n == 5 && x1.n == 5 && x2.n == 5 && x3.n == 5) return fe_asm_col4_5(c0, c1, c2, c3, x0, x1, x2, x3), true;
+#endif
+  (void)c0, (void)x0, (void)c1, (void)x1, (void)c2, (void)x2, (void)c3, (void)x3;
+  return false;
+}
+
 // ---------------------------------------------------------------------------
 // Products.  A product is ten column chains of v_mad_i64_i32 (column k collects
 // f_i g_j for i + j = k, and 19 f_i g_j for i + j = k + 10; products of two odd
@@ -441,6 +453,41 @@ CG_HD void fe_fold_triple(fe& h0, const Op0& op0, fe& h1, const Op1& op1, fe& h2
   fe_fold_finish<Op2::kFloor>(h2, s2);
 }
 
+// Four chains in lockstep (CG_FE_QUAD: the point formulas' four independent products).
+template <typename Op0, typename Op1, typename Op2, typename Op3>
+CG_HD void fe_fold_quad(fe& h0, const Op0& op0, fe& h1, const Op1& op1, fe& h2, const Op2& op2, fe& h3,
+                        const Op3& op3) {
+  CG_BOUNDS_CHAIN(op0);
+  CG_BOUNDS_CHAIN(op1);
+  CG_BOUNDS_CHAIN(op2);
+  CG_BOUNDS_CHAIN(op3);
+  FeFoldState s0, s1, s2, s3;
+  s0.c = s1.c = s2.c = s3.c = 0;
+  CG_UNROLL for (int k = 0; k < 10; ++k) {
+    s0.acc = s0.c;
+    s1.acc = s1.c;
+    s2.acc = s2.c;
+    s3.acc = s3.c;
+    if (!fe_col_asm(s0.acc, fe_col_ops(op0, k), s1.acc, fe_col_ops(op1, k), s2.acc, fe_col_ops(op2, k), s3.acc,
+                    fe_col_ops(op3, k))) {
+      CG_UNROLL for (int i = 0; i < 10; ++i) {
+        s0.acc = op0(k, i, s0.acc);
+        s1.acc = op1(k, i, s1.acc);
+        s2.acc = op2(k, i, s2.acc);
+        s3.acc = op3(k, i, s3.acc);
+      }
+    }
+    fe_fold_carry<Op0::kFloor>(s0, k);
+    fe_fold_carry<Op1::kFloor>(s1, k);
+    fe_fold_carry<Op2::kFloor>(s2, k);
+    fe_fold_carry<Op3::kFloor>(s3, k);
+  }
+  fe_fold_finish<Op0::kFloor>(h0, s0);
+  fe_fold_finish<Op1::kFloor>(h1, s1);
+  fe_fold_finish<Op2::kFloor>(h2, s2);
+  fe_fold_finish<Op3::kFloor>(h3, s3);
+}
+
 // Product descriptors (the op objects copy their inputs, so outputs may alias any
 // source).  Suffix F = floor carries; Mul2 / Sq2 = doubled product.
 template <bool FLOOR, int SCALE>
@@ -479,6 +526,15 @@ template <typename A, typename B, typename C>
 CG_HD void fe_triple(fe& h0, const A& a, fe& h1, const B& b, fe& h2, const C& c) {
   fe_fold_triple(h0, fe_op(a), h1, fe_op(b), h2, fe_op(c));
 }
+template <typename A, typename B, typename C, typename D>
+CG_HD void fe_quad(fe& h0, const A& a, fe& h1, const B& b, fe& h2, const C& c, fe& h3, const D& d) {
+  fe_fold_quad(h0, fe_op(a), h1, fe_op(b), h2, fe_op(c), h3, fe_op(d));
+}
+// CG_FE_QUAD = 1: the point formulas run their four independent products as one
+// 4-chain group instead of two pairs (more ILP, more live registers).
+#ifndef CG_FE_QUAD
+#define CG_FE_QUAD 0
+#endif
 
 // h = f * g, f^2, 2 f^2 (rounding carries: limbs |h_k| <= 2^(w-1) + small)
 CG_HD void fe_mul(fe& h, const fe& f, const fe& g) { fe_one(h, FeMul{f, g}); }

@@ -376,3 +376,28 @@ def test_compact_ed25519_layout_vs_oracle(gpu_ctx, oracle, monkeypatch, chunks):
                                w.msg_len)
         got = crypto.verify_packed(gpu_ctx, b, mode)
         assert np.array_equal(got, exp), np.flatnonzero(got != exp)[:10]
+
+
+@pytest.mark.parametrize("split,overlap,signers", [("2", "1", 0), ("3", "0", 0), ("2", "1", 40)])
+def test_prepared_batch_split_and_overlap_vs_oracle(gpu_ctx, oracle, monkeypatch, split, overlap, signers):
+    """cg_batch_verify's scheduling variants on one prepared batch: the Ed25519 subset as
+    index pieces on two streams (CORDA_AMD_ED_SPLIT, pieces >= 65,536), the points kernel
+    beside the hash kernel or after it (CORDA_AMD_ED_OVERLAP), distinct signers and 40
+    repeated ones (the key-reuse path: both lanes wait for the per-key tables) — verdicts
+    and accept bitmap identical to the oracle's, verified twice."""
+    monkeypatch.setenv("CORDA_AMD_ED_SPLIT", split)
+    monkeypatch.setenv("CORDA_AMD_ED_OVERLAP", overlap)
+    n = 3 * 65536 + 777
+    w = datagen.make_batch(n, msg_bytes=32, seed=51, key_base=800_000, key_reuse=signers)
+    w = datagen.add_ed25519_adversarial(w, frac=0.02, seed=19)
+    adv = np.array([c != "valid" for c in w.classes])
+    check = np.union1d(np.flatnonzero(adv), np.arange(0, n, 997))
+    exp_sub = oracle_verdicts(oracle, w.subset(check), MODE_IS_VALID)
+    b = crypto.PackedBatch(w.n, w.scheme, w.pk, w.pk_stride, w.sig, w.sig_stride, w.sig_len, w.msg, w.msg_off,
+                           w.msg_len)
+    pb = crypto.PreparedBatch(gpu_ctx, b)
+    for _ in range(2):
+        got = pb.verify(MODE_IS_VALID)
+        assert (got[~adv] == ACCEPT).all()
+        assert np.array_equal(got[check], exp_sub)
+    pb.close()
