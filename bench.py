@@ -448,29 +448,29 @@ def run_ed25519(args, dist):
 
     elapsed = timed(dist, ctx, step, args.steps, args.warmup)
     ks = kstats(ctx, ED_KERNELS + ED_REUSE_KERNELS)
-    ks_step, split_note = None, None
-    if ks.get("ed25519_msm", {}).get("launches", 0) > args.steps:
-        # the step ran the batch as index pieces on two streams (launch_verify's split), so a
-        # piece's kernel overlaps another piece's and its HIP-event span is stretched: the
-        # roofline takes each kernel alone, from a short pass with the split off (same batch)
-        ks_step = ks
-        prev = os.environ.get("CORDA_AMD_ED_SPLIT")
-        os.environ["CORDA_AMD_ED_SPLIT"] = "1"
-        try:
-            ctx.set_profiling(True)
-            ctx.reset_stats()
-            for _ in range(3):
-                step()
-            ks = kstats(ctx, ED_KERNELS + ED_REUSE_KERNELS)
-            ctx.set_profiling(False)
-        finally:
-            if prev is None:
-                del os.environ["CORDA_AMD_ED_SPLIT"]
+    # In the timed step the points kernel runs beside the hash kernel (CORDA_AMD_ED_OVERLAP) and a
+    # split batch runs as pieces on two streams, so those HIP-event spans overlap: the per-kernel
+    # times and the roofline come from 3 extra steps with both off (each kernel alone over the
+    # whole batch); the timed step's own spans are kept as kernels_in_step.
+    ks_step = ks
+    prev = {k: os.environ.get(k) for k in ("CORDA_AMD_ED_SPLIT", "CORDA_AMD_ED_OVERLAP")}
+    os.environ["CORDA_AMD_ED_SPLIT"] = "1"
+    os.environ["CORDA_AMD_ED_OVERLAP"] = "0"
+    try:
+        ctx.set_profiling(True)
+        ctx.reset_stats()
+        for _ in range(3):
+            step()
+        ks = kstats(ctx, ED_KERNELS + ED_REUSE_KERNELS)
+        ctx.set_profiling(False)
+    finally:
+        for k, v in prev.items():
+            if v is None:
+                os.environ.pop(k, None)
             else:
-                os.environ["CORDA_AMD_ED_SPLIT"] = prev
-        split_note = (f"the timed step ran the batch as {ks_step['ed25519_msm']['launches'] // args.steps} pieces on "
-                      "two streams (kernels_in_step: per-piece spans, overlapped); kernels / roofline: 3 extra "
-                      "steps with CORDA_AMD_ED_SPLIT=1, each kernel over the whole batch alone")
+                os.environ[k] = v
+    split_note = ("kernels / roofline: 3 extra steps with CORDA_AMD_ED_SPLIT=1 CORDA_AMD_ED_OVERLAP=0 (each kernel "
+                  "alone over the whole batch); kernels_in_step: the timed steps' own spans (points beside hash)")
 
     # verdict check (outside the timed region): untouched elements must accept
     verdict = pb.verify(MODE_IS_VALID)
@@ -564,7 +564,7 @@ def run_ed25519(args, dist):
         "prep_kernels": {k: {"achieved": v["achieved"], "frac": v["frac"], "avg_launch_ms": v["avg_launch_ms"],
                              "valu_instr_per_unit": v["valu_instr_per_unit"]} for k, v in prep.items()},
         "kernels": ks,
-        **({"kernels_in_step": ks_step, "kernel_timing_note": split_note} if ks_step else {}),
+        "kernels_in_step": ks_step, "kernel_timing_note": split_note,
         "latency": {"p50_device_ms": round(statistics.median(lat_dev) * 1e3, 3) if lat_dev else None,
                     "p50_e2e_ms": round(statistics.median(lat_e2e) * 1e3, 3) if lat_e2e else None,
                     "e2e_batch": e2e_n, "runs": args.latency_runs,
