@@ -60,7 +60,13 @@ def main():
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "e2e_sweep.json"))
     ap.add_argument("--sizes", default="4096,16384,65536,262144")
     ap.add_argument("--runs", type=int, default=15)
+    ap.add_argument("--grid", default=None,
+                    help="settings to try instead of the built-in list: ';'-separated, each ','-separated "
+                         "VAR=value pairs ('' = library defaults), e.g. 'CORDA_AMD_VERIFY_HEAD=0.25;'")
+    ap.add_argument("--pageable-only", action="store_true")
     a = ap.parse_args()
+    settings = SETTINGS if a.grid is None else [
+        dict(kv.split("=", 1) for kv in g.split(",") if kv) for g in a.grid.split(";")]
     import datagen
     from corda_amd import Context, crypto
     from corda_amd._lib import ACCEPT, MODE_IS_VALID
@@ -73,10 +79,10 @@ def main():
             b = crypto.PackedBatch(s.n, None, np.ascontiguousarray(s.pk[:, :32]), 32,
                                    np.ascontiguousarray(s.sig[:, :64]), 64, None, s.msg, s.msg_off, s.msg_len)
             nbytes = sum(x.nbytes for x in (b.pk, b.sig, b.msg, b.msg_off, b.msg_len))
-            for pinned in (False, True):
+            for pinned in ((False,) if a.pageable_only else (False, True)):
                 if pinned:
                     ctx.register_host(b.pk, b.sig, b.msg, b.msg_off, b.msg_len)
-                for st in SETTINGS:
+                for st in settings:
                     for k in KEYS:
                         os.environ.pop(k, None)
                     os.environ.update(st)
