@@ -369,13 +369,7 @@ CG_HD uint32_t ecdsa_prep(const uint32_t qx[8], const uint32_t qy[8], uint32_t d
 #ifndef CG_EC_PREFETCH
 #define CG_EC_PREFETCH 1
 #endif
-// CG_EC_COMPACT = 1: one addition site for both digits of a window (see the loop).
-#ifndef CG_EC_COMPACT
-#define CG_EC_COMPACT 0
-#endif
-#if CG_EC_COMPACT && CG_EC_PREFETCH
-#error "CG_EC_COMPACT and CG_EC_PREFETCH are alternative loop shapes"
-#endif
+
 template <class C, typename GetQ, typename GetG>
 CG_HD void ecdsa_joint(jpt& acc, uint32_t d1[9], uint32_t d2[9], GetQ&& getQ, GetG&& getG) {
   jpt t, tg;
@@ -409,21 +403,6 @@ CG_HD void ecdsa_joint(jpt& acc, uint32_t d1[9], uint32_t d2[9], GetQ&& getQ, Ge
     constexpr uint32_t kHalf = 1u << (kGWin - 1);
     const uint32_t nq = eq < 8, aq = nq ? 8 - eq : eq - 8;
     const uint32_t ng = eg < kHalf, ag = ng ? kHalf - eg : eg - kHalf;
-#if CG_EC_COMPACT
-    // one mixed-addition site for the Q digit and the G digit (a rolled loop over the
-    // two slots): the window's loop body holds one ec_add instead of two
-    CG_NOUNROLL for (uint32_t slot = 0; slot < 1 + has_g; ++slot) {
-      const uint32_t neg = slot ? ng : nq, a = slot ? ag : aq;
-      if (slot) getG(a == 0 ? 1u : a, t);
-      else getQ(a == 0 ? 1u : a, t);
-      f26 ny;
-      f26_neg(ny, t.Y);
-      f26_select(t.Y, t.Y, ny, neg);
-      t.inf = 0;
-      ec_add<C, true>(acc, acc, t, a == 0);
-    }
-    continue;
-#endif
 #if CG_EC_PREFETCH
     getQ(aq == 0 ? 1u : aq, t);
     if (has_g) getG(ag == 0 ? 1u : ag, tg);
@@ -648,49 +627,6 @@ CG_HD void ecdsa_joint_glv(jpt& acc, uint32_t nd, uint32_t dk1[9], uint32_t dk2[
     }
     dk1[0] <<= 4;
     dk2[0] <<= 4;
-#if CG_EC_COMPACT
-    // one mixed-addition site for all of the window's digits: Q, phi(Q), then (every
-    // fourth window) the G / 2^128 G table digits
-    const bool gwin = (i & 3) == 0 && i <= 32;
-    uint32_t eg = 0, eh = gtop;
-    if (gwin && i != 32) {
-      eg = glo[3] >> 16;
-      eh = ghi[3] >> 16;
-      CG_UNROLL for (int w = 3; w > 0; --w) {
-        glo[w] = glo[w] << 16 | glo[w - 1] >> 16;
-        ghi[w] = ghi[w] << 16 | ghi[w - 1] >> 16;
-      }
-      glo[0] <<= 16;
-      ghi[0] <<= 16;
-    }
-    const uint32_t skip = i == 32 ? 1u : 0u, nslot = gwin ? 4u - skip : 2u;
-    CG_NOUNROLL for (uint32_t s = 0; s < nslot; ++s) {
-      const uint32_t slot = s < 2 ? s : s + skip;
-      uint32_t neg, a;
-      if (slot < 2) {
-        const uint32_t e = slot ? e2 : e1;
-        neg = (e < 8) ^ (slot ? neg2 : neg1);
-        a = e < 8 ? 8 - e : e - 8;
-        getQ(a == 0 ? 1u : a, t);
-        if (slot) {
-          f26 beta;
-          F26<C>::beta(beta);
-          f26_mul<C>(t.X, t.X, beta);  // phi(X:Y:Z) = (beta X : Y : Z)
-        }
-      } else {
-        const uint32_t e = slot == 3 ? eh : eg;
-        neg = e < 0x8000u;
-        a = neg ? 0x8000u - e : e - 0x8000u;
-        getG(slot - 2, a == 0 ? 1u : a, t);
-      }
-      f26 ny;
-      f26_neg(ny, t.Y);
-      f26_select(t.Y, t.Y, ny, neg);
-      t.inf = 0;
-      ec_add<C, true>(acc, acc, t, a == 0);
-    }
-    continue;
-#endif
     // +-|digit| * Q, then +-|digit| * phi(Q): one add site in a rolled loop keeps
     // the register footprint of a single Jacobian addition
     CG_NOUNROLL for (uint32_t slot = 0; slot < 2; ++slot) {

@@ -42,9 +42,6 @@ constexpr int kATabEntries = 9;                          // per-lane tables, 4-b
 constexpr int kBTabEntries = (1 << (kBWin - 1)) + 1;     // shared tables, |d| <= 2^(kBWin-1)
 constexpr int kDigitWords = 24;    // A nibbles (8) | R nibbles (8) | B digits (8 words, 256 bits)
 constexpr int kMinDigits = 32;     // the loop always covers bit positions 0..127 (B tables)
-#ifndef CG_MSM_COMPACT
-#define CG_MSM_COMPACT 0
-#endif
 
 // Status word of the hash/points phases: verdict (bits 0-7; V_COMPUTE while the
 // MSM must decide), radix-16 digit count (bits 8-15), R sign flag (bit 16).
@@ -323,10 +320,6 @@ CG_HD uint32_t ed25519_msm(uint32_t ndig, const uint32_t dig[kDigitWords], uint3
   // digit is added to the identity (no doublings).  The A entry of a window is
   // loaded before its four doublings (40 VGPRs held across them), so the load's
   // latency hides under ~3,600 VALU instructions instead of stalling the addition.
-  // CG_MSM_COMPACT = 1: one p1p1 -> p3 + cached-addition site serves both slots (A,
-  // then R) and one p1p1 -> p3 + mixed-addition site both B tables (rolled loops): the
-  // kernel's code 164 KB -> 63 KB, but the MSM measured 1.5 % slower (r03e, one box:
-  // 7.08-7.12 vs 6.97-7.01 ms per 1 M), so instruction fetch is not what holds it back.
   const int nwin = (int)ndig;
   CG_NOUNROLL for (int j = nwin - 1; j >= 0; --j) {
     const uint32_t ea = da[7] >> 28, er = dr[7] >> 28;
@@ -351,37 +344,6 @@ CG_HD uint32_t ed25519_msm(uint32_t ndig, const uint32_t dig[kDigitWords], uint3
       bh[3] >>= kBWin;
     }
     getA(na ? 8 - ea : ea - 8, ca);
-#if CG_MSM_COMPACT
-    int s0 = 0;
-    if (j != nwin - 1) {
-      CG_NOUNROLL for (int k = 0; k < 3; ++k) {
-        ge_p1p1_to_p2(r2, t);
-        ge_p2_dbl<false>(t, r2);
-      }
-      ge_p1p1_to_p2(r2, t);
-      ge_p2_dbl<true>(t, r2);  // the additions follow (ge_p1p1_to_p3)
-    } else {
-      ge_add_cached(t, ge_identity_p3(), ca, na);  // constant operand: mostly folded away
-      s0 = 1;
-    }
-    uint32_t neg = na;
-    CG_NOUNROLL for (int s = s0; s < 2; ++s) {  // slot 0: A (entry loaded above), slot 1: R
-      if (s) {
-        getR(nr ? 8 - er : er - 8, ca);
-        neg = nr ^ rneg;
-      }
-      ge_p1p1_to_p3(r3, t);
-      ge_add_cached(t, r3, ca, neg);
-    }
-    if (bwin) {
-      CG_NOUNROLL for (int tb = 0; tb < 2; ++tb) {
-        const uint32_t e = tb ? eh : el, nb = e < kHalf;
-        getB(2 * tb, nb ? kHalf - e : e - kHalf, pb);
-        ge_p1p1_to_p3<true>(r3, t);
-        ge_madd(t, r3, pb, nb);
-      }
-    }
-#else
     const uint32_t nl = el < kHalf, nh = eh < kHalf;
     if (j != nwin - 1) {
       CG_NOUNROLL for (int k = 0; k < 3; ++k) {
@@ -406,7 +368,6 @@ CG_HD uint32_t ed25519_msm(uint32_t ndig, const uint32_t dig[kDigitWords], uint3
       ge_p1p1_to_p3<true>(r3, t);
       ge_madd(t, r3, pb, nh);
     }
-#endif
   }
   // identity <=> x = X/Z = 0 and y = Y/T = 1
   fe d;
