@@ -2187,6 +2187,120 @@ uint32_t pmt_scan(size_t n_ftx, const uint32_t* node_start, const uint8_t* node_
 
 bool hash_less(const std::array<uint8_t, 32>& a, const std::array<uint8_t, 32>& b) { return a < b; }
 
+// cg_ftx_verify_batch's device part as a pipeline over ftx-index chunks (the
+// non-validating notary's whole crypto path is host bytes in, one status byte out;
+// round 2 uploaded everything, then hashed: PCIe and kernels back to back).  Chunk k's
+// rows — the arena prefix its components reach, their offsets / lengths / nonces, its
+// node programs, roots and host-scanned status — go out on copy_stream while chunk k-1's
+// leaf hashes and tree evaluations run on ctx->stream; each chunk's node programs are
+// scanned on the host (depth, malformed) right before its upload, so that scan overlaps
+// the earlier chunks' copies.  Kernels index components and nodes absolutely (the chunk
+// passes offset comp_start / node_start / roots / status pointers), so results land in
+// place.  CORDA_AMD_FTX_CHUNKS / _MIN_CHUNK override the split.
+cg_status ftx_pipeline(cg_ctx* ctx, size_t n_ftx, const uint8_t* arena, size_t arena_bytes, const uint64_t* comp_off,
+                       const uint32_t* comp_len, const uint32_t* comp_start, const uint8_t* nonces,
+                       const uint32_t* node_start, const uint8_t* node_kind, const uint8_t* node_hash,
+                       const uint8_t* root_hashes, uint8_t* result_out, size_t n_comp, size_t n_node, TxDev& d,
+                       uint32_t*& nonces_d, uint32_t*& node_start_d, uint8_t*& kind_d, uint32_t*& node_hash_d,
+                       uint32_t*& roots_d, uint8_t*& status_d, std::vector<uint32_t*>& stacks,
+                       std::vector<hipEvent_t>& ev) {
+  size_t kmax = 6, min_chunk = 65536;
+  if (const char* e = std::getenv("CORDA_AMD_FTX_CHUNKS")) kmax = std::max(1, std::atoi(e));
+  if (const char* e = std::getenv("CORDA_AMD_FTX_MIN_CHUNK")) min_chunk = std::max(1, std::atoi(e));
+  const size_t K = std::max<size_t>(1, std::min<size_t>(kmax, n_ftx / min_chunk));
+  std::vector<size_t> tb(K + 1);
+  for (size_t k = 0; k <= K; ++k) tb[k] = k == K ? n_ftx : n_ftx * k / K;
+  cg_status st;
+  if ((st = dalloc(ctx, &d.arena, arena_bytes + 16, "alloc ftx arena")) != CG_OK ||
+      (st = dalloc(ctx, &d.comp_off, std::max<size_t>(n_comp, 1), "alloc comp_off")) != CG_OK ||
+      (st = dalloc(ctx, &d.comp_len, std::max<size_t>(n_comp, 1), "alloc comp_len")) != CG_OK ||
+      (st = dalloc(ctx, &d.comp_start, n_ftx + 1, "alloc comp_start")) != CG_OK ||
+      (st = dalloc(ctx, &nonces_d, 8 * std::max<size_t>(n_comp, 1), "alloc nonces")) != CG_OK ||
+      (st = dalloc(ctx, &d.comp_tx, std::max<size_t>(n_comp, 1), "alloc comp_tx")) != CG_OK ||
+      (st = dalloc(ctx, &d.leaves, 8 * std::max<size_t>(n_comp, 1), "alloc leaves")) != CG_OK ||
+      (st = dalloc(ctx, &node_start_d, n_ftx + 1, "alloc node_start")) != CG_OK ||
+      (st = dalloc(ctx, &kind_d, std::max<size_t>(n_node, 1), "alloc node_kind")) != CG_OK ||
+      (st = dalloc(ctx, &node_hash_d, 8 * std::max<size_t>(n_node, 1), "alloc node_hash")) != CG_OK ||
+      (st = dalloc(ctx, &roots_d, 8 * n_ftx, "alloc roots")) != CG_OK ||
+      (st = dalloc(ctx, &status_d, n_ftx, "alloc status")) != CG_OK)
+    return st;
+  // the host-scanned status bytes go out through page-locked staging (a pageable copy
+  // would hold the host); without it they are copied from result_out, which the final
+  // download overwrites
+  uint8_t* host_status = result_out;
+  if (ctx->pin_cap < n_ftx) {
+    if (ctx->pin) (void)hipHostFree(ctx->pin);  // idle: every earlier call ended with a sync
+    ctx->pin = nullptr;
+    ctx->pin_cap = 0;
+    if (hipHostMalloc((void**)&ctx->pin, n_ftx, hipHostMallocDefault) == hipSuccess) ctx->pin_cap = n_ftx;
+    else (void)hipGetLastError();
+  }
+  if (ctx->pin_cap >= n_ftx) host_status = ctx->pin;
+  ev.assign(K, nullptr);
+  for (hipEvent_t& e : ev) CG_TRY(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming), "ftx pipeline event");
+  CG_TRY(ctx, hipMemsetAsync(ctx->err_flag, 0, 4, ctx->stream), "clear error flag");
+  CG_TRY(ctx, hipMemsetAsync(d.arena + arena_bytes, 0, 16, ctx->copy_stream), "pad ftx arena");
+  std::vector<uint32_t> depth(K, 1);
+  uint64_t up_to = 0;
+  hipStream_t cs = ctx->copy_stream;
+  auto enqueue_upload = [&](size_t k) -> cg_status {
+    const size_t t0 = tb[k], t1 = tb[k + 1];
+    const size_t c0 = comp_start[t0], c1 = comp_start[t1], j0 = node_start[t0], j1 = node_start[t1];
+    depth[k] = pmt_scan(t1 - t0, node_start + t0, node_kind, host_status + t0);
+    const uint64_t from = up_to;
+    for (size_t c = c0; c < c1; ++c)
+      up_to = std::max<uint64_t>(up_to, std::min<uint64_t>(comp_off[c] + comp_len[c], arena_bytes));
+    Timed t(ctx, "h2d_ftx", (up_to - from) + (c1 - c0) * 44 + (j1 - j0) * 33 + (t1 - t0) * 41, cs);
+    auto put = [&](void* dst, const void* src, size_t bytes, const char* what) -> cg_status {
+      if (bytes) CG_TRY(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, cs), what);
+      return CG_OK;
+    };
+    cg_status s2;
+    if ((s2 = put(d.arena + from, arena + from, up_to - from, "upload ftx arena")) != CG_OK ||
+        (s2 = put(d.comp_off + c0, comp_off + c0, (c1 - c0) * 8, "upload comp_off")) != CG_OK ||
+        (s2 = put(d.comp_len + c0, comp_len + c0, (c1 - c0) * 4, "upload comp_len")) != CG_OK ||
+        (s2 = put(d.comp_start + t0, comp_start + t0, (t1 - t0 + 1) * 4, "upload comp_start")) != CG_OK ||
+        (s2 = put(nonces_d + 8 * c0, nonces + 32 * c0, (c1 - c0) * 32, "upload nonces")) != CG_OK ||
+        (s2 = put(node_start_d + t0, node_start + t0, (t1 - t0 + 1) * 4, "upload node_start")) != CG_OK ||
+        (s2 = put(kind_d + j0, node_kind + j0, j1 - j0, "upload node_kind")) != CG_OK ||
+        (s2 = put(node_hash_d + 8 * j0, node_hash + 32 * j0, (j1 - j0) * 32, "upload node_hash")) != CG_OK ||
+        (s2 = put(roots_d + 8 * t0, root_hashes + 32 * t0, (t1 - t0) * 32, "upload roots")) != CG_OK ||
+        (s2 = put(status_d + t0, host_status + t0, t1 - t0, "upload status")) != CG_OK)
+      return s2;
+    CG_TRY(ctx, hipEventRecord(ev[k], cs), "ftx pipeline record");
+    return CG_OK;
+  };
+  if ((st = enqueue_upload(0)) != CG_OK) return st;
+  if (K > 1 && (st = enqueue_upload(1)) != CG_OK) return st;
+  for (size_t k = 0; k < K; ++k) {
+    const size_t t0 = tb[k], t1 = tb[k + 1], nk = t1 - t0;
+    const uint32_t c0 = comp_start[t0], c1 = comp_start[t1];
+    uint32_t* stack = nullptr;
+    if ((st = dalloc(ctx, &stack, (size_t)8 * depth[k] * std::max<size_t>(nk, 1), "alloc pmt stack")) != CG_OK) return st;
+    stacks.push_back(stack);
+    CG_TRY(ctx, hipStreamWaitEvent(ctx->stream, ev[k], 0), "ftx pipeline wait");
+    CG_TRY(ctx, cg::launch_tx_index(d.comp_start + t0, nullptr, (uint32_t)nk, d.comp_tx, nullptr, nullptr, ctx->stream),
+           "launch tx index");
+    {
+      Timed tm(ctx, "merkle_leaf", c1 - c0);
+      CG_TRY(ctx,
+             cg::launch_merkle_leaf(d.arena, arena_bytes, d.comp_off, d.comp_len, d.comp_start + t0, d.comp_tx, nullptr,
+                                    nonces_d, c0, c1, d.leaves, ctx->err_flag, ctx->stream),
+             "launch merkle leaf");
+    }
+    {
+      Timed tm(ctx, "pmt_eval", nk);
+      CG_TRY(ctx,
+             cg::launch_pmt_eval(node_start_d + t0, kind_d, node_hash_d, d.comp_start + t0, d.leaves, roots_d + 8 * t0,
+                                 (uint32_t)nk, stack, status_d + t0, ctx->stream),
+             "launch pmt eval");
+    }
+    if (k + 2 < K && (st = enqueue_upload(k + 2)) != CG_OK) return st;
+  }
+  CG_TRY(ctx, hipMemcpyAsync(result_out, status_d, n_ftx, hipMemcpyDeviceToHost, ctx->stream), "download ftx status");
+  return CG_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -2206,50 +2320,15 @@ cg_status cg_ftx_verify_batch(cg_ctx* ctx, size_t n_ftx, const uint8_t* arena, s
     if (comp_start[t + 1] < comp_start[t] || node_start[t + 1] < node_start[t])
       return fail(ctx, CG_E_INVALID_ARGUMENT, "comp_start / node_start not monotone");
   if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, CG_E_DEVICE, "hipSetDevice");
-  std::vector<uint8_t> status(n_ftx);
-  uint32_t depth = 1;
   const size_t n_comp = comp_start[n_ftx], n_node = node_start[n_ftx];
   TxDev d;
-  uint32_t *nonces_d = nullptr, *node_start_d = nullptr, *node_hash_d = nullptr, *roots_d = nullptr,
-           *stack_d = nullptr;
+  uint32_t *nonces_d = nullptr, *node_start_d = nullptr, *node_hash_d = nullptr, *roots_d = nullptr;
   uint8_t *kind_d = nullptr, *status_d = nullptr;
-  cg_status st;
-  if ((st = dalloc(ctx, &d.arena, arena_bytes + 16, "alloc ftx arena")) == CG_OK &&
-      (st = upload(ctx, &d.comp_off, comp_off, n_comp, "upload comp_off")) == CG_OK &&
-      (st = upload(ctx, &d.comp_len, comp_len, n_comp, "upload comp_len")) == CG_OK &&
-      (st = upload(ctx, &d.comp_start, comp_start, n_ftx + 1, "upload comp_start")) == CG_OK &&
-      (st = upload(ctx, &nonces_d, (const uint32_t*)nonces, 8 * n_comp, "upload nonces")) == CG_OK &&
-      (st = dalloc(ctx, &d.comp_tx, n_comp, "alloc comp_tx")) == CG_OK &&
-      (st = dalloc(ctx, &d.leaves, 8 * n_comp, "alloc leaves")) == CG_OK &&
-      (st = upload(ctx, &node_start_d, node_start, n_ftx + 1, "upload node_start")) == CG_OK &&
-      (st = upload(ctx, &kind_d, node_kind, n_node, "upload node_kind")) == CG_OK &&
-      (st = upload(ctx, &node_hash_d, (const uint32_t*)node_hash, 8 * n_node, "upload node_hash")) == CG_OK &&
-      (st = upload(ctx, &roots_d, (const uint32_t*)root_hashes, 8 * n_ftx, "upload roots")) == CG_OK &&
-      (st = (arena_bytes ? hip_ok(ctx, hipMemcpyAsync(d.arena, arena, arena_bytes, hipMemcpyHostToDevice, ctx->stream),
-                                  "upload ftx arena")
-                         : CG_OK)) == CG_OK &&
-      // the host pass over the node programs runs while the uploads above are in flight
-      (depth = pmt_scan(n_ftx, node_start, node_kind, status.data()), true) &&
-      (st = upload(ctx, &status_d, status.data(), n_ftx, "upload status")) == CG_OK &&
-      (st = dalloc(ctx, &stack_d, (size_t)8 * depth * n_ftx, "alloc pmt stack")) == CG_OK) {
-    hipError_t e = hipSuccess;
-    if (e == hipSuccess) e = hipMemsetAsync(d.arena + arena_bytes, 0, 16, ctx->stream);
-    if (e == hipSuccess) e = hipMemsetAsync(ctx->err_flag, 0, 4, ctx->stream);
-    if (e == hipSuccess)
-      e = cg::launch_tx_index(d.comp_start, nullptr, (uint32_t)n_ftx, d.comp_tx, nullptr, nullptr, ctx->stream);
-    if (e == hipSuccess) {
-      Timed tm(ctx, "merkle_leaf", n_comp);
-      e = cg::launch_merkle_leaf(d.arena, arena_bytes, d.comp_off, d.comp_len, d.comp_start, d.comp_tx, nullptr,
-                                 nonces_d, 0, (uint32_t)n_comp, d.leaves, ctx->err_flag, ctx->stream);
-    }
-    if (e == hipSuccess) {
-      Timed tm(ctx, "pmt_eval", n_ftx);
-      e = cg::launch_pmt_eval(node_start_d, kind_d, node_hash_d, d.comp_start, d.leaves, roots_d, (uint32_t)n_ftx,
-                              stack_d, status_d, ctx->stream);
-    }
-    if (e == hipSuccess) e = hipMemcpyAsync(result_out, status_d, n_ftx, hipMemcpyDeviceToHost, ctx->stream);
-    if (e != hipSuccess) st = hip_fail(ctx, e, "ftx verify");
-  }
+  std::vector<uint32_t*> stacks;
+  std::vector<hipEvent_t> ev;
+  cg_status st = ftx_pipeline(ctx, n_ftx, arena, arena_bytes, comp_off, comp_len, comp_start, nonces, node_start,
+                              node_kind, node_hash, root_hashes, result_out, n_comp, n_node, d, nonces_d,
+                              node_start_d, kind_d, node_hash_d, roots_d, status_d, stacks, ev);
   if (st == CG_OK) st = read_err_flag(ctx);
   // txs whose root matched but whose included-leaf multiset is too large for one lane:
   // compare sorted hash lists here (the hashes were computed on the device)
@@ -2283,9 +2362,13 @@ cg_status cg_ftx_verify_batch(cg_ctx* ctx, size_t n_ftx, const uint8_t* arena, s
     result_out[t] = a == b ? cg::kPmtTrue : cg::kPmtFalse;
   }
   (void)hipStreamSynchronize(ctx->stream);
+  (void)hipStreamSynchronize(ctx->copy_stream);
   for (const void* p : {(const void*)nonces_d, (const void*)node_start_d, (const void*)node_hash_d,
-                        (const void*)roots_d, (const void*)stack_d, (const void*)kind_d, (const void*)status_d})
+                        (const void*)roots_d, (const void*)kind_d, (const void*)status_d})
     dfree(ctx, p);
+  for (uint32_t* p : stacks) dfree(ctx, p);
+  for (hipEvent_t e : ev)
+    if (e) (void)hipEventDestroy(e);
   d.release(ctx);
   collect_timings(ctx);
   return st;

@@ -175,8 +175,18 @@ def _ftx_call(ctx, a, n):
     return out
 
 
+@pytest.fixture(params=[None, ("5", "3")], ids=["ftx-default-chunks", "ftx-5-chunks"])
+def ftx_chunks(request, monkeypatch):
+    """cg_ftx_verify_batch's upload/kernel pipeline: library defaults, and forced onto
+    5 small ftx-index chunks (CORDA_AMD_FTX_CHUNKS / _MIN_CHUNK)."""
+    if request.param:
+        monkeypatch.setenv("CORDA_AMD_FTX_CHUNKS", request.param[0])
+        monkeypatch.setenv("CORDA_AMD_FTX_MIN_CHUNK", request.param[1])
+    return request.param
+
+
 @pytest.mark.gpu
-def test_ftx_golden(gpu_ctx, golden_ftx):
+def test_ftx_golden(gpu_ctx, golden_ftx, ftx_chunks):
     """Every FilteredTransaction fixture (PartialMerkleTreeTest.kt cases recast, deep
     chain, > 256 included leaves, malformed programs) in one device batch, then each
     row alone (no cross-row state)."""
@@ -212,7 +222,7 @@ def test_ftx_python_mirror(gpu_ctx, golden_ftx):
 
 
 @pytest.mark.gpu
-def test_ftx_notary_shapes_vs_oracle(gpu_ctx, oracle):
+def test_ftx_notary_shapes_vs_oracle(gpu_ctx, oracle, ftx_chunks):
     """Config-4 transactions filtered as NotaryFlow.kt:72 does (inputs + time window),
     tiled with 5 % adversarial copies, against the C oracle and the generator's truth."""
     w = datagen.tile_ftx_batch(datagen.make_ftx_batch(3000, seed=21), 20000, adversarial=0.05, seed=3)
