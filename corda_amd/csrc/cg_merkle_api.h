@@ -31,6 +31,9 @@ hipError_t launch_first_bad(const uint8_t* verdict, const uint32_t* sig_start, u
 enum : uint8_t { kPmtTrue = 0, kPmtFalse = 1, kPmtNoLeaves = 2, kPmtMalformed = 3, kPmtHostCheck = 4 };
 enum : uint8_t { kPmtIncluded = 0, kPmtLeaf = 1, kPmtNode = 2 };
 constexpr uint32_t kPmtMaxLane = 256;
+// Node-program well-formedness (status) and per-wave deepest stack (depth_w[(n + 63) / 64]).
+hipError_t launch_pmt_scan(const uint32_t* node_start, const uint8_t* node_kind, uint32_t n, uint8_t* status,
+                           uint32_t* depth_w, hipStream_t s);
 hipError_t launch_pmt_eval(const uint32_t* node_start, const uint8_t* node_kind, const uint32_t* node_hash,
                            const uint32_t* comp_start, const uint32_t* leaves, const uint32_t* roots, uint32_t n,
                            uint32_t* stack, uint8_t* status, hipStream_t s);

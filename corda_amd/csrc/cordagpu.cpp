@@ -967,6 +967,12 @@ cg_status join_ecdsa_streams(cg_ctx* ctx) {
 // (the verify pipeline runs two chunks at once on disjoint halves); 0 otherwise.
 // Ed25519 points kernels beside the hash kernels on `pts_stream` (null: after them on
 // the same stream); CORDA_AMD_ED_OVERLAP=0 turns it off.
+// CORDA_AMD_ED_FUSE=1: the balanced path's points and MSM kernels as one kernel
+bool ed_fuse_enabled() {
+  const char* e = std::getenv("CORDA_AMD_ED_FUSE");
+  return e && std::atoi(e) != 0;
+}
+
 bool ed_overlap_enabled() {
   const char* e = std::getenv("CORDA_AMD_ED_OVERLAP");
   return !e || std::atoi(e) != 0;
@@ -1070,6 +1076,7 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = 
       hipStream_t ed_lane[2] = {ctx->stream, ctx->hash_stream};
       // prepared-batch verify (this call owns the streams): points beside hash on the idle copy stream
       hipStream_t pts = pts_stream ? pts_stream : (join_streams && ed_overlap_enabled() ? ctx->copy_stream : nullptr);
+      const bool fuse = ed_fuse_enabled();
       if (split > 1) {
         CG_TRY(ctx, hipStreamWaitEvent(ctx->hash_stream, ctx->ev_fork, 0), "fork ed25519 split");
       }
@@ -1104,6 +1111,19 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = 
           d.key_index = b->ed_key_index + base;
           d.ktab = ctx->ed_ktab;
           d.kstat = ctx->ed_kstat;
+        }
+        if (fuse && !b->ed_key_index) {  // points + MSM as one kernel after the hash kernel
+          {
+            Timed t(ctx, "ed25519_hash", cnt);
+            CG_TRY(ctx, cg::launch_ed25519_hash(d, cnt, (uint32_t)mode, ctx->stream), "launch ed25519_hash");
+          }
+          Timed t(ctx, "ed25519_points_msm", cnt);
+          CG_TRY(ctx,
+                 cg::launch_ed25519_points_msm(d, cnt, b->ed_index ? b->ed_index + base : nullptr,
+                                               b->ed_index ? b->verdict : b->verdict + base, ctx->stream),
+                 "launch ed25519_points_msm");
+          base += cnt;
+          continue;
         }
         if (pts) {
           // the points kernel needs only the rows (ready where this lane stands now):
@@ -2160,41 +2180,16 @@ cg_status cg_tx_verify_signatures_except(cg_ctx* ctx, int mode, size_t n_tx, con
 
 namespace {
 
-// Host pass over the post-order node programs: each must be exactly one tree
-// (kinds 0..2, a Node never underflows, one value left).  Returns the deepest
-// stack any tx needs; malformed txs get kPmtMalformed in status.
-uint32_t pmt_scan(size_t n_ftx, const uint32_t* node_start, const uint8_t* node_kind, uint8_t* status) {
-  uint32_t max_depth = 1;
-  for (size_t t = 0; t < n_ftx; ++t) {
-    uint64_t sp = 0, deepest = 0;
-    bool bad = node_start[t + 1] == node_start[t];
-    for (uint32_t j = node_start[t]; j < node_start[t + 1] && !bad; ++j) {
-      const uint8_t k = node_kind[j];
-      if (k == cg::kPmtIncluded || k == cg::kPmtLeaf) {
-        deepest = ++sp > deepest ? sp : deepest;
-      } else if (k == cg::kPmtNode && sp >= 2) {
-        --sp;
-      } else {
-        bad = true;
-      }
-    }
-    bad = bad || sp != 1;
-    status[t] = bad ? cg::kPmtMalformed : cg::kPmtTrue;
-    if (!bad && deepest > max_depth) max_depth = (uint32_t)deepest;
-  }
-  return max_depth;
-}
-
 bool hash_less(const std::array<uint8_t, 32>& a, const std::array<uint8_t, 32>& b) { return a < b; }
 
 // cg_ftx_verify_batch's device part as a pipeline over ftx-index chunks (the
 // non-validating notary's whole crypto path is host bytes in, one status byte out;
-// round 2 uploaded everything, then hashed: PCIe and kernels back to back).  Chunk k's
-// rows — the arena prefix its components reach, their offsets / lengths / nonces, its
-// node programs, roots and host-scanned status — go out on copy_stream while chunk k-1's
-// leaf hashes and tree evaluations run on ctx->stream; each chunk's node programs are
-// scanned on the host (depth, malformed) right before its upload, so that scan overlaps
-// the earlier chunks' copies.  Kernels index components and nodes absolutely (the chunk
+// round 2 uploaded everything, then hashed: PCIe and kernels back to back).  Every
+// chunk's rows — the arena prefix its components reach, their offsets / lengths /
+// nonces, its node programs and roots — go out on copy_stream back to back; chunk k's
+// node programs are then scanned on the host (depth, malformed) while the copies run,
+// its status bytes go out on hash_stream, and its leaf hashes and tree evaluation run on
+// ctx->stream as soon as both are in, beside the later chunks' copies.  Kernels index components and nodes absolutely (the chunk
 // passes offset comp_start / node_start / roots / status pointers), so results land in
 // place.  CORDA_AMD_FTX_CHUNKS / _MIN_CHUNK override the split.
 cg_status ftx_pipeline(cg_ctx* ctx, size_t n_ftx, const uint8_t* arena, size_t arena_bytes, const uint64_t* comp_off,
@@ -2224,18 +2219,23 @@ cg_status ftx_pipeline(cg_ctx* ctx, size_t n_ftx, const uint8_t* arena, size_t a
       (st = dalloc(ctx, &roots_d, 8 * n_ftx, "alloc roots")) != CG_OK ||
       (st = dalloc(ctx, &status_d, n_ftx, "alloc status")) != CG_OK)
     return st;
-  // the host-scanned status bytes go out through page-locked staging (a pageable copy
-  // would hold the host); without it they are copied from result_out, which the final
-  // download overwrites
-  uint8_t* host_status = result_out;
-  if (ctx->pin_cap < n_ftx) {
+  // per-wave deepest stacks of each chunk's node programs come back through page-locked
+  // memory (the evaluation stack is sized from their maximum)
+  const size_t dw_words = ((n_ftx + 255) / 256) * 4 + 4 * K;
+  uint32_t* depth_w_d = nullptr;
+  if ((st = dalloc(ctx, &depth_w_d, dw_words, "alloc pmt depths")) != CG_OK) return st;
+  stacks.push_back(depth_w_d);  // freed with the stacks
+  if (ctx->pin_cap < dw_words * 4) {
     if (ctx->pin) (void)hipHostFree(ctx->pin);  // idle: every earlier call ended with a sync
     ctx->pin = nullptr;
     ctx->pin_cap = 0;
-    if (hipHostMalloc((void**)&ctx->pin, n_ftx, hipHostMallocDefault) == hipSuccess) ctx->pin_cap = n_ftx;
-    else (void)hipGetLastError();
+    if (hipHostMalloc((void**)&ctx->pin, dw_words * 4, hipHostMallocDefault) != hipSuccess) {
+      (void)hipGetLastError();
+      return fail(ctx, CG_E_OUT_OF_MEMORY, "page-locked staging for the pmt depths");
+    }
+    ctx->pin_cap = dw_words * 4;
   }
-  if (ctx->pin_cap >= n_ftx) host_status = ctx->pin;
+  uint32_t* depth_w_h = (uint32_t*)ctx->pin;
   ev.assign(K, nullptr);
   for (hipEvent_t& e : ev) CG_TRY(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming), "ftx pipeline event");
   CG_TRY(ctx, hipMemsetAsync(ctx->err_flag, 0, 4, ctx->stream), "clear error flag");
@@ -2243,42 +2243,64 @@ cg_status ftx_pipeline(cg_ctx* ctx, size_t n_ftx, const uint8_t* arena, size_t a
   std::vector<uint32_t> depth(K, 1);
   uint64_t up_to = 0;
   hipStream_t cs = ctx->copy_stream;
-  auto enqueue_upload = [&](size_t k) -> cg_status {
+  auto put = [&](void* dst, const void* src, size_t bytes, hipStream_t q, const char* what) -> cg_status {
+    if (bytes) CG_TRY(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, q), what);
+    return CG_OK;
+  };
+  // 1. every chunk's bulk rows on copy_stream, back to back (the host work in between is
+  //    one pass over the chunk's component offsets); event ev[k]
+  for (size_t k = 0; k < K; ++k) {
     const size_t t0 = tb[k], t1 = tb[k + 1];
     const size_t c0 = comp_start[t0], c1 = comp_start[t1], j0 = node_start[t0], j1 = node_start[t1];
-    depth[k] = pmt_scan(t1 - t0, node_start + t0, node_kind, host_status + t0);
     const uint64_t from = up_to;
     for (size_t c = c0; c < c1; ++c)
       up_to = std::max<uint64_t>(up_to, std::min<uint64_t>(comp_off[c] + comp_len[c], arena_bytes));
-    Timed t(ctx, "h2d_ftx", (up_to - from) + (c1 - c0) * 44 + (j1 - j0) * 33 + (t1 - t0) * 41, cs);
-    auto put = [&](void* dst, const void* src, size_t bytes, const char* what) -> cg_status {
-      if (bytes) CG_TRY(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, cs), what);
-      return CG_OK;
-    };
-    cg_status s2;
-    if ((s2 = put(d.arena + from, arena + from, up_to - from, "upload ftx arena")) != CG_OK ||
-        (s2 = put(d.comp_off + c0, comp_off + c0, (c1 - c0) * 8, "upload comp_off")) != CG_OK ||
-        (s2 = put(d.comp_len + c0, comp_len + c0, (c1 - c0) * 4, "upload comp_len")) != CG_OK ||
-        (s2 = put(d.comp_start + t0, comp_start + t0, (t1 - t0 + 1) * 4, "upload comp_start")) != CG_OK ||
-        (s2 = put(nonces_d + 8 * c0, nonces + 32 * c0, (c1 - c0) * 32, "upload nonces")) != CG_OK ||
-        (s2 = put(node_start_d + t0, node_start + t0, (t1 - t0 + 1) * 4, "upload node_start")) != CG_OK ||
-        (s2 = put(kind_d + j0, node_kind + j0, j1 - j0, "upload node_kind")) != CG_OK ||
-        (s2 = put(node_hash_d + 8 * j0, node_hash + 32 * j0, (j1 - j0) * 32, "upload node_hash")) != CG_OK ||
-        (s2 = put(roots_d + 8 * t0, root_hashes + 32 * t0, (t1 - t0) * 32, "upload roots")) != CG_OK ||
-        (s2 = put(status_d + t0, host_status + t0, t1 - t0, "upload status")) != CG_OK)
-      return s2;
+    Timed t(ctx, "h2d_ftx", (up_to - from) + (c1 - c0) * 44 + (j1 - j0) * 33 + (t1 - t0) * 40, cs);
+    if ((st = put(d.arena + from, arena + from, up_to - from, cs, "upload ftx arena")) != CG_OK ||
+        (st = put(d.comp_off + c0, comp_off + c0, (c1 - c0) * 8, cs, "upload comp_off")) != CG_OK ||
+        (st = put(d.comp_len + c0, comp_len + c0, (c1 - c0) * 4, cs, "upload comp_len")) != CG_OK ||
+        (st = put(d.comp_start + t0, comp_start + t0, (t1 - t0 + 1) * 4, cs, "upload comp_start")) != CG_OK ||
+        (st = put(nonces_d + 8 * c0, nonces + 32 * c0, (c1 - c0) * 32, cs, "upload nonces")) != CG_OK ||
+        (st = put(node_start_d + t0, node_start + t0, (t1 - t0 + 1) * 4, cs, "upload node_start")) != CG_OK ||
+        (st = put(kind_d + j0, node_kind + j0, j1 - j0, cs, "upload node_kind")) != CG_OK ||
+        (st = put(node_hash_d + 8 * j0, node_hash + 32 * j0, (j1 - j0) * 32, cs, "upload node_hash")) != CG_OK ||
+        (st = put(roots_d + 8 * t0, root_hashes + 32 * t0, (t1 - t0) * 32, cs, "upload roots")) != CG_OK)
+      return st;
     CG_TRY(ctx, hipEventRecord(ev[k], cs), "ftx pipeline record");
-    return CG_OK;
-  };
-  if ((st = enqueue_upload(0)) != CG_OK) return st;
-  if (K > 1 && (st = enqueue_upload(1)) != CG_OK) return st;
+  }
+  // 2. per chunk: its node programs checked on the device (k_pmt_scan: status, per-wave
+  //    deepest stack) as soon as its rows are in, the depths read back (the host waits
+  //    for this chunk's copy, not for later ones), then its leaf and tree kernels
+  hipEvent_t ev_depth = nullptr;
+  struct EvFree {
+    hipEvent_t& e;
+    ~EvFree() {
+      if (e) (void)hipEventDestroy(e);
+    }
+  } ev_depth_free{ev_depth};
+  CG_TRY(ctx, hipEventCreateWithFlags(&ev_depth, hipEventDisableTiming), "ftx pipeline event");
+  size_t dw_off = 0;
   for (size_t k = 0; k < K; ++k) {
     const size_t t0 = tb[k], t1 = tb[k + 1], nk = t1 - t0;
     const uint32_t c0 = comp_start[t0], c1 = comp_start[t1];
+    const size_t nw = ((nk + 255) / 256) * 4;
+    CG_TRY(ctx, hipStreamWaitEvent(ctx->stream, ev[k], 0), "ftx pipeline wait");
+    {
+      Timed tm(ctx, "pmt_scan", nk);
+      CG_TRY(ctx, cg::launch_pmt_scan(node_start_d + t0, kind_d, (uint32_t)nk, status_d + t0, depth_w_d + dw_off,
+                                      ctx->stream),
+             "launch pmt scan");
+    }
+    CG_TRY(ctx, hipMemcpyAsync(depth_w_h + dw_off, depth_w_d + dw_off, nw * 4, hipMemcpyDeviceToHost, ctx->stream),
+           "download pmt depths");
+    CG_TRY(ctx, hipEventRecord(ev_depth, ctx->stream), "ftx pipeline record");
+    CG_TRY(ctx, hipEventSynchronize(ev_depth), "ftx pipeline depths");
+    depth[k] = 1;
+    for (size_t w = 0; w < nw; ++w) depth[k] = std::max(depth[k], depth_w_h[dw_off + w]);
+    dw_off += nw;
     uint32_t* stack = nullptr;
     if ((st = dalloc(ctx, &stack, (size_t)8 * depth[k] * std::max<size_t>(nk, 1), "alloc pmt stack")) != CG_OK) return st;
     stacks.push_back(stack);
-    CG_TRY(ctx, hipStreamWaitEvent(ctx->stream, ev[k], 0), "ftx pipeline wait");
     CG_TRY(ctx, cg::launch_tx_index(d.comp_start + t0, nullptr, (uint32_t)nk, d.comp_tx, nullptr, nullptr, ctx->stream),
            "launch tx index");
     {
@@ -2295,7 +2317,6 @@ cg_status ftx_pipeline(cg_ctx* ctx, size_t n_ftx, const uint8_t* arena, size_t a
                                  (uint32_t)nk, stack, status_d + t0, ctx->stream),
              "launch pmt eval");
     }
-    if (k + 2 < K && (st = enqueue_upload(k + 2)) != CG_OK) return st;
   }
   CG_TRY(ctx, hipMemcpyAsync(result_out, status_d, n_ftx, hipMemcpyDeviceToHost, ctx->stream), "download ftx status");
   return CG_OK;
@@ -2363,6 +2384,7 @@ cg_status cg_ftx_verify_batch(cg_ctx* ctx, size_t n_ftx, const uint8_t* arena, s
   }
   (void)hipStreamSynchronize(ctx->stream);
   (void)hipStreamSynchronize(ctx->copy_stream);
+  (void)hipStreamSynchronize(ctx->hash_stream);
   for (const void* p : {(const void*)nonces_d, (const void*)node_start_d, (const void*)node_hash_d,
                         (const void*)roots_d, (const void*)kind_d, (const void*)status_d})
     dfree(ctx, p);

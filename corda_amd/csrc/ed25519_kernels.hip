@@ -37,7 +37,13 @@ namespace {
 #define CG_MSM_WAVES 2
 #endif
 
-constexpr int kTabLimbs = 40;  // cached point: 4 fe x 10 limbs
+// CG_ED_TAB_PACK = 1: a table entry is its four coordinates as canonical 255-bit values
+// (8 words each): 128 B = one cache line per entry instead of 160 B over two or three;
+// the points kernel canonicalises on store, the MSM unpacks (floor-shaped limbs).
+#ifndef CG_ED_TAB_PACK
+#define CG_ED_TAB_PACK 1
+#endif
+constexpr int kTabLimbs = CG_ED_TAB_PACK ? 32 : 40;  // words per cached point: 4 fe x 8 packed / 10 limbs
 constexpr int kLaneEntries = 2 * kATabEntries;
 constexpr int kBStride = 32;   // shared-table entry (precomputed point, 3 fe x 10 limbs) padded to one 128-byte line
 
@@ -84,6 +90,16 @@ __global__ __launch_bounds__(256) void cg_ed25519_hash(const uint32_t* __restric
 }
 
 CG_DEV void store_cached(int4* dst, size_t qs, const ge_cached& c) {
+#if CG_ED_TAB_PACK
+  uint32_t w[4][8];
+  fe_tobytes(w[0], c.YplusX);
+  fe_tobytes(w[1], c.YminusX);
+  fe_tobytes(w[2], c.Z);
+  fe_tobytes(w[3], c.T2d);
+  CG_UNROLL for (int f = 0; f < 4; ++f)
+    CG_UNROLL for (int h = 0; h < 2; ++h)
+      dst[(2 * f + h) * qs] = make_int4((int)w[f][4 * h], (int)w[f][4 * h + 1], (int)w[f][4 * h + 2], (int)w[f][4 * h + 3]);
+#else
   int32_t v[kTabLimbs];
   CG_UNROLL for (int l = 0; l < 10; ++l) {
     v[l] = c.YplusX.v[l];
@@ -93,9 +109,25 @@ CG_DEV void store_cached(int4* dst, size_t qs, const ge_cached& c) {
   }
   CG_UNROLL for (int q = 0; q < kTabLimbs / 4; ++q)
     dst[q * qs] = make_int4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+#endif
 }
 
 CG_DEV void load_cached(const int4* src, size_t qs, ge_cached& c) {
+#if CG_ED_TAB_PACK
+  uint32_t w[4][8];
+  CG_UNROLL for (int f = 0; f < 4; ++f)
+    CG_UNROLL for (int h = 0; h < 2; ++h) {
+      const int4 x = src[(2 * f + h) * qs];
+      w[f][4 * h] = (uint32_t)x.x;
+      w[f][4 * h + 1] = (uint32_t)x.y;
+      w[f][4 * h + 2] = (uint32_t)x.z;
+      w[f][4 * h + 3] = (uint32_t)x.w;
+    }
+  fe_frombytes(c.YplusX, w[0]);
+  fe_frombytes(c.YminusX, w[1]);
+  fe_frombytes(c.Z, w[2]);
+  fe_frombytes(c.T2d, w[3]);
+#else
   int32_t v[kTabLimbs];
   CG_UNROLL for (int q = 0; q < kTabLimbs / 4; ++q) {
     const int4 x = src[q * qs];
@@ -110,6 +142,7 @@ CG_DEV void load_cached(const int4* src, size_t qs, ge_cached& c) {
     c.Z.v[l] = v[20 + l];
     c.T2d.v[l] = v[30 + l];
   }
+#endif
 }
 
 #ifndef CG_POINTS_WAVES
@@ -229,7 +262,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_MSM_WAVE
   }
   uint32_t dig[kDigitWords];
   CG_UNROLL for (int w = 0; w < kDigitWords; ++w) dig[w] = digits[(size_t)w * scap + i];
+#if CG_MSM_FAKE_TABLE  // timing experiment only (wrong verdicts): every lane reads lane 0's tables
+  const LaneTab lt = lane_table(const_cast<int32_t*>(table), 0, scap);
+#else
   const LaneTab lt = lane_table(const_cast<int32_t*>(table), i, scap);
+#endif
   const uint32_t ok = ed25519_msm(
       ndig, dig, ed_status_rneg(st),
       [&](uint32_t k, ge_cached& c) { load_cached(lt.entry(k), lt.qstride, c); },
@@ -271,6 +308,52 @@ CG_DEV void load_bentry(const int32_t* btab_g, uint32_t t, uint32_t k, ge_precom
     p.xy2d.v[l] = v[20 + l];
   }
 }
+
+// Points + MSM in one kernel (CORDA_AMD_ED_FUSE=1): each lane decodes A and R, writes
+// its tables and reads them straight back in its MSM — the reads then hit the L2 / MALL
+// lines the same CU just wrote instead of HBM (the two-kernel form writes the whole
+// batch's ~2.4-3 GB of tables before the first read).  Same verdict merge as the
+// separate kernels.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_MSM_WAVES, CG_MSM_WAVES))) void cg_ed25519_pm(
+    const uint32_t* __restrict__ pk, const uint32_t* __restrict__ sig, const uint32_t* __restrict__ status,
+    const uint32_t* __restrict__ digits, int32_t* __restrict__ table, const int32_t* __restrict__ btab_g, uint32_t n,
+    uint32_t cap, uint32_t scap, const uint32_t* __restrict__ out_index, uint8_t* __restrict__ verdict) {
+  CG_WAVE_PRIO(0);
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool in = i < n;
+  const uint32_t st = in ? status[i] : 0u;
+  uint32_t v = V_REJECT;
+  const LaneTab lt = lane_table(table, in ? i : 0u, scap);
+  if (in) {
+    uint32_t pkw[8], rw[8];
+    CG_UNROLL for (int w = 0; w < 8; ++w) {
+      pkw[w] = pk[(size_t)w * cap + i];
+      rw[w] = sig[(size_t)w * cap + i];
+    }
+    ge_p3 negA, R;
+    v = ed_merge_verdict(st, ed25519_points_stage(pkw, rw, V_COMPUTE, negA, R));
+    if (v == V_COMPUTE) {
+      ed25519_build_table(negA, [&](int k, const ge_cached& c) { store_cached(lt.entry(k), lt.qstride, c); });
+      ed25519_build_table(R, [&](int k, const ge_cached& c) { store_cached(lt.entry(kATabEntries + k), lt.qstride, c); });
+    }
+  }
+  const bool live = in && v == V_COMPUTE;
+  const uint32_t ndig = wave_max(live ? ed_status_ndig(st) : 0u);
+  if (!in) return;
+  const uint32_t dst = out_index ? out_index[i] : i;
+  if (!live) {
+    verdict[dst] = (uint8_t)v;
+    return;
+  }
+  uint32_t dig[kDigitWords];
+  CG_UNROLL for (int w = 0; w < kDigitWords; ++w) dig[w] = digits[(size_t)w * scap + i];
+  const uint32_t ok = ed25519_msm(
+      ndig, dig, ed_status_rneg(st), [&](uint32_t k, ge_cached& c) { load_cached(lt.entry(k), lt.qstride, c); },
+      [&](uint32_t k, ge_cached& c) { load_cached(lt.entry(kATabEntries + k), lt.qstride, c); },
+      [&](uint32_t t, uint32_t k, ge_precomp& p) { load_bentry(btab_g, t, k, p); });
+  verdict[dst] = ok ? (uint8_t)V_ACCEPT : (uint8_t)V_REJECT;
+}
+
 
 CG_DEV uint32_t wave_or(uint32_t v) { return __ballot(v != 0) != 0ull; }
 
@@ -354,6 +437,14 @@ hipError_t launch_ed25519_points(const Ed25519Dev& d, uint32_t n, hipStream_t s)
   else
     hipLaunchKernelGGL(cg_ed25519_points, dim3((n + 255) / 256), dim3(256), 0, s, d.pk, d.sig, n, d.cap, d.scap,
                        d.pstat, d.table);
+  return hipGetLastError();
+}
+
+hipError_t launch_ed25519_points_msm(const Ed25519Dev& d, uint32_t n, const uint32_t* out_index, uint8_t* verdict,
+                                     hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(cg_ed25519_pm, dim3((n + 255) / 256), dim3(256), 0, s, d.pk, d.sig, d.status, d.digits, d.table,
+                     d.btab, n, d.cap, d.scap, out_index, verdict);
   return hipGetLastError();
 }
 
