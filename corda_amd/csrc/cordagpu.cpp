@@ -2203,8 +2203,12 @@ cg_status ftx_pipeline(cg_ctx* ctx, size_t n_ftx, const uint8_t* arena, size_t a
   if (const char* e = std::getenv("CORDA_AMD_FTX_CHUNKS")) kmax = std::max(1, std::atoi(e));
   if (const char* e = std::getenv("CORDA_AMD_FTX_MIN_CHUNK")) min_chunk = std::max(1, std::atoi(e));
   const size_t K = std::max<size_t>(1, std::min<size_t>(kmax, n_ftx / min_chunk));
+  // the last chunk's kernels run after the last byte: it gets `tail` of a regular chunk
+  double tail = 0.5;
+  if (const char* e = std::getenv("CORDA_AMD_FTX_TAIL")) tail = std::min(1.0, std::max(0.1, std::atof(e)));
   std::vector<size_t> tb(K + 1);
-  for (size_t k = 0; k <= K; ++k) tb[k] = k == K ? n_ftx : n_ftx * k / K;
+  const double wsum = (double)(K - 1) + (K > 1 ? tail : 1.0);
+  for (size_t k = 0; k <= K; ++k) tb[k] = k == K ? n_ftx : (size_t)((double)n_ftx * (double)k / wsum);
   cg_status st;
   if ((st = dalloc(ctx, &d.arena, arena_bytes + 16, "alloc ftx arena")) != CG_OK ||
       (st = dalloc(ctx, &d.comp_off, std::max<size_t>(n_comp, 1), "alloc comp_off")) != CG_OK ||
@@ -2251,7 +2255,12 @@ cg_status ftx_pipeline(cg_ctx* ctx, size_t n_ftx, const uint8_t* arena, size_t a
   //    one pass over the chunk's component offsets); event ev[k]
   for (size_t k = 0; k < K; ++k) {
     const size_t t0 = tb[k], t1 = tb[k + 1];
+    for (size_t t = t0; t < t1; ++t)
+      if (comp_start[t + 1] < comp_start[t] || node_start[t + 1] < node_start[t])
+        return fail(ctx, CG_E_INVALID_ARGUMENT, "comp_start / node_start not monotone");
     const size_t c0 = comp_start[t0], c1 = comp_start[t1], j0 = node_start[t0], j1 = node_start[t1];
+    if (c1 > n_comp || j1 > n_node)  // (a later decrease: the buffers were sized from the last entries)
+      return fail(ctx, CG_E_INVALID_ARGUMENT, "comp_start / node_start not monotone");
     const uint64_t from = up_to;
     for (size_t c = c0; c < c1; ++c)
       up_to = std::max<uint64_t>(up_to, std::min<uint64_t>(comp_off[c] + comp_len[c], arena_bytes));
@@ -2337,9 +2346,8 @@ cg_status cg_ftx_verify_batch(cg_ctx* ctx, size_t n_ftx, const uint8_t* arena, s
   if (!comp_start || !node_start || !root_hashes || !result_out || (node_start[n_ftx] && (!node_kind || !node_hash)) ||
       (comp_start[n_ftx] && (!comp_off || !comp_len || !arena || !nonces)))
     return fail(ctx, CG_E_INVALID_ARGUMENT, "null pointer");
-  for (size_t t = 0; t < n_ftx; ++t)
-    if (comp_start[t + 1] < comp_start[t] || node_start[t + 1] < node_start[t])
-      return fail(ctx, CG_E_INVALID_ARGUMENT, "comp_start / node_start not monotone");
+  // (comp_start / node_start monotonicity is checked chunk by chunk in ftx_pipeline,
+  // before any kernel runs, beside the earlier chunks' copies)
   if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, CG_E_DEVICE, "hipSetDevice");
   const size_t n_comp = comp_start[n_ftx], n_node = node_start[n_ftx];
   TxDev d;

@@ -198,6 +198,28 @@ def test_ftx_golden(gpu_ctx, golden_ftx, ftx_chunks):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("field", ["comp_start", "node_start"])
+def test_ftx_non_monotone_starts_are_invalid_argument(gpu_ctx, golden_ftx, ftx_chunks, field):
+    """A comp_start / node_start that decreases — in a middle chunk, or only at its very end
+    (the device buffers are sized from the last entry, so an earlier chunk reaching past it
+    must be refused before its copies) — is CG_E_INVALID_ARGUMENT, and the next valid call
+    on the same context verifies correctly."""
+    from test_oracle import _ftx_flat
+    from corda_amd._lib import CordaGpuError
+    a = list(_ftx_flat(golden_ftx))
+    idx = 3 if field == "comp_start" else 5
+    n = len(golden_ftx)
+    for where in (n // 2, n):
+        bad = a[idx].copy()
+        bad[where - 1] = bad[where] + 1  # entry `where` now below its predecessor
+        b = list(a)
+        b[idx] = bad
+        with pytest.raises(CordaGpuError):
+            _ftx_call(gpu_ctx, b, n)
+    assert _ftx_call(gpu_ctx, a, n).tolist() == [r["result"] for r in golden_ftx]
+
+
+@pytest.mark.gpu
 def test_ftx_python_mirror(gpu_ctx, golden_ftx):
     """FilteredTransaction.verify through the Python mirror: True/False, and
     MerkleTreeException for a tx without included leaves."""
