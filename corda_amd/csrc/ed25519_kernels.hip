@@ -4,7 +4,7 @@
 //   cg_ed25519_hash     SHA-512 challenge, scalars, half-size reduction, digits —
 //                       integer/hash work, no field arithmetic beyond Abyte
 //   cg_ed25519_points   decode A and R (two square roots), tables k*(-A) and k*R
-//                       (k = 0..8) written to HBM scratch; independent of the hash
+//                       (k = 1..8) written to HBM scratch; independent of the hash
 //                       kernel (its own verdict word pstat), so the two may run side
 //                       by side
 //   cg_ed25519_msm      [b]B + [c0](-A) + [c1](+-R) over ~132 shared bit positions
@@ -17,11 +17,13 @@
 //   pk[w*cap+i] (8 words), sig[w*cap+i] (16 words: R then S), sig_len[i],
 //   msg_off[i] (u64, into the arena), msg_len[i]; scratch (`scap` = chunk):
 //   status[i] (verdict | digit count << 8 | R sign << 16), digits[w*scap+i]
-//   (24 words), and the per-signature tables entries 0..8 = k*(-A), 9..17 = k*R
-//   (cached points, 40 limbs = ten int4 quads) lane-contiguous: table[(i*18 + e)*40 + l],
-//   so an entry is ten 16-byte loads from two to three 128-byte lines of its lane.
+//   (24 words), and the per-signature tables entries 0..7 = k*(-A), 8..15 = k*R for
+//   k = 1..8 (cached points packed to 32 words = one 128-byte line, CG_ED_TAB_PACK)
+//   lane-contiguous: table[(i*16 + e)*32 + w], 2 KB per lane; a zero digit reads one
+//   shared identity entry (CG_ED_TAB_NO0; with CG_ED_TAB_NO0=0 entries k = 0..8, 18
+//   per lane, as in round 2; CG_ED_TAB_PACK=0: 40 limbs, ten int4 quads per entry).
 //   CG_ED_TAB_SOA=1 lays them quad-major across lanes instead (int4
-//   table[(e*10 + q)*scap + i]: each of a wave's ten loads one contiguous 1 KB run, no
+//   table[(e*10 + q)*scap + i]: each of a wave's loads one contiguous 1 KB run, no
 //   over-fetch) — measured slower (r03c, one box: msm 7.11 -> 8.35 ms, points 2.47 ->
 //   3.9 ms per 1 M; an entry's ten quads sit scap * 16 B = 16 MB apart, ten pages per
 //   entry instead of one), so the lane-contiguous layout stays.
@@ -44,7 +46,13 @@ namespace {
 #define CG_ED_TAB_PACK 1
 #endif
 constexpr int kTabLimbs = CG_ED_TAB_PACK ? 32 : 40;  // words per cached point: 4 fe x 8 packed / 10 limbs
-constexpr int kLaneEntries = 2 * kATabEntries;
+// CG_ED_TAB_NO0 = 1: the lane tables keep k = 1..8 only (16 entries, 2 KB per lane
+// packed); a zero digit reads one shared identity entry (L1 / L2 resident) instead.
+#ifndef CG_ED_TAB_NO0
+#define CG_ED_TAB_NO0 1
+#endif
+constexpr int kSlotsPerPoint = CG_ED_TAB_NO0 ? kATabEntries - 1 : kATabEntries;
+constexpr int kLaneEntries = 2 * kSlotsPerPoint;
 constexpr int kBStride = 32;   // shared-table entry (precomputed point, 3 fe x 10 limbs) padded to one 128-byte line
 
 #ifndef CG_ED_TAB_SOA
@@ -57,6 +65,7 @@ struct LaneTab {
   size_t kstride, qstride;
   CG_DEV int4* entry(uint32_t k) const { return base + (size_t)k * kstride; }
 };
+static_assert(!(CG_ED_TAB_NO0 && CG_ED_TAB_SOA), "CG_ED_TAB_NO0 needs the lane-contiguous layout");
 CG_DEV LaneTab lane_table(int32_t* table, uint32_t i, uint32_t scap) {
 #if CG_ED_TAB_SOA
   return {reinterpret_cast<int4*>(table) + i, (size_t)(kTabLimbs / 4) * scap, scap};
@@ -88,6 +97,16 @@ __global__ __launch_bounds__(256) void cg_ed25519_hash(const uint32_t* __restric
   if (pre != V_COMPUTE) return;
   CG_UNROLL for (int w = 0; w < kDigitWords; ++w) digits[(size_t)w * scap + i] = dig[w];
 }
+
+// The shared identity entry (1, 1, 1, 0) in the table's entry format (CG_ED_TAB_NO0).
+#if CG_ED_TAB_NO0 && CG_ED_TAB_PACK
+__device__ __attribute__((aligned(128))) const int4 g_ident_entry[kTabLimbs / 4] = {
+    {1, 0, 0, 0}, {0, 0, 0, 0}, {1, 0, 0, 0}, {0, 0, 0, 0}, {1, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
+#elif CG_ED_TAB_NO0
+__device__ __attribute__((aligned(128))) const int4 g_ident_entry[kTabLimbs / 4] = {
+    {1, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 1, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {1, 0, 0, 0}, {0, 0, 0, 0},
+    {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
+#endif
 
 CG_DEV void store_cached(int4* dst, size_t qs, const ge_cached& c) {
 #if CG_ED_TAB_PACK
@@ -145,6 +164,22 @@ CG_DEV void load_cached(const int4* src, size_t qs, ge_cached& c) {
 #endif
 }
 
+// Entry k (0..8) of point p (0: -A, 1: R; a per-signature table holding R only uses
+// p = 0) of a lane's table: stored k for the full tables, k - 1 with CG_ED_TAB_NO0 (and
+// k = 0 reads the shared identity entry).
+CG_DEV void store_slot(const LaneTab& lt, int p, int k, const ge_cached& c) {
+  if (CG_ED_TAB_NO0 && k == 0) return;
+  store_cached(lt.entry(p * kSlotsPerPoint + k - CG_ED_TAB_NO0), lt.qstride, c);
+}
+CG_DEV void load_slot(const LaneTab& lt, int p, uint32_t k, ge_cached& c) {
+#if CG_ED_TAB_NO0
+  const int4* src = k ? lt.entry(p * kSlotsPerPoint + k - 1) : g_ident_entry;
+  load_cached(src, 1, c);
+#else
+  load_cached(lt.entry(p * kSlotsPerPoint + k), lt.qstride, c);
+#endif
+}
+
 #ifndef CG_POINTS_WAVES
 #define CG_POINTS_WAVES 2
 #endif
@@ -167,8 +202,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_POINTS_W
   pstat[i] = v;
   if (v != V_COMPUTE) return;
   const LaneTab lt = lane_table(table, i, scap);
-  ed25519_build_table(negA, [&](int k, const ge_cached& c) { store_cached(lt.entry(k), lt.qstride, c); });
-  ed25519_build_table(R, [&](int k, const ge_cached& c) { store_cached(lt.entry(kATabEntries + k), lt.qstride, c); });
+  ed25519_build_table(negA, [&](int k, const ge_cached& c) { store_slot(lt, 0, k, c); });
+  ed25519_build_table(R, [&](int k, const ge_cached& c) { store_slot(lt, 1, k, c); });
 }
 
 // Key-reuse path, once per distinct key and verify call: decode A and build its
@@ -207,7 +242,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_POINTS_W
   pstat[i] = v;
   if (v != V_COMPUTE) return;
   const LaneTab lt = lane_table(table, i, scap);
-  ed25519_build_table(R, [&](int k, const ge_cached& c) { store_cached(lt.entry(k), lt.qstride, c); });
+  ed25519_build_table(R, [&](int k, const ge_cached& c) { store_slot(lt, 0, k, c); });
 }
 
 // The shared B tables: entry k of table t = k * 2^(64 t) B in affine form, t = 0..3,
@@ -269,8 +304,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_MSM_WAVE
 #endif
   const uint32_t ok = ed25519_msm(
       ndig, dig, ed_status_rneg(st),
-      [&](uint32_t k, ge_cached& c) { load_cached(lt.entry(k), lt.qstride, c); },
-      [&](uint32_t k, ge_cached& c) { load_cached(lt.entry(kATabEntries + k), lt.qstride, c); },
+      [&](uint32_t k, ge_cached& c) { load_slot(lt, 0, k, c); },
+      [&](uint32_t k, ge_cached& c) { load_slot(lt, 1, k, c); },
       [&](uint32_t t, uint32_t k, ge_precomp& p) {
         // one 128-byte line per entry: eight 16-byte loads (L2 / MALL resident table)
         const int4* b = reinterpret_cast<const int4*>(btab_g + ((size_t)t * kBTabEntries + k) * kBStride);
@@ -333,8 +368,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_MSM_WAVE
     ge_p3 negA, R;
     v = ed_merge_verdict(st, ed25519_points_stage(pkw, rw, V_COMPUTE, negA, R));
     if (v == V_COMPUTE) {
-      ed25519_build_table(negA, [&](int k, const ge_cached& c) { store_cached(lt.entry(k), lt.qstride, c); });
-      ed25519_build_table(R, [&](int k, const ge_cached& c) { store_cached(lt.entry(kATabEntries + k), lt.qstride, c); });
+      ed25519_build_table(negA, [&](int k, const ge_cached& c) { store_slot(lt, 0, k, c); });
+      ed25519_build_table(R, [&](int k, const ge_cached& c) { store_slot(lt, 1, k, c); });
     }
   }
   const bool live = in && v == V_COMPUTE;
@@ -348,8 +383,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_MSM_WAVE
   uint32_t dig[kDigitWords];
   CG_UNROLL for (int w = 0; w < kDigitWords; ++w) dig[w] = digits[(size_t)w * scap + i];
   const uint32_t ok = ed25519_msm(
-      ndig, dig, ed_status_rneg(st), [&](uint32_t k, ge_cached& c) { load_cached(lt.entry(k), lt.qstride, c); },
-      [&](uint32_t k, ge_cached& c) { load_cached(lt.entry(kATabEntries + k), lt.qstride, c); },
+      ndig, dig, ed_status_rneg(st), [&](uint32_t k, ge_cached& c) { load_slot(lt, 0, k, c); },
+      [&](uint32_t k, ge_cached& c) { load_slot(lt, 1, k, c); },
       [&](uint32_t t, uint32_t k, ge_precomp& p) { load_bentry(btab_g, t, k, p); });
   verdict[dst] = ok ? (uint8_t)V_ACCEPT : (uint8_t)V_REJECT;
 }
@@ -387,7 +422,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_MSM_WAVE
       [&](uint32_t t, uint32_t k, ge_cached& c) CG_LINLINE {
         load_cached(kt + (t * kATabEntries + k) * (kTabLimbs / 4), 1, c);
       },
-      [&](uint32_t k, ge_cached& c) CG_LINLINE { load_cached(lt.entry(k), lt.qstride, c); },
+      [&](uint32_t k, ge_cached& c) CG_LINLINE { load_slot(lt, 0, k, c); },
       [&](uint32_t t, uint32_t k, ge_precomp& p) CG_LINLINE { load_bentry(btab_g, t, k, p); });
   verdict[dst] = ok ? (uint8_t)V_ACCEPT : (uint8_t)V_REJECT;
 }
