@@ -8,8 +8,9 @@ Crypto.doVerify, Crypto.kt:472-483) and compared element by element with the
 C restatement of i2p eddsa 0.2.0 (oracle/, test infrastructure only).
 
 The default size, 2^19, takes about 10 s on the box. Set
-CORDA_AMD_PARITY_N=10000000 for the full 10 M run; its log is committed as
-profiles/r01q_parity_10m.txt.
+CORDA_AMD_PARITY_N=10000000 for the full 10 M run (with CORDA_AMD_PARITY_EC_N for
+the ECDSA test's size); the final round-3 log is
+profiles/r03y_parity_10m_ed25519_2m_ecdsa.txt (about 200 s on the box).
 """
 from __future__ import annotations
 
