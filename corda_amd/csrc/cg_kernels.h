@@ -20,7 +20,7 @@ struct Ed25519Dev {
   uint32_t* status = nullptr;    // [scap] hash phase: verdict | digit count << 8 | R sign << 16
   uint32_t* pstat = nullptr;     // [scap] points phase: KEY_INVALID / REJECT (R) / COMPUTE
   uint32_t* digits = nullptr;    // [24][scap]
-  int32_t* table = nullptr;      // [scap][18][40] lane-contiguous k*(-A), k*R (ed25519_kernels.hip)
+  int32_t* table = nullptr;      // [scap][17][32] lane-contiguous k*(-A), k*R, k = 1..8 (ed25519_kernels.hip)
   const int32_t* btab = nullptr; // [2][kBTabEntries][30] shared k*B, k*2^128 B tables
   // key-reuse path (null key_index: the balanced path): per-signature index of the
   // signer's distinct-key slot, the per-key tables k * 2^(64 t) (-A) and key status

@@ -19,7 +19,8 @@
 //   status[i] (verdict | digit count << 8 | R sign << 16), digits[w*scap+i]
 //   (24 words), and the per-signature tables entries 0..7 = k*(-A), 8..15 = k*R for
 //   k = 1..8 (cached points packed to 32 words = one 128-byte line, CG_ED_TAB_PACK)
-//   lane-contiguous: table[(i*16 + e)*32 + w], 2 KB per lane; a zero digit reads one
+//   lane-contiguous: table[(i*17 + e)*32 + w] (one pad entry: CG_ED_TAB_PAD), 2,176 B per
+//   lane; a zero digit reads one
 //   shared identity entry (CG_ED_TAB_NO0; with CG_ED_TAB_NO0=0 entries k = 0..8, 18
 //   per lane, as in round 2; CG_ED_TAB_PACK=0: 40 limbs, ten int4 quads per entry).
 //   CG_ED_TAB_SOA=1 lays them quad-major across lanes instead (int4
@@ -52,7 +53,15 @@ constexpr int kTabLimbs = CG_ED_TAB_PACK ? 32 : 40;  // words per cached point: 
 #define CG_ED_TAB_NO0 1
 #endif
 constexpr int kSlotsPerPoint = CG_ED_TAB_NO0 ? kATabEntries - 1 : kATabEntries;
-constexpr int kLaneEntries = 2 * kSlotsPerPoint;
+// CG_ED_TAB_PAD: unused entries after a lane's table, so the lane stride is not a
+// power of two: at 16 entries = 2 KB every lane of a wave writes into the same L2
+// channel and set, lines leave L2 before their eight 16-byte stores have merged and
+// the points kernel wrote 3.4 KB per verify for its 2 KB of entries; 17 entries:
+// 2.1 KB (r03k PMC).
+#ifndef CG_ED_TAB_PAD
+#define CG_ED_TAB_PAD 1
+#endif
+constexpr int kLaneEntries = 2 * kSlotsPerPoint + CG_ED_TAB_PAD;
 constexpr int kBStride = 32;   // shared-table entry (precomputed point, 3 fe x 10 limbs) padded to one 128-byte line
 
 #ifndef CG_ED_TAB_SOA
