@@ -289,61 +289,57 @@ CG_HD void shl_nibbles(uint32_t x[8], uint32_t n) {
 }
 
 // MSM phase: P = [b]B + [c0](-A) + [c1](+-R) over ndig radix-16 positions (ndig
-// uniform across the wave, >= 32).  getA(k, cached&) loads k*(-A), getR(k,
-// cached&) loads k*R, getB(t, k, precomp&) loads k * 2^(64 t) B (t = 0 or 2 here),
-// k <= 2^(kBWin-1).
+// uniform across the wave, >= 32).  getDig(w) returns digit word w (the
+// kDigitWords layout of ed25519_hash_stage; read when a window needs it, so the 24
+// words are not held in registers through the loop).  loadA(k, RawA&) starts the
+// fetch of k*(-A) and unpackA(RawA&, cached&) completes it as limbs; loadA is called
+// before a window's doublings and unpackA after them, so a fetch issued early hides
+// its latency under the doublings while only its storage form (packed words, an
+// LDS slot, or just k for a late load) stays live; loadR / unpackR the same for k*R
+// (unpacked before the R addition).  getB(t, k, precomp&) loads k * 2^(64 t) B
+// (t = 0 or 2 here), k <= 2^(kBWin-1).
 // Returns 1 iff P is the identity.
-template <typename GetA, typename GetR, typename GetB>
-CG_HD uint32_t ed25519_msm(uint32_t ndig, const uint32_t dig[kDigitWords], uint32_t rneg, GetA&& getA, GetR&& getR,
-                           GetB&& getB) {
-  uint32_t da[8], dr[8], bh[4], bl[4];
-  CG_UNROLL for (int w = 0; w < 8; ++w) {
-    da[w] = dig[w];
-    dr[w] = dig[8 + w];
-  }
-  CG_UNROLL for (int w = 0; w < 4; ++w) {
-    bh[w] = dig[16 + w];  // B digits 31..16 (the 2^128 B table), most significant first
-    bl[w] = dig[20 + w];  // B digits 15..0 (the B table)
-  }
-  shl_nibbles(da, 64 - ndig);  // top digit to the top nibble
-  shl_nibbles(dr, 64 - ndig);
+template <typename RawA, typename RawR, typename GetDig, typename LoadA, typename UnpackA, typename LoadR,
+          typename UnpackR, typename GetB>
+CG_HD uint32_t ed25519_msm(uint32_t ndig, GetDig&& getDig, uint32_t rneg, LoadA&& loadA, UnpackA&& unpackA,
+                           LoadR&& loadR, UnpackR&& unpackR, GetB&& getB) {
   ge_p2 r2;
   ge_p3 r3;
   ge_p1p1 t;  // identity: x = X/Z = 0, y = Y/T = 1
   ge_cached ca;
   ge_precomp pb;
+  RawA ra;
+  RawR rr;
   fe_0(t.X);
   fe_1(t.Y);
   fe_1(t.Z);
   fe_1(t.T);
   // one iteration per 4-bit window, most significant first; the first window's
-  // digit is added to the identity (no doublings).  The A entry of a window is
-  // loaded before its four doublings (40 VGPRs held across them), so the load's
-  // latency hides under ~3,600 VALU instructions instead of stalling the addition.
+  // digit is added to the identity (no doublings).  Digit word j/8 of c0 and |c1|
+  // holds the window's nibble (j % 8); the B digits are 16-bit fields of words
+  // 16..23, the first-used (top) window's digit in the low half of words 16 / 20.
   const int nwin = (int)ndig;
+  uint32_t wa = 0, wr = 0;
   CG_NOUNROLL for (int j = nwin - 1; j >= 0; --j) {
-    const uint32_t ea = da[7] >> 28, er = dr[7] >> 28;
-    CG_UNROLL for (int w = 7; w >= 1; --w) {
-      da[w] = (da[w] << 4) | (da[w - 1] >> 28);
-      dr[w] = (dr[w] << 4) | (dr[w - 1] >> 28);
+    if (j == nwin - 1 || (j & 7) == 7) {  // wave-uniform
+      wa = getDig(j >> 3);
+      wr = getDig(8 + (j >> 3));
     }
-    da[0] <<= 4;
-    dr[0] <<= 4;
+    const uint32_t sh = 4 * (uint32_t)(j & 7);
+    const uint32_t ea = (wa >> sh) & 15u, er = (wr >> sh) & 15u;
     const uint32_t na = ea < 8, nr = er < 8;
     const bool bwin = ((4 * j) & (kBWin - 1)) == 0 && 4 * j < 128;
     constexpr uint32_t kMask = (1u << kBWin) - 1, kHalf = 1u << (kBWin - 1);
+    static_assert(kBWin == 16 || kBWin == 8, "B digit fields are 8 or 16 bits");
     uint32_t el = 0, eh = 0;
     if (bwin) {
-      el = bl[0] & kMask;
-      eh = bh[0] & kMask;
-      CG_UNROLL for (int w = 0; w < 3; ++w) {
-        bl[w] = bl[w] >> kBWin | bl[w + 1] << (32 - kBWin);
-        bh[w] = bh[w] >> kBWin | bh[w + 1] << (32 - kBWin);
-      }
-      bl[3] >>= kBWin;
-      bh[3] >>= kBWin;
+      const uint32_t s = (uint32_t)(128 / kBWin - 1) - (uint32_t)(4 * j) / kBWin;  // use order, top window first
+      const uint32_t per = 32 / kBWin, fsh = kBWin * (s % per);
+      el = (getDig(20 + (int)(s / per)) >> fsh) & kMask;
+      eh = (getDig(16 + (int)(s / per)) >> fsh) & kMask;
     }
-    getA(na ? 8 - ea : ea - 8, ca);
+    loadA(na ? 8 - ea : ea - 8, ra);
+    loadR(nr ? 8 - er : er - 8, rr);
     const uint32_t nl = el < kHalf, nh = eh < kHalf;
     if (j != nwin - 1) {
       CG_NOUNROLL for (int k = 0; k < 3; ++k) {
@@ -353,12 +349,14 @@ CG_HD uint32_t ed25519_msm(uint32_t ndig, const uint32_t dig[kDigitWords], uint3
       ge_p1p1_to_p2(r2, t);
       ge_p2_dbl<true>(t, r2);  // the additions follow (ge_p1p1_to_p3)
       ge_p1p1_to_p3(r3, t);
+      unpackA(ra, ca);
       ge_add_cached(t, r3, ca, na);
     } else {
+      unpackA(ra, ca);
       ge_add_cached(t, ge_identity_p3(), ca, na);  // constant operand: mostly folded away
     }
-    getR(nr ? 8 - er : er - 8, ca);
     ge_p1p1_to_p3(r3, t);
+    unpackR(rr, ca);
     ge_add_cached(t, r3, ca, nr ^ rneg);
     if (bwin) {
       getB(0, nl ? kHalf - el : el - kHalf, pb);

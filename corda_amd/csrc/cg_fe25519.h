@@ -538,6 +538,14 @@ CG_HD void fe_quad(fe& h0, const A& a, fe& h1, const B& b, fe& h2, const C& c, f
 #ifndef CG_FE_QUAD
 #define CG_FE_QUAD 1
 #endif
+// Per formula (register pressure differs: p1p1 -> p3 shares its operands between the
+// four products, the doubling's squarings and the cached addition's products do not).
+#ifndef CG_FE_QUAD_DBL
+#define CG_FE_QUAD_DBL CG_FE_QUAD
+#endif
+#ifndef CG_FE_QUAD_ADD
+#define CG_FE_QUAD_ADD CG_FE_QUAD
+#endif
 
 // h = f * g, f^2, 2 f^2 (rounding carries: limbs |h_k| <= 2^(w-1) + small)
 CG_HD void fe_mul(fe& h, const fe& f, const fe& g) { fe_one(h, FeMul{f, g}); }

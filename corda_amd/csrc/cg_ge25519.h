@@ -88,7 +88,7 @@ template <bool ADD_READY = false>
 CG_HD void ge_p2_dbl(ge_p1p1& r, const ge_p2& p) {
   fe s, xx, yy, zz2, ss;
   fe_add_p(s, p.X, p.Y);
-#if CG_FE_QUAD
+#if CG_FE_QUAD_DBL
   fe_quad(xx, FeSqF{p.X}, yy, FeSqF{p.Y}, zz2, FeSq2{p.Z}, ss, FeSqF{s});
 #else
   fe_pair(xx, FeSqF{p.X}, yy, FeSqF{p.Y});
@@ -130,7 +130,7 @@ CG_HD void ge_add_cached(ge_p1p1& r, const ge_p3& p, const ge_cached& q, uint32_
   fe_cneg(t2d, q.T2d, neg);
   fe_add(a, p.Y, p.X);
   fe_sub(b, p.Y, p.X);
-#if CG_FE_QUAD
+#if CG_FE_QUAD_ADD
   fe_quad(A, FeMulF{a, qa}, B, FeMulF{b, qb}, C, FeMulF{t2d, p.T}, D2, FeMul2F{p.Z, q.Z});  // D2 = 2 Z Zq
 #else
   fe_pair(A, FeMulF{a, qa}, B, FeMulF{b, qb});

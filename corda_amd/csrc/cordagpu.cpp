@@ -62,8 +62,16 @@ class CopyPool {
     const void* src;
     size_t bytes;
   };
+  // A worker that cannot be created (resource exhaustion) leaves the pool with the
+  // ones that were: the caller's thread copies too, so zero workers still work.
   explicit CopyPool(int workers) {
-    for (int t = 0; t < workers; ++t) th_.emplace_back([this] { loop(); });
+    for (int t = 0; t < workers; ++t) {
+      try {
+        th_.emplace_back([this] { loop(); });
+      } catch (...) {
+        break;
+      }
+    }
   }
   ~CopyPool() {
     {
@@ -267,6 +275,12 @@ void collect_timings(cg_ctx* ctx) {
 // Requests are rounded to 1/8 of their power-of-two size class so that repeated
 // batches of similar shape hit the cache; a cached block is reused for requests of
 // at least half its size.  All users run on ctx->stream, so reuse is stream-ordered.
+// min(off + len, bytes) without the wrap of off + len (an element or component
+// outside the arena is rejected by its own check; this only sizes upload prefixes).
+inline uint64_t clamped_end(uint64_t off, uint64_t len, uint64_t bytes) {
+  return off >= bytes ? bytes : off + std::min<uint64_t>(len, bytes - off);
+}
+
 size_t round_block(size_t bytes) {
   if (bytes <= 4096) return (bytes + 255) & ~(size_t)255;
   size_t p = 1;
@@ -486,7 +500,8 @@ cg_status check_inputs(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const ui
   bool has_ed = false, has_ec = false;
   for (size_t i = 0; i < n; ++i) {
     const uint8_t s = scheme_id ? scheme_id[i] : CG_SCHEME_EDDSA_ED25519_SHA512;
-    if (m.off_host && (uint64_t)m.off_host[i] + m.len_host[i] > m.bytes)
+    // off > bytes || len > bytes - off: the sum off + len could wrap for a huge off
+    if (m.off_host && (m.off_host[i] > m.bytes || m.len_host[i] > m.bytes - m.off_host[i]))
       return fail(ctx, CG_E_INVALID_ARGUMENT, "message out of arena bounds at element " + std::to_string(i));
     if (s & CG_SCHEME_FLAG_KEY_INVALID) continue;  // never read beyond its verdict
     if (s == CG_SCHEME_EDDSA_ED25519_SHA512) has_ed = true;
@@ -1295,8 +1310,8 @@ cg_status verify_pipeline(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
   // checked against the arena before its copy goes out).
   std::vector<uint64_t> aend(K + 1, 0);
   for (size_t k = 0, u = 0; k < K; ++k) {
-    for (size_t i = cb[k]; i < cb[k + 1]; ++i) u = std::max<uint64_t>(u, msg_off[i] + msg_len[i]);
-    aend[k + 1] = u = std::min<uint64_t>(u, msg_bytes);
+    for (size_t i = cb[k]; i < cb[k + 1]; ++i) u = std::max<uint64_t>(u, clamped_end(msg_off[i], msg_len[i], msg_bytes));
+    aend[k + 1] = u;
   }
   // Pinned inputs: the copies are asynchronous.  Pageable inputs go through the
   // context's two page-locked ring slots, filled by the copy workers (chunk k+1's
@@ -1308,10 +1323,19 @@ cg_status verify_pipeline(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
   bool ring = !pinned && K > 1;
   if (const char* e = std::getenv("CORDA_AMD_VERIFY_RING")) ring = ring && std::atoi(e) != 0;
   const size_t row_bytes = 12 + pk_stride + sig_stride + (sig_len ? 4 : 0);
+  size_t slot = 0;
+  for (size_t k = 0; k < K; ++k)
+    slot = std::max(slot, (size_t)(aend[k + 1] - aend[k]) + (cb[k + 1] - cb[k]) * row_bytes + 6 * 256);
   if (ring) {
-    size_t slot = 0;
-    for (size_t k = 0; k < K; ++k)
-      slot = std::max(slot, (size_t)(aend[k + 1] - aend[k]) + (cb[k + 1] - cb[k]) * row_bytes + 6 * 256);
+    // The slots stay page-locked until cg_close, so their size is capped
+    // (CORDA_AMD_RING_MAX_MB, default 256 MB per slot): a call whose chunk would need
+    // more — e.g. an arena packed in reverse element order, whose first chunk's prefix
+    // is the whole arena — copies its pageable buffers synchronously instead.
+    size_t cap_mb = 256;
+    if (const char* e = std::getenv("CORDA_AMD_RING_MAX_MB")) cap_mb = (size_t)std::max(1, std::atoi(e));
+    if (slot > (cap_mb << 20)) ring = false;
+  }
+  if (ring) {
     if (ctx->ring_cap < slot) {
       for (uint8_t*& rb : ctx->ring) {
         if (rb) (void)hipHostFree(rb);  // idle: every earlier call ended with a sync
@@ -1856,7 +1880,7 @@ cg_status tx_pipeline(cg_ctx* ctx, int mode, size_t n_tx, const uint8_t* arena, 
   auto enqueue_upload = [&](size_t k) -> cg_status {
     const uint64_t from = up_to;
     for (uint32_t c = comp_start[tb[k]]; c < comp_start[tb[k + 1]]; ++c)
-      up_to = std::max<uint64_t>(up_to, std::min<uint64_t>(comp_off[c] + comp_len[c], arena_bytes));
+      up_to = std::max<uint64_t>(up_to, clamped_end(comp_off[c], comp_len[c], arena_bytes));
     if (up_to > from) {
       Timed t(ctx, "h2d_arena", up_to - from, ctx->copy_stream);
       CG_TRY(ctx, hipMemcpyAsync(d.arena + from, arena + from, up_to - from, hipMemcpyHostToDevice, ctx->copy_stream),
@@ -2186,12 +2210,15 @@ bool hash_less(const std::array<uint8_t, 32>& a, const std::array<uint8_t, 32>& 
 // non-validating notary's whole crypto path is host bytes in, one status byte out;
 // round 2 uploaded everything, then hashed: PCIe and kernels back to back).  Every
 // chunk's rows — the arena prefix its components reach, their offsets / lengths /
-// nonces, its node programs and roots — go out on copy_stream back to back; chunk k's
-// node programs are then scanned on the host (depth, malformed) while the copies run,
-// its status bytes go out on hash_stream, and its leaf hashes and tree evaluation run on
-// ctx->stream as soon as both are in, beside the later chunks' copies.  Kernels index components and nodes absolutely (the chunk
-// passes offset comp_start / node_start / roots / status pointers), so results land in
-// place.  CORDA_AMD_FTX_CHUNKS / _MIN_CHUNK override the split.
+// nonces, its node programs and roots — go out on copy_stream back to back.  Once a
+// chunk's bytes are in, k_pmt_scan checks its node programs on the device (well-formed
+// post-order tree, else MALFORMED in the status bytes; the deepest stack per wave) on
+// ctx->stream, and the host waits once per chunk (hipEventSynchronize on ev_depth) for
+// the per-wave depths, which size that chunk's evaluation stack; its leaf hashes and
+// tree evaluation then run on ctx->stream beside the later chunks' copies.  Kernels
+// index components and nodes absolutely (the chunk passes offset comp_start /
+// node_start / roots / status pointers), so results land in place.
+// CORDA_AMD_FTX_CHUNKS / _MIN_CHUNK override the split.
 cg_status ftx_pipeline(cg_ctx* ctx, size_t n_ftx, const uint8_t* arena, size_t arena_bytes, const uint64_t* comp_off,
                        const uint32_t* comp_len, const uint32_t* comp_start, const uint8_t* nonces,
                        const uint32_t* node_start, const uint8_t* node_kind, const uint8_t* node_hash,
@@ -2263,7 +2290,7 @@ cg_status ftx_pipeline(cg_ctx* ctx, size_t n_ftx, const uint8_t* arena, size_t a
       return fail(ctx, CG_E_INVALID_ARGUMENT, "comp_start / node_start not monotone");
     const uint64_t from = up_to;
     for (size_t c = c0; c < c1; ++c)
-      up_to = std::max<uint64_t>(up_to, std::min<uint64_t>(comp_off[c] + comp_len[c], arena_bytes));
+      up_to = std::max<uint64_t>(up_to, clamped_end(comp_off[c], comp_len[c], arena_bytes));
     Timed t(ctx, "h2d_ftx", (up_to - from) + (c1 - c0) * 44 + (j1 - j0) * 33 + (t1 - t0) * 40, cs);
     if ((st = put(d.arena + from, arena + from, up_to - from, cs, "upload ftx arena")) != CG_OK ||
         (st = put(d.comp_off + c0, comp_off + c0, (c1 - c0) * 8, cs, "upload comp_off")) != CG_OK ||

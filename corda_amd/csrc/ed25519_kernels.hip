@@ -39,6 +39,13 @@ namespace {
 #ifndef CG_MSM_WAVES
 #define CG_MSM_WAVES 2
 #endif
+// the same for the fused points + MSM kernel and the key-reuse MSM
+#ifndef CG_PM_WAVES
+#define CG_PM_WAVES 2
+#endif
+#ifndef CG_MSM_R_WAVES
+#define CG_MSM_R_WAVES 2
+#endif
 
 // CG_ED_TAB_PACK = 1: a table entry is its four coordinates as canonical 255-bit values
 // (8 words each): 128 B = one cache line per entry instead of 160 B over two or three;
@@ -189,6 +196,38 @@ CG_DEV void load_slot(const LaneTab& lt, int p, uint32_t k, ge_cached& c) {
 #endif
 }
 
+// A table entry in its storage form (the MSM fetches the A entry of a window before
+// the window's doublings and unpacks it after them: 32 packed words live across the
+// doublings instead of 40 limbs).
+#if CG_ED_TAB_PACK && CG_ED_TAB_NO0
+struct RawEntry {
+  int4 q[kTabLimbs / 4];
+};
+CG_DEV void fetch_slot(const LaneTab& lt, int p, uint32_t k, RawEntry& r) {
+  const int4* src = k ? lt.entry(p * kSlotsPerPoint + k - 1) : g_ident_entry;
+  CG_UNROLL for (int q = 0; q < kTabLimbs / 4; ++q) r.q[q] = src[q];
+}
+CG_DEV void unpack_entry(const RawEntry& r, ge_cached& c) {
+  uint32_t w[4][8];
+  CG_UNROLL for (int f = 0; f < 4; ++f)
+    CG_UNROLL for (int h = 0; h < 2; ++h) {
+      const int4 x = r.q[2 * f + h];
+      w[f][4 * h] = (uint32_t)x.x;
+      w[f][4 * h + 1] = (uint32_t)x.y;
+      w[f][4 * h + 2] = (uint32_t)x.z;
+      w[f][4 * h + 3] = (uint32_t)x.w;
+    }
+  fe_frombytes(c.YplusX, w[0]);
+  fe_frombytes(c.YminusX, w[1]);
+  fe_frombytes(c.Z, w[2]);
+  fe_frombytes(c.T2d, w[3]);
+}
+#else
+using RawEntry = ge_cached;
+CG_DEV void fetch_slot(const LaneTab& lt, int p, uint32_t k, RawEntry& r) { load_slot(lt, p, k, r); }
+CG_DEV void unpack_entry(const RawEntry& r, ge_cached& c) { c = r; }
+#endif
+
 #ifndef CG_POINTS_WAVES
 #define CG_POINTS_WAVES 2
 #endif
@@ -287,54 +326,6 @@ CG_DEV uint32_t wave_max(uint32_t v) {
   return v;
 }
 
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_MSM_WAVES, CG_MSM_WAVES))) void cg_ed25519_msm(
-    const uint32_t* __restrict__ sig, const uint32_t* __restrict__ status, const uint32_t* __restrict__ pstat,
-    const uint32_t* __restrict__ digits, const int32_t* __restrict__ table, const int32_t* __restrict__ btab_g,
-    uint32_t n, uint32_t cap, uint32_t scap, const uint32_t* __restrict__ out_index, uint8_t* __restrict__ verdict) {
-  CG_WAVE_PRIO(0);
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t st = i < n ? status[i] : 0u;
-  const uint32_t v = i < n ? ed_merge_verdict(st, pstat[i]) : 0u;
-  const bool live = i < n && v == V_COMPUTE;
-  // every lane of the wave walks the same bit positions: the longest scalar sets the length
-  const uint32_t ndig = wave_max(live ? ed_status_ndig(st) : 0u);
-  if (i >= n) return;
-  const uint32_t dst = out_index ? out_index[i] : i;
-  if (!live) {
-    verdict[dst] = (uint8_t)v;
-    return;
-  }
-  uint32_t dig[kDigitWords];
-  CG_UNROLL for (int w = 0; w < kDigitWords; ++w) dig[w] = digits[(size_t)w * scap + i];
-#if CG_MSM_FAKE_TABLE  // timing experiment only (wrong verdicts): every lane reads lane 0's tables
-  const LaneTab lt = lane_table(const_cast<int32_t*>(table), 0, scap);
-#else
-  const LaneTab lt = lane_table(const_cast<int32_t*>(table), i, scap);
-#endif
-  const uint32_t ok = ed25519_msm(
-      ndig, dig, ed_status_rneg(st),
-      [&](uint32_t k, ge_cached& c) { load_slot(lt, 0, k, c); },
-      [&](uint32_t k, ge_cached& c) { load_slot(lt, 1, k, c); },
-      [&](uint32_t t, uint32_t k, ge_precomp& p) {
-        // one 128-byte line per entry: eight 16-byte loads (L2 / MALL resident table)
-        const int4* b = reinterpret_cast<const int4*>(btab_g + ((size_t)t * kBTabEntries + k) * kBStride);
-        int32_t v[kBStride];
-        CG_UNROLL for (int q = 0; q < kBStride / 4; ++q) {
-          const int4 x = b[q];
-          v[4 * q] = x.x;
-          v[4 * q + 1] = x.y;
-          v[4 * q + 2] = x.z;
-          v[4 * q + 3] = x.w;
-        }
-        CG_UNROLL for (int l = 0; l < 10; ++l) {
-          p.yplusx.v[l] = v[l];
-          p.yminusx.v[l] = v[10 + l];
-          p.xy2d.v[l] = v[20 + l];
-        }
-      });
-  verdict[dst] = ok ? (uint8_t)V_ACCEPT : (uint8_t)V_REJECT;
-}
-
 CG_DEV void load_bentry(const int32_t* btab_g, uint32_t t, uint32_t k, ge_precomp& p) {
   // one 128-byte line per entry: eight 16-byte loads (L2 / MALL resident table)
   const int4* b = reinterpret_cast<const int4*>(btab_g + ((size_t)t * kBTabEntries + k) * kBStride);
@@ -353,12 +344,112 @@ CG_DEV void load_bentry(const int32_t* btab_g, uint32_t t, uint32_t k, ge_precom
   }
 }
 
+// Staging of the lane-table entries in the MSM loop (ed25519_msm's loadX / unpackX).
+//   registers (default): the A entry's packed words are fetched before a window's
+//     doublings and held across them; the R entry is loaded just before its addition.
+//   CG_MSM_LDS_A = 1: the A entry goes HBM -> LDS by LDS-DMA (global_load_lds_dwordx4,
+//     no VGPR destination) before the doublings and is read back (ds_read_b128) after
+//     them: 32 fewer VGPRs live across the doublings, 32 KB of LDS per 256-lane block.
+//   CG_MSM_LDS_R = 1 (with LDS_A): the R entry too, fetched at the same time (64 KB
+//     per block: at most 2 blocks per CU).
+// LDS image per wave and entry: [quad][lane] int4 — one DMA instruction writes 64
+// lanes x 16 B contiguously, so quad q of lane l sits at base + (q * 64 + l) * 16.
+#ifndef CG_MSM_LDS_A
+#define CG_MSM_LDS_A 0
+#endif
+#ifndef CG_MSM_LDS_R
+#define CG_MSM_LDS_R 0
+#endif
+static_assert(!CG_MSM_LDS_A || (CG_ED_TAB_PACK && CG_ED_TAB_NO0), "LDS staging needs the packed, identity-free tables");
+static_assert(!CG_MSM_LDS_R || CG_MSM_LDS_A, "CG_MSM_LDS_R needs CG_MSM_LDS_A");
+constexpr int kMsmWavesPerBlock = 4;
+constexpr int kLdsEntries = CG_MSM_LDS_A + CG_MSM_LDS_R;
+struct LdsSlot {};
+struct LateSlot {
+  uint32_t k;
+};
+#if CG_MSM_LDS_A
+// wbase: the wave's LDS image of one entry (a pointer into a __shared__ array)
+CG_DEV void lds_fetch(int4* wbase, const LaneTab& lt, int p, uint32_t k) {
+  const int4* src = k ? lt.entry(p * kSlotsPerPoint + k - 1) : g_ident_entry;
+#if defined(__HIP_DEVICE_COMPILE__)
+  CG_UNROLL for (int q = 0; q < kTabLimbs / 4; ++q)
+    __builtin_amdgcn_global_load_lds((const void*)(src + q),
+                                     (__attribute__((address_space(3))) void*)(wbase + q * 64), 16, 0, 0);
+#else
+  (void)wbase, (void)src;
+#endif
+}
+CG_DEV void lds_unpack(const int4* wbase, uint32_t lane, ge_cached& c) {
+  RawEntry r;
+  CG_UNROLL for (int q = 0; q < kTabLimbs / 4; ++q) r.q[q] = wbase[q * 64 + lane];
+  unpack_entry(r, c);
+}
+#endif
+
+CG_DEV uint32_t msm_lane(uint32_t ndig, const uint32_t* dig, uint32_t scap, uint32_t rneg, const LaneTab& lt,
+                         const int32_t* btab_g) {
+  auto getDig = [&](int w) CG_LINLINE { return dig[(size_t)w * scap]; };
+  auto getB = [&](uint32_t t, uint32_t k, ge_precomp& p) CG_LINLINE { load_bentry(btab_g, t, k, p); };
+#if CG_MSM_LDS_A
+  __shared__ int4 s_ent[kMsmWavesPerBlock * kLdsEntries * (kTabLimbs / 4) * 64];
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  int4* wa = s_ent + (size_t)wave * kLdsEntries * (kTabLimbs / 4) * 64;
+  auto loadA = [&](uint32_t k, LdsSlot&) CG_LINLINE { lds_fetch(wa, lt, 0, k); };
+  auto unpackA = [&](LdsSlot&, ge_cached& c) CG_LINLINE { lds_unpack(wa, lane, c); };
+#if CG_MSM_LDS_R
+  int4* wr = wa + (kTabLimbs / 4) * 64;
+  auto loadR = [&](uint32_t k, LdsSlot&) CG_LINLINE { lds_fetch(wr, lt, 1, k); };
+  auto unpackR = [&](LdsSlot&, ge_cached& c) CG_LINLINE { lds_unpack(wr, lane, c); };
+  return ed25519_msm<LdsSlot, LdsSlot>(ndig, getDig, rneg, loadA, unpackA, loadR, unpackR, getB);
+#else
+  auto loadR = [&](uint32_t k, LateSlot& r) CG_LINLINE { r.k = k; };
+  auto unpackR = [&](LateSlot& r, ge_cached& c) CG_LINLINE { load_slot(lt, 1, r.k, c); };
+  return ed25519_msm<LdsSlot, LateSlot>(ndig, getDig, rneg, loadA, unpackA, loadR, unpackR, getB);
+#endif
+#else
+  auto loadA = [&](uint32_t k, RawEntry& r) CG_LINLINE { fetch_slot(lt, 0, k, r); };
+  auto unpackA = [&](const RawEntry& r, ge_cached& c) CG_LINLINE { unpack_entry(r, c); };
+  auto loadR = [&](uint32_t k, LateSlot& r) CG_LINLINE { r.k = k; };
+  auto unpackR = [&](LateSlot& r, ge_cached& c) CG_LINLINE { load_slot(lt, 1, r.k, c); };
+  return ed25519_msm<RawEntry, LateSlot>(ndig, getDig, rneg, loadA, unpackA, loadR, unpackR, getB);
+#endif
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_MSM_WAVES, CG_MSM_WAVES))) void cg_ed25519_msm(
+    const uint32_t* __restrict__ sig, const uint32_t* __restrict__ status, const uint32_t* __restrict__ pstat,
+    const uint32_t* __restrict__ digits, const int32_t* __restrict__ table, const int32_t* __restrict__ btab_g,
+    uint32_t n, uint32_t cap, uint32_t scap, const uint32_t* __restrict__ out_index, uint8_t* __restrict__ verdict) {
+  CG_WAVE_PRIO(0);
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t st = i < n ? status[i] : 0u;
+  const uint32_t v = i < n ? ed_merge_verdict(st, pstat[i]) : 0u;
+  const bool live = i < n && v == V_COMPUTE;
+  // every lane of the wave walks the same bit positions: the longest scalar sets the length
+  const uint32_t ndig = wave_max(live ? ed_status_ndig(st) : 0u);
+  if (i >= n) return;
+  const uint32_t dst = out_index ? out_index[i] : i;
+  if (!live) {
+    verdict[dst] = (uint8_t)v;
+    return;
+  }
+  const uint32_t* dig = digits + i;
+#if CG_MSM_FAKE_TABLE  // timing experiment only (wrong verdicts): every lane reads lane 0's tables
+  const LaneTab lt = lane_table(const_cast<int32_t*>(table), 0, scap);
+#else
+  const LaneTab lt = lane_table(const_cast<int32_t*>(table), i, scap);
+#endif
+  const uint32_t ok = msm_lane(ndig, dig, scap, ed_status_rneg(st), lt, btab_g);
+  verdict[dst] = ok ? (uint8_t)V_ACCEPT : (uint8_t)V_REJECT;
+}
+
+
 // Points + MSM in one kernel (CORDA_AMD_ED_FUSE=1): each lane decodes A and R, writes
 // its tables and reads them straight back in its MSM — the reads then hit the L2 / MALL
 // lines the same CU just wrote instead of HBM (the two-kernel form writes the whole
 // batch's ~2.4-3 GB of tables before the first read).  Same verdict merge as the
 // separate kernels.
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_MSM_WAVES, CG_MSM_WAVES))) void cg_ed25519_pm(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_PM_WAVES, CG_PM_WAVES))) void cg_ed25519_pm(
     const uint32_t* __restrict__ pk, const uint32_t* __restrict__ sig, const uint32_t* __restrict__ status,
     const uint32_t* __restrict__ digits, int32_t* __restrict__ table, const int32_t* __restrict__ btab_g, uint32_t n,
     uint32_t cap, uint32_t scap, const uint32_t* __restrict__ out_index, uint8_t* __restrict__ verdict) {
@@ -389,12 +480,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_MSM_WAVE
     verdict[dst] = (uint8_t)v;
     return;
   }
-  uint32_t dig[kDigitWords];
-  CG_UNROLL for (int w = 0; w < kDigitWords; ++w) dig[w] = digits[(size_t)w * scap + i];
-  const uint32_t ok = ed25519_msm(
-      ndig, dig, ed_status_rneg(st), [&](uint32_t k, ge_cached& c) { load_slot(lt, 0, k, c); },
-      [&](uint32_t k, ge_cached& c) { load_slot(lt, 1, k, c); },
-      [&](uint32_t t, uint32_t k, ge_precomp& p) { load_bentry(btab_g, t, k, p); });
+  const uint32_t* dig = digits + i;
+  const uint32_t ok = msm_lane(ndig, dig, scap, ed_status_rneg(st), lt, btab_g);
   verdict[dst] = ok ? (uint8_t)V_ACCEPT : (uint8_t)V_REJECT;
 }
 
@@ -403,7 +490,7 @@ CG_DEV uint32_t wave_or(uint32_t v) { return __ballot(v != 0) != 0ull; }
 
 // MSM of the key-reuse split (cg_ed25519.h ed25519_msm_reuse): per-key A tables,
 // per-lane R table, four shared B tables; 60 doublings.
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_MSM_WAVES, CG_MSM_WAVES))) void cg_ed25519_msm_r(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_MSM_R_WAVES, CG_MSM_R_WAVES))) void cg_ed25519_msm_r(
     const uint32_t* __restrict__ status, const uint32_t* __restrict__ pstat, const uint32_t* __restrict__ digits,
     const int32_t* __restrict__ table, const int32_t* __restrict__ ktab, const uint32_t* __restrict__ key_index,
     const int32_t* __restrict__ btab_g, uint32_t n, uint32_t scap, const uint32_t* __restrict__ out_index,

@@ -94,7 +94,22 @@ def allgather_bitmap(local_words, bounds: list[int], rank: int, group=None):
     return torch.cat([out[r][:words[r]] for r in range(world)])
 
 
-def gather_ordered(local_words, bounds: list[int], out=None, ordered=None, group=None):
+def check_bounds(bounds: list[int], world: int, n_local: int | None = None, rank: int = 0) -> None:
+    """Shard boundaries as ``gather_ordered`` needs them: ``world + 1`` entries from 0,
+    non-decreasing, interior ones multiples of 32; with ``n_local``, the rank's own
+    element count must be its shard's (a mismatch would misplace its words silently)."""
+    if len(bounds) != world + 1:
+        raise ValueError(f"{len(bounds)} shard boundaries for {world} ranks")
+    if bounds[0] != 0 or any(bounds[r + 1] < bounds[r] for r in range(world)):
+        raise ValueError("shard boundaries must start at 0 and be non-decreasing")
+    if any(x % 32 for x in bounds[1:-1]):
+        raise ValueError("shard boundaries must be multiples of 32")
+    if n_local is not None and n_local != bounds[rank + 1] - bounds[rank]:
+        raise ValueError(f"rank {rank} holds {n_local} elements, its shard [{bounds[rank]}, {bounds[rank + 1]}) "
+                         f"has {bounds[rank + 1] - bounds[rank]}")
+
+
+def gather_ordered(local_words, bounds: list[int], out=None, ordered=None, group=None, n_local: int | None = None):
     """C1 for shards of any sizes in ONE collective: every rank contributes
     ``words_max`` = the largest shard's word count (its own words zero-padded, as
     ``all_gather_into_tensor`` needs equal pieces), then rank r's
@@ -103,12 +118,12 @@ def gather_ordered(local_words, bounds: list[int], out=None, ordered=None, group
     shard has ``words_max`` words the gathered buffer is already in index order and no
     copy runs.  ``local_words``: int32 tensor of at least ``words_max`` words (the tail
     past the rank's own words must be zero); ``out`` / ``ordered``: optional preallocated
-    buffers of ``world * words_max`` / ``ceil(n / 32)`` words.  Returns the global bitmap."""
+    buffers of ``world * words_max`` / ``ceil(n / 32)`` words; ``n_local``: the rank's
+    element count, checked against its shard.  Returns the global bitmap."""
     import torch
     import torch.distributed as dist
     world = len(bounds) - 1
-    if any(x % 32 for x in bounds[1:-1]):
-        raise ValueError("shard boundaries must be multiples of 32")
+    check_bounds(bounds, dist.get_world_size(group), n_local, dist.get_rank(group) if n_local is not None else 0)
     words = [(bounds[r + 1] - bounds[r] + 31) // 32 for r in range(world)]
     wmax = max(max(words), 1)
     if local_words.numel() < wmax:
@@ -189,7 +204,7 @@ class ShardBacklog:
         import torch
         import torch.distributed as dist
         if self.bounds is not None:
-            return gather_ordered(self.bitmap, self.bounds, out, ordered, group)
+            return gather_ordered(self.bitmap, self.bounds, out, ordered, group, n_local=self.n)
         world = dist.get_world_size(group)
         if out is None:
             out = torch.zeros(self.words * world, dtype=torch.int32, device=self.bitmap.device)

@@ -125,6 +125,11 @@ static int gpu_mode(void) {
   b.msg_len[1] = 2; /* past the 1-byte arena */
   CHECK(verify(ctx, &b) == CG_E_INVALID_ARGUMENT, "message out of arena");
   b.msg_len[1] = 1;
+  b.msg_off[1] = UINT64_MAX - 7; /* off + len wraps to 8: still outside the arena */
+  b.msg_len[1] = 16;
+  CHECK(verify(ctx, &b) == CG_E_INVALID_ARGUMENT, "wrapping message offset");
+  b.msg_off[1] = 0;
+  b.msg_len[1] = 1;
   b.sig_len[2] = 73; /* ECDSA signature longer than its stride */
   CHECK(verify(ctx, &b) == CG_E_INVALID_ARGUMENT, "oversized ECDSA sig_len");
   b.sig_len[2] = 8;

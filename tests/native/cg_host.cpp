@@ -90,9 +90,10 @@ int cgh_ed25519_verify_nd(const uint8_t* pk_bytes, const uint8_t* sig_bytes, uin
   ed25519_build_table(negA, [&](int k, const ge_cached& c) { ta[k] = c; });
   ed25519_build_table(R, [&](int k, const ge_cached& c) { tr[k] = c; });
   if (force_ndig > ndig) ndig = force_ndig;
-  const uint32_t ok = ed25519_msm(
-      ndig, dig, rneg, [&](uint32_t k, ge_cached& c) { c = ta[k]; }, [&](uint32_t k, ge_cached& c) { c = tr[k]; },
-      [&](uint32_t t, uint32_t k, ge_precomp& p) { p = g_btab[t][k]; });
+  const uint32_t ok = ed25519_msm<ge_cached, ge_cached>(
+      ndig, [&](int w) { return dig[w]; }, rneg, [&](uint32_t k, ge_cached& c) { c = ta[k]; },
+      [&](const ge_cached& r, ge_cached& c) { c = r; }, [&](uint32_t k, ge_cached& c) { c = tr[k]; },
+      [&](const ge_cached& r, ge_cached& c) { c = r; }, [&](uint32_t t, uint32_t k, ge_precomp& p) { p = g_btab[t][k]; });
   return ok ? (int)V_ACCEPT : (int)V_REJECT;
 }
 

@@ -88,6 +88,18 @@ def test_shard_bounds():
             assert all(x % 32 == 0 for x in b[1:-1])
 
 
+def test_check_bounds_rejects_mismatched_shards():
+    """gather_ordered's validation (a bad bounds list would misplace words silently)."""
+    from corda_amd.dist import check_bounds, shard_bounds
+    b = shard_bounds(1000, 3)
+    check_bounds(b, 3)
+    check_bounds(b, 3, n_local=b[2] - b[1], rank=1)
+    for bad, world, kw in ((b, 2, {}), ([32] + b[1:], 3, {}), ([0, 64, 32, 1000], 3, {}), ([0, 33, 64, 1000], 3, {}),
+                           (b, 3, {"n_local": b[1] + 1, "rank": 0})):
+        with pytest.raises(ValueError):
+            check_bounds(bad, world, **kw)
+
+
 def test_pack_bits_matches_device_layout():
     from corda_amd.dist import pack_bits
     m = np.zeros(70, bool)

@@ -103,8 +103,9 @@ def test_config3_full_size_mixed_batch(gpu_ctx, oracle):
     signatures, 1 KB messages, 1 % adversarial over D1-D8 (both curves' pipelines
     concurrently on their streams, several ECDSA scratch chunks).  Size-independent
     properties at full size: every untouched signature accepts; the adversarial
-    subset's verdicts equal the oracle's element for element."""
-    n, pool = 1 << 20, 1 << 15
+    subset's verdicts equal the oracle's element for element.  Each curve's 2^20
+    signatures tile 2^18 distinct (key, message, signature) tuples."""
+    n, pool = 1 << 20, 1 << 18
     p = datagen.make_batch(2 * pool, msg_bytes=1024, scheme=np.repeat(np.array([2, 3], np.uint8), pool), seed=77,
                            key_base=7_000_000)
     k1 = p.subset(np.arange(pool)).tiled(n)

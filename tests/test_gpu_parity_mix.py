@@ -7,10 +7,12 @@ chunk is verified on the GPU in both modes (Crypto.isValid, Crypto.kt:534-541;
 Crypto.doVerify, Crypto.kt:472-483) and compared element by element with the
 C restatement of i2p eddsa 0.2.0 (oracle/, test infrastructure only).
 
-The default size, 2^19, takes about 10 s on the box. Set
-CORDA_AMD_PARITY_N=10000000 for the full 10 M run (with CORDA_AMD_PARITY_EC_N for
-the ECDSA test's size); the final round-3 log is
-profiles/r03y_parity_10m_ed25519_2m_ecdsa.txt (about 200 s on the box).
+The default is the north star's full size: 10,000,000 Ed25519 signatures and
+2,097,152 ECDSA ones (about 200 s on the box together, most of it host-side
+signing and the CPU oracle). CORDA_AMD_PARITY_N / CORDA_AMD_PARITY_EC_N lower them
+for quick runs. Each test writes its summary (sizes, mismatches per mode, verdict
+counts, accepts per adversarial class) to gpurun_out/parity_summary_*.json and
+prints it, so the result can be read after a `-q` run.
 """
 from __future__ import annotations
 
@@ -33,7 +35,7 @@ import datagen  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 
-N = int(os.environ.get("CORDA_AMD_PARITY_N", 1 << 19))
+N = int(os.environ.get("CORDA_AMD_PARITY_N", 10_000_000))
 CHUNK = 1 << 21
 ADV = 0.10
 
@@ -44,6 +46,14 @@ def _oracle(oracle, w, mode, threads):
                                ctypes.c_size_t(w.sig_stride), ptr(w.sig_len), ptr(w.msg), ptr(w.msg_off),
                                ptr(w.msg_len), ctypes.c_size_t(w.n), mode, threads, ptr(out))
     return out[:w.n]
+
+
+def _write_summary(name, summary):
+    """The summary as JSON under gpurun_out/ (merged back from a gpurun box)."""
+    out = os.path.join(ROOT, "gpurun_out")
+    os.makedirs(out, exist_ok=True)
+    with open(os.path.join(out, f"parity_summary_{name}.json"), "w") as f:
+        json.dump(summary, f, indent=1)
 
 
 def test_adversarial_mix_vs_oracle(gpu_ctx, oracle):
@@ -83,17 +93,18 @@ def test_adversarial_mix_vs_oracle(gpu_ctx, oracle):
                "accepts_by_class_is_valid": dict(sorted(accepts_by_class.items())),
                "seconds": round(time.perf_counter() - t0, 1)}
     print("parity summary " + json.dumps(summary), flush=True)
-    assert mismatches[MODE_IS_VALID] == 0 and mismatches[MODE_DO_VERIFY] == 0, first_bad[:10]
+    _write_summary("ed25519", summary)
+    assert mismatches[MODE_IS_VALID] == 0 and mismatches[MODE_DO_VERIFY] == 0, (first_bad[:10], summary)
 
 
-EC_N = int(os.environ.get("CORDA_AMD_PARITY_EC_N", 1 << 16))
+EC_N = int(os.environ.get("CORDA_AMD_PARITY_EC_N", 2_097_152))
 EC_CHUNK = 1 << 19
 
 
 def test_ecdsa_adversarial_mix_vs_oracle(gpu_ctx, oracle):
     """The same run for ECDSA: K1 and R1 interleaved, 32 B ids, 10 % adversarial
-    over D1–D8, both modes, against the BC 1.57 restatement. Default 2^16;
-    CORDA_AMD_PARITY_EC_N raises it (log: profiles/r01q_parity_ecdsa_2m.txt)."""
+    over D1–D8, both modes, against the BC 1.57 restatement. Default 2,097,152
+    (CORDA_AMD_PARITY_EC_N overrides it)."""
     threads = min(16, os.cpu_count() or 1)
     t0 = time.perf_counter()
     mismatches = {MODE_IS_VALID: 0, MODE_DO_VERIFY: 0}
@@ -132,4 +143,5 @@ def test_ecdsa_adversarial_mix_vs_oracle(gpu_ctx, oracle):
                "accepts_by_class_is_valid": dict(sorted(accepts_by_class.items())),
                "seconds": round(time.perf_counter() - t0, 1)}
     print("ecdsa parity summary " + json.dumps(summary), flush=True)
-    assert mismatches[MODE_IS_VALID] == 0 and mismatches[MODE_DO_VERIFY] == 0, first_bad[:10]
+    _write_summary("ecdsa", summary)
+    assert mismatches[MODE_IS_VALID] == 0 and mismatches[MODE_DO_VERIFY] == 0, (first_bad[:10], summary)
