@@ -54,6 +54,7 @@ import socket
 import statistics
 import subprocess
 import sys
+import tempfile
 import time
 
 import numpy as np
@@ -263,6 +264,61 @@ ED_KERNELS = [*ED_PREP_KERNELS, "ed25519_msm"]
 ED_REUSE_KERNELS = ["ed25519_keyprep"]  # the key-reuse path only (distinct keys decoded once per verify)
 
 
+def timeline_path(rank):
+    """The library's span log (CORDA_AMD_TIMELINE, read once by libcordagpu at its first
+    timed call): set before the first Context so the e2e span breakdown can be read."""
+    path = os.path.join(tempfile.gettempdir(), f"corda_amd_timeline_{os.getpid()}_{rank}.txt")
+    os.environ.setdefault("CORDA_AMD_TIMELINE", path)
+    return os.environ["CORDA_AMD_TIMELINE"]
+
+
+def e2e_spans(ctx, call, path):
+    """Where one host-buffer call's time goes: the call runs once with the library's
+    HIP-event spans on, and its timeline group (times relative to the 'call' span's
+    begin, recorded at the library's entry on idle streams) is summarised: the call's
+    GPU span, host pre-work before the first H2D copy, the copies, each kernel's first
+    start / last end / summed duration, and what the host wall adds after the last
+    device event (the final sync's wake-up, the Python wrapper)."""
+    with open(path, "w"):
+        pass
+    ctx.set_profiling(True)
+    t0 = time.perf_counter()
+    call()
+    wall = (time.perf_counter() - t0) * 1e3
+    ctx.set_profiling(False)
+    try:
+        groups = [g for g in open(path).read().split("# call\n") if g.strip()]
+    except OSError:
+        return None
+    if not groups:
+        return None
+    rows = [(n, float(a), float(b)) for n, a, b in (ln.split() for ln in groups[-1].splitlines())]
+    spans = {}
+    for n, a, b in rows:
+        e = spans.setdefault(n, {"count": 0, "first_start_ms": a, "last_end_ms": b, "sum_ms": 0.0})
+        e["count"] += 1
+        e["first_start_ms"] = min(e["first_start_ms"], a)
+        e["last_end_ms"] = max(e["last_end_ms"], b)
+        e["sum_ms"] += b - a
+    for e in spans.values():
+        for k in ("first_start_ms", "last_end_ms", "sum_ms"):
+            e[k] = round(e[k], 3)
+    call_ms = spans.get("call", {}).get("last_end_ms")
+    h2d = [v for k, v in spans.items() if k.startswith("h2d")]
+    kern = [v for k, v in spans.items() if k.startswith("ed25519") or k == "stage"]
+    out = {"wall_ms": round(wall, 3), "call_gpu_ms": call_ms, "spans": spans}
+    if h2d:
+        out["host_pre_ms"] = round(min(v["first_start_ms"] for v in h2d), 3)
+        out["h2d_end_ms"] = round(max(v["last_end_ms"] for v in h2d), 3)
+    if kern:
+        out["kernels_end_ms"] = round(max(v["last_end_ms"] for v in kern), 3)
+        if h2d:
+            out["kernels_after_last_h2d_ms"] = round(out["kernels_end_ms"] - out["h2d_end_ms"], 3)
+    if call_ms is not None:
+        out["host_after_gpu_ms"] = round(wall - call_ms, 3)
+    return out
+
+
 def kstats(ctx, names):
     out = {}
     for k in names:
@@ -430,6 +486,7 @@ def run_ed25519(args, dist):
         w = datagen.add_ed25519_adversarial(w, frac=args.adversarial, seed=1 + rank)
     t_gen = time.perf_counter() - t_gen
 
+    tl_path = timeline_path(rank)
     ctx = Context(dist.local_rank)
     pb = crypto.PreparedBatch(ctx, crypto.PackedBatch(w.n, w.scheme, w.pk, w.pk_stride, w.sig, w.sig_stride,
                                                       w.sig_len, w.msg, w.msg_off, w.msg_len))
@@ -479,7 +536,7 @@ def run_ed25519(args, dist):
     accepts = int((verdict == ACCEPT).sum())
 
     # p50 batch latency: device-only (resident batch) and end-to-end (H2D + kernels + D2H)
-    lat_dev, lat_e2e, lat_small = [], [], {}
+    lat_dev, lat_e2e, lat_small, lat_small_off, spans = [], [], {}, {}, {}
     e2e_bytes, e2e_ok, h2d_peak = 0, None, None
     e2e_n = min(n, 1 << 18)
     if rank == 0:
@@ -502,19 +559,36 @@ def run_ed25519(args, dist):
         e2e_ok = bool(np.array_equal(crypto.verify_packed(ctx, sb, MODE_IS_VALID), verdict[:e2e_n]))
         for _ in range(args.latency_runs):
             t1 = time.perf_counter(); crypto.verify_packed(ctx, sb, MODE_IS_VALID); lat_e2e.append(time.perf_counter() - t1)
+        spans[e2e_n] = e2e_spans(ctx, lambda: crypto.verify_packed(ctx, sb, MODE_IS_VALID), tl_path)
         h2d_peak = pcie_h2d_peak_GBps(dist.local_rank)
-        # serving-size batches (a notary's request queue): end-to-end p50 from host buffers
-        for bn in (4096, 65536):
+        # serving-size batches (a notary's request queue): end-to-end p50 from host buffers,
+        # with the latency mode (two lanes per signature for pieces <= CORDA_AMD_ED_PAIR_MAX)
+        # as the library chooses it and, beside it, forced off
+        for bn in (4096, 16384, 65536):
             if bn > n:
                 continue
             s2 = w.subset(np.arange(bn))
             b2 = crypto.PackedBatch(s2.n, s2.scheme, s2.pk, s2.pk_stride, s2.sig, s2.sig_stride, s2.sig_len,
                                     s2.msg, s2.msg_off, s2.msg_len)
-            crypto.verify_packed(ctx, b2, MODE_IS_VALID)
-            ts = []
-            for _ in range(args.latency_runs):
-                t1 = time.perf_counter(); crypto.verify_packed(ctx, b2, MODE_IS_VALID); ts.append(time.perf_counter() - t1)
-            lat_small[bn] = round(statistics.median(ts) * 1e3, 3)
+            for dest, env in ((lat_small, None), (lat_small_off, "0")):
+                prev = os.environ.get("CORDA_AMD_ED_PAIR_MAX")
+                if env is not None:
+                    os.environ["CORDA_AMD_ED_PAIR_MAX"] = env
+                try:
+                    got2 = crypto.verify_packed(ctx, b2, MODE_IS_VALID)
+                    ts = []
+                    for _ in range(args.latency_runs):
+                        t1 = time.perf_counter(); crypto.verify_packed(ctx, b2, MODE_IS_VALID); ts.append(time.perf_counter() - t1)
+                    dest[bn] = {"p50_ms": round(statistics.median(ts) * 1e3, 3),
+                                "verdicts_match": bool(np.array_equal(got2, verdict[:bn]))}
+                    if env is None:
+                        spans[bn] = e2e_spans(ctx, lambda: crypto.verify_packed(ctx, b2, MODE_IS_VALID), tl_path)
+                finally:
+                    if env is not None:
+                        if prev is None:
+                            os.environ.pop("CORDA_AMD_ED_PAIR_MAX", None)
+                        else:
+                            os.environ["CORDA_AMD_ED_PAIR_MAX"] = prev
 
     value = n * world * args.steps / elapsed
     model = OP_MODEL["ed25519_1kb" if msg_bytes > 32 else "ed25519_32b"]
@@ -576,7 +650,11 @@ def run_ed25519(args, dist):
                     "h2d_peak_GBps": h2d_peak if lat_e2e else None,
                     "e2e_pcie_frac": round(e2e_bytes / statistics.median(lat_e2e) / 1e9 / h2d_peak, 4)
                     if lat_e2e else None,
-                    "p50_e2e_ms_by_batch": lat_small},
+                    "p50_e2e_ms_by_batch": lat_small,
+                    "p50_e2e_ms_by_batch_latency_mode_off": lat_small_off,
+                    "e2e_spans": spans,
+                    "e2e_spans_note": "one profiled call per size (HIP events on, so slightly slower than the p50 "
+                                      "runs); times in ms from the library's entry ('call' span begin)"},
         "cpu_baseline": cpu,
         "checks": {"accepts": accepts, "untouched_all_accept": untouched_ok, "datagen_s": round(t_gen, 1)},
     })
@@ -913,7 +991,9 @@ def run_backlog(args, dist):
     lo, hi = bounds[rank], bounds[rank + 1]
     n = hi - lo
     chunk = 1 << 24
-    pool = min(args.pool * 8, n)
+    # distinct signed tuples per rank, tiled to the shard: 2^23 by default — about the
+    # most the box's 16 host threads sign (keygen + sign, OpenSSL) in a minute
+    pool = min(args.pool if args.pool_set else 1 << 23, n)
     msg_bytes = args.msg_bytes or 32
     t_gen = time.perf_counter()
     p = datagen.make_batch(pool, msg_bytes=msg_bytes, seed=42 + rank, key_base=(2 << 32) + rank * pool,
@@ -923,6 +1003,7 @@ def run_backlog(args, dist):
         os.environ["CORDA_AMD_KEY_REUSE"] = "0"
     ctx = Context(dist.local_rank)
     adv_ok = [True]
+    first = {}
     t_stage = time.perf_counter()
 
     def chunks():
@@ -933,10 +1014,13 @@ def run_backlog(args, dist):
                 w = datagen.add_ed25519_adversarial(w, frac=args.adversarial, seed=1000 * rank + c0 // chunk)
             pb = crypto.PackedBatch(w.n, w.scheme, w.pk, w.pk_stride, w.sig, w.sig_stride, w.sig_len, w.msg,
                                     w.msg_off, w.msg_len)
-            if c0 == 0:  # verdict spot check on the first chunk
+            if c0 == 0:  # verdict spot check on the first chunk; its head is the CPU-baseline sample
                 v = crypto.verify_packed(ctx, pb, MODE_IS_VALID)
                 adv = np.array([c != "valid" for c in w.classes])
                 adv_ok[0] = bool((v[~adv] == ACCEPT).all())
+                if rank == 0 and world == 1 and not args.no_cpu_baseline:
+                    k = min(args.cpu_sample or 1 << 19, m)
+                    first["sample"], first["verdicts"] = w.subset(np.arange(k)), v[:k].copy()
             yield pb
 
     # the rank's shard staged as 2^24-element chunks verified into one device bitmap (C1 input)
@@ -965,6 +1049,16 @@ def run_backlog(args, dist):
                          msm.get("avg_launch_ms", 0) / 1e3, model["msm"])
     roof["pmc_note"] = "instruction counts from the config-2 (1 KB message) PMC pass; the msm kernel does not " \
                        "read messages, so its count per verify is the same for 32 B ids"
+    cpu = None
+    if first:
+        threads = cpu_threads()
+        sample = first["sample"]
+        cv, dt = oracle_verify(sample, threads)
+        cpu = {"value": round(sample.n / dt, 1), "unit": "verifies/s", "cores": threads, "kind": "port",
+               "sample": f"first {sample.n} signatures of rank 0's first chunk ({msg_bytes} B ids, incl. its "
+                         f"adversarial elements), C i2p-exact restatement (oracle/liboracle.so) on {threads} threads "
+                         f"of '{host_cpu_model()}', {dt:.1f} s wall",
+               "verdicts_match_gpu": bool(np.array_equal(cv, first["verdicts"]))}
     line = base_line(args, dist, "Ed25519 verifies/sec (100M notary backlog)", "verifies/s", value,
                      elapsed * 1e3 / args.steps, {
                          "workload": f"BASELINE config 5: {total} EDDSA_ED25519_SHA512 signatures over {msg_bytes} B "
@@ -978,8 +1072,9 @@ def run_backlog(args, dist):
                      scaling="strong")
     line.update({
         "roofline": roof,
-        "kernels": ks, "cpu_baseline": None,
+        "kernels": ks, "cpu_baseline": cpu,
         "checks": {"first_chunk_untouched_all_accept": adv_ok[0], "datagen_s": round(t_gen, 1),
+                   "distinct_tuples_per_rank": pool,
                    "stage_s": round(t_stage, 1), "chunks": len(sizes)}})
     backlog.close()
     ctx.close()

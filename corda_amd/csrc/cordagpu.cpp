@@ -44,6 +44,8 @@ constexpr uint32_t kEdChunk = 1u << 21;  // Ed25519 scratch chunk (elements)
 // cg_batch_verify of a large Ed25519 subset: pieces on two streams (launch_verify);
 // CORDA_AMD_ED_SPLIT overrides the count, pieces stay >= kEdSplitMin elements
 constexpr uint32_t kEdSplitMin = 65536;
+// Ed25519 pieces up to this size run in the latency mode (two lanes per signature)
+constexpr uint32_t kEdPairMaxDefault = 16384;
 constexpr uint32_t kEdSplitDefault = 1;  // r03d A/B: 2 or 4 pieces measured no faster (95-96 M/s either way)
 
 struct Stat {
@@ -170,6 +172,10 @@ struct cg_ctx {
   size_t ring_cap = 0;
   CopyPool* pool = nullptr;
   bool profiling = false;
+  // the "call" span of a profiled cg_verify_batch: begin recorded at entry (the
+  // streams are idle then, so it marks the host's entry on the GPU clock), end after
+  // the verdicts' D2H copy, just before the final sync (end_call_span)
+  hipEvent_t call_begin = nullptr;
   std::map<std::string, Stat> stats;
   std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending;
   std::vector<hipEvent_t> event_pool;
@@ -239,6 +245,23 @@ struct Timed {
   }
 };
 
+void begin_call_span(cg_ctx* ctx) {
+  if (!ctx->profiling || ctx->call_begin) return;
+  ctx->call_begin = take_event(ctx);
+  if (ctx->call_begin) (void)hipEventRecord(ctx->call_begin, ctx->stream);
+}
+void end_call_span(cg_ctx* ctx) {
+  if (!ctx->call_begin) return;
+  hipEvent_t e = take_event(ctx);
+  if (e) {
+    (void)hipEventRecord(e, ctx->stream);
+    ctx->pending.insert(ctx->pending.begin(), {"call", {ctx->call_begin, e}});  // first: the timeline's reference
+  } else {
+    ctx->event_pool.push_back(ctx->call_begin);
+  }
+  ctx->call_begin = nullptr;
+}
+
 void collect_timings(cg_ctx* ctx) {
   // CORDA_AMD_TIMELINE=<file>: every timed span of the call appended as
   // "name items start_ms end_ms" relative to the call's first span (tools/timeline.py)
@@ -271,16 +294,16 @@ void collect_timings(cg_ctx* ctx) {
   ctx->pending.clear();
 }
 
-// ---------------------------------------------------------------- device blocks
-// Requests are rounded to 1/8 of their power-of-two size class so that repeated
-// batches of similar shape hit the cache; a cached block is reused for requests of
-// at least half its size.  All users run on ctx->stream, so reuse is stream-ordered.
 // min(off + len, bytes) without the wrap of off + len (an element or component
 // outside the arena is rejected by its own check; this only sizes upload prefixes).
 inline uint64_t clamped_end(uint64_t off, uint64_t len, uint64_t bytes) {
   return off >= bytes ? bytes : off + std::min<uint64_t>(len, bytes - off);
 }
 
+// ---------------------------------------------------------------- device blocks
+// Requests are rounded to 1/8 of their power-of-two size class so that repeated
+// batches of similar shape hit the cache; a cached block is reused for requests of
+// at least half its size.  All users run on ctx->stream, so reuse is stream-ordered.
 size_t round_block(size_t bytes) {
   if (bytes <= 4096) return (bytes + 255) & ~(size_t)255;
   size_t p = 1;
@@ -430,6 +453,9 @@ struct cg_batch {
   // the K4 DER parse that opens every verify (BC decodes the DER inside each
   // engineVerify call); null in tx-pipeline batches, whose staging parse already sits
   // inside the pipeline's own timed run
+  const void* raw_kept[3] = {nullptr, nullptr, nullptr};  // MsgSrc::keep_raw: staging's raw rows
+  const uint8_t* arena_pending = nullptr;  // host arena still to upload (launch_verify, beside the points kernel)
+  size_t arena_pending_bytes = 0;
   uint8_t* ec_rows[2] = {nullptr, nullptr};     // [ec[c].n][ec_sig_stride]
   uint32_t* ec_row_len[2] = {nullptr, nullptr};  // [ec[c].n], or null: every row is ec_sig_stride long
   size_t ec_sig_stride = 0;
@@ -463,6 +489,7 @@ void batch_free(cg_ctx* ctx, cg_batch* b) {
     dfree(ctx, b->ec_rows[c]);
     dfree(ctx, b->ec_row_len[c]);
   }
+  for (const void* p : b->raw_kept) dfree(ctx, p);
   delete b;
 }
 
@@ -487,6 +514,9 @@ struct MsgSrc {
   // host sync (the caller keeps the batch until its own final sync)
   uint8_t* verdict_dev = nullptr;
   bool async = false;
+  // one-chunk cg_verify_batch: the raw rows stay with the batch (freed by batch_free
+  // after the call's final sync) instead of a host sync at the end of staging
+  bool keep_raw = false;
 };
 
 cg_status check_inputs(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const uint8_t* pk, size_t pk_stride,
@@ -706,6 +736,14 @@ int key_reuse_forced() {
   return e && (e[0] == '0' || e[0] == '1') ? e[0] - '0' : -1;
 }
 
+// Latency mode (ed25519_kernels.hip cg_ed25519_points_pair / _msm_pair: two lanes per
+// signature) for Ed25519 pieces of at most this many signatures on the balanced path;
+// CORDA_AMD_ED_PAIR_MAX overrides (0: never).
+uint32_t ed_pair_max() {
+  const char* e = std::getenv("CORDA_AMD_ED_PAIR_MAX");
+  return e ? (uint32_t)std::max(0, std::atoi(e)) : kEdPairMaxDefault;
+}
+
 bool key_reuse_mode(uint32_t n, uint32_t n_keys) {
   const int forced = key_reuse_forced();
   if (forced >= 0) return forced == 1;
@@ -739,6 +777,10 @@ cg_status stage_key_dedupe(cg_ctx* ctx, cg_batch* b, const uint8_t* pk, size_t p
   const uint32_t ne = b->n_ed;
   const int forced = key_reuse_forced();
   if (forced == 0 || (ne < 64 && forced != 1)) return CG_OK;
+  // automatic mode and a batch the latency mode will verify: the key-reuse path's
+  // per-key table build (~190 doublings, one wave per 64 keys) would be the longest
+  // chain of the call, and the exact count is a host round trip
+  if (forced != 1 && ne <= ed_pair_max()) return CG_OK;
   if (forced != 1 && !key_sample_suggests_reuse(pk, pk_stride, idx0, ne)) return CG_OK;
   uint32_t tsize = 1;
   while (tsize < 2 * ne) tsize <<= 1;
@@ -858,7 +900,16 @@ cg_status create_batch(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const ui
     b->meta_owned = false;
   } else {
     if ((st = dalloc(ctx, &b->arena, m.bytes + 16, "alloc arena")) != CG_OK) return bail(st);
-    if (m.bytes) {
+    // one-chunk host verify of an Ed25519-only batch: the message arena goes up later,
+    // from launch_verify, once the points kernel (which needs only keys and R) is
+    // running — the copy then overlaps it (no ECDSA kernel reads the arena earlier)
+    const bool defer_arena = m.keep_raw && m.bytes && idx[1].empty() && idx[2].empty() && !idx[0].empty();
+    Timed t(ctx, "h2d_stage", (defer_arena ? 0 : m.bytes) + 12 * n +
+                                  (raw_owned ? n * (pk_stride + sig_stride + (sig_len ? 4 : 0)) : 0));
+    if (defer_arena) {
+      b->arena_pending = m.host;
+      b->arena_pending_bytes = m.bytes;
+    } else if (m.bytes) {
       const hipError_t e = hipMemcpyAsync(b->arena, m.host, m.bytes, hipMemcpyHostToDevice, ctx->stream);
       if (e != hipSuccess) return bail(hip_fail(ctx, e, "upload arena"));
     }
@@ -866,6 +917,11 @@ cg_status create_batch(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const ui
     if (e != hipSuccess) return bail(hip_fail(ctx, e, "pad arena"));
     if ((st = upload(ctx, &b->msg_off_all, m.off_host, n, "upload msg_off")) != CG_OK) return bail(st);
     if ((st = upload(ctx, &b->msg_len_all, m.len_host, n, "upload msg_len")) != CG_OK) return bail(st);
+    if (raw_owned) {
+      if ((st = upload(ctx, &pk_raw, pk, n * pk_stride, "upload pk")) != CG_OK) return bail(st);
+      if ((st = upload(ctx, &sig_raw, sig, n * sig_stride, "upload sig")) != CG_OK) return bail(st);
+      if (sig_len && (st = upload(ctx, &sl_raw, sig_len, n, "upload sig_len")) != CG_OK) return bail(st);
+    }
   }
   if (!raw_owned) {
     pk_raw = const_cast<uint8_t*>(m.pk_dev);
@@ -875,7 +931,7 @@ cg_status create_batch(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const ui
       const hipError_t e = hipStreamWaitEvent(ctx->stream, m.raw_ready, 0);
       if (e != hipSuccess) return bail(hip_fail(ctx, e, "wait raw rows"));
     }
-  } else {
+  } else if (m.dev) {
     if ((st = upload(ctx, &pk_raw, pk, n * pk_stride, "upload pk")) != CG_OK) return bail(st);
     if ((st = upload(ctx, &sig_raw, sig, n * sig_stride, "upload sig")) != CG_OK) return bail(st);
     if (sig_len && (st = upload(ctx, &sl_raw, sig_len, n, "upload sig_len")) != CG_OK) return bail(st);
@@ -941,10 +997,19 @@ cg_status create_batch(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const ui
   }
   // the host index vectors die here: wait for the copies that read them (unless every
   // one went through the pinned staging area of an asynchronous tx-pipeline stage)
-  hipError_t e = (m.async && ctx->pin_fallbacks == fallbacks0) ? hipSuccess : hipStreamSynchronize(ctx->stream);
+  if (m.keep_raw && raw_owned) {  // freed with the batch, after the caller's sync
+    b->raw_kept[0] = pk_raw;
+    b->raw_kept[1] = sig_raw;
+    b->raw_kept[2] = sl_raw;
+    pk_raw = sig_raw = nullptr;
+    sl_raw = nullptr;
+  }
+  hipError_t e = ((m.async || m.keep_raw) && ctx->pin_fallbacks == fallbacks0) ? hipSuccess
+                                                                               : hipStreamSynchronize(ctx->stream);
   free_raw();
   if (e != hipSuccess) return bail(hip_fail(ctx, e, "stage sync"));
-  if (!m.async) collect_timings(ctx);  // (it waits on every pending span: the pipeline collects at its end)
+  if (!m.async && !m.keep_raw && !ctx->call_begin)
+    collect_timings(ctx);  // (it waits on every pending span: the pipeline collects at its end)
   *out = b;
   return CG_OK;
 }
@@ -992,6 +1057,7 @@ bool ed_overlap_enabled() {
   const char* e = std::getenv("CORDA_AMD_ED_OVERLAP");
   return !e || std::atoi(e) != 0;
 }
+
 
 cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = true, uint32_t scratch_off = 0,
                         hipStream_t pts_stream = nullptr) {
@@ -1092,6 +1158,7 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = 
       // prepared-batch verify (this call owns the streams): points beside hash on the idle copy stream
       hipStream_t pts = pts_stream ? pts_stream : (join_streams && ed_overlap_enabled() ? ctx->copy_stream : nullptr);
       const bool fuse = ed_fuse_enabled();
+      const uint32_t pair_max = ed_pair_max();
       if (split > 1) {
         CG_TRY(ctx, hipStreamWaitEvent(ctx->hash_stream, ctx->ev_fork, 0), "fork ed25519 split");
       }
@@ -1127,7 +1194,24 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = 
           d.ktab = ctx->ed_ktab;
           d.kstat = ctx->ed_kstat;
         }
+        const bool pair = !b->ed_key_index && !fuse && cnt <= pair_max;  // latency mode
+        auto launch_points = [&](hipStream_t ps) -> cg_status {
+          Timed t(ctx, pair ? "ed25519_points_pair" : "ed25519_points", cnt, ps);
+          CG_TRY(ctx, pair ? cg::launch_ed25519_points_pair(d, cnt, ps) : cg::launch_ed25519_points(d, cnt, ps),
+                 "launch ed25519_points");
+          return CG_OK;
+        };
+        auto upload_pending_arena = [&]() -> cg_status {  // create_batch's deferred arena (one-chunk verify)
+          if (!b->arena_pending) return CG_OK;
+          Timed t(ctx, "h2d_arena", b->arena_pending_bytes);
+          CG_TRY(ctx, hipMemcpyAsync(b->arena, b->arena_pending, b->arena_pending_bytes, hipMemcpyHostToDevice,
+                                     ctx->stream), "upload arena");
+          b->arena_pending = nullptr;
+          return CG_OK;
+        };
         if (fuse && !b->ed_key_index) {  // points + MSM as one kernel after the hash kernel
+          cg_status s3 = upload_pending_arena();
+          if (s3 != CG_OK) return s3;
           {
             Timed t(ctx, "ed25519_hash", cnt);
             CG_TRY(ctx, cg::launch_ed25519_hash(d, cnt, (uint32_t)mode, ctx->stream), "launch ed25519_hash");
@@ -1146,33 +1230,31 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = 
           CG_TRY(ctx, hipEventRecord(ctx->ev_pts_in, ctx->stream), "fork points");
           CG_TRY(ctx, hipStreamWaitEvent(pts, ctx->ev_pts_in, 0), "fork points");
           if (keys_pending && piece == 0) CG_TRY(ctx, hipStreamWaitEvent(pts, ctx->ev_keys, 0), "wait keyprep");
-          {
-            Timed t(ctx, "ed25519_points", cnt, pts);
-            CG_TRY(ctx, cg::launch_ed25519_points(d, cnt, pts), "launch ed25519_points");
-          }
+          if ((s2 = launch_points(pts)) != CG_OK) return s2;
           CG_TRY(ctx, hipEventRecord(ctx->ev_pts_done, pts), "points done");
+          if ((s2 = upload_pending_arena()) != CG_OK) return s2;
           {
             Timed t(ctx, "ed25519_hash", cnt);
             CG_TRY(ctx, cg::launch_ed25519_hash(d, cnt, (uint32_t)mode, ctx->stream), "launch ed25519_hash");
           }
           CG_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_pts_done, 0), "join points");
         } else {
+          if ((s2 = upload_pending_arena()) != CG_OK) return s2;
           {
             Timed t(ctx, "ed25519_hash", cnt);
             CG_TRY(ctx, cg::launch_ed25519_hash(d, cnt, (uint32_t)mode, ctx->stream), "launch ed25519_hash");
           }
           if (keys_pending && piece < std::min<uint32_t>(split, 2))  // each lane's first points kernel
             CG_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_keys, 0), "wait keyprep");
-          {
-            Timed t(ctx, "ed25519_points", cnt);
-            CG_TRY(ctx, cg::launch_ed25519_points(d, cnt, ctx->stream), "launch ed25519_points");
-          }
+          if ((s2 = launch_points(ctx->stream)) != CG_OK) return s2;
         }
         {
-          Timed t(ctx, "ed25519_msm", cnt);
+          Timed t(ctx, pair ? "ed25519_msm_pair" : "ed25519_msm", cnt);
+          const uint32_t* oi = b->ed_index ? b->ed_index + base : nullptr;
+          uint8_t* vd = b->ed_index ? b->verdict : b->verdict + base;
           CG_TRY(ctx,
-                 cg::launch_ed25519_msm(d, cnt, b->ed_index ? b->ed_index + base : nullptr,
-                                        b->ed_index ? b->verdict : b->verdict + base, ctx->stream),
+                 pair ? cg::launch_ed25519_msm_pair(d, cnt, oi, vd, ctx->stream)
+                      : cg::launch_ed25519_msm(d, cnt, oi, vd, ctx->stream),
                  "launch ed25519_msm");
         }
         base += cnt;
@@ -1244,8 +1326,12 @@ struct VerifyRun {
 // shortens what runs after the last byte).  CORDA_AMD_VERIFY_CHUNKS / _MIN_CHUNK /
 // _HEAD / _TAIL override (tuning, tests).
 std::vector<size_t> verify_chunk_bounds(size_t n) {
+  // head 0.25: the host stages the first chunk's pageable bytes before any DMA can
+  // start (r04d spans: 0.37 ms at 0.5); tail 0.4: the last chunk — the only one whose
+  // kernels run after the last byte — stays within the latency mode (kEdPairMaxDefault)
+  // for 2^18-element calls
   size_t kmax = 8, min_chunk = 32768;
-  double head = 0.5, tail = 0.5;
+  double head = 0.25, tail = 0.4;
   if (const char* e = std::getenv("CORDA_AMD_VERIFY_CHUNKS")) kmax = std::max(1, std::atoi(e));
   if (const char* e = std::getenv("CORDA_AMD_VERIFY_MIN_CHUNK")) min_chunk = std::max(1, std::atoi(e));
   if (const char* e = std::getenv("CORDA_AMD_VERIFY_HEAD")) head = std::min(2.0, std::max(0.05, std::atof(e)));
@@ -1545,11 +1631,15 @@ cg_status cg_batch_verify(cg_ctx* ctx, cg_batch* b, int mode, uint8_t* verdict_o
   if (device_bitmap_out)
     CG_TRY(ctx, hipMemcpyAsync(device_bitmap_out, b->bitmap, nwords * 4, hipMemcpyDeviceToDevice, ctx->stream),
            "copy device bitmap");
-  if (verdict_out)
-    CG_TRY(ctx, hipMemcpyAsync(verdict_out, b->verdict, n, hipMemcpyDeviceToHost, ctx->stream), "download verdict");
-  if (accept_bitmap_out)
-    CG_TRY(ctx, hipMemcpyAsync(accept_bitmap_out, b->bitmap, nwords * 4, hipMemcpyDeviceToHost, ctx->stream),
-           "download bitmap");
+  {
+    Timed t(ctx, "d2h_verdict", (verdict_out ? n : 0) + (accept_bitmap_out ? nwords * 4 : 0));
+    if (verdict_out)
+      CG_TRY(ctx, hipMemcpyAsync(verdict_out, b->verdict, n, hipMemcpyDeviceToHost, ctx->stream), "download verdict");
+    if (accept_bitmap_out)
+      CG_TRY(ctx, hipMemcpyAsync(accept_bitmap_out, b->bitmap, nwords * 4, hipMemcpyDeviceToHost, ctx->stream),
+             "download bitmap");
+  }
+  end_call_span(ctx);
   CG_TRY(ctx, hipStreamSynchronize(ctx->stream), "verify sync");
   collect_timings(ctx);
   return CG_OK;
@@ -1577,11 +1667,25 @@ cg_status cg_verify_batch(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
   if (!ctx) return CG_E_INVALID_ARGUMENT;
   if (n && !verdict_out) return fail(ctx, CG_E_INVALID_ARGUMENT, "null verdict_out");
   if (n == 0) return CG_OK;
+  if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, CG_E_DEVICE, "hipSetDevice");
+  begin_call_span(ctx);
+  struct CallSpanEnd {  // an early error return drops the span
+    cg_ctx* c;
+    ~CallSpanEnd() {
+      if (c->call_begin) c->event_pool.push_back(c->call_begin);
+      c->call_begin = nullptr;
+    }
+  } call_span_end{ctx};
   const std::vector<size_t> cb = verify_chunk_bounds(n);
-  if (cb.size() == 2) {  // one chunk: stage, then verify
+  if (cb.size() == 2) {  // one chunk: stage, then verify, with one host sync at the end
+    MsgSrc m;
+    m.host = msg;
+    m.bytes = msg_bytes;
+    m.off_host = msg_off;
+    m.len_host = msg_len;
+    m.keep_raw = true;
     cg_batch* b = nullptr;
-    cg_status st = cg_batch_create(ctx, n, scheme_id, pk, pk_stride, sig, sig_stride, sig_len, msg, msg_bytes,
-                                   msg_off, msg_len, &b);
+    cg_status st = create_batch(ctx, n, scheme_id, pk, pk_stride, sig, sig_stride, sig_len, m, &b);
     if (st != CG_OK) return st;
     st = cg_batch_verify(ctx, b, mode, verdict_out, accept_bitmap_out, nullptr);
     cg_batch_destroy(ctx, b);
@@ -1602,9 +1706,13 @@ cg_status cg_verify_batch(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
   st = verify_pipeline(ctx, n, mode, scheme_id, pk, pk_stride, sig, sig_stride, sig_len, msg, msg_bytes, msg_off,
                        msg_len, cb, r);
   hipError_t e = hipSuccess;
-  if (st == CG_OK) e = hipMemcpyAsync(verdict_out, r.verdict, n, hipMemcpyDeviceToHost, ctx->stream);
-  if (st == CG_OK && e == hipSuccess && accept_bitmap_out)
-    e = hipMemcpyAsync(accept_bitmap_out, r.bitmap, (n + 31) / 32 * 4, hipMemcpyDeviceToHost, ctx->stream);
+  {
+    Timed t(ctx, "d2h_verdict", n + (accept_bitmap_out ? (n + 31) / 32 * 4 : 0));
+    if (st == CG_OK) e = hipMemcpyAsync(verdict_out, r.verdict, n, hipMemcpyDeviceToHost, ctx->stream);
+    if (st == CG_OK && e == hipSuccess && accept_bitmap_out)
+      e = hipMemcpyAsync(accept_bitmap_out, r.bitmap, (n + 31) / 32 * 4, hipMemcpyDeviceToHost, ctx->stream);
+  }
+  end_call_span(ctx);
   if (st == CG_OK && e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
   if (st == CG_OK && e != hipSuccess) st = hip_fail(ctx, e, "download verdicts");
   r.release(ctx);

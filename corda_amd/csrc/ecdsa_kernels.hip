@@ -361,19 +361,17 @@ __global__ __launch_bounds__(256) void cg_ecdsa_prep_a(const uint32_t* __restric
 // Phase 1b: w = s^-1 (Montgomery form) -> u1 = e w, u2 = r w (one Montgomery product
 // each lands in the plain domain) -> digits (secp256k1 also splits u2, GLV); the
 // k*Q table to affine with the Z inverses: x = X / Z^2, y = Y / Z^3.
+// prep_b's per-lane work (shared by the kernel and the folded MSM prologue): u1 = e w,
+// u2 = r w from w = s^-1 (Montgomery form: one Montgomery product lands in the plain
+// domain), their digits (secp256k1: the GLV split; returns the status' aux byte), and
+// the lane's k*Q table to affine with the batched Z inverses: x = X / Z^2, y = Y / Z^3,
+// written as the per-lane lines the MSM reads.
 template <class C>
-__global__ __launch_bounds__(256) void cg_ecdsa_prep_b(const uint32_t* __restrict__ rs, uint32_t n, uint32_t cap,
-                                                       uint32_t scap, uint32_t* __restrict__ status,
-                                                       const uint32_t* __restrict__ ework,
-                                                       const uint32_t* __restrict__ leaf_n,
-                                                       const uint32_t* __restrict__ leaf_p,
-                                                       uint32_t* __restrict__ digits, const uint32_t* __restrict__ qjac,
-                                                       uint32_t* __restrict__ qtab, uint32_t glv_full_mod,
-                                                       uint32_t index_base) {
-  CG_WAVE_PRIO(2);
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n || status[i] != 0xff) return;
-  uint32_t w[8], e[8], r[8], u1[8], u2[8], d1[9], d2[9], d3[9], aux = 0;
+CG_DEV uint32_t ecdsa_prep_b_lane(const uint32_t* rs, uint32_t i, uint32_t n, uint32_t cap, uint32_t scap,
+                                  const uint32_t* ework, const uint32_t* leaf_n, const uint32_t* leaf_p,
+                                  const uint32_t* qjac, uint32_t* qtab, bool glv_full, uint32_t d1[9], uint32_t d2[9],
+                                  uint32_t d3[9]) {
+  uint32_t w[8], e[8], r[8], u1[8], u2[8], aux = 0;
   gl_get<8>(w, leaf_n + (size_t)i * 8);
   CG_UNROLL for (int k = 0; k < 8; ++k) {
     e[k] = ework[(size_t)k * scap + i];
@@ -382,19 +380,14 @@ __global__ __launch_bounds__(256) void cg_ecdsa_prep_b(const uint32_t* __restric
   mn_mul<C>(u1, e, w);
   mn_mul<C>(u2, r, w);
   if constexpr (C::kScheme == 2) {
-    aux = ecdsa_k1_digits(u1, u2, d1, d2, d3, glv_full_mod != 0 && (index_base + i) % glv_full_mod == 0);
+    aux = ecdsa_k1_digits(u1, u2, d1, d2, d3, glv_full);
   } else {
     recode_g(d1, u1);
     recode16_65(d2, u2);
-  }
-  status[i] = 0xff | aux << 8;
-  CG_UNROLL for (int k = 0; k < 9; ++k) {
-    digits[(size_t)k * scap + i] = d1[k];
-    digits[(size_t)(9 + k) * scap + i] = d2[k];
-    if constexpr (C::kScheme == 2) digits[(size_t)(18 + k) * scap + i] = d3[k];
+    CG_UNROLL for (int k = 0; k < 9; ++k) d3[k] = 0;
   }
   // the table to affine, from the Jacobian prep_a wrote word-major into the per-lane
-  // lines the MSM reads (x = X / Z^2, y = Y / Z^3; k*Q for k = 1 is affine already)
+  // lines the MSM reads (k*Q for k = 1 is affine already)
   CG_NOUNROLL for (int k = 1; k <= 8; ++k) {
     f26 zi, zi2, zi3, X, Y;
     const uint32_t* jb = qjac + (size_t)(k - 1) * 20 * scap + i;
@@ -416,6 +409,31 @@ __global__ __launch_bounds__(256) void cg_ecdsa_prep_b(const uint32_t* __restric
     f26_mul<C>(Y, Y, zi3);
     q_store(base, X, Y);
   }
+  return aux;
+}
+
+// Phase 1b as its own kernel (CG_EC_FOLD_PREPB = 0): digits to HBM for the MSM.
+template <class C>
+__global__ __launch_bounds__(256) void cg_ecdsa_prep_b(const uint32_t* __restrict__ rs, uint32_t n, uint32_t cap,
+                                                       uint32_t scap, uint32_t* __restrict__ status,
+                                                       const uint32_t* __restrict__ ework,
+                                                       const uint32_t* __restrict__ leaf_n,
+                                                       const uint32_t* __restrict__ leaf_p,
+                                                       uint32_t* __restrict__ digits, const uint32_t* __restrict__ qjac,
+                                                       uint32_t* __restrict__ qtab, uint32_t glv_full_mod,
+                                                       uint32_t index_base) {
+  CG_WAVE_PRIO(2);
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || status[i] != 0xff) return;
+  uint32_t d1[9], d2[9], d3[9];
+  const uint32_t aux = ecdsa_prep_b_lane<C>(rs, i, n, cap, scap, ework, leaf_n, leaf_p, qjac, qtab,
+                                            glv_full_mod != 0 && (index_base + i) % glv_full_mod == 0, d1, d2, d3);
+  status[i] = 0xff | aux << 8;
+  CG_UNROLL for (int k = 0; k < 9; ++k) {
+    digits[(size_t)k * scap + i] = d1[k];
+    digits[(size_t)(9 + k) * scap + i] = d2[k];
+    if constexpr (C::kScheme == 2) digits[(size_t)(18 + k) * scap + i] = d3[k];
+  }
 }
 
 // Two waves per SIMD (<= 256 VGPRs); the GLV loop keeps one add site per formula
@@ -428,19 +446,48 @@ constexpr int ecdsa_msm_waves_min() { return CG_ECDSA_MSM_WAVES; }
 template <class C>
 constexpr int ecdsa_msm_waves_max() { return 8; }
 
+// CG_EC_FOLD_PREPB = 1 (default): prep_b's work runs as the MSM kernel's prologue
+// (ecdsa_prep_b_lane; digits stay in registers).  As a kernel of its own it was
+// latency-bound (r03g2 PMC: 0.19 / 0.14 of peak, 74-79 % of wave cycles waiting on
+// its loads); in the prologue those waits overlap the other MSM waves' arithmetic.
+#ifndef CG_EC_FOLD_PREPB
+#define CG_EC_FOLD_PREPB 1
+#endif
 template <class C>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ecdsa_msm_waves_min<C>(), ecdsa_msm_waves_max<C>())))
 void cg_ecdsa_msm(const uint32_t* __restrict__ rs,
                                                     const uint32_t* __restrict__ status,
                                                     const uint32_t* __restrict__ digits,
-                                                    const uint32_t* __restrict__ qtab,
+                                                    uint32_t* __restrict__ qtab,
                                                     const uint32_t* __restrict__ gtab_g, uint32_t n, uint32_t cap,
                                                     uint32_t scap, const uint32_t* __restrict__ out_index,
-                                                    uint8_t* __restrict__ verdict) {
+                                                    uint8_t* __restrict__ verdict, const uint32_t* __restrict__ ework,
+                                                    const uint32_t* __restrict__ leaf_n,
+                                                    const uint32_t* __restrict__ leaf_p,
+                                                    const uint32_t* __restrict__ qjac, uint32_t glv_full_mod,
+                                                    uint32_t index_base) {
   CG_WAVE_PRIO(1);
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t st = i < n ? status[i] : 0u;
+  uint32_t st = i < n ? status[i] : 0u;
   const bool live = i < n && (st & 0xff) == 0xff;
+  uint32_t d1[9], d2[9], d3[9];
+#if CG_EC_FOLD_PREPB
+  (void)digits;
+  if (live) {
+    const uint32_t aux = ecdsa_prep_b_lane<C>(rs, i, n, cap, scap, ework, leaf_n, leaf_p, qjac, qtab,
+                                              glv_full_mod != 0 && (index_base + i) % glv_full_mod == 0, d1, d2, d3);
+    st = 0xff | aux << 8;
+  }
+#else
+  (void)ework, (void)leaf_n, (void)leaf_p, (void)qjac, (void)glv_full_mod, (void)index_base;
+  if (live) {
+    CG_UNROLL for (int w = 0; w < 9; ++w) {
+      d1[w] = digits[(size_t)w * scap + i];
+      d2[w] = digits[(size_t)(9 + w) * scap + i];
+      d3[w] = C::kScheme == 2 ? digits[(size_t)(18 + w) * scap + i] : 0u;
+    }
+  }
+#endif
   // secp256k1: every lane of the wave walks the longest split scalar's digits
   const uint32_t nd = C::kScheme == 2 ? wave_max_u32(live ? (st >> 8) & 0xff : 0u) : 0u;
   if (i >= n) return;
@@ -449,15 +496,10 @@ void cg_ecdsa_msm(const uint32_t* __restrict__ rs,
     verdict[dst] = (uint8_t)st;
     return;
   }
-  uint32_t d1[9], d2[9], d3[9], r[8];
-  CG_UNROLL for (int w = 0; w < 9; ++w) {
-    d1[w] = digits[(size_t)w * scap + i];
-    d2[w] = digits[(size_t)(9 + w) * scap + i];
-    d3[w] = C::kScheme == 2 ? digits[(size_t)(18 + w) * scap + i] : 0u;
-  }
+  uint32_t r[8];
   CG_UNROLL for (int w = 0; w < 8; ++w) r[w] = rs[(size_t)w * cap + i];
   auto getQ = [&](uint32_t k, jpt& p) CG_LINLINE {
-        q_load(q_entry(const_cast<uint32_t*>(qtab), i, k), p.X, p.Y);  // affine (cg_ecdsa_prep_b): Z implied
+        q_load(q_entry(qtab, i, k), p.X, p.Y);  // affine (ecdsa_prep_b_lane): Z implied
         p.inf = 0;
       };
   auto getG = [&](uint32_t t, uint32_t k, jpt& p) CG_LINLINE {
@@ -600,9 +642,11 @@ hipError_t launch_prep(const EcdsaBatch& b, EcdsaConsts* cc, uint32_t base, uint
   hipLaunchKernelGGL(cg_inv_roots<C>, dim3(1), dim3(128), 0, s, c->inv + vn[ln], c->invp + vp[lp]);
   launch_inv_down<InvN<C>>(c->inv, vn, tn, mn, ln, s);
   launch_inv_down<InvP<C>>(c->invp, vp, tp, mp, lp, s);
+#if !CG_EC_FOLD_PREPB
   hipLaunchKernelGGL(cg_ecdsa_prep_b<C>, grid_for(cnt), dim3(256), 0, s, b.rs + base, cnt, b.n, c->scap, c->status,
                      c->ework, c->inv + vn[0], c->invp + vp[0], c->digits, c->qjac, c->qtab, cc->glv_full_mod,
                      base);
+#endif
   return hipGetLastError();
 }
 
@@ -611,8 +655,13 @@ hipError_t launch_msm(const EcdsaBatch& b, EcdsaConsts* cc, uint32_t base, uint3
                       hipStream_t s) {
   const uint32_t* gt = cc->gtab[C::kScheme == 2 ? 0 : 1];
   const EcScratch* c = &cc->sc[C::kScheme == 2 ? 0 : 1];
+  // the batched inversions' leaves (their inverses after the down-sweep): level 0
+  size_t vn[kInvMaxLevels + 1], vp[kInvMaxLevels + 1];
+  inv_layout(cnt, 8, vn, nullptr, nullptr);
+  inv_layout(7 * cnt, 10, vp, nullptr, nullptr);
   hipLaunchKernelGGL(cg_ecdsa_msm<C>, grid_for(cnt), dim3(256), 0, s, b.rs + base, c->status, c->digits, c->qtab, gt,
-                     cnt, b.n, c->scap, b.index + base, verdict);
+                     cnt, b.n, c->scap, b.index + base, verdict, c->ework, c->inv + vn[0], c->invp + vp[0], c->qjac,
+                     cc->glv_full_mod, base);
   return hipGetLastError();
 }
 

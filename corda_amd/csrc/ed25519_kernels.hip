@@ -362,13 +362,13 @@ CG_DEV void load_bentry(const int32_t* btab_g, uint32_t t, uint32_t k, ge_precom
 #endif
 static_assert(!CG_MSM_LDS_A || (CG_ED_TAB_PACK && CG_ED_TAB_NO0), "LDS staging needs the packed, identity-free tables");
 static_assert(!CG_MSM_LDS_R || CG_MSM_LDS_A, "CG_MSM_LDS_R needs CG_MSM_LDS_A");
-constexpr int kMsmWavesPerBlock = 4;
-constexpr int kLdsEntries = CG_MSM_LDS_A + CG_MSM_LDS_R;
 struct LdsSlot {};
 struct LateSlot {
   uint32_t k;
 };
 #if CG_MSM_LDS_A
+constexpr int kMsmWavesPerBlock = 4;
+constexpr int kLdsEntries = CG_MSM_LDS_A + CG_MSM_LDS_R;
 // wbase: the wave's LDS image of one entry (a pointer into a __shared__ array)
 CG_DEV void lds_fetch(int4* wbase, const LaneTab& lt, int p, uint32_t k) {
   const int4* src = k ? lt.entry(p * kSlotsPerPoint + k - 1) : g_ident_entry;
@@ -486,6 +486,82 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_PM_WAVES
 }
 
 
+// ---------------------------------------------------------------- latency mode
+// Small batches (a notary's request queue: ValidatingNotaryFlow.kt:34-40) leave most
+// SIMDs idle and each signature's dependent chain sets the call's time, so the points
+// and MSM phases run with TWO lanes per signature (lanes 2i, 2i+1 of the grid):
+//   cg_ed25519_points_pair  lane p decodes one point (p = 0: A -> -A, KEY_INVALID when
+//                           it has no root; p = 1: R, strict, REJECT) and builds its
+//                           eight table entries; its verdict byte goes to byte p of
+//                           pstat[i] (the two lanes store different bytes of the word)
+//   cg_ed25519_msm_pair     lane p runs ed25519_msm_lane (p = 0: [c0](-A) + [b_lo]B,
+//                           p = 1: [c1](+-R) + [b_hi] 2^128 B) over the shared window
+//                           positions; the two partial sums meet through a lane swap
+//                           (ed25519_pair_combine), lane 0 writes the verdict
+// Per signature ~1.4x the MSM work of cg_ed25519_msm, on a chain ~30 % shorter.
+#ifndef CG_PAIR_WAVES
+#define CG_PAIR_WAVES 2
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_POINTS_WAVES, 8))) void cg_ed25519_points_pair(
+    const uint32_t* __restrict__ pk, const uint32_t* __restrict__ sig, uint32_t n, uint32_t cap, uint32_t scap,
+    uint32_t* __restrict__ pstat, int32_t* __restrict__ table) {
+  CG_WAVE_PRIO(1);
+  const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t i = l >> 1, p = l & 1;
+  if (i >= n) return;
+  const uint32_t* src = p ? sig : pk;  // R is words 0..7 of the signature rows
+  uint32_t w[8];
+  CG_UNROLL for (int k = 0; k < 8; ++k) w[k] = src[(size_t)k * cap + i];
+  ge_p3 P;
+  uint32_t ok = ge_frombytes_i2p(P, w);
+  if (p) {
+    ok = ok && ge_strict_check(P, w);
+  } else {
+    fe_neg_p(P.X, P.X);  // -A kept floor-shaped, as ed25519_points_stage
+    fe_neg_p(P.T, P.T);
+  }
+  reinterpret_cast<uint8_t*>(pstat)[4 * (size_t)i + p] = (uint8_t)(ok ? V_COMPUTE : p ? V_REJECT : V_KEY_INVALID);
+  if (!ok) return;
+  const LaneTab lt = lane_table(table, i, scap);
+  ed25519_build_table(P, [&](int k, const ge_cached& c) { store_slot(lt, (int)p, k, c); });
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_PAIR_WAVES, CG_PAIR_WAVES))) void cg_ed25519_msm_pair(
+    const uint32_t* __restrict__ status, const uint32_t* __restrict__ pstat, const uint32_t* __restrict__ digits,
+    const int32_t* __restrict__ table, const int32_t* __restrict__ btab_g, uint32_t n, uint32_t scap,
+    const uint32_t* __restrict__ out_index, uint8_t* __restrict__ verdict) {
+  CG_WAVE_PRIO(0);
+  const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t i = l >> 1, p = l & 1;
+  const bool in = i < n;
+  const uint32_t st = in ? status[i] : 0u;
+  const uint32_t pw = in ? pstat[i] : 0u;
+  // ed25519_points_stage precedence: A's KEY_INVALID first, then (after the hash
+  // phase's verdict, ed_merge_verdict) R's REJECT
+  const uint32_t pa = pw & 0xff, pr = (pw >> 8) & 0xff;
+  const uint32_t v = in ? ed_merge_verdict(st, pa != V_COMPUTE ? pa : pr) : 0u;
+  const bool live = in && v == V_COMPUTE;
+  const uint32_t ndig = wave_max(live ? ed_status_ndig(st) : 0u);
+  if (!in) return;
+  const uint32_t dst = out_index ? out_index[i] : i;
+  if (!live) {  // both lanes of a signature take the same branch
+    if (p == 0) verdict[dst] = (uint8_t)v;
+    return;
+  }
+  const uint32_t* dig = digits + i;
+  const LaneTab lt = lane_table(const_cast<int32_t*>(table), i, scap);
+  ge_p1p1 t;
+  ed25519_msm_lane<RawEntry>(
+      t, ndig, p, [&](int w) CG_LINLINE { return dig[(size_t)w * scap]; }, p ? ed_status_rneg(st) : 0u,
+      [&](uint32_t k, RawEntry& r) CG_LINLINE { fetch_slot(lt, (int)p, k, r); },
+      [&](const RawEntry& r, ge_cached& c) CG_LINLINE { unpack_entry(r, c); },
+      [&](uint32_t tb, uint32_t k, ge_precomp& q) CG_LINLINE { load_bentry(btab_g, tb, k, q); });
+  const uint32_t ok = ed25519_pair_combine(t, [&](fe& x) CG_LINLINE {
+    CG_UNROLL for (int k = 0; k < 10; ++k) x.v[k] = __shfl_xor(x.v[k], 1, 64);
+  });
+  if (p == 0) verdict[dst] = ok ? (uint8_t)V_ACCEPT : (uint8_t)V_REJECT;
+}
+
 CG_DEV uint32_t wave_or(uint32_t v) { return __ballot(v != 0) != 0ull; }
 
 // MSM of the key-reuse split (cg_ed25519.h ed25519_msm_reuse): per-key A tables,
@@ -576,6 +652,21 @@ hipError_t launch_ed25519_points_msm(const Ed25519Dev& d, uint32_t n, const uint
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(cg_ed25519_pm, dim3((n + 255) / 256), dim3(256), 0, s, d.pk, d.sig, d.status, d.digits, d.table,
                      d.btab, n, d.cap, d.scap, out_index, verdict);
+  return hipGetLastError();
+}
+
+hipError_t launch_ed25519_points_pair(const Ed25519Dev& d, uint32_t n, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(cg_ed25519_points_pair, dim3((2 * n + 255) / 256), dim3(256), 0, s, d.pk, d.sig, n, d.cap, d.scap,
+                     d.pstat, d.table);
+  return hipGetLastError();
+}
+
+hipError_t launch_ed25519_msm_pair(const Ed25519Dev& d, uint32_t n, const uint32_t* out_index, uint8_t* verdict,
+                                   hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(cg_ed25519_msm_pair, dim3((2 * n + 255) / 256), dim3(256), 0, s, d.status, d.pstat, d.digits,
+                     d.table, d.btab, n, d.scap, out_index, verdict);
   return hipGetLastError();
 }
 

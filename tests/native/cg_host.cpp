@@ -102,6 +102,41 @@ int cgh_ed25519_verify(const uint8_t* pk_bytes, const uint8_t* sig_bytes, uint32
   return cgh_ed25519_verify_nd(pk_bytes, sig_bytes, sig_len, msg, msg_len, mode, 0, 0);
 }
 
+// The latency mode's two lanes (ed25519_msm_lane, p = 0 and 1) run one after the other,
+// then each lane's ed25519_pair_combine with the other's partial sum; returns -1 if
+// the two lanes disagree (they must not).
+int cgh_ed25519_verify_pair(const uint8_t* pk_bytes, const uint8_t* sig_bytes, uint32_t sig_len, const uint8_t* msg,
+                            uint32_t msg_len, uint32_t mode, uint32_t force_ndig) {
+  init_btab();
+  uint32_t pk[8], sig[16] = {0};
+  memcpy(pk, pk_bytes, 32);
+  memcpy(sig, sig_bytes, sig_len < 64 ? sig_len : 64);
+  uint32_t dig[kDigitWords], ndig, rneg;
+  uint32_t pre = ed25519_hash_stage(pk, sig, sig_len, msg, msg_len, mode, dig, ndig, rneg);
+  ge_p3 negA, R;
+  pre = ed25519_points_stage(pk, sig, pre, negA, R);
+  if (pre != V_COMPUTE) return (int)pre;
+  ge_cached tab[2][kATabEntries];
+  ed25519_build_table(negA, [&](int k, const ge_cached& c) { tab[0][k] = c; });
+  ed25519_build_table(R, [&](int k, const ge_cached& c) { tab[1][k] = c; });
+  if (force_ndig > ndig) ndig = force_ndig;
+  ge_p1p1 t[2];
+  for (uint32_t p = 0; p < 2; ++p)
+    ed25519_msm_lane<ge_cached>(
+        t[p], ndig, p, [&](int w) { return dig[w]; }, p ? rneg : 0u, [&](uint32_t k, ge_cached& c) { c = tab[p][k]; },
+        [&](const ge_cached& r, ge_cached& c) { c = r; }, [&](uint32_t tb, uint32_t k, ge_precomp& q) { q = g_btab[tb][k]; });
+  uint32_t ok[2];
+  for (int p = 0; p < 2; ++p) {
+    ge_p3 q;
+    ge_p1p1_to_p3(q, t[p ^ 1]);
+    const fe* src[4] = {&q.X, &q.Y, &q.Z, &q.T};
+    int c = 0;
+    ok[p] = ed25519_pair_combine(t[p], [&](fe& x) { x = *src[c++]; });
+  }
+  if (ok[0] != ok[1]) return -1;
+  return ok[0] ? (int)V_ACCEPT : (int)V_REJECT;
+}
+
 // The key-reuse path's phases (keyprep -> hash<REUSE> -> points_r -> msm_reuse) for
 // one signature; wide forces the all-chunk loop a fallback lane elsewhere in the
 // wave would cause; full_length forces this lane's own (h, 1) fallback.

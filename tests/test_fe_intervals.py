@@ -386,6 +386,17 @@ def msm_states(C, tab_a, tab_r, btab, rounds=4):
     return st
 
 
+def pair_combine(C, st):
+    """ed25519_pair_combine (latency mode): each lane's partial sum — the output of its
+    last addition (ADD or MADD: ed25519_msm_lane ends every window with one) — to p3,
+    the partner's p3 to cached, one cached addition, the identity test."""
+    src = p3_union(st["ADD"], st["MADD"])
+    own = to_p3(C, src)
+    s = add_cached(C, own, p3_to_cached(C, own))
+    for fe in (s[0], fe_sub(s[1], s[3])):
+        assert all(abs(a) < 1 << 29 and abs(b) < 1 << 29 for a, b in fe)
+
+
 def test_limb_bounds_hold_for_all_inputs():
     C = Checker()
     A = decode(C)
@@ -394,7 +405,10 @@ def test_limb_bounds_hold_for_all_inputs():
     tab_r = lane_table(C, R)
     tab_k = key_tables(C, A)
     btab = btab_entry(C)
-    msm_states(C, p3_union(tab_a, tab_k), tab_r, btab)
+    # the balanced and key-reuse loops; the latency mode's lanes (ed25519_msm_lane) run
+    # a subset of the same transitions (no ADD -> ADD), so their states are covered too
+    st = msm_states(C, p3_union(tab_a, tab_k), tab_r, btab)
+    pair_combine(C, st)
     # 19-scaled operands within int32 (|g| <= 113025455 = 1.684 * 2^26), f sides below
     # 2^28, columns below 2^62 (int64 has a factor 2 of headroom on top)
     assert C.max_g <= (2 ** 31 - 1) // 19

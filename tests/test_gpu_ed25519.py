@@ -417,3 +417,34 @@ def test_fused_points_msm_vs_oracle(gpu_ctx, oracle, golden_ed25519, monkeypatch
     w = datagen.add_ed25519_adversarial(datagen.make_batch(5000, msg_bytes=77, seed=61, key_base=900_000),
                                         frac=0.25, seed=7)
     assert np.array_equal(gpu_verdicts(gpu_ctx, w, mode), oracle_verdicts(oracle, w, mode))
+
+
+@pytest.mark.parametrize("pair_max", ["0", "1000000"])
+@pytest.mark.parametrize("mode", [MODE_IS_VALID, MODE_DO_VERIFY])
+def test_latency_mode_on_and_off_vs_oracle(gpu_ctx, oracle, golden_ed25519, monkeypatch, pair_max, mode):
+    """The latency mode (cg_ed25519_points_pair / cg_ed25519_msm_pair: two lanes per
+    signature, used for small pieces, CORDA_AMD_ED_PAIR_MAX) forced on for every size and
+    forced off: every golden class and a mutated 4,096-signature batch (the serving size
+    it is for) against the golden verdicts and the oracle, plus the forced (h, 1)
+    fallback on every 3rd lane (64-window loops beside ~33-window ones in one wave)."""
+    from corda_amd._lib import DEBUG_FORCE_FULL_LENGTH
+    monkeypatch.setenv("CORDA_AMD_ED_PAIR_MAX", pair_max)
+    g = golden_ed25519
+    b = crypto.pack(crypto.EDDSA_ED25519_SHA512, [bytes.fromhex(e["pk"]) for e in g],
+                    [bytes.fromhex(e["sig"]) for e in g], [bytes.fromhex(e["msg"]) for e in g])
+    key = "is_valid" if mode == MODE_IS_VALID else "do_verify"
+    exp_g = np.array([e[key] for e in g], dtype=np.uint8)
+    got_g = crypto.verify_packed(gpu_ctx, b, mode)
+    assert np.array_equal(got_g, exp_g), [(g[i]["cls"], int(got_g[i]), int(exp_g[i]))
+                                          for i in np.flatnonzero(got_g != exp_g)[:10]]
+    w = datagen.add_ed25519_adversarial(datagen.make_batch(4096, msg_bytes=1024, seed=71, key_base=950_000),
+                                        frac=0.25, seed=9)
+    exp = oracle_verdicts(oracle, w, mode)
+    got = gpu_verdicts(gpu_ctx, w, mode)
+    assert np.array_equal(got, exp), [(w.classes[i], int(got[i]), int(exp[i])) for i in np.flatnonzero(got != exp)[:10]]
+    gpu_ctx.set_debug(DEBUG_FORCE_FULL_LENGTH, 3)
+    try:
+        assert np.array_equal(gpu_verdicts(gpu_ctx, w, mode), exp)
+        assert np.array_equal(crypto.verify_packed(gpu_ctx, b, mode), exp_g)
+    finally:
+        gpu_ctx.set_debug(DEBUG_FORCE_FULL_LENGTH, 0)
