@@ -44,8 +44,11 @@ constexpr uint32_t kEdChunk = 1u << 21;  // Ed25519 scratch chunk (elements)
 // cg_batch_verify of a large Ed25519 subset: pieces on two streams (launch_verify);
 // CORDA_AMD_ED_SPLIT overrides the count, pieces stay >= kEdSplitMin elements
 constexpr uint32_t kEdSplitMin = 65536;
-// Ed25519 pieces up to this size run in the latency mode (two lanes per signature)
-constexpr uint32_t kEdPairMaxDefault = 16384;
+// Ed25519 pieces up to this size run in the latency mode (two lanes per signature):
+// r04f/r04g sweeps (host-buffer verify p50, 1 KB messages): 16,384 1.13 -> 1.02 ms,
+// 32,768 1.51 -> 1.37 ms with it, 65,536 2.21 -> 2.36 ms (slower: two waves per SIMD
+// already), so the crossover lies between 32k and 64k signatures
+constexpr uint32_t kEdPairMaxDefault = 40000;
 constexpr uint32_t kEdSplitDefault = 1;  // r03d A/B: 2 or 4 pieces measured no faster (95-96 M/s either way)
 
 struct Stat {

@@ -254,11 +254,13 @@ def test_key_reuse_path_golden_fixtures(gpu_ctx, golden_ed25519, key_reuse):
 @pytest.mark.parametrize("key_reuse", [None, "1"], indirect=True)
 @pytest.mark.parametrize("n_keys", [1, 16, 300])
 def test_key_reuse_random_signers_vs_oracle(gpu_ctx, oracle, key_reuse, n_keys):
-    """A notary-backlog shape: 20k signatures by n_keys signers (automatic mode picks
-    the key-reuse path), 25 % mutated over E1-E12, both modes, against the oracle;
-    and again with the (h, 1) fallback forced on every 5th signature (wide waves)."""
+    """A notary-backlog shape: 48k signatures by n_keys signers (automatic mode picks
+    the key-reuse path: the batch is above the latency mode's 40k, below which the
+    balanced two-lane path is the shorter chain), 25 % mutated over E1-E12, both modes,
+    against the oracle; and again with the (h, 1) fallback forced on every 5th
+    signature (wide waves)."""
     from corda_amd._lib import DEBUG_FORCE_FULL_LENGTH
-    w = datagen.make_batch(20_000, msg_bytes=48, seed=n_keys, key_base=4_000_000, key_reuse=n_keys)
+    w = datagen.make_batch(48_000, msg_bytes=48, seed=n_keys, key_base=4_000_000, key_reuse=n_keys)
     w = datagen.add_ed25519_adversarial(w, frac=0.25, seed=n_keys + 1)
     for mod in (0, 5):
         gpu_ctx.set_debug(DEBUG_FORCE_FULL_LENGTH, mod)
@@ -268,7 +270,7 @@ def test_key_reuse_random_signers_vs_oracle(gpu_ctx, oracle, key_reuse, n_keys):
                 assert np.array_equal(got, oracle_verdicts(oracle, w, mode)), (mod, mode)
         finally:
             gpu_ctx.set_debug(DEBUG_FORCE_FULL_LENGTH, 0)
-    assert (got == ACCEPT).sum() > 14000
+    assert (got == ACCEPT).sum() > 33000
 
 
 @pytest.mark.parametrize("key_reuse", [None], indirect=True)
