@@ -25,7 +25,10 @@
 //
 // Constants: tools/gen_fp26_consts.py.
 #pragma once
+#include <type_traits>
+
 #include "cg_common.h"
+#include "cg_fp26_asm.h"
 #include "cg_mp256.h"
 
 namespace cg {
@@ -100,12 +103,18 @@ CG_HD int32_t f26_kpin(int32_t x) {
 
 // 64-bit column accumulator barrier (see fe_pin64 in cg_fe25519.h): keeps a column
 // chain in source order, the carry as the first mad's addend.
+// CG_F26_PIN64 = 0 drops the barrier (A/B: LLVM may then reassociate the chains; every
+// barrier-defined register costs an s_nop before its next VALU read).
+#ifndef CG_F26_PIN64
+#define CG_F26_PIN64 1
+#endif
 CG_HD int64_t f26_pin64(int64_t x) {
-#if defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__) && CG_F26_PIN64
   asm("" : "+v"(x));
 #endif
   return x;
 }
+
 
 // Constants (p, R mod p, ...) as SGPR values: uniform, so they neither take VGPRs
 // nor get hoisted out of the hot loops into VGPRs.
@@ -123,12 +132,17 @@ struct F26<CurveR1> {
   // terms m_s p_(k-s) of the earlier steps land in column k (p_3 = 2^18, p_7 =
   // 2^10, p_8 = -2^16, p_9 = 2^22); then m_k = t_k mod 2^26 (-p^-1 = 1), and with
   // p_0 = -1 the exact quotient (t_k - m_k) / 2^26 = t_k >> 26 is the carry.
-  CG_HDM static int64_t red_terms(int k, const int32_t m[10], int64_t acc) {
-    if (k >= 3 && k - 3 <= 9) acc = f26_pin64(acc + (int64_t)m[k - 3] * f26_kpin(1 << 18));
-    if (k >= 7 && k - 7 <= 9) acc = f26_pin64(acc + (int64_t)m[k - 7] * f26_kpin(1 << 10));
-    if (k >= 8 && k - 8 <= 9) acc = f26_pin64(acc + (int64_t)m[k - 8] * f26_kpin(-(1 << 16)));
-    if (k >= 9 && k - 9 <= 9) acc = f26_pin64(acc + (int64_t)m[k - 9] * f26_kpin(1 << 22));
-    return acc;
+  // (m_(k-off), p_off) for the offsets reaching column k; returns their number
+  static constexpr int nr(int k) {
+    return (k >= 3 && k - 3 <= 9) + (k >= 7 && k - 7 <= 9) + (k >= 8 && k - 8 <= 9) + (k >= 9 && k - 9 <= 9);
+  }
+  CG_HDM static int red_list(int k, const int32_t m[10], int32_t ra[4], int32_t rb[4]) {
+    int n = 0;
+    if (k >= 3 && k - 3 <= 9) ra[n] = m[k - 3], rb[n++] = f26_kpin(1 << 18);
+    if (k >= 7 && k - 7 <= 9) ra[n] = m[k - 7], rb[n++] = f26_kpin(1 << 10);
+    if (k >= 8 && k - 8 <= 9) ra[n] = m[k - 8], rb[n++] = f26_kpin(-(1 << 16));
+    if (k >= 9 && k - 9 <= 9) ra[n] = m[k - 9], rb[n++] = f26_kpin(1 << 22);
+    return n;
   }
   CG_HDM static int64_t step(int64_t acc, int32_t& m) {
     m = (int32_t)((uint32_t)acc & (uint32_t)kF26Mask);
@@ -170,10 +184,12 @@ template <>
 struct F26<CurveK1> {
   static constexpr uint32_t kPinv = 0x2253531u;  // 977^-1 = -p^-1 mod 2^26
   // p_1 = -2^6, p_9 = 2^22; m_k = t_k (-p^-1) mod 2^26, carry (t_k - 977 m_k) / 2^26
-  CG_HDM static int64_t red_terms(int k, const int32_t m[10], int64_t acc) {
-    if (k >= 1 && k - 1 <= 9) acc = f26_pin64(acc + (int64_t)m[k - 1] * f26_kpin(-(1 << 6)));
-    if (k >= 9 && k - 9 <= 9) acc = f26_pin64(acc + (int64_t)m[k - 9] * f26_kpin(1 << 22));
-    return acc;
+  static constexpr int nr(int k) { return (k >= 1 && k - 1 <= 9) + (k >= 9 && k - 9 <= 9); }
+  CG_HDM static int red_list(int k, const int32_t m[10], int32_t ra[4], int32_t rb[4]) {
+    int n = 0;
+    if (k >= 1 && k - 1 <= 9) ra[n] = m[k - 1], rb[n++] = f26_kpin(-(1 << 6));
+    if (k >= 9 && k - 9 <= 9) ra[n] = m[k - 9], rb[n++] = f26_kpin(1 << 22);
+    return n;
   }
   CG_HDM static int64_t step(int64_t acc, int32_t& m) {
     m = (int32_t)(((uint32_t)acc * kPinv) & (uint32_t)kF26Mask);
@@ -263,6 +279,7 @@ struct F26MulOp {
     const int i = (k > 9 ? k - 9 : 0) + n;
     return i <= 9 && i <= k;
   }
+  static constexpr int np(int k) { return (k < 9 ? k : 9) - (k > 9 ? k - 9 : 0) + 1; }
   CG_HDM int32_t a(int k, int n) const { return f[(k > 9 ? k - 9 : 0) + n]; }
   CG_HDM int32_t b(int k, int n) const { return g[k - ((k > 9 ? k - 9 : 0) + n)]; }
 };
@@ -283,6 +300,7 @@ struct F26SqrOp {
     const int i = (k > 9 ? k - 9 : 0) + n;
     return 2 * i <= k;
   }
+  static constexpr int np(int k) { return k / 2 - (k > 9 ? k - 9 : 0) + 1; }
   CG_HDM int32_t a(int k, int n) const {
     const int i = (k > 9 ? k - 9 : 0) + n;
     return 2 * i == k ? f[i] : f2[i];
@@ -298,22 +316,50 @@ struct F26SumOp {
   Op1 o1;
   CG_HDM F26SumOp(const Op0& a, const Op1& b) : o0(a), o1(b) {}
   CG_HDM bool has(int k, int n) const { return n < Op0::kTerms ? o0.has(k, n) : o1.has(k, n - Op0::kTerms); }
+  static constexpr int np(int k) { return Op0::np(k) + Op1::np(k); }
   CG_HDM int32_t a(int k, int n) const { return n < Op0::kTerms ? o0.a(k, n) : o1.a(k, n - Op0::kTerms); }
   CG_HDM int32_t b(int k, int n) const { return n < Op0::kTerms ? o0.b(k, n) : o1.b(k, n - Op0::kTerms); }
 };
+
+// CG_FP26_ASM = 1 (cg_fp26_asm.h): each column of one chain, or of two interleaved
+// chains, is one inline-asm statement (tools/gen_fp26_asm.py); 0: the C chain with a
+// barrier after every mad.  Columns are compile-time indices (f26_static_for), so each
+// column's shape selects its statement with no runtime dispatch.
+template <int I, int N, typename F>
+CG_HD void f26_static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    f26_static_for<I + 1, N>(f);
+  }
+}
 
 template <class C>
 struct F26Chain {
   int32_t m[10];
   int64_t c;
   CG_HDM F26Chain() : c(0) {}
+  // column k's products, then the reduction terms of the steps s < k that reach it
   template <typename Op>
-  CG_HDM void column(f26& h, const Op& op, int k) {
-    int64_t acc = c;
+  CG_HDM void terms(F26ColTerms& x, const Op& op, int k) const {
+    int np = 0;
     CG_UNROLL for (int n = 0; n < Op::kTerms; ++n) {
-      if (op.has(k, n)) acc = f26_pin64(acc + (int64_t)op.a(k, n) * op.b(k, n));
+      if (op.has(k, n)) {
+        x.a[np] = op.a(k, n);
+        x.b[np] = op.b(k, n);
+        ++np;
+      }
     }
-    acc = F26<C>::red_terms(k, m, acc);
+    (void)F26<C>::red_list(k, m, x.ra, x.rb);
+  }
+  template <int NP, int NR>
+  CG_HDM int64_t chain(const F26ColTerms& x) const {
+    int64_t acc = c;
+    CG_UNROLL for (int n = 0; n < NP; ++n) acc = f26_pin64(acc + (int64_t)x.a[n] * x.b[n]);
+    CG_UNROLL for (int n = 0; n < NR; ++n) acc = f26_pin64(acc + (int64_t)x.ra[n] * x.rb[n]);
+    return acc;
+  }
+  // step k (k <= 9: m_k and the exact quotient) or an output limb (k >= 10)
+  CG_HDM void finish(f26& h, int64_t acc, int k) {
     if (k <= 9) {
       c = F26<C>::step(acc, m[k]);
     } else if (k < 18) {
@@ -324,22 +370,47 @@ struct F26Chain {
       h.v[9] = (int32_t)(acc >> 26);
     }
   }
+  template <int K, typename Op>
+  CG_HDM void column(f26& h, const Op& op) {
+    constexpr int NP = Op::np(K), NR = F26<C>::nr(K);
+    F26ColTerms x;
+    terms(x, op, K);
+    int64_t acc = c;
+    if constexpr (F26Asm1<NP, NR>::ok) {
+      F26Asm1<NP, NR>::run(acc, x);
+    } else {
+      acc = chain<NP, NR>(x);
+    }
+    finish(h, acc, K);
+  }
 };
 
 template <class C, typename Op>
 CG_HD void f26_chain(f26& h, const Op& op) {
   F26Chain<C> s;
-  CG_UNROLL for (int k = 0; k < 19; ++k) s.column(h, op, k);
+  f26_static_for<0, 19>([&](auto kk) CG_LINLINE { s.template column<decltype(kk)::value>(h, op); });
   F26<C>::fold(h);
 }
 template <class C, typename Op0, typename Op1>
 CG_HD void f26_chain_pair(f26& h0, const Op0& op0, f26& h1, const Op1& op1) {
   F26Chain<C> s0, s1;
   f26 r0, r1;
-  CG_UNROLL for (int k = 0; k < 19; ++k) {
-    s0.column(r0, op0, k);
-    s1.column(r1, op1, k);
-  }
+  f26_static_for<0, 19>([&](auto kk) CG_LINLINE {
+    constexpr int K = decltype(kk)::value;
+    constexpr int NP0 = Op0::np(K), NP1 = Op1::np(K), NR = F26<C>::nr(K);
+    F26ColTerms x0, x1;
+    s0.terms(x0, op0, K);
+    s1.terms(x1, op1, K);
+    int64_t a0 = s0.c, a1 = s1.c;
+    if constexpr (F26Asm2<NP0, NP1, NR>::ok) {
+      F26Asm2<NP0, NP1, NR>::run(a0, x0, a1, x1);
+    } else {
+      a0 = s0.template chain<NP0, NR>(x0);
+      a1 = s1.template chain<NP1, NR>(x1);
+    }
+    s0.finish(r0, a0, K);
+    s1.finish(r1, a1, K);
+  });
   F26<C>::fold(r0);
   F26<C>::fold(r1);
   h0 = r0;

@@ -5,7 +5,7 @@
 # come from $AB_ARGS.  Each variant runs twice, interleaved; results go to gpurun_out/ab.txt.
 set -e
 names=${*:-base new}
-for rep in 1 2; do
+for rep in $(seq 1 ${AB_REPS:-2}); do
   for v in $names; do
     lib=${v%%\%*}
     envs=()
