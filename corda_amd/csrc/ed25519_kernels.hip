@@ -91,8 +91,20 @@ CG_DEV LaneTab lane_table(int32_t* table, uint32_t i, uint32_t scap) {
 #endif
 }
 
+// Occupancy target of the hash kernel (0: the compiler's choice, 3 waves / SIMD at 138
+// VGPRs).  4 waves (128 VGPRs, 26 dwords spilled in the balanced path) hides more of
+// the serial SHA-512 rounds' latency: hash 1.355 -> 1.31 ms per 10 M chunk-set, config 2
+// +0.8 % (profiles/r04o_ab.txt, 3 interleaved reps).
+#ifndef CG_HASH_WAVES
+#define CG_HASH_WAVES 4
+#endif
+#if CG_HASH_WAVES
+#define CG_HASH_ATTR __attribute__((amdgpu_waves_per_eu(CG_HASH_WAVES, 8)))
+#else
+#define CG_HASH_ATTR
+#endif
 template <bool REUSE>
-__global__ __launch_bounds__(256) void cg_ed25519_hash(const uint32_t* __restrict__ pk, const uint32_t* __restrict__ sig,
+__global__ __launch_bounds__(256) CG_HASH_ATTR void cg_ed25519_hash(const uint32_t* __restrict__ pk, const uint32_t* __restrict__ sig,
                                                        const uint32_t* __restrict__ sig_len,
                                                        const uint8_t* __restrict__ arena,
                                                        const uint64_t* __restrict__ msg_off,

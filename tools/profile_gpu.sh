@@ -7,6 +7,9 @@
 set -e
 TAG=${1:?tag}
 export TMPDIR=/tmp
+# every launch alone on the GPU (no points kernel beside the hash kernel), so the trace's
+# per-kernel durations are the isolated ones the bench's `kernels` table reports
+export CORDA_AMD_ED_OVERLAP=0
 O=$GRAFT_REPO_ROOT/gpurun_out/prof_$TAG
 mkdir -p "$O"
 ARGS="bench.py --steps 3 --warmup 1 --no-cpu-baseline --latency-runs 1 ${BENCH_EXTRA:-}"
