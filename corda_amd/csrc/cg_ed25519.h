@@ -211,6 +211,16 @@ CG_HD void ed25519_build_table(const ge_p3& P, Put&& put) {
   }
 }
 
+// P <- 2^64 P (64 doublings): the key-reuse path's per-key tables and the four-lane
+// latency mode's high-half points.
+CG_HD void ge_p3_dbl64(ge_p3& P) {
+  ge_p1p1 x;
+  CG_NOUNROLL for (int i = 0; i < 64; ++i) {
+    ge_p3_dbl(x, P);
+    ge_p1p1_to_p3(P, x);
+  }
+}
+
 // Per distinct key of the key-reuse path: decode A once (i2p, A.2) and build the
 // tables k * 2^(64 t) (-A), t = 0..3, k = 0..8; put(t, k, cached).  Returns 0 when
 // the key has no square root (KEY_INVALID for every signature by it).
@@ -220,14 +230,8 @@ CG_HD uint32_t ed25519_key_tables(const uint32_t pk[8], Put&& put) {
   if (!ge_frombytes_i2p(P, pk)) return 0;
   fe_neg_p(P.X, P.X);
   fe_neg_p(P.T, P.T);
-  ge_p1p1 x;
   CG_NOUNROLL for (int t = 0; t < 4; ++t) {
-    if (t) {
-      CG_NOUNROLL for (int i = 0; i < 64; ++i) {
-        ge_p3_dbl(x, P);
-        ge_p1p1_to_p3(P, x);
-      }
-    }
+    if (t) ge_p3_dbl64(P);
     ed25519_build_table(P, [&](int k, const ge_cached& c) CG_LINLINE { put(t, k, c); });
   }
   return 1;
@@ -373,17 +377,23 @@ CG_HD uint32_t ed25519_msm(uint32_t ndig, GetDig&& getDig, uint32_t rneg, LoadA&
   return fe_iszero(t.X) & fe_iszero(d);
 }
 
-// Latency mode (small batches: two lanes per signature, so each lane's dependent chain
-// is ~30 % shorter).  Lane p computes one half of ed25519_msm's sum over the same
-// window positions: p = 0 the term [c0](-A) and the low B half [b_lo]B, p = 1 the term
-// [c1](+-R) and [b_hi](2^128 B).  getDig / loadT / unpackT / getB as in ed25519_msm,
-// for the lane's own table (loadT(k, Raw&): k * (its point)) and B table 2p; flip =
-// rneg for p = 1, 0 for p = 0.  Every lane runs the same instruction stream (only its
-// data differ), so the two halves of a signature may share a wave.  Leaves the
-// lane's partial sum in t (p1p1); ed25519_pair_combine adds the two.
-template <typename Raw, typename GetDig, typename LoadT, typename UnpackT, typename GetB>
+// Latency mode (small batches: two or four lanes per signature, so each lane's
+// dependent chain is shorter).  LANES = 2: lane p computes one half of ed25519_msm's
+// sum over the same window positions: p = 0 the term [c0](-A) and the low B half
+// [b_lo]B, p = 1 the term [c1](+-R) and [b_hi](2^128 B).  LANES = 4: lane q = 2 h + u
+// takes half h of that split (h = 0: c0 and b_lo, h = 1: c1 and b_hi) and of it the
+// digits u = 0: 0..15, u = 1: 16.. over the point 2^(64 u) (its own table) — the
+// scalar's 64-bit halves, so ndig - 16 windows (~64 doublings instead of ~128) —
+// and the B windows in bits 64 u .. 64 u + 63 of the half over table 2^(64 u) B.
+// getDig / loadT / unpackT / getB as in ed25519_msm, for the lane's own table
+// (loadT(k, Raw&): k * (its point)); flip = rneg for the R lanes, 0 for the A lanes.
+// Every lane runs the same instruction stream (only its data differ), so the parts
+// of a signature may share a wave.  Leaves the lane's partial sum in t (p1p1);
+// ed25519_lane_sum / ed25519_pair_combine add them.
+template <typename Raw, int LANES = 2, typename GetDig, typename LoadT, typename UnpackT, typename GetB>
 CG_HD void ed25519_msm_lane(ge_p1p1& t, uint32_t ndig, uint32_t p, GetDig&& getDig, uint32_t flip, LoadT&& loadT,
                             UnpackT&& unpackT, GetB&& getB) {
+  static_assert(LANES == 2 || LANES == 4, "two or four lanes per signature");
   ge_p2 r2;
   ge_p3 r3;
   ge_cached ca;
@@ -393,18 +403,26 @@ CG_HD void ed25519_msm_lane(ge_p1p1& t, uint32_t ndig, uint32_t p, GetDig&& getD
   fe_1(t.Y);
   fe_1(t.Z);
   fe_1(t.T);
-  const int nwin = (int)ndig;
-  const int dbase = 8 * (int)p, bbase = p ? 16 : 20;
+  const uint32_t h = LANES == 4 ? p >> 1 : p, u = LANES == 4 ? p & 1 : 0u;
+  // windows: all ndig (LANES 2), or digits 16.. of the half in the high lane (ndig >= 32
+  // always, so every lane runs ndig - 16 >= 16 windows; the low lane's digits 16.. are
+  // zero for it)
+  const int nwin = LANES == 4 ? (int)ndig - 16 : (int)ndig;
+  constexpr int kBSpan = LANES == 4 ? 64 : 128;  // bits of the B half a lane covers
+  const int dbase = 8 * (int)h + 2 * (int)u, bbase = h ? 16 : 20;
+  const uint32_t btab = 2 * h + u;
   uint32_t wd = 0;
   CG_NOUNROLL for (int j = nwin - 1; j >= 0; --j) {
     if (j == nwin - 1 || (j & 7) == 7) wd = getDig(dbase + (j >> 3));  // wave-uniform
-    const uint32_t e = (wd >> (4 * (uint32_t)(j & 7))) & 15u;
+    uint32_t e = (wd >> (4 * (uint32_t)(j & 7))) & 15u;
+    if (LANES == 4 && j >= 16) e = u ? e : 8u;  // (digit 0: the high lane's)
     const uint32_t ne = e < 8;
-    const bool bwin = ((4 * j) & (kBWin - 1)) == 0 && 4 * j < 128;
+    const bool bwin = ((4 * j) & (kBWin - 1)) == 0 && 4 * j < kBSpan;
     constexpr uint32_t kMask = (1u << kBWin) - 1, kHalf = 1u << (kBWin - 1);
     uint32_t eb = 0;
     if (bwin) {
-      const uint32_t s = (uint32_t)(128 / kBWin - 1) - (uint32_t)(4 * j) / kBWin;
+      const uint32_t pos = 4 * (uint32_t)j + 64 * u;  // bit position in the 128-bit half
+      const uint32_t s = (uint32_t)(128 / kBWin - 1) - pos / kBWin;
       const uint32_t per = 32 / kBWin, fsh = kBWin * (s % per);
       eb = (getDig(bbase + (int)(s / per)) >> fsh) & kMask;
     }
@@ -425,18 +443,17 @@ CG_HD void ed25519_msm_lane(ge_p1p1& t, uint32_t ndig, uint32_t p, GetDig&& getD
     }
     if (bwin) {
       const uint32_t nb = eb < kHalf;
-      getB(2 * p, nb ? kHalf - eb : eb - kHalf, pb);
+      getB(btab, nb ? kHalf - eb : eb - kHalf, pb);
       ge_p1p1_to_p3<true>(r3, t);
       ge_madd(t, r3, pb, nb);
     }
   }
 }
 
-// The two lanes' partial sums of a signature added and tested: t is this lane's
-// (p1p1), xchg(fe&) replaces a field element by the partner lane's.  Both lanes
-// compute the same verdict.  Returns 1 iff t0 + t1 is the identity.
+// t += the partner lane's partial sum: t is this lane's (p1p1), xchg(fe&) replaces a
+// field element by the partner lane's.  Both lanes end with the same sum.
 template <typename Xchg>
-CG_HD uint32_t ed25519_pair_combine(const ge_p1p1& t, Xchg&& xchg) {
+CG_HD void ed25519_lane_sum(ge_p1p1& t, Xchg&& xchg) {
   ge_p3 own, other;
   ge_p1p1_to_p3(own, t);
   other = own;
@@ -446,8 +463,16 @@ CG_HD uint32_t ed25519_pair_combine(const ge_p1p1& t, Xchg&& xchg) {
   xchg(other.T);
   ge_cached c;
   ge_p3_to_cached(c, other);
-  ge_p1p1 s;
-  ge_add_cached(s, own, c, 0);
+  ge_add_cached(t, own, c, 0);
+}
+
+// The two lanes' partial sums of a signature added and tested (xchg as in
+// ed25519_lane_sum).  Both lanes compute the same verdict.  Returns 1 iff t0 + t1 is
+// the identity.
+template <typename Xchg>
+CG_HD uint32_t ed25519_pair_combine(const ge_p1p1& t, Xchg&& xchg) {
+  ge_p1p1 s = t;
+  ed25519_lane_sum(s, xchg);
   fe d;
   fe_sub(d, s.Y, s.T);
   return fe_iszero(s.X) & fe_iszero(d);

@@ -51,11 +51,13 @@ hipError_t launch_key_dedupe(const uint32_t* pk, uint32_t n, uint32_t cap, uint3
                              uint32_t* key_first, hipStream_t s);
 hipError_t launch_ed25519_msm(const Ed25519Dev& d, uint32_t n, const uint32_t* out_index, uint8_t* verdict,
                               hipStream_t s);
-// Latency mode (two lanes per signature, balanced path only: d.key_index null): the
-// points phase (pstat bytes 4i / 4i+1: A's and R's verdicts) and the MSM
-hipError_t launch_ed25519_points_pair(const Ed25519Dev& d, uint32_t n, hipStream_t s);
-hipError_t launch_ed25519_msm_pair(const Ed25519Dev& d, uint32_t n, const uint32_t* out_index, uint8_t* verdict,
-                                   hipStream_t s);
+// Latency mode (lanes = 2 or 4 lanes per signature, balanced path only: d.key_index
+// null): the points phase (pstat byte 4i + q: lane q's point verdict) and the MSM.
+// lanes = 4 keeps its tables in scratch slots [0, 2n) of the view: the caller sizes
+// the scratch for 2n lanes past the view's start.
+hipError_t launch_ed25519_points_lanes(const Ed25519Dev& d, uint32_t n, uint32_t lanes, hipStream_t s);
+hipError_t launch_ed25519_msm_lanes(const Ed25519Dev& d, uint32_t n, uint32_t lanes, const uint32_t* out_index,
+                                    uint8_t* verdict, hipStream_t s);
 
 // Staging: element-major host layout -> SoA words.  `idx` (optional) gathers a
 // per-scheme subset.  Byte-granular so any stride works.

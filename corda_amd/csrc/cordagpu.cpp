@@ -49,6 +49,9 @@ constexpr uint32_t kEdSplitMin = 65536;
 // 32,768 1.51 -> 1.37 ms with it, 65,536 2.21 -> 2.36 ms (slower: two waves per SIMD
 // already), so the crossover lies between 32k and 64k signatures
 constexpr uint32_t kEdPairMaxDefault = 40000;
+// ... and up to this size with four lanes per signature (the scalars' 64-bit halves
+// over 2^64-multiple tables: ~64 doublings per lane instead of ~128)
+constexpr uint32_t kEdQuadMaxDefault = 32768;
 constexpr uint32_t kEdSplitDefault = 1;  // r03d A/B: 2 or 4 pieces measured no faster (95-96 M/s either way)
 
 struct Stat {
@@ -739,12 +742,18 @@ int key_reuse_forced() {
   return e && (e[0] == '0' || e[0] == '1') ? e[0] - '0' : -1;
 }
 
-// Latency mode (ed25519_kernels.hip cg_ed25519_points_pair / _msm_pair: two lanes per
+// Latency mode (ed25519_kernels.hip cg_ed25519_points_lanes / _msm_lanes: two lanes per
 // signature) for Ed25519 pieces of at most this many signatures on the balanced path;
 // CORDA_AMD_ED_PAIR_MAX overrides (0: never).
 uint32_t ed_pair_max() {
   const char* e = std::getenv("CORDA_AMD_ED_PAIR_MAX");
   return e ? (uint32_t)std::max(0, std::atoi(e)) : kEdPairMaxDefault;
+}
+// Four lanes per signature for latency-mode pieces of at most this many signatures;
+// CORDA_AMD_ED_QUAD_MAX overrides (0: never).
+uint32_t ed_quad_max() {
+  const char* e = std::getenv("CORDA_AMD_ED_QUAD_MAX");
+  return e ? (uint32_t)std::max(0, std::atoi(e)) : kEdQuadMaxDefault;
 }
 
 bool key_reuse_mode(uint32_t n, uint32_t n_keys) {
@@ -1144,7 +1153,13 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = 
       }
     }
     if (b->n_ed) {
-      cg_status s2 = ensure_ed_scratch(ctx, b->n_ed);
+      const bool fuse = ed_fuse_enabled();
+      const uint32_t pair_max = ed_pair_max();
+      // four lanes per signature: tables in 2n scratch slots, so only where this call
+      // owns the whole scratch (not inside verify_pipeline's two halves)
+      const bool quad_ok = join_streams && scratch_off == 0 && !b->ed_key_index && !fuse &&
+                           b->n_ed <= std::min(pair_max, ed_quad_max());
+      cg_status s2 = ensure_ed_scratch(ctx, quad_ok ? 2 * b->n_ed : b->n_ed);
       if (s2 != CG_OK) return s2;
       const uint32_t span = ctx->ed_scap - scratch_off;  // scratch lanes this batch may use
       // Large batches run as `split` index pieces alternating between ctx->stream and
@@ -1160,8 +1175,6 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = 
       hipStream_t ed_lane[2] = {ctx->stream, ctx->hash_stream};
       // prepared-batch verify (this call owns the streams): points beside hash on the idle copy stream
       hipStream_t pts = pts_stream ? pts_stream : (join_streams && ed_overlap_enabled() ? ctx->copy_stream : nullptr);
-      const bool fuse = ed_fuse_enabled();
-      const uint32_t pair_max = ed_pair_max();
       if (split > 1) {
         CG_TRY(ctx, hipStreamWaitEvent(ctx->hash_stream, ctx->ev_fork, 0), "fork ed25519 split");
       }
@@ -1198,9 +1211,11 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = 
           d.kstat = ctx->ed_kstat;
         }
         const bool pair = !b->ed_key_index && !fuse && cnt <= pair_max;  // latency mode
+        // (quad_ok: one piece, scratch sized for 2 cnt slots above)
+        const uint32_t lanes = !pair ? 1u : quad_ok && split == 1 && 2 * (uint64_t)cnt <= ctx->ed_scap ? 4u : 2u;
         auto launch_points = [&](hipStream_t ps) -> cg_status {
-          Timed t(ctx, pair ? "ed25519_points_pair" : "ed25519_points", cnt, ps);
-          CG_TRY(ctx, pair ? cg::launch_ed25519_points_pair(d, cnt, ps) : cg::launch_ed25519_points(d, cnt, ps),
+          Timed t(ctx, lanes == 4 ? "ed25519_points_quad" : pair ? "ed25519_points_pair" : "ed25519_points", cnt, ps);
+          CG_TRY(ctx, pair ? cg::launch_ed25519_points_lanes(d, cnt, lanes, ps) : cg::launch_ed25519_points(d, cnt, ps),
                  "launch ed25519_points");
           return CG_OK;
         };
@@ -1252,11 +1267,11 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = 
           if ((s2 = launch_points(ctx->stream)) != CG_OK) return s2;
         }
         {
-          Timed t(ctx, pair ? "ed25519_msm_pair" : "ed25519_msm", cnt);
+          Timed t(ctx, lanes == 4 ? "ed25519_msm_quad" : pair ? "ed25519_msm_pair" : "ed25519_msm", cnt);
           const uint32_t* oi = b->ed_index ? b->ed_index + base : nullptr;
           uint8_t* vd = b->ed_index ? b->verdict : b->verdict + base;
           CG_TRY(ctx,
-                 pair ? cg::launch_ed25519_msm_pair(d, cnt, oi, vd, ctx->stream)
+                 pair ? cg::launch_ed25519_msm_lanes(d, cnt, lanes, oi, vd, ctx->stream)
                       : cg::launch_ed25519_msm(d, cnt, oi, vd, ctx->stream),
                  "launch ed25519_msm");
         }

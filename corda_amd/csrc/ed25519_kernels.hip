@@ -103,6 +103,10 @@ CG_DEV LaneTab lane_table(int32_t* table, uint32_t i, uint32_t scap) {
 #else
 #define CG_HASH_ATTR
 #endif
+// Wave priority of the hash kernel (it runs beside the points kernel, CG_WAVE_PRIO).
+#ifndef CG_HASH_PRIO
+#define CG_HASH_PRIO 1
+#endif
 template <bool REUSE>
 __global__ __launch_bounds__(256) CG_HASH_ATTR void cg_ed25519_hash(const uint32_t* __restrict__ pk, const uint32_t* __restrict__ sig,
                                                        const uint32_t* __restrict__ sig_len,
@@ -112,7 +116,7 @@ __global__ __launch_bounds__(256) CG_HASH_ATTR void cg_ed25519_hash(const uint32
                                                        uint32_t scap, uint32_t mode, uint32_t* __restrict__ status,
                                                        uint32_t* __restrict__ digits, uint32_t full_mod,
                                                        uint32_t index_base) {
-  CG_WAVE_PRIO(1);
+  CG_WAVE_PRIO(CG_HASH_PRIO);
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint32_t pkw[8], sw[16], dig[kDigitWords], ndig, rneg;
@@ -501,77 +505,94 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_PM_WAVES
 // ---------------------------------------------------------------- latency mode
 // Small batches (a notary's request queue: ValidatingNotaryFlow.kt:34-40) leave most
 // SIMDs idle and each signature's dependent chain sets the call's time, so the points
-// and MSM phases run with TWO lanes per signature (lanes 2i, 2i+1 of the grid):
-//   cg_ed25519_points_pair  lane p decodes one point (p = 0: A -> -A, KEY_INVALID when
-//                           it has no root; p = 1: R, strict, REJECT) and builds its
-//                           eight table entries; its verdict byte goes to byte p of
-//                           pstat[i] (the two lanes store different bytes of the word)
-//   cg_ed25519_msm_pair     lane p runs ed25519_msm_lane (p = 0: [c0](-A) + [b_lo]B,
-//                           p = 1: [c1](+-R) + [b_hi] 2^128 B) over the shared window
-//                           positions; the two partial sums meet through a lane swap
-//                           (ed25519_pair_combine), lane 0 writes the verdict
-// Per signature ~1.4x the MSM work of cg_ed25519_msm, on a chain ~30 % shorter.
+// and MSM phases run with LANES = 2 or 4 lanes per signature (lanes LANES i + q):
+//   cg_ed25519_points_lanes  lane q decodes one point — half h = q (LANES 2) or q / 2
+//                            (LANES 4): h = 0 A -> -A, KEY_INVALID when it has no root;
+//                            h = 1 R, strict, REJECT — takes it to 2^64 P in the odd
+//                            lanes of LANES 4 (64 doublings), and builds its eight
+//                            table entries; its verdict byte goes to byte q of pstat[i]
+//                            (the lanes store different bytes of the word).  Tables:
+//                            LANES 2 in lane slot i (points -A, R), LANES 4 in slots
+//                            2i (-A, 2^64 (-A)) and 2i + 1 (R, 2^64 R): 2n slots.
+//   cg_ed25519_msm_lanes     lane q runs ed25519_msm_lane<LANES> (LANES 2: q = 0
+//                            [c0](-A) + [b_lo]B, q = 1 [c1](+-R) + [b_hi] 2^128 B; LANES
+//                            4 each of those over the scalars' 64-bit halves) over the
+//                            shared window positions; the partial sums meet through
+//                            lane swaps (ed25519_lane_sum, ed25519_pair_combine), lane 0
+//                            writes the verdict
+// Per signature ~1.4x (2 lanes) / ~1.7x (4 lanes) the MSM work of cg_ed25519_msm, on a
+// chain ~30 % / ~60 % shorter.
 #ifndef CG_PAIR_WAVES
 #define CG_PAIR_WAVES 2
 #endif
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_POINTS_WAVES, 8))) void cg_ed25519_points_pair(
+template <int LANES>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_POINTS_WAVES, 8))) void cg_ed25519_points_lanes(
     const uint32_t* __restrict__ pk, const uint32_t* __restrict__ sig, uint32_t n, uint32_t cap, uint32_t scap,
     uint32_t* __restrict__ pstat, int32_t* __restrict__ table) {
   CG_WAVE_PRIO(1);
   const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t i = l >> 1, p = l & 1;
+  const uint32_t i = l / LANES, q = l % LANES;
+  const uint32_t h = LANES == 4 ? q >> 1 : q, u = LANES == 4 ? q & 1 : 0u;
   if (i >= n) return;
-  const uint32_t* src = p ? sig : pk;  // R is words 0..7 of the signature rows
+  const uint32_t* src = h ? sig : pk;  // R is words 0..7 of the signature rows
   uint32_t w[8];
   CG_UNROLL for (int k = 0; k < 8; ++k) w[k] = src[(size_t)k * cap + i];
   ge_p3 P;
   uint32_t ok = ge_frombytes_i2p(P, w);
-  if (p) {
+  if (h) {
     ok = ok && ge_strict_check(P, w);
   } else {
     fe_neg_p(P.X, P.X);  // -A kept floor-shaped, as ed25519_points_stage
     fe_neg_p(P.T, P.T);
   }
-  reinterpret_cast<uint8_t*>(pstat)[4 * (size_t)i + p] = (uint8_t)(ok ? V_COMPUTE : p ? V_REJECT : V_KEY_INVALID);
+  reinterpret_cast<uint8_t*>(pstat)[4 * (size_t)i + q] = (uint8_t)(ok ? V_COMPUTE : h ? V_REJECT : V_KEY_INVALID);
   if (!ok) return;
-  const LaneTab lt = lane_table(table, i, scap);
-  ed25519_build_table(P, [&](int k, const ge_cached& c) { store_slot(lt, (int)p, k, c); });
+  if (u) ge_p3_dbl64(P);
+  const LaneTab lt = lane_table(table, LANES == 4 ? 2 * i + h : i, scap);
+  ed25519_build_table(P, [&](int k, const ge_cached& c) { store_slot(lt, (int)(LANES == 4 ? u : h), k, c); });
 }
 
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_PAIR_WAVES, CG_PAIR_WAVES))) void cg_ed25519_msm_pair(
+template <int LANES>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_PAIR_WAVES, CG_PAIR_WAVES))) void cg_ed25519_msm_lanes(
     const uint32_t* __restrict__ status, const uint32_t* __restrict__ pstat, const uint32_t* __restrict__ digits,
     const int32_t* __restrict__ table, const int32_t* __restrict__ btab_g, uint32_t n, uint32_t scap,
     const uint32_t* __restrict__ out_index, uint8_t* __restrict__ verdict) {
   CG_WAVE_PRIO(0);
   const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t i = l >> 1, p = l & 1;
+  const uint32_t i = l / LANES, q = l % LANES;
+  const uint32_t h = LANES == 4 ? q >> 1 : q, u = LANES == 4 ? q & 1 : 0u;
   const bool in = i < n;
   const uint32_t st = in ? status[i] : 0u;
   const uint32_t pw = in ? pstat[i] : 0u;
   // ed25519_points_stage precedence: A's KEY_INVALID first, then (after the hash
-  // phase's verdict, ed_merge_verdict) R's REJECT
-  const uint32_t pa = pw & 0xff, pr = (pw >> 8) & 0xff;
+  // phase's verdict, ed_merge_verdict) R's REJECT (byte 1 / byte 2 for LANES 2 / 4)
+  const uint32_t pa = pw & 0xff, pr = (pw >> (LANES == 4 ? 16 : 8)) & 0xff;
   const uint32_t v = in ? ed_merge_verdict(st, pa != V_COMPUTE ? pa : pr) : 0u;
   const bool live = in && v == V_COMPUTE;
   const uint32_t ndig = wave_max(live ? ed_status_ndig(st) : 0u);
   if (!in) return;
   const uint32_t dst = out_index ? out_index[i] : i;
-  if (!live) {  // both lanes of a signature take the same branch
-    if (p == 0) verdict[dst] = (uint8_t)v;
+  if (!live) {  // every lane of a signature takes the same branch
+    if (q == 0) verdict[dst] = (uint8_t)v;
     return;
   }
   const uint32_t* dig = digits + i;
-  const LaneTab lt = lane_table(const_cast<int32_t*>(table), i, scap);
+  const LaneTab lt = lane_table(const_cast<int32_t*>(table), LANES == 4 ? 2 * i + h : i, scap);
+  const int slot = (int)(LANES == 4 ? u : h);
   ge_p1p1 t;
-  ed25519_msm_lane<RawEntry>(
-      t, ndig, p, [&](int w) CG_LINLINE { return dig[(size_t)w * scap]; }, p ? ed_status_rneg(st) : 0u,
-      [&](uint32_t k, RawEntry& r) CG_LINLINE { fetch_slot(lt, (int)p, k, r); },
+  ed25519_msm_lane<RawEntry, LANES>(
+      t, ndig, q, [&](int w) CG_LINLINE { return dig[(size_t)w * scap]; }, h ? ed_status_rneg(st) : 0u,
+      [&](uint32_t k, RawEntry& r) CG_LINLINE { fetch_slot(lt, slot, k, r); },
       [&](const RawEntry& r, ge_cached& c) CG_LINLINE { unpack_entry(r, c); },
-      [&](uint32_t tb, uint32_t k, ge_precomp& q) CG_LINLINE { load_bentry(btab_g, tb, k, q); });
+      [&](uint32_t tb, uint32_t k, ge_precomp& p) CG_LINLINE { load_bentry(btab_g, tb, k, p); });
+  if (LANES == 4)
+    ed25519_lane_sum(t, [&](fe& x) CG_LINLINE {
+      CG_UNROLL for (int k = 0; k < 10; ++k) x.v[k] = __shfl_xor(x.v[k], 1, 64);
+    });
   const uint32_t ok = ed25519_pair_combine(t, [&](fe& x) CG_LINLINE {
-    CG_UNROLL for (int k = 0; k < 10; ++k) x.v[k] = __shfl_xor(x.v[k], 1, 64);
+    CG_UNROLL for (int k = 0; k < 10; ++k) x.v[k] = __shfl_xor(x.v[k], LANES / 2, 64);
   });
-  if (p == 0) verdict[dst] = ok ? (uint8_t)V_ACCEPT : (uint8_t)V_REJECT;
+  if (q == 0) verdict[dst] = ok ? (uint8_t)V_ACCEPT : (uint8_t)V_REJECT;
 }
 
 CG_DEV uint32_t wave_or(uint32_t v) { return __ballot(v != 0) != 0ull; }
@@ -667,18 +688,33 @@ hipError_t launch_ed25519_points_msm(const Ed25519Dev& d, uint32_t n, const uint
   return hipGetLastError();
 }
 
-hipError_t launch_ed25519_points_pair(const Ed25519Dev& d, uint32_t n, hipStream_t s) {
+hipError_t launch_ed25519_points_lanes(const Ed25519Dev& d, uint32_t n, uint32_t lanes, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(cg_ed25519_points_pair, dim3((2 * n + 255) / 256), dim3(256), 0, s, d.pk, d.sig, n, d.cap, d.scap,
-                     d.pstat, d.table);
+  if (lanes != 2 && lanes != 4) return hipErrorInvalidValue;
+  // four lanes: tables in scratch slots [0, 2n) of this view (the caller sized scap for it)
+  if (lanes == 4 && (uint64_t)2 * n > d.scap) return hipErrorInvalidValue;
+  const dim3 grid((uint32_t)(((uint64_t)lanes * n + 255) / 256));
+  if (lanes == 4)
+    hipLaunchKernelGGL(cg_ed25519_points_lanes<4>, grid, dim3(256), 0, s, d.pk, d.sig, n, d.cap, d.scap, d.pstat,
+                       d.table);
+  else
+    hipLaunchKernelGGL(cg_ed25519_points_lanes<2>, grid, dim3(256), 0, s, d.pk, d.sig, n, d.cap, d.scap, d.pstat,
+                       d.table);
   return hipGetLastError();
 }
 
-hipError_t launch_ed25519_msm_pair(const Ed25519Dev& d, uint32_t n, const uint32_t* out_index, uint8_t* verdict,
-                                   hipStream_t s) {
+hipError_t launch_ed25519_msm_lanes(const Ed25519Dev& d, uint32_t n, uint32_t lanes, const uint32_t* out_index,
+                                    uint8_t* verdict, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(cg_ed25519_msm_pair, dim3((2 * n + 255) / 256), dim3(256), 0, s, d.status, d.pstat, d.digits,
-                     d.table, d.btab, n, d.scap, out_index, verdict);
+  if (lanes != 2 && lanes != 4) return hipErrorInvalidValue;
+  if (lanes == 4 && (uint64_t)2 * n > d.scap) return hipErrorInvalidValue;
+  const dim3 grid((uint32_t)(((uint64_t)lanes * n + 255) / 256));
+  if (lanes == 4)
+    hipLaunchKernelGGL(cg_ed25519_msm_lanes<4>, grid, dim3(256), 0, s, d.status, d.pstat, d.digits, d.table, d.btab, n,
+                       d.scap, out_index, verdict);
+  else
+    hipLaunchKernelGGL(cg_ed25519_msm_lanes<2>, grid, dim3(256), 0, s, d.status, d.pstat, d.digits, d.table, d.btab, n,
+                       d.scap, out_index, verdict);
   return hipGetLastError();
 }
 

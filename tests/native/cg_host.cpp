@@ -137,6 +137,56 @@ int cgh_ed25519_verify_pair(const uint8_t* pk_bytes, const uint8_t* sig_bytes, u
   return ok[0] ? (int)V_ACCEPT : (int)V_REJECT;
 }
 
+// The four-lane latency mode: lane q = 2 h + u runs ed25519_msm_lane<4> over point
+// h (-A / R) taken to 2^(64 u) (ge_p3_dbl64, as cg_ed25519_points_lanes<4>), then the
+// lane sums with partner q ^ 1 and the combine with q ^ 2, in the kernel's order;
+// returns -1 if the four lanes disagree.
+int cgh_ed25519_verify_quad(const uint8_t* pk_bytes, const uint8_t* sig_bytes, uint32_t sig_len, const uint8_t* msg,
+                            uint32_t msg_len, uint32_t mode, uint32_t force_ndig) {
+  init_btab();
+  uint32_t pk[8], sig[16] = {0};
+  memcpy(pk, pk_bytes, 32);
+  memcpy(sig, sig_bytes, sig_len < 64 ? sig_len : 64);
+  uint32_t dig[kDigitWords], ndig, rneg;
+  uint32_t pre = ed25519_hash_stage(pk, sig, sig_len, msg, msg_len, mode, dig, ndig, rneg);
+  ge_p3 P[4];
+  pre = ed25519_points_stage(pk, sig, pre, P[0], P[2]);
+  if (pre != V_COMPUTE) return (int)pre;
+  P[1] = P[0];
+  P[3] = P[2];
+  ge_p3_dbl64(P[1]);
+  ge_p3_dbl64(P[3]);
+  static ge_cached tab[4][kATabEntries];
+  for (int q = 0; q < 4; ++q) ed25519_build_table(P[q], [&](int k, const ge_cached& c) { tab[q][k] = c; });
+  if (force_ndig > ndig) ndig = force_ndig;
+  ge_p1p1 t[4];
+  for (uint32_t q = 0; q < 4; ++q)
+    ed25519_msm_lane<ge_cached, 4>(
+        t[q], ndig, q, [&](int w) { return dig[w]; }, (q >> 1) ? rneg : 0u, [&](uint32_t k, ge_cached& c) { c = tab[q][k]; },
+        [&](const ge_cached& r, ge_cached& c) { c = r; }, [&](uint32_t tb, uint32_t k, ge_precomp& x) { x = g_btab[tb][k]; });
+  // a lane's xchg hands it the partner's p3 form of the partner's running sum
+  auto partner_of = [](const ge_p1p1& pt, ge_p3& x) { ge_p1p1_to_p3(x, pt); };
+  ge_p1p1 s[4];
+  for (int q = 0; q < 4; ++q) {  // level 1: q + (q ^ 1), both from the values before the swap
+    ge_p3 x;
+    partner_of(t[q ^ 1], x);
+    const fe* src[4] = {&x.X, &x.Y, &x.Z, &x.T};
+    int c = 0;
+    s[q] = t[q];
+    ed25519_lane_sum(s[q], [&](fe& v) { v = *src[c++]; });
+  }
+  uint32_t ok[4];
+  for (int q = 0; q < 4; ++q) {  // level 2: with q ^ 2, and the identity test
+    ge_p3 x;
+    partner_of(s[q ^ 2], x);
+    const fe* src[4] = {&x.X, &x.Y, &x.Z, &x.T};
+    int c = 0;
+    ok[q] = ed25519_pair_combine(s[q], [&](fe& v) { v = *src[c++]; });
+  }
+  if (ok[0] != ok[1] || ok[0] != ok[2] || ok[0] != ok[3]) return -1;
+  return ok[0] ? (int)V_ACCEPT : (int)V_REJECT;
+}
+
 // The key-reuse path's phases (keyprep -> hash<REUSE> -> points_r -> msm_reuse) for
 // one signature; wide forces the all-chunk loop a fallback lane elsewhere in the
 // wave would cause; full_length forces this lane's own (h, 1) fallback.

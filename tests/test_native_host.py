@@ -34,8 +34,9 @@ def host():
                                           ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]
     lib.cgh_ed25519_verify_reuse.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p,
                                              ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]
-    lib.cgh_ed25519_verify_pair.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p,
-                                            ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]
+    for fn in ("cgh_ed25519_verify_pair", "cgh_ed25519_verify_quad"):
+        getattr(lib, fn).argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p,
+                                     ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]
     return lib
 
 
@@ -229,16 +230,20 @@ def test_verify_random_mutations_vs_oracle(host, oracle):
                 oracle.oracle_ed25519_verify(p, sg, len(sg), m, len(m), 0)
 
 
-def test_verify_pair_lanes_golden_and_mutations(host, golden_ed25519, oracle):
+@pytest.mark.parametrize("fn", ["cgh_ed25519_verify_pair", "cgh_ed25519_verify_quad"])
+def test_verify_latency_lanes_golden_and_mutations(host, golden_ed25519, oracle, fn):
     """The latency mode's split of the MSM over two lanes (ed25519_msm_lane p = 0 / 1 +
-    ed25519_pair_combine): every golden row in both modes, then valid signatures and
-    single-bit mutations of R, S, M and A against the oracle, with padded digit counts;
-    both lanes must reach the same verdict (-1 otherwise)."""
+    ed25519_pair_combine) and over four (ed25519_msm_lane<4> over the 64-bit halves and
+    the 2^64-multiple tables, ed25519_lane_sum + ed25519_pair_combine): every golden row
+    in both modes, then valid signatures and single-bit mutations of R, S, M and A
+    against the oracle, with padded digit counts (64: the full-length digit range of a
+    fallback lane); every lane must reach the same verdict (-1 otherwise)."""
+    verify = getattr(host, fn)
     for e in golden_ed25519:
         pk, sig, msg = (bytes.fromhex(e[k]) for k in ("pk", "sig", "msg"))
         for nd in (0, 64):
-            assert host.cgh_ed25519_verify_pair(pk, sig, len(sig), msg, len(msg), 0, nd) == e["is_valid"], e["cls"]
-        assert host.cgh_ed25519_verify_pair(pk, sig, len(sig), msg, len(msg), 1, 0) == e["do_verify"], e["cls"]
+            assert verify(pk, sig, len(sig), msg, len(msg), 0, nd) == e["is_valid"], e["cls"]
+        assert verify(pk, sig, len(sig), msg, len(msg), 1, 0) == e["do_verify"], e["cls"]
     rnd = random.Random(17)
     for _ in range(250):
         seed, msg = rnd.randbytes(32), rnd.randbytes(rnd.randint(1, 300))
@@ -251,7 +256,7 @@ def test_verify_pair_lanes_golden_and_mutations(host, golden_ed25519, oracle):
             cases.append((bytes(b), sig, msg) if part == 3 else (pk, bytes(b), msg) if part < 2 else (pk, sig, bytes(b)))
         for p, sg, m in cases:
             nd = rnd.choice([0, 0, 34, 64])
-            assert host.cgh_ed25519_verify_pair(p, sg, len(sg), m, len(m), 0, nd) == \
+            assert verify(p, sg, len(sg), m, len(m), 0, nd) == \
                 oracle.oracle_ed25519_verify(p, sg, len(sg), m, len(m), 0)
 
 
@@ -270,8 +275,9 @@ def test_field_bounds_whole_pipeline(golden_ed25519, oracle):
     lib = ctypes.CDLL(so)
     lib.cgh_ed25519_verify_nd.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p,
                                           ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]
-    lib.cgh_ed25519_verify_pair.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p,
-                                            ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]
+    for fn in ("cgh_ed25519_verify_pair", "cgh_ed25519_verify_quad"):
+        getattr(lib, fn).argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p,
+                                     ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]
     cases = [(bytes.fromhex(e["pk"]), bytes.fromhex(e["sig"]), bytes.fromhex(e["msg"]), e["is_valid"])
              for e in golden_ed25519]
     rnd = random.Random(9)
@@ -285,8 +291,9 @@ def test_field_bounds_whole_pipeline(golden_ed25519, oracle):
     for i, (pk, sig, msg, exp) in enumerate(cases):
         nd, full = ((0, 0), (0, 1), (64, 0))[i % 3]
         assert lib.cgh_ed25519_verify_nd(pk, sig, len(sig), msg, len(msg), 0, nd, full) == exp
-        if i % 2 == 0:  # the latency mode's two-lane split (its own operation sequences)
+        if i % 2 == 0:  # the latency mode's two- and four-lane splits (their own operation sequences)
             assert lib.cgh_ed25519_verify_pair(pk, sig, len(sig), msg, len(msg), 0, nd) == exp
+            assert lib.cgh_ed25519_verify_quad(pk, sig, len(sig), msg, len(msg), 0, nd) == exp
     ml, lc = ctypes.c_int64(), ctypes.c_double()
     lib.cgh_bounds_report(ctypes.byref(ml), ctypes.byref(lc))
     # inputs stay below 1.69 * 2^26 (19 * limb fits int32), column sums far inside int64
