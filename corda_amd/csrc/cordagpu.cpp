@@ -138,6 +138,8 @@ class CopyPool {
 
 struct cg_ctx {
   int device = -1;
+  uint32_t n_cu = 256;                  // compute units (hipDeviceProp)
+  uint32_t lds_per_cu = 160 * 1024;     // LDS bytes per CU on gfx950 (the only target cg_open accepts)
   hipStream_t stream = nullptr;
   hipStream_t copy_stream = nullptr;  // host-to-device uploads overlapped with `stream` (tx pipeline)
   hipStream_t hash_stream = nullptr;  // tx pipeline: Merkle ids of chunk k+1 beside chunk k's signatures
@@ -626,6 +628,7 @@ cg_status cg_open(int device, cg_ctx** out) {
   cg_ctx* ctx = new (std::nothrow) cg_ctx();
   if (!ctx) return CG_E_OUT_OF_MEMORY;
   ctx->device = device;
+  ctx->n_cu = (uint32_t)std::max(1, prop.multiProcessorCount);
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
     delete ctx;
     return CG_E_DEVICE;
@@ -748,6 +751,18 @@ int key_reuse_forced() {
 uint32_t ed_pair_max() {
   const char* e = std::getenv("CORDA_AMD_ED_PAIR_MAX");
   return e ? (uint32_t)std::max(0, std::atoi(e)) : kEdPairMaxDefault;
+}
+// Latency mode: the hash and points kernels run side by side with a few blocks each,
+// and the dispatcher packs those blocks onto the same CUs, where they slow each other
+// (4,096 signatures: hash 0.16 -> 0.26 ms beside the points kernel, r04r spans).  Each
+// block then reserves more than half a CU's LDS (dynamic, unused), so no CU holds two
+// of them and the blocks spread over idle CUs — when all of them fit at once
+// (blocks <= CUs).  CORDA_AMD_ED_SPREAD_LDS (bytes, 0: off) overrides the reservation.
+uint32_t ed_spread_lds(const cg_ctx* ctx, uint64_t blocks) {
+  const uint32_t want = ctx->lds_per_cu / 2 + 4096;
+  const char* e = std::getenv("CORDA_AMD_ED_SPREAD_LDS");
+  const uint32_t lds = e ? (uint32_t)std::max(0, std::atoi(e)) : want;
+  return blocks <= ctx->n_cu ? std::min(lds, ctx->lds_per_cu) : 0u;
 }
 // Four lanes per signature for latency-mode pieces of at most this many signatures;
 // CORDA_AMD_ED_QUAD_MAX overrides (0: never).
@@ -1213,6 +1228,7 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = 
         const bool pair = !b->ed_key_index && !fuse && cnt <= pair_max;  // latency mode
         // (quad_ok: one piece, scratch sized for 2 cnt slots above)
         const uint32_t lanes = !pair ? 1u : quad_ok && split == 1 && 2 * (uint64_t)cnt <= ctx->ed_scap ? 4u : 2u;
+        if (pair) d.spread_lds = ed_spread_lds(ctx, ((uint64_t)lanes * cnt + 255) / 256 + (cnt + 255) / 256);
         auto launch_points = [&](hipStream_t ps) -> cg_status {
           Timed t(ctx, lanes == 4 ? "ed25519_points_quad" : pair ? "ed25519_points_pair" : "ed25519_points", cnt, ps);
           CG_TRY(ctx, pair ? cg::launch_ed25519_points_lanes(d, cnt, lanes, ps) : cg::launch_ed25519_points(d, cnt, ps),
