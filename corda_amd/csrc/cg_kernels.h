@@ -29,9 +29,9 @@ struct Ed25519Dev {
   const uint32_t* kstat = nullptr;
   uint32_t full_mod = 0;         // test hook: lanes with (index_base + i) % full_mod == 0 take (c0, c1) = (h, 1)
   uint32_t index_base = 0;       // index of this chunk's first element in the Ed25519 subset
-  // latency mode: dynamic LDS each hash / points block reserves (0: none), so that the
+  // latency mode: dynamic LDS each points / hash block reserves (0: none), so that the
   // two kernels' few blocks, running side by side, land on different CUs
-  uint32_t spread_lds = 0;
+  uint32_t spread_lds = 0, spread_lds_hash = 0;
 };
 
 size_t ed25519_btab_words();

@@ -178,6 +178,9 @@ struct cg_ctx {
   // filled by the copy workers while the other slot's DMA runs
   uint8_t* ring[2] = {nullptr, nullptr};
   size_t ring_cap = 0;
+  // page-locked bounce buffer of the host-buffer verify's verdict download (grow-only)
+  uint8_t* dl_pin = nullptr;
+  size_t dl_pin_cap = 0;
   CopyPool* pool = nullptr;
   bool profiling = false;
   // the "call" span of a profiled cg_verify_batch: begin recorded at entry (the
@@ -693,6 +696,7 @@ void cg_close(cg_ctx* ctx) {
     if (ctx->pin) (void)hipHostFree(ctx->pin);
     for (uint8_t* r : ctx->ring)
       if (r) (void)hipHostFree(r);
+    if (ctx->dl_pin) (void)hipHostFree(ctx->dl_pin);
     delete ctx->pool;
     delete ctx;
   } catch (...) {
@@ -754,15 +758,23 @@ uint32_t ed_pair_max() {
 }
 // Latency mode: the hash and points kernels run side by side with a few blocks each,
 // and the dispatcher packs those blocks onto the same CUs, where they slow each other
-// (4,096 signatures: hash 0.16 -> 0.26 ms beside the points kernel, r04r spans).  Each
-// block then reserves more than half a CU's LDS (dynamic, unused), so no CU holds two
-// of them and the blocks spread over idle CUs — when all of them fit at once
-// (blocks <= CUs).  CORDA_AMD_ED_SPREAD_LDS (bytes, 0: off) overrides the reservation.
-uint32_t ed_spread_lds(const cg_ctx* ctx, uint64_t blocks) {
-  const uint32_t want = ctx->lds_per_cu / 2 + 4096;
+// (4,096 signatures: hash 0.16 -> 0.26 ms beside the points kernel, r04r spans).  The
+// blocks then reserve LDS (dynamic, unused) so that no CU holds a hash block beside
+// another block: hash blocks more than half a CU's LDS, points blocks more than half
+// too when every block fits on its own CU, else exactly half (two points blocks may
+// share a CU, a hash block never joins them) when that fits; otherwise nothing.
+// CORDA_AMD_ED_SPREAD_LDS=0 turns it off.  Sets d.spread_lds / d.spread_lds_hash.
+void ed_spread_lds(const cg_ctx* ctx, cg::Ed25519Dev& d, uint64_t points_blocks, uint64_t hash_blocks) {
   const char* e = std::getenv("CORDA_AMD_ED_SPREAD_LDS");
-  const uint32_t lds = e ? (uint32_t)std::max(0, std::atoi(e)) : want;
-  return blocks <= ctx->n_cu ? std::min(lds, ctx->lds_per_cu) : 0u;
+  d.spread_lds = d.spread_lds_hash = 0;
+  if (e && std::atoi(e) == 0) return;
+  const uint32_t half = ctx->lds_per_cu / 2;
+  if (points_blocks + hash_blocks <= ctx->n_cu) {
+    d.spread_lds = d.spread_lds_hash = half + 4096;
+  } else if ((points_blocks + 1) / 2 + hash_blocks <= ctx->n_cu) {
+    d.spread_lds = half;
+    d.spread_lds_hash = half + 4096;
+  }
 }
 // Four lanes per signature for latency-mode pieces of at most this many signatures;
 // CORDA_AMD_ED_QUAD_MAX overrides (0: never).
@@ -1070,8 +1082,9 @@ cg_status join_ecdsa_streams(cg_ctx* ctx) {
 // join_streams = false (the tx pipeline): a successful exit leaves the ECDSA work
 // running on its streams and skips the bitmap; the caller joins once after the last
 // batch and frees the batches only after its final sync.
-// scratch_off: the batch's Ed25519 lanes use scratch lanes [scratch_off, scratch_off + n_ed)
-// (the verify pipeline runs two chunks at once on disjoint halves); 0 otherwise.
+// scratch_off / scratch_lanes: the batch's Ed25519 lanes may use scratch lanes
+// [scratch_off, scratch_off + scratch_lanes) (0: to the end; the verify pipeline runs
+// two chunks at once on disjoint halves); the four-lane latency mode needs 2 n_ed.
 // Ed25519 points kernels beside the hash kernels on `pts_stream` (null: after them on
 // the same stream); CORDA_AMD_ED_OVERLAP=0 turns it off.
 // CORDA_AMD_ED_FUSE=1: the balanced path's points and MSM kernels as one kernel
@@ -1087,7 +1100,7 @@ bool ed_overlap_enabled() {
 
 
 cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = true, uint32_t scratch_off = 0,
-                        hipStream_t pts_stream = nullptr) {
+                        hipStream_t pts_stream = nullptr, uint32_t scratch_lanes = 0) {
   const size_t n = b->n;
   bool joins[2] = {false, false};
   cg_status st = CG_OK;
@@ -1170,12 +1183,13 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = 
     if (b->n_ed) {
       const bool fuse = ed_fuse_enabled();
       const uint32_t pair_max = ed_pair_max();
-      // four lanes per signature: tables in 2n scratch slots, so only where this call
-      // owns the whole scratch (not inside verify_pipeline's two halves)
-      const bool quad_ok = join_streams && scratch_off == 0 && !b->ed_key_index && !fuse &&
-                           b->n_ed <= std::min(pair_max, ed_quad_max());
-      cg_status s2 = ensure_ed_scratch(ctx, quad_ok ? 2 * b->n_ed : b->n_ed);
+      // four lanes per signature: tables in 2 n_ed scratch slots — grown for it only where
+      // this call owns the whole scratch; inside a pipeline only if its region has room
+      const bool quad_want = !b->ed_key_index && !fuse && b->n_ed <= std::min(pair_max, ed_quad_max());
+      cg_status s2 = ensure_ed_scratch(ctx, quad_want && join_streams && scratch_off == 0 ? 2 * b->n_ed : b->n_ed);
       if (s2 != CG_OK) return s2;
+      const uint32_t region = scratch_lanes ? scratch_lanes : ctx->ed_scap - scratch_off;
+      const bool quad_ok = quad_want && 2 * (uint64_t)b->n_ed <= region;
       const uint32_t span = ctx->ed_scap - scratch_off;  // scratch lanes this batch may use
       // Large batches run as `split` index pieces alternating between ctx->stream and
       // hash_stream (each piece on its own scratch lanes), so one piece's kernels fill
@@ -1226,9 +1240,9 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = 
           d.kstat = ctx->ed_kstat;
         }
         const bool pair = !b->ed_key_index && !fuse && cnt <= pair_max;  // latency mode
-        // (quad_ok: one piece, scratch sized for 2 cnt slots above)
-        const uint32_t lanes = !pair ? 1u : quad_ok && split == 1 && 2 * (uint64_t)cnt <= ctx->ed_scap ? 4u : 2u;
-        if (pair) d.spread_lds = ed_spread_lds(ctx, ((uint64_t)lanes * cnt + 255) / 256 + (cnt + 255) / 256);
+        // (quad_ok: one piece with 2 cnt scratch slots in its region)
+        const uint32_t lanes = !pair ? 1u : quad_ok && split == 1 ? 4u : 2u;
+        if (pair) ed_spread_lds(ctx, d, ((uint64_t)lanes * cnt + 255) / 256, (cnt + 255) / 256);
         auto launch_points = [&](hipStream_t ps) -> cg_status {
           Timed t(ctx, lanes == 4 ? "ed25519_points_quad" : pair ? "ed25519_points_pair" : "ed25519_points", cnt, ps);
           CG_TRY(ctx, pair ? cg::launch_ed25519_points_lanes(d, cnt, lanes, ps) : cg::launch_ed25519_points(d, cnt, ps),
@@ -1403,6 +1417,39 @@ bool host_is_pinned(const void* p) {
     return false;
   }
   return a.type == hipMemoryTypeHost;
+}
+
+// The end of a host-buffer verify: verdicts (and the accept bitmap) to the caller's
+// buffers, then the stream sync.  Pageable buffers take the copies through a
+// page-locked bounce buffer (DMA, then a host memcpy after the sync): a pageable
+// device-to-host copy is staged by the runtime, ~0.17 ms for 262,144 verdicts (r04l
+// spans) against ~0.01 ms of DMA.
+cg_status download_verdicts(cg_ctx* ctx, uint8_t* verdict_out, const uint8_t* verdict, size_t n,
+                            uint32_t* bitmap_out, const uint32_t* bitmap, size_t nwords) {
+  const size_t vb = verdict_out ? (n + 255) & ~(size_t)255 : 0, bb = bitmap_out ? nwords * 4 : 0;
+  bool bounce = (verdict_out && !host_is_pinned(verdict_out)) || (bitmap_out && !host_is_pinned(bitmap_out));
+  if (bounce && ctx->dl_pin_cap < vb + bb) {
+    if (ctx->dl_pin) (void)hipHostFree(ctx->dl_pin);  // idle: every earlier call ended with a sync
+    ctx->dl_pin = nullptr;
+    ctx->dl_pin_cap = 0;
+    if (hipHostMalloc((void**)&ctx->dl_pin, vb + bb, hipHostMallocDefault) == hipSuccess) ctx->dl_pin_cap = vb + bb;
+    else (void)hipGetLastError();
+  }
+  bounce = bounce && ctx->dl_pin_cap >= vb + bb;
+  uint8_t* vdst = bounce ? ctx->dl_pin : verdict_out;
+  uint32_t* bdst = bounce ? reinterpret_cast<uint32_t*>(ctx->dl_pin + vb) : bitmap_out;
+  {
+    Timed t(ctx, "d2h_verdict", (verdict_out ? n : 0) + bb);
+    if (verdict_out) CG_TRY(ctx, hipMemcpyAsync(vdst, verdict, n, hipMemcpyDeviceToHost, ctx->stream), "download verdict");
+    if (bitmap_out) CG_TRY(ctx, hipMemcpyAsync(bdst, bitmap, bb, hipMemcpyDeviceToHost, ctx->stream), "download bitmap");
+  }
+  end_call_span(ctx);
+  CG_TRY(ctx, hipStreamSynchronize(ctx->stream), "verify sync");
+  if (bounce) {
+    if (verdict_out) std::memcpy(verdict_out, vdst, n);
+    if (bitmap_out) std::memcpy(bitmap_out, bdst, bb);
+  }
+  return CG_OK;
 }
 
 cg_status verify_pipeline(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme_id, const uint8_t* pk,
@@ -1622,7 +1669,8 @@ cg_status verify_pipeline(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
     // builds them waits for the other lane's chunk, which may still read them
     if (dual && b->ed_key_index)
       CG_TRY(ctx, hipStreamWaitEvent(ctx->stream, done[L ^ 1], 0), "verify pipeline wait");
-    st = launch_verify(ctx, b, mode, /*join_streams=*/false, dual ? (uint32_t)(L * max_cnt[0]) : 0, pts);
+    st = launch_verify(ctx, b, mode, /*join_streams=*/false, dual ? (uint32_t)(L * max_cnt[0]) : 0, pts,
+                       dual ? max_cnt[0] : 0);
     if (st != CG_OK) return st;
     CG_TRY(ctx, hipEventRecord(done[L], ctx->stream), "verify pipeline record");
     if ((st = upload_through(k + 1 + ahead)) != CG_OK) return st;
@@ -1665,16 +1713,8 @@ cg_status cg_batch_verify(cg_ctx* ctx, cg_batch* b, int mode, uint8_t* verdict_o
   if (device_bitmap_out)
     CG_TRY(ctx, hipMemcpyAsync(device_bitmap_out, b->bitmap, nwords * 4, hipMemcpyDeviceToDevice, ctx->stream),
            "copy device bitmap");
-  {
-    Timed t(ctx, "d2h_verdict", (verdict_out ? n : 0) + (accept_bitmap_out ? nwords * 4 : 0));
-    if (verdict_out)
-      CG_TRY(ctx, hipMemcpyAsync(verdict_out, b->verdict, n, hipMemcpyDeviceToHost, ctx->stream), "download verdict");
-    if (accept_bitmap_out)
-      CG_TRY(ctx, hipMemcpyAsync(accept_bitmap_out, b->bitmap, nwords * 4, hipMemcpyDeviceToHost, ctx->stream),
-             "download bitmap");
-  }
-  end_call_span(ctx);
-  CG_TRY(ctx, hipStreamSynchronize(ctx->stream), "verify sync");
+  st = download_verdicts(ctx, verdict_out, b->verdict, n, accept_bitmap_out, b->bitmap, nwords);
+  if (st != CG_OK) return st;
   collect_timings(ctx);
   return CG_OK;
   CG_API_END(ctx)
@@ -1739,16 +1779,7 @@ cg_status cg_verify_batch(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
   } guard{r, ctx};
   st = verify_pipeline(ctx, n, mode, scheme_id, pk, pk_stride, sig, sig_stride, sig_len, msg, msg_bytes, msg_off,
                        msg_len, cb, r);
-  hipError_t e = hipSuccess;
-  {
-    Timed t(ctx, "d2h_verdict", n + (accept_bitmap_out ? (n + 31) / 32 * 4 : 0));
-    if (st == CG_OK) e = hipMemcpyAsync(verdict_out, r.verdict, n, hipMemcpyDeviceToHost, ctx->stream);
-    if (st == CG_OK && e == hipSuccess && accept_bitmap_out)
-      e = hipMemcpyAsync(accept_bitmap_out, r.bitmap, (n + 31) / 32 * 4, hipMemcpyDeviceToHost, ctx->stream);
-  }
-  end_call_span(ctx);
-  if (st == CG_OK && e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
-  if (st == CG_OK && e != hipSuccess) st = hip_fail(ctx, e, "download verdicts");
+  if (st == CG_OK) st = download_verdicts(ctx, verdict_out, r.verdict, n, accept_bitmap_out, r.bitmap, (n + 31) / 32);
   r.release(ctx);
   collect_timings(ctx);
   return st;

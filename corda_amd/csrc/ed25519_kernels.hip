@@ -659,7 +659,7 @@ hipError_t launch_ed25519_hash(const Ed25519Dev& d, uint32_t n, uint32_t mode, h
     hipLaunchKernelGGL(cg_ed25519_hash<true>, dim3((n + 255) / 256), dim3(256), 0, s, d.pk, d.sig, d.sig_len, d.arena,
                        d.msg_off, d.msg_len, n, d.cap, d.scap, mode, d.status, d.digits, d.full_mod, d.index_base);
   else
-    hipLaunchKernelGGL(cg_ed25519_hash<false>, dim3((n + 255) / 256), dim3(256), d.spread_lds, s, d.pk, d.sig, d.sig_len,
+    hipLaunchKernelGGL(cg_ed25519_hash<false>, dim3((n + 255) / 256), dim3(256), d.spread_lds_hash, s, d.pk, d.sig, d.sig_len,
                        d.arena, d.msg_off, d.msg_len, n, d.cap, d.scap, mode, d.status, d.digits, d.full_mod,
                        d.index_base);
   return hipGetLastError();
