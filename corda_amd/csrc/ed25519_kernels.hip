@@ -282,7 +282,9 @@ CG_DEV int4* key_table(int32_t* ktab, uint32_t j) {
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_POINTS_WAVES, 8))) void cg_ed25519_keyprep(
     const uint32_t* __restrict__ pk, uint32_t cap, const uint32_t* __restrict__ key_first, uint32_t n_keys,
     int32_t* __restrict__ ktab, uint32_t* __restrict__ kstat) {
-  CG_WAVE_PRIO(1);
+  // the longest chain of the key-reuse path (decode + 192 doublings per key, few
+  // blocks) and the points / MSM kernels wait for it: above the hash kernel beside it
+  CG_WAVE_PRIO(3);
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n_keys) return;
   const uint32_t e = key_first[j];
