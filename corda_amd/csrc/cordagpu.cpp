@@ -1342,11 +1342,9 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = 
 // (each chunk's three kernels are a serial ~1 ms chain per lane, whatever its size).
 struct VerifyRun {
   uint8_t* arena = nullptr;
-  uint64_t* off = nullptr;
-  uint32_t* len = nullptr;
-  uint8_t* pk = nullptr;
-  uint8_t* sig = nullptr;
-  uint32_t* sl = nullptr;
+  // every chunk's per-element arrays as one chunk-major block (ChunkRows): a staged
+  // chunk's rows go up in one DMA
+  uint8_t* rows = nullptr;
   uint8_t* verdict = nullptr;
   uint32_t* bitmap = nullptr;
   std::vector<hipEvent_t> ev;
@@ -1359,12 +1357,9 @@ struct VerifyRun {
     for (hipEvent_t e : ev)
       if (e) (void)hipEventDestroy(e);
     ev.clear();
-    for (const void* p : {(const void*)arena, (const void*)off, (const void*)len, (const void*)pk, (const void*)sig,
-                          (const void*)sl, (const void*)verdict, (const void*)bitmap})
-      dfree(ctx, p);
-    arena = pk = sig = verdict = nullptr;
-    off = nullptr;
-    len = sl = bitmap = nullptr;
+    for (const void* p : {(const void*)arena, (const void*)rows, (const void*)verdict, (const void*)bitmap}) dfree(ctx, p);
+    arena = rows = verdict = nullptr;
+    bitmap = nullptr;
   }
 };
 
@@ -1452,17 +1447,33 @@ cg_status download_verdicts(cg_ctx* ctx, uint8_t* verdict_out, const uint8_t* ve
   return CG_OK;
 }
 
+// A chunk's per-element arrays inside VerifyRun::rows (and inside its ring slot, after
+// the arena piece, in the same layout): msg_off, msg_len, key rows, signature rows,
+// signature lengths, each 256-byte aligned.
+struct ChunkRows {
+  size_t off, len, pk, sig, sl, bytes;  // byte offsets from the chunk's base; total size
+  ChunkRows(size_t cnt, size_t pk_stride, size_t sig_stride, bool has_sl) {
+    auto a = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    off = 0;
+    len = off + a(cnt * 8);
+    pk = len + a(cnt * 4);
+    sig = pk + a(cnt * pk_stride);
+    sl = sig + a(cnt * sig_stride);
+    bytes = sl + (has_sl ? a(cnt * 4) : 0);
+  }
+};
+
 cg_status verify_pipeline(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme_id, const uint8_t* pk,
                           size_t pk_stride, const uint8_t* sig, size_t sig_stride, const uint32_t* sig_len,
                           const uint8_t* msg, size_t msg_bytes, const uint64_t* msg_off, const uint32_t* msg_len,
                           const std::vector<size_t>& cb, VerifyRun& r) {
   const size_t K = cb.size() - 1;
   cg_status st;
+  std::vector<size_t> rows_at(K + 1, 0);  // chunk k's rows at r.rows + rows_at[k]
+  for (size_t k = 0; k < K; ++k)
+    rows_at[k + 1] = rows_at[k] + ChunkRows(cb[k + 1] - cb[k], pk_stride, sig_stride, sig_len).bytes;
   if ((st = dalloc(ctx, &r.arena, msg_bytes + 16, "alloc arena")) != CG_OK ||
-      (st = dalloc(ctx, &r.off, n, "alloc msg_off")) != CG_OK || (st = dalloc(ctx, &r.len, n, "alloc msg_len")) != CG_OK ||
-      (st = dalloc(ctx, &r.pk, n * pk_stride, "alloc pk rows")) != CG_OK ||
-      (st = dalloc(ctx, &r.sig, n * sig_stride, "alloc sig rows")) != CG_OK ||
-      (sig_len && (st = dalloc(ctx, &r.sl, n, "alloc sig_len rows")) != CG_OK) ||
+      (st = dalloc(ctx, &r.rows, rows_at[K], "alloc rows")) != CG_OK ||
       (st = dalloc(ctx, &r.verdict, n, "alloc verdict")) != CG_OK ||
       (st = dalloc(ctx, &r.bitmap, (n + 31) / 32, "alloc bitmap")) != CG_OK)
     return st;
@@ -1492,7 +1503,7 @@ cg_status verify_pipeline(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
   const size_t row_bytes = 12 + pk_stride + sig_stride + (sig_len ? 4 : 0);
   size_t slot = 0;
   for (size_t k = 0; k < K; ++k)
-    slot = std::max(slot, (size_t)(aend[k + 1] - aend[k]) + (cb[k + 1] - cb[k]) * row_bytes + 6 * 256);
+    slot = std::max(slot, (size_t)((aend[k + 1] - aend[k] + 255) & ~(uint64_t)255) + (rows_at[k + 1] - rows_at[k]));
   if (ring) {
     // The slots stay page-locked until cg_close, so their size is capped
     // (CORDA_AMD_RING_MAX_MB, default 256 MB per slot): a call whose chunk would need
@@ -1527,6 +1538,8 @@ cg_status verify_pipeline(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
       ctx->pool = new CopyPool(workers);
     }
   }
+  const char* od = std::getenv("CORDA_AMD_VERIFY_ONE_DMA");
+  const bool one_dma = !od || std::atoi(od) != 0;
   auto enqueue_upload = [&](size_t k) -> cg_status {
     const size_t lo = cb[k], hi = cb[k + 1];
     // the chunk's inputs are checked just before they go out (the host scan then
@@ -1540,25 +1553,31 @@ cg_status verify_pipeline(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
                                  sig + lo * sig_stride, sig_stride, sig_len ? sig_len + lo : nullptr, mc);
     if (cst != CG_OK) return cst;
     // (device destination, host source, bytes) of the chunk: its arena piece and rows
+    const ChunkRows cr(hi - lo, pk_stride, sig_stride, sig_len);
+    uint8_t* const rb = r.rows + rows_at[k];
     std::vector<CopyPool::Piece> pieces = {
         {r.arena + aend[k], msg + aend[k], (size_t)(aend[k + 1] - aend[k])},
-        {r.off + lo, msg_off + lo, (hi - lo) * 8},
-        {r.len + lo, msg_len + lo, (hi - lo) * 4},
-        {r.pk + lo * pk_stride, pk + lo * pk_stride, (hi - lo) * pk_stride},
-        {r.sig + lo * sig_stride, sig + lo * sig_stride, (hi - lo) * sig_stride}};
-    if (sig_len) pieces.push_back({r.sl + lo, sig_len + lo, (hi - lo) * 4});
+        {rb + cr.off, msg_off + lo, (hi - lo) * 8},
+        {rb + cr.len, msg_len + lo, (hi - lo) * 4},
+        {rb + cr.pk, pk + lo * pk_stride, (hi - lo) * pk_stride},
+        {rb + cr.sig, sig + lo * sig_stride, (hi - lo) * sig_stride}};
+    if (sig_len) pieces.push_back({rb + cr.sl, sig_len + lo, (hi - lo) * 4});
     hipStream_t cs = ctx->copy_stream;
     if (ring) {  // stage into slot k % 2 (free once chunk k-2's copies are done)
       uint8_t* slot = ctx->ring[k & 1];
       if (k >= 2) CG_TRY(ctx, hipEventSynchronize(r.ev[k - 2]), "verify ring wait");
-      std::vector<CopyPool::Piece> staged;
-      size_t o = 0;
-      for (CopyPool::Piece& p : pieces) {
-        staged.push_back({slot + o, p.src, p.bytes});
-        p.src = slot + o;  // the DMA now reads the slot
-        o += (p.bytes + 255) & ~(size_t)255;
-      }
+      // the slot: the arena piece, then the rows in their device layout, so the rows
+      // go up in one DMA (each extra DMA costs ~9 us of engine time, r04 ubench)
+      const size_t abytes = (size_t)(aend[k + 1] - aend[k]), rows0 = (abytes + 255) & ~(size_t)255;
+      std::vector<CopyPool::Piece> staged = {{slot, msg + aend[k], abytes}};
+      for (size_t i = 1; i < pieces.size(); ++i)
+        staged.push_back({slot + rows0 + (size_t)(static_cast<uint8_t*>(pieces[i].dst) - rb), pieces[i].src, pieces[i].bytes});
       ctx->pool->run(staged);
+      if (one_dma) {
+        pieces = {{r.arena + aend[k], slot, abytes}, {rb, slot + rows0, cr.bytes}};
+      } else {  // (A/B: one DMA per array, as before)
+        for (size_t i = 0; i < pieces.size(); ++i) pieces[i].src = staged[i].dst;
+      }
     }
     {
       Timed t(ctx, "h2d_verify", (aend[k + 1] - aend[k]) + (hi - lo) * row_bytes, cs);
@@ -1652,11 +1671,13 @@ cg_status verify_pipeline(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
     MsgSrc m;
     m.dev = r.arena;
     m.bytes = msg_bytes;
-    m.off_dev = r.off + lo;
-    m.len_dev = r.len + lo;
-    m.pk_dev = r.pk + lo * pk_stride;
-    m.sig_dev = r.sig + lo * sig_stride;
-    m.sl_dev = sig_len ? r.sl + lo : nullptr;
+    const ChunkRows cr(hi - lo, pk_stride, sig_stride, sig_len);
+    uint8_t* const rb = r.rows + rows_at[k];
+    m.off_dev = reinterpret_cast<uint64_t*>(rb + cr.off);
+    m.len_dev = reinterpret_cast<uint32_t*>(rb + cr.len);
+    m.pk_dev = rb + cr.pk;
+    m.sig_dev = rb + cr.sig;
+    m.sl_dev = sig_len ? reinterpret_cast<const uint32_t*>(rb + cr.sl) : nullptr;
     m.raw_ready = r.ev[k];
     m.verdict_dev = r.verdict + lo;
     m.async = true;
