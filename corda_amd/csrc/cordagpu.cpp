@@ -155,6 +155,7 @@ struct cg_ctx {
   hipEvent_t ev_keys = nullptr;  // key-reuse path: per-key tables ready (keyprep runs on ec_stream[0])
   hipEvent_t ev_split = nullptr;  // prepared-batch verify: the Ed25519 pieces on hash_stream are done
   hipEvent_t ev_pts_in = nullptr, ev_pts_done = nullptr;  // Ed25519 points kernel beside the hash kernel
+  hipEvent_t ev_arena = nullptr;  // one-chunk verify: the deferred arena copy (on hash_stream) is done
   std::string err;
   int32_t* btab = nullptr;
   // Ed25519 chunk scratch
@@ -645,7 +646,8 @@ cg_status cg_open(int device, cg_ctx** out) {
       hipEventCreateWithFlags(&ctx->ev_keys, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_split, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_pts_in, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&ctx->ev_pts_done, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&ctx->ev_pts_done, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->ev_arena, hipEventDisableTiming) != hipSuccess) {
     cg_close(ctx);
     return CG_E_DEVICE;
   }
@@ -691,7 +693,7 @@ void cg_close(cg_ctx* ctx) {
     if (ctx->ec_stream[1] && ctx->ec_stream[1] != ctx->ec_stream[0]) (void)hipStreamDestroy(ctx->ec_stream[1]);
     if (ctx->ec_stream[0]) (void)hipStreamDestroy(ctx->ec_stream[0]);
     for (hipEvent_t e : {ctx->ev_fork, ctx->ev_join[0], ctx->ev_join[1], ctx->ev_keys, ctx->ev_split, ctx->ev_pts_in,
-                         ctx->ev_pts_done})
+                         ctx->ev_pts_done, ctx->ev_arena})
       if (e) (void)hipEventDestroy(e);
     if (ctx->pin) (void)hipHostFree(ctx->pin);
     for (uint8_t* r : ctx->ring)
@@ -1249,16 +1251,33 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = 
                  "launch ed25519_points");
           return CG_OK;
         };
-        auto upload_pending_arena = [&]() -> cg_status {  // create_batch's deferred arena (one-chunk verify)
+        // create_batch's deferred arena (one-chunk verify).  Beside the points kernel (the
+        // pts path) an arena of 6 MB or more goes on hash_stream, so its copy starts as soon
+        // as it is issued instead of behind the staging kernel on ctx->stream, and the hash
+        // kernel waits for it (r04ad: 8,192-65,536 x 1 KB -0.02..0.05 ms; at 4,096 the
+        // cross-stream wait cost more than the copy's head start, +0.01 ms).
+        // CORDA_AMD_ARENA_BESIDE=0 keeps it on ctx->stream.
+        auto upload_pending_arena = [&](bool beside) -> cg_status {
           if (!b->arena_pending) return CG_OK;
-          Timed t(ctx, "h2d_arena", b->arena_pending_bytes);
-          CG_TRY(ctx, hipMemcpyAsync(b->arena, b->arena_pending, b->arena_pending_bytes, hipMemcpyHostToDevice,
-                                     ctx->stream), "upload arena");
+          const char* ab = std::getenv("CORDA_AMD_ARENA_BESIDE");
+          hipStream_t as = beside && split == 1 && b->arena_pending_bytes >= ((size_t)6 << 20) &&
+                                   !(ab && std::atoi(ab) == 0)
+                               ? ctx->hash_stream
+                               : ctx->stream;
+          {
+            Timed t(ctx, "h2d_arena", b->arena_pending_bytes, as);
+            CG_TRY(ctx, hipMemcpyAsync(b->arena, b->arena_pending, b->arena_pending_bytes, hipMemcpyHostToDevice, as),
+                   "upload arena");
+          }
           b->arena_pending = nullptr;
+          if (as != ctx->stream) {
+            CG_TRY(ctx, hipEventRecord(ctx->ev_arena, as), "arena done");
+            CG_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_arena, 0), "wait arena");
+          }
           return CG_OK;
         };
         if (fuse && !b->ed_key_index) {  // points + MSM as one kernel after the hash kernel
-          cg_status s3 = upload_pending_arena();
+          cg_status s3 = upload_pending_arena(false);
           if (s3 != CG_OK) return s3;
           {
             Timed t(ctx, "ed25519_hash", cnt);
@@ -1280,14 +1299,14 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = 
           if (keys_pending && piece == 0) CG_TRY(ctx, hipStreamWaitEvent(pts, ctx->ev_keys, 0), "wait keyprep");
           if ((s2 = launch_points(pts)) != CG_OK) return s2;
           CG_TRY(ctx, hipEventRecord(ctx->ev_pts_done, pts), "points done");
-          if ((s2 = upload_pending_arena()) != CG_OK) return s2;
+          if ((s2 = upload_pending_arena(true)) != CG_OK) return s2;
           {
             Timed t(ctx, "ed25519_hash", cnt);
             CG_TRY(ctx, cg::launch_ed25519_hash(d, cnt, (uint32_t)mode, ctx->stream), "launch ed25519_hash");
           }
           CG_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_pts_done, 0), "join points");
         } else {
-          if ((s2 = upload_pending_arena()) != CG_OK) return s2;
+          if ((s2 = upload_pending_arena(false)) != CG_OK) return s2;
           {
             Timed t(ctx, "ed25519_hash", cnt);
             CG_TRY(ctx, cg::launch_ed25519_hash(d, cnt, (uint32_t)mode, ctx->stream), "launch ed25519_hash");
