@@ -212,13 +212,21 @@ CG_HD void ed25519_build_table(const ge_p3& P, Put&& put) {
 }
 
 // P <- 2^64 P (64 doublings): the key-reuse path's per-key tables and the four-lane
-// latency mode's high-half points.
+// latency mode's high-half points.  The 63 intermediate results stay projective
+// (ge_p1p1_to_p2, 3 products) as in the MSM's doubling runs; only the last one is taken
+// to p3 (4 products).
 CG_HD void ge_p3_dbl64(ge_p3& P) {
   ge_p1p1 x;
-  CG_NOUNROLL for (int i = 0; i < 64; ++i) {
-    ge_p3_dbl(x, P);
-    ge_p1p1_to_p3(P, x);
+  ge_p2 q;
+  q.X = P.X;
+  q.Y = P.Y;
+  q.Z = P.Z;
+  CG_NOUNROLL for (int i = 0; i < 63; ++i) {
+    ge_p2_dbl<false>(x, q);
+    ge_p1p1_to_p2(q, x);
   }
+  ge_p2_dbl<true>(x, q);
+  ge_p1p1_to_p3(P, x);
 }
 
 // Per distinct key of the key-reuse path: decode A once (i2p, A.2) and build the

@@ -316,14 +316,22 @@ def lane_table(C, P3):
     return tab
 
 
+def dbl64(C, P3):
+    """ge_p3_dbl64 (the key-reuse path's per-key tables, the four-lane latency mode's
+    high-half points): 63 x (p2_dbl<false> + to_p2) from the point's (X, Y, Z), then
+    p2_dbl<true> + to_p3"""
+    q = P3[:3]
+    for _ in range(3):  # ranges settle after one round; iterate for the fixed point
+        q = p3_union(q, to_p2(C, dbl(C, q, False)))
+    return p3_union(P3, to_p3(C, dbl(C, q, True)))
+
+
 def key_tables(C, P3):
-    """ed25519_key_tables: -A, then 64 x (p3_dbl + to_p3) between the four tables"""
+    """ed25519_key_tables: -A, then ge_p3_dbl64 between the four tables"""
     P = negate_p3(P3)
     tab = lane_table(C, P)
     for _ in range(3):
-        for _ in range(3):  # ranges settle after one round; iterate for the fixed point
-            x = dbl(C, P[:3], True)
-            P = p3_union(P, to_p3(C, x))
+        P = p3_union(P, dbl64(C, P))
         tab = p3_union(tab, lane_table(C, P))
     return tab
 
@@ -395,14 +403,6 @@ def pair_combine(C, st):
     s = add_cached(C, own, p3_to_cached(C, own))
     for fe in (s[0], fe_sub(s[1], s[3])):
         assert all(abs(a) < 1 << 29 and abs(b) < 1 << 29 for a, b in fe)
-
-
-def dbl64(C, P3):
-    """ge_p3_dbl64 (the four-lane latency mode's high-half points): 64 x (p3_dbl + to_p3)"""
-    P = P3
-    for _ in range(3):  # ranges settle after one round; iterate for the fixed point
-        P = p3_union(P, to_p3(C, dbl(C, P[:3], True)))
-    return P
 
 
 def quad_combine(C, st):
