@@ -289,19 +289,26 @@ def test_key_reuse_prepared_batch_bitmap(gpu_ctx, oracle, key_reuse):
     pb.close()
 
 
-@pytest.mark.parametrize("chunks,min_chunk,tail", [("9", "700", "0.3"), ("3", "1", "1.0")])
-def test_host_verify_pipeline_small_chunks_vs_oracle(gpu_ctx, oracle, monkeypatch, chunks, min_chunk, tail):
+@pytest.mark.parametrize("chunks,min_chunk,tail,variant", [("9", "700", "0.3", "default"), ("3", "1", "1.0", "default"),
+                                                          ("9", "700", "0.3", "one_dma_off"),
+                                                          ("4", "700", "0.4", "pinned_in")])
+def test_host_verify_pipeline_small_chunks_vs_oracle(gpu_ctx, oracle, monkeypatch, chunks, min_chunk, tail, variant):
     """cg_verify_batch's pipeline (chunk k's upload on the copy stream beside chunk k-1's
     kernels) forced onto small, ragged chunks: a mixed batch — Ed25519 from distinct and
     from 12 repeated signers (the key-reuse path inside a chunk), secp256k1, P-256, an
     unsupported scheme id and wrong-length keys — whose arena is packed in REVERSE element
     order (the first chunk's messages sit at the end, so its prefix is the whole arena),
-    in both modes, verdicts and accept bitmap against the oracle."""
+    in both modes, verdicts and accept bitmap against the oracle.  Variants: each staged
+    chunk's rows as one DMA (default) or one per array (CORDA_AMD_VERIFY_ONE_DMA=0), and
+    page-locked inputs (cg_register_host: no staging ring, direct DMAs; the pageable
+    verdict buffers then come back through the bounce buffer)."""
     from corda_amd import dist as D
     from corda_amd._lib import KEY_INVALID, UNSUPPORTED
     monkeypatch.setenv("CORDA_AMD_VERIFY_CHUNKS", chunks)
     monkeypatch.setenv("CORDA_AMD_VERIFY_MIN_CHUNK", min_chunk)
     monkeypatch.setenv("CORDA_AMD_VERIFY_TAIL", tail)
+    if variant == "one_dma_off":
+        monkeypatch.setenv("CORDA_AMD_VERIFY_ONE_DMA", "0")
     sch = np.random.default_rng(12).choice(np.array([2, 3, 4, 4, 4], np.uint8), size=5200)
     w = datagen.make_batch(len(sch), msg_bytes=70, scheme=sch, seed=23, key_base=620_000)
     w = datagen.add_ecdsa_adversarial(w, frac=0.2, seed=4)
@@ -337,15 +344,52 @@ def test_host_verify_pipeline_small_chunks_vs_oracle(gpu_ctx, oracle, monkeypatc
                             b.msg_len)
     oracle_w = datagen.Workload(n, b.scheme & 0x7F, b.pk, b.pk_stride, b.sig, b.sig_stride, b.sig_len, arena,
                                 new_off, b.msg_len)
-    for mode in (MODE_IS_VALID, MODE_DO_VERIFY):
-        exp = oracle_verdicts(oracle, oracle_w, mode)
-        exp[bad_key] = KEY_INVALID
-        exp[unsup] = UNSUPPORTED
-        got, bm = crypto.verify_packed(gpu_ctx, b2, mode, bitmap=True)
-        bad = np.flatnonzero(got != exp)
-        assert bad.size == 0, [(int(i), int(schemes[i]), int(got[i]), int(exp[i])) for i in bad[:10]]
-        assert np.array_equal(bm.view(np.int32), D.pack_bits(exp == ACCEPT).view(np.int32))
+    pinned = (b2.scheme, b2.pk, b2.sig, b2.sig_len, arena, new_off, b2.msg_len) if variant == "pinned_in" else ()
+    gpu_ctx.register_host(*pinned)
+    try:
+        for mode in (MODE_IS_VALID, MODE_DO_VERIFY):
+            exp = oracle_verdicts(oracle, oracle_w, mode)
+            exp[bad_key] = KEY_INVALID
+            exp[unsup] = UNSUPPORTED
+            got, bm = crypto.verify_packed(gpu_ctx, b2, mode, bitmap=True)
+            bad = np.flatnonzero(got != exp)
+            assert bad.size == 0, [(int(i), int(schemes[i]), int(got[i]), int(exp[i])) for i in bad[:10]]
+            assert np.array_equal(bm.view(np.int32), D.pack_bits(exp == ACCEPT).view(np.int32))
+    finally:
+        gpu_ctx.unregister_host(*pinned)
     assert (exp == ACCEPT).sum() > 0.6 * n
+
+
+@pytest.mark.parametrize("beside", [None, "0"])
+def test_one_chunk_large_arena_and_pinned_outputs_vs_oracle(gpu_ctx, oracle, monkeypatch, beside):
+    """The one-chunk host verify with an arena large enough (8,192 x 1 KB) that its deferred
+    copy runs on its own stream beside the staging and points kernels (and with that
+    turned off, CORDA_AMD_ARENA_BESIDE=0), 25 % mutated, in both modes; then the same call
+    with page-locked verdict and bitmap buffers (the download's direct path instead of
+    the bounce buffer) — verdicts and bitmap against the oracle."""
+    from corda_amd import dist as D
+    if beside is not None:
+        monkeypatch.setenv("CORDA_AMD_ARENA_BESIDE", beside)
+    w = datagen.add_ed25519_adversarial(datagen.make_batch(8192, msg_bytes=1024, seed=83, key_base=970_000),
+                                        frac=0.25, seed=13)
+    assert len(w.msg) >= 6 << 20
+    for mode in (MODE_IS_VALID, MODE_DO_VERIFY):
+        exp = oracle_verdicts(oracle, w, mode)
+        got = gpu_verdicts(gpu_ctx, w, mode)
+        bad = np.flatnonzero(got != exp)
+        assert bad.size == 0, [(w.classes[i], int(got[i]), int(exp[i])) for i in bad[:10]]
+    verdict = np.empty(w.n, np.uint8)
+    bm = np.zeros((w.n + 31) // 32, np.uint32)
+    gpu_ctx.register_host(verdict, bm)
+    try:
+        gpu_ctx.check(gpu_ctx.lib.cg_verify_batch(gpu_ctx.h, w.n, MODE_IS_VALID, ptr(w.scheme), ptr(w.pk), w.pk_stride,
+                                                  ptr(w.sig), w.sig_stride, ptr(w.sig_len), ptr(w.msg), len(w.msg),
+                                                  ptr(w.msg_off), ptr(w.msg_len), ptr(verdict), ptr(bm)))
+    finally:
+        gpu_ctx.unregister_host(verdict, bm)
+    exp = oracle_verdicts(oracle, w, MODE_IS_VALID)
+    assert np.array_equal(verdict, exp)
+    assert np.array_equal(bm.view(np.int32), D.pack_bits(exp == ACCEPT).view(np.int32))
 
 
 @pytest.mark.parametrize("chunks", [None, "5"])
