@@ -211,23 +211,24 @@ CG_HD void ed25519_build_table(const ge_p3& P, Put&& put) {
   }
 }
 
-// P <- 2^64 P (64 doublings): the key-reuse path's per-key tables and the four-lane
-// latency mode's high-half points.  The 63 intermediate results stay projective
+// P <- 2^64 P (64 doublings): the key-reuse path's per-key tables and the latency
+// mode's higher-part points (2^(4 u D) P, ge_p3_dbl_n).  The 63 intermediate results stay projective
 // (ge_p1p1_to_p2, 3 products) as in the MSM's doubling runs; only the last one is taken
 // to p3 (4 products).
-CG_HD void ge_p3_dbl64(ge_p3& P) {
+CG_HD void ge_p3_dbl_n(ge_p3& P, uint32_t n) {  // P <- 2^n P, n >= 1 (may differ across lanes)
   ge_p1p1 x;
   ge_p2 q;
   q.X = P.X;
   q.Y = P.Y;
   q.Z = P.Z;
-  CG_NOUNROLL for (int i = 0; i < 63; ++i) {
+  CG_NOUNROLL for (uint32_t i = 1; i < n; ++i) {
     ge_p2_dbl<false>(x, q);
     ge_p1p1_to_p2(q, x);
   }
   ge_p2_dbl<true>(x, q);
   ge_p1p1_to_p3(P, x);
 }
+CG_HD void ge_p3_dbl64(ge_p3& P) { ge_p3_dbl_n(P, 64); }
 
 // Per distinct key of the key-reuse path: decode A once (i2p, A.2) and build the
 // tables k * 2^(64 t) (-A), t = 0..3, k = 0..8; put(t, k, cached).  Returns 0 when
@@ -245,10 +246,12 @@ CG_HD uint32_t ed25519_key_tables(const uint32_t pk[8], Put&& put) {
   return 1;
 }
 
-// Entry k (0 <= k <= 2^(kBWin-1)) of shared table t in affine precomputed form:
-// k * 2^(64 t) B, t = 0..3 (the balanced split uses t = 0 and 2; the key-reuse
-// split all four).  One call per lane of the table-building kernel at context
-// creation (and on the host for the tests).
+// Entry k (0 <= k <= 2^(kBWin-1)) of shared table s in affine precomputed form:
+// k * 2^(32 s) B, s = 0..7 (kBTables): the balanced split uses s = 0 and 4, the
+// key-reuse split and the four-lane latency mode s = 0, 2, 4, 6, the eight-lane mode
+// all eight.  One call per lane of the table-building kernel at context creation (and
+// on the host for the tests).
+constexpr int kBTables = 8;
 CG_HD void ed25519_btab_entry(ge_precomp& out, uint32_t t, uint32_t k) {
   const uint32_t benc[8] = {0x66666658u, 0x66666666u, 0x66666666u, 0x66666666u,
                             0x66666666u, 0x66666666u, 0x66666666u, 0x66666666u};
@@ -256,7 +259,7 @@ CG_HD void ed25519_btab_entry(ge_precomp& out, uint32_t t, uint32_t k) {
   ge_p3 P, R;
   ge_p1p1 x;
   ge_frombytes_i2p(P, benc);
-  CG_NOUNROLL for (uint32_t i = 0; i < 64 * t; ++i) {
+  CG_NOUNROLL for (uint32_t i = 0; i < 32 * t; ++i) {
     ge_p3_dbl(x, P);
     ge_p1p1_to_p3(P, x);
   }
@@ -308,8 +311,8 @@ CG_HD void shl_nibbles(uint32_t x[8], uint32_t n) {
 // before a window's doublings and unpackA after them, so a fetch issued early hides
 // its latency under the doublings while only its storage form (packed words, an
 // LDS slot, or just k for a late load) stays live; loadR / unpackR the same for k*R
-// (unpacked before the R addition).  getB(t, k, precomp&) loads k * 2^(64 t) B
-// (t = 0 or 2 here), k <= 2^(kBWin-1).
+// (unpacked before the R addition).  getB(s, k, precomp&) loads k * 2^(32 s) B
+// (s = 0 or 4 here), k <= 2^(kBWin-1).
 // Returns 1 iff P is the identity.
 template <typename RawA, typename RawR, typename GetDig, typename LoadA, typename UnpackA, typename LoadR,
           typename UnpackR, typename GetB>
@@ -374,7 +377,7 @@ CG_HD uint32_t ed25519_msm(uint32_t ndig, GetDig&& getDig, uint32_t rneg, LoadA&
       getB(0, nl ? kHalf - el : el - kHalf, pb);
       ge_p1p1_to_p3<true>(r3, t);
       ge_madd(t, r3, pb, nl);
-      getB(2, nh ? kHalf - eh : eh - kHalf, pb);
+      getB(4, nh ? kHalf - eh : eh - kHalf, pb);
       ge_p1p1_to_p3<true>(r3, t);
       ge_madd(t, r3, pb, nh);
     }
@@ -385,23 +388,26 @@ CG_HD uint32_t ed25519_msm(uint32_t ndig, GetDig&& getDig, uint32_t rneg, LoadA&
   return fe_iszero(t.X) & fe_iszero(d);
 }
 
-// Latency mode (small batches: two or four lanes per signature, so each lane's
+// Latency mode (small batches: two, four or eight lanes per signature, so each lane's
 // dependent chain is shorter).  LANES = 2: lane p computes one half of ed25519_msm's
 // sum over the same window positions: p = 0 the term [c0](-A) and the low B half
-// [b_lo]B, p = 1 the term [c1](+-R) and [b_hi](2^128 B).  LANES = 4: lane q = 2 h + u
-// takes half h of that split (h = 0: c0 and b_lo, h = 1: c1 and b_hi) and of it the
-// digits u = 0: 0..15, u = 1: 16.. over the point 2^(64 u) (its own table) — the
-// scalar's 64-bit halves, so ndig - 16 windows (~64 doublings instead of ~128) —
-// and the B windows in bits 64 u .. 64 u + 63 of the half over table 2^(64 u) B.
-// getDig / loadT / unpackT / getB as in ed25519_msm, for the lane's own table
-// (loadT(k, Raw&): k * (its point)); flip = rneg for the R lanes, 0 for the A lanes.
-// Every lane runs the same instruction stream (only its data differ), so the parts
-// of a signature may share a wave.  Leaves the lane's partial sum in t (p1p1);
+// [b_lo]B, p = 1 the term [c1](+-R) and [b_hi](2^128 B).  LANES = 4 / 8: lane
+// q = P h + u (P = LANES / 2 parts per half) takes half h of that split (h = 0: c0 and
+// b_lo, h = 1: c1 and b_hi) and of it part u of the scalar's digits — D = 32 / P digits
+// from u D (the top part: up to ndig) over the point 2^(4 u D) P (its own table), so
+// ndig - (P - 1) D windows (LANES 4: ~64 doublings, LANES 8: ~32, instead of ~128) —
+// and the B windows in bits 4 u D .. 4 (u + 1) D - 1 of the half over the shared table
+// 2^(128 h + 4 u D) B.  getDig / loadT / unpackT / getB as in ed25519_msm, for the lane's
+// own table (loadT(k, Raw&): k * (its point)); flip = rneg for the R lanes, 0 for the
+// A lanes.  Every lane runs the same instruction stream (only its data differ), so the
+// parts of a signature may share a wave.  Leaves the lane's partial sum in t (p1p1);
 // ed25519_lane_sum / ed25519_pair_combine add them.
 template <typename Raw, int LANES = 2, typename GetDig, typename LoadT, typename UnpackT, typename GetB>
 CG_HD void ed25519_msm_lane(ge_p1p1& t, uint32_t ndig, uint32_t p, GetDig&& getDig, uint32_t flip, LoadT&& loadT,
                             UnpackT&& unpackT, GetB&& getB) {
-  static_assert(LANES == 2 || LANES == 4, "two or four lanes per signature");
+  static_assert(LANES == 2 || LANES == 4 || LANES == 8, "two, four or eight lanes per signature");
+  constexpr int P = LANES / 2, D = 32 / P;  // parts per half, digits per part
+  static_assert(((4 * D) % kBWin) == 0, "a part covers whole B windows");
   ge_p2 r2;
   ge_p3 r3;
   ge_cached ca;
@@ -411,25 +417,23 @@ CG_HD void ed25519_msm_lane(ge_p1p1& t, uint32_t ndig, uint32_t p, GetDig&& getD
   fe_1(t.Y);
   fe_1(t.Z);
   fe_1(t.T);
-  const uint32_t h = LANES == 4 ? p >> 1 : p, u = LANES == 4 ? p & 1 : 0u;
-  // windows: all ndig (LANES 2), or digits 16.. of the half in the high lane (ndig >= 32
-  // always, so every lane runs ndig - 16 >= 16 windows; the low lane's digits 16.. are
-  // zero for it)
-  const int nwin = LANES == 4 ? (int)ndig - 16 : (int)ndig;
-  constexpr int kBSpan = LANES == 4 ? 64 : 128;  // bits of the B half a lane covers
-  const int dbase = 8 * (int)h + 2 * (int)u, bbase = h ? 16 : 20;
-  const uint32_t btab = 2 * h + u;
+  const uint32_t h = p / P, u = p % P;
+  // windows: the top part's (ndig >= 32 always, so every lane runs ndig - (P-1) D >= D
+  // windows; the lower parts' digits from D on are zero for them)
+  const int nwin = (int)ndig - (P - 1) * D;
+  const int dbase = 8 * (int)h + (int)u * (D / 8), bbase = h ? 16 : 20;
+  const uint32_t btab = 4 * h + u * (D / 8);
   uint32_t wd = 0;
   CG_NOUNROLL for (int j = nwin - 1; j >= 0; --j) {
     if (j == nwin - 1 || (j & 7) == 7) wd = getDig(dbase + (j >> 3));  // wave-uniform
     uint32_t e = (wd >> (4 * (uint32_t)(j & 7))) & 15u;
-    if (LANES == 4 && j >= 16) e = u ? e : 8u;  // (digit 0: the high lane's)
+    if (P > 1 && j >= D) e = u == P - 1 ? e : 8u;  // (digit 0: a higher part's)
     const uint32_t ne = e < 8;
-    const bool bwin = ((4 * j) & (kBWin - 1)) == 0 && 4 * j < kBSpan;
+    const bool bwin = ((4 * j) & (kBWin - 1)) == 0 && j < D;
     constexpr uint32_t kMask = (1u << kBWin) - 1, kHalf = 1u << (kBWin - 1);
     uint32_t eb = 0;
     if (bwin) {
-      const uint32_t pos = 4 * (uint32_t)j + 64 * u;  // bit position in the 128-bit half
+      const uint32_t pos = 4 * (uint32_t)j + 4 * D * u;  // bit position in the 128-bit half
       const uint32_t s = (uint32_t)(128 / kBWin - 1) - pos / kBWin;
       const uint32_t per = 32 / kBWin, fsh = kBWin * (s % per);
       eb = (getDig(bbase + (int)(s / per)) >> fsh) & kMask;
@@ -490,7 +494,7 @@ CG_HD uint32_t ed25519_pair_combine(const ge_p1p1& t, Xchg&& xchg) {
 // [c1](+-R) with 16-digit chunks c0_t of c0's signed radix-16 digits (t = 0..3) and
 // |c1| < 2^66: 16 (or 17 when some lane's c1 needs a 17th digit) windows — ~64
 // doublings instead of ~130 — four per-key A tables (getA(t, k, .)), the lane's R
-// table, and 16-bit B windows over the four shared tables 2^(64 t) B (getB(t, k, .)).
+// table, and 16-bit B windows over the four shared tables 2^(64 t) B (getB(2 t, k, .)).
 // c3w (wave-uniform): chunk 3 is added in the c3w lowest windows only (its digits
 // are zero above; 16 for a fallback lane's 253-bit c0).  Returns 1 iff P is the
 // identity.
@@ -570,7 +574,7 @@ CG_HD uint32_t ed25519_msm_reuse(uint32_t c3w, uint32_t win17, const uint32_t di
         bt[2] = bt[3];
         bt[3] = nx;
         const uint32_t n = e < kHalf;
-        getB(c, n ? kHalf - e : e - kHalf, pb);
+        getB(2 * c, n ? kHalf - e : e - kHalf, pb);
         ge_p1p1_to_p3<true>(r3, t);
         ge_madd(t, r3, pb, n);
       }

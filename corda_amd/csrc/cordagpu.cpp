@@ -52,6 +52,11 @@ constexpr uint32_t kEdPairMaxDefault = 40000;
 // ... and up to this size with four lanes per signature (the scalars' 64-bit halves
 // over 2^64-multiple tables: ~64 doublings per lane instead of ~128)
 constexpr uint32_t kEdQuadMaxDefault = 32768;
+// ... and up to this size with eight (32-bit parts over 2^(32 u)-multiple tables: ~32
+// doublings per lane): r04ap, 1 KB messages, 2,048-6,144 signatures -0.012..0.015 ms
+// against four lanes, 8,192 +0.07 ms — past ~7,280 signatures the eight-lane points
+// blocks and the hash blocks no longer get a CU each (ed_spread_lds)
+constexpr uint32_t kEdOctMaxDefault = 7168;
 constexpr uint32_t kEdSplitDefault = 1;  // r03d A/B: 2 or 4 pieces measured no faster (95-96 M/s either way)
 
 struct Stat {
@@ -784,6 +789,11 @@ uint32_t ed_quad_max() {
   const char* e = std::getenv("CORDA_AMD_ED_QUAD_MAX");
   return e ? (uint32_t)std::max(0, std::atoi(e)) : kEdQuadMaxDefault;
 }
+// Eight lanes per signature up to this many; CORDA_AMD_ED_OCT_MAX overrides (0: never).
+uint32_t ed_oct_max() {
+  const char* e = std::getenv("CORDA_AMD_ED_OCT_MAX");
+  return e ? (uint32_t)std::max(0, std::atoi(e)) : kEdOctMaxDefault;
+}
 
 bool key_reuse_mode(uint32_t n, uint32_t n_keys) {
   const int forced = key_reuse_forced();
@@ -1188,10 +1198,13 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = 
       // four lanes per signature: tables in 2 n_ed scratch slots — grown for it only where
       // this call owns the whole scratch; inside a pipeline only if its region has room
       const bool quad_want = !b->ed_key_index && !fuse && b->n_ed <= std::min(pair_max, ed_quad_max());
-      cg_status s2 = ensure_ed_scratch(ctx, quad_want && join_streams && scratch_off == 0 ? 2 * b->n_ed : b->n_ed);
+      const bool oct_want = quad_want && b->n_ed <= ed_oct_max();
+      cg_status s2 = ensure_ed_scratch(
+          ctx, quad_want && join_streams && scratch_off == 0 ? (oct_want ? 4 : 2) * b->n_ed : b->n_ed);
       if (s2 != CG_OK) return s2;
       const uint32_t region = scratch_lanes ? scratch_lanes : ctx->ed_scap - scratch_off;
       const bool quad_ok = quad_want && 2 * (uint64_t)b->n_ed <= region;
+      const bool oct_ok = oct_want && 4 * (uint64_t)b->n_ed <= region;
       const uint32_t span = ctx->ed_scap - scratch_off;  // scratch lanes this batch may use
       // Large batches run as `split` index pieces alternating between ctx->stream and
       // hash_stream (each piece on its own scratch lanes), so one piece's kernels fill
@@ -1242,11 +1255,15 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = 
           d.kstat = ctx->ed_kstat;
         }
         const bool pair = !b->ed_key_index && !fuse && cnt <= pair_max;  // latency mode
-        // (quad_ok: one piece with 2 cnt scratch slots in its region)
-        const uint32_t lanes = !pair ? 1u : quad_ok && split == 1 ? 4u : 2u;
+        // (quad_ok / oct_ok: one piece with 2 / 4 cnt scratch slots in its region)
+        const uint32_t lanes = !pair ? 1u : oct_ok && split == 1 ? 8u : quad_ok && split == 1 ? 4u : 2u;
         if (pair) ed_spread_lds(ctx, d, ((uint64_t)lanes * cnt + 255) / 256, (cnt + 255) / 256);
         auto launch_points = [&](hipStream_t ps) -> cg_status {
-          Timed t(ctx, lanes == 4 ? "ed25519_points_quad" : pair ? "ed25519_points_pair" : "ed25519_points", cnt, ps);
+          Timed t(ctx, lanes == 8   ? "ed25519_points_oct"
+                       : lanes == 4 ? "ed25519_points_quad"
+                       : pair       ? "ed25519_points_pair"
+                                    : "ed25519_points",
+                  cnt, ps);
           CG_TRY(ctx, pair ? cg::launch_ed25519_points_lanes(d, cnt, lanes, ps) : cg::launch_ed25519_points(d, cnt, ps),
                  "launch ed25519_points");
           return CG_OK;
@@ -1316,7 +1333,8 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = 
           if ((s2 = launch_points(ctx->stream)) != CG_OK) return s2;
         }
         {
-          Timed t(ctx, lanes == 4 ? "ed25519_msm_quad" : pair ? "ed25519_msm_pair" : "ed25519_msm", cnt);
+          Timed t(ctx, lanes == 8 ? "ed25519_msm_oct" : lanes == 4 ? "ed25519_msm_quad" : pair ? "ed25519_msm_pair" : "ed25519_msm",
+                  cnt);
           const uint32_t* oi = b->ed_index ? b->ed_index + base : nullptr;
           uint8_t* vd = b->ed_index ? b->verdict : b->verdict + base;
           CG_TRY(ctx,

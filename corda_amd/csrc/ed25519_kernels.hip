@@ -314,14 +314,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_POINTS_W
   ed25519_build_table(R, [&](int k, const ge_cached& c) { store_slot(lt, 0, k, c); });
 }
 
-// The shared B tables: entry k of table t = k * 2^(64 t) B in affine form, t = 0..3,
-// one lane per entry (4 * (2^(kBWin-1) + 1) lanes), at context creation.
-constexpr int kBTables = 4;
+// The shared B tables: entry k of table s = k * 2^(32 s) B in affine form, s = 0..7,
+// one lane per entry (8 * (2^(kBWin-1) + 1) lanes), at context creation.
 __global__ __launch_bounds__(256) void cg_ed25519_btab_build(int32_t* __restrict__ btab) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= kBTables * (uint32_t)kBTabEntries) return;
   ge_precomp e;
-  ed25519_btab_entry(e, i / kBTabEntries, i % kBTabEntries);  // table t = k * 2^(64 t) B
+  ed25519_btab_entry(e, i / kBTabEntries, i % kBTabEntries);  // table s = k * 2^(32 s) B
   int32_t* o = btab + (size_t)i * kBStride;
   CG_UNROLL for (int l = 0; l < 10; ++l) {
     o[l] = e.yplusx.v[l];
@@ -530,6 +529,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_PM_WAVES
 #ifndef CG_PAIR_WAVES
 #define CG_PAIR_WAVES 2
 #endif
+// Lane q of signature i: its half h, part u, and where its table lives (scratch slot,
+// point 0 / 1 of the slot): LANES 2 slot i, point h; LANES 4 / 8 slot P i + (P / 2) h +
+// u / 2, point u % 2 (P = LANES / 2: the signature's 2 P tables in P slots).
+template <int LANES>
+struct LaneOf {
+  static constexpr uint32_t P = LANES / 2;
+  uint32_t h, u, slot;
+  int point;
+  CG_DEV LaneOf(uint32_t i, uint32_t q) : h(q / P), u(q % P) {
+    slot = LANES == 2 ? i : P * i + (P / 2) * h + u / 2;
+    point = LANES == 2 ? (int)h : (int)(u & 1);
+  }
+};
+
 template <int LANES>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_POINTS_WAVES, 8))) void cg_ed25519_points_lanes(
     const uint32_t* __restrict__ pk, const uint32_t* __restrict__ sig, uint32_t n, uint32_t cap, uint32_t scap,
@@ -537,24 +550,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_POINTS_W
   CG_WAVE_PRIO(1);
   const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t i = l / LANES, q = l % LANES;
-  const uint32_t h = LANES == 4 ? q >> 1 : q, u = LANES == 4 ? q & 1 : 0u;
+  const LaneOf<LANES> lo(i, q);
   if (i >= n) return;
-  const uint32_t* src = h ? sig : pk;  // R is words 0..7 of the signature rows
+  const uint32_t* src = lo.h ? sig : pk;  // R is words 0..7 of the signature rows
   uint32_t w[8];
   CG_UNROLL for (int k = 0; k < 8; ++k) w[k] = src[(size_t)k * cap + i];
   ge_p3 P;
   uint32_t ok = ge_frombytes_i2p(P, w);
-  if (h) {
+  if (lo.h) {
     ok = ok && ge_strict_check(P, w);
   } else {
     fe_neg_p(P.X, P.X);  // -A kept floor-shaped, as ed25519_points_stage
     fe_neg_p(P.T, P.T);
   }
-  reinterpret_cast<uint8_t*>(pstat)[4 * (size_t)i + q] = (uint8_t)(ok ? V_COMPUTE : h ? V_REJECT : V_KEY_INVALID);
+  // verdict bytes: LANES 2 / 4 byte q (A in bytes 0 (and 1), R in byte 1 / 2 (and 3));
+  // LANES 8 only the part-0 lanes, bytes 0 and 2
+  if (LANES != 8 || lo.u == 0)
+    reinterpret_cast<uint8_t*>(pstat)[4 * (size_t)i + (LANES == 8 ? 2 * lo.h : q)] =
+        (uint8_t)(ok ? V_COMPUTE : lo.h ? V_REJECT : V_KEY_INVALID);
   if (!ok) return;
-  if (u) ge_p3_dbl64(P);
-  const LaneTab lt = lane_table(table, LANES == 4 ? 2 * i + h : i, scap);
-  ed25519_build_table(P, [&](int k, const ge_cached& c) { store_slot(lt, (int)(LANES == 4 ? u : h), k, c); });
+  if (lo.u) ge_p3_dbl_n(P, 4 * (32 / LaneOf<LANES>::P) * lo.u);  // 2^(4 u D) P
+  const LaneTab lt = lane_table(table, lo.slot, scap);
+  ed25519_build_table(P, [&](int k, const ge_cached& c) { store_slot(lt, lo.point, k, c); });
 }
 
 template <int LANES>
@@ -565,13 +582,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_PAIR_WAV
   CG_WAVE_PRIO(0);
   const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t i = l / LANES, q = l % LANES;
-  const uint32_t h = LANES == 4 ? q >> 1 : q, u = LANES == 4 ? q & 1 : 0u;
+  const LaneOf<LANES> lo(i, q);
   const bool in = i < n;
   const uint32_t st = in ? status[i] : 0u;
   const uint32_t pw = in ? pstat[i] : 0u;
   // ed25519_points_stage precedence: A's KEY_INVALID first, then (after the hash
-  // phase's verdict, ed_merge_verdict) R's REJECT (byte 1 / byte 2 for LANES 2 / 4)
-  const uint32_t pa = pw & 0xff, pr = (pw >> (LANES == 4 ? 16 : 8)) & 0xff;
+  // phase's verdict, ed_merge_verdict) R's REJECT (byte 1 / byte 2 for LANES 2 / 4, 8)
+  const uint32_t pa = pw & 0xff, pr = (pw >> (LANES == 2 ? 8 : 16)) & 0xff;
   const uint32_t v = in ? ed_merge_verdict(st, pa != V_COMPUTE ? pa : pr) : 0u;
   const bool live = in && v == V_COMPUTE;
   const uint32_t ndig = wave_max(live ? ed_status_ndig(st) : 0u);
@@ -582,17 +599,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_PAIR_WAV
     return;
   }
   const uint32_t* dig = digits + i;
-  const LaneTab lt = lane_table(const_cast<int32_t*>(table), LANES == 4 ? 2 * i + h : i, scap);
-  const int slot = (int)(LANES == 4 ? u : h);
+  const LaneTab lt = lane_table(const_cast<int32_t*>(table), lo.slot, scap);
   ge_p1p1 t;
   ed25519_msm_lane<RawEntry, LANES>(
-      t, ndig, q, [&](int w) CG_LINLINE { return dig[(size_t)w * scap]; }, h ? ed_status_rneg(st) : 0u,
-      [&](uint32_t k, RawEntry& r) CG_LINLINE { fetch_slot(lt, slot, k, r); },
+      t, ndig, q, [&](int w) CG_LINLINE { return dig[(size_t)w * scap]; }, lo.h ? ed_status_rneg(st) : 0u,
+      [&](uint32_t k, RawEntry& r) CG_LINLINE { fetch_slot(lt, lo.point, k, r); },
       [&](const RawEntry& r, ge_cached& c) CG_LINLINE { unpack_entry(r, c); },
       [&](uint32_t tb, uint32_t k, ge_precomp& p) CG_LINLINE { load_bentry(btab_g, tb, k, p); });
-  if (LANES == 4)
+  // the partial sums meet in log2(LANES) swaps, the last one with the identity test
+  CG_UNROLL for (int m = 1; m < LANES / 2; m *= 2)
     ed25519_lane_sum(t, [&](fe& x) CG_LINLINE {
-      CG_UNROLL for (int k = 0; k < 10; ++k) x.v[k] = __shfl_xor(x.v[k], 1, 64);
+      CG_UNROLL for (int k = 0; k < 10; ++k) x.v[k] = __shfl_xor(x.v[k], m, 64);
     });
   const uint32_t ok = ed25519_pair_combine(t, [&](fe& x) CG_LINLINE {
     CG_UNROLL for (int k = 0; k < 10; ++k) x.v[k] = __shfl_xor(x.v[k], LANES / 2, 64);
@@ -695,11 +712,14 @@ hipError_t launch_ed25519_points_msm(const Ed25519Dev& d, uint32_t n, const uint
 
 hipError_t launch_ed25519_points_lanes(const Ed25519Dev& d, uint32_t n, uint32_t lanes, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  if (lanes != 2 && lanes != 4) return hipErrorInvalidValue;
-  // four lanes: tables in scratch slots [0, 2n) of this view (the caller sized scap for it)
-  if (lanes == 4 && (uint64_t)2 * n > d.scap) return hipErrorInvalidValue;
+  if (lanes != 2 && lanes != 4 && lanes != 8) return hipErrorInvalidValue;
+  // four / eight lanes: tables in scratch slots [0, lanes / 2 n) of this view (the caller sized scap for it)
+  if (lanes > 2 && (uint64_t)lanes / 2 * n > d.scap) return hipErrorInvalidValue;
   const dim3 grid((uint32_t)(((uint64_t)lanes * n + 255) / 256));
-  if (lanes == 4)
+  if (lanes == 8)
+    hipLaunchKernelGGL(cg_ed25519_points_lanes<8>, grid, dim3(256), d.spread_lds, s, d.pk, d.sig, n, d.cap, d.scap, d.pstat,
+                       d.table);
+  else if (lanes == 4)
     hipLaunchKernelGGL(cg_ed25519_points_lanes<4>, grid, dim3(256), d.spread_lds, s, d.pk, d.sig, n, d.cap, d.scap, d.pstat,
                        d.table);
   else
@@ -711,10 +731,13 @@ hipError_t launch_ed25519_points_lanes(const Ed25519Dev& d, uint32_t n, uint32_t
 hipError_t launch_ed25519_msm_lanes(const Ed25519Dev& d, uint32_t n, uint32_t lanes, const uint32_t* out_index,
                                     uint8_t* verdict, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  if (lanes != 2 && lanes != 4) return hipErrorInvalidValue;
-  if (lanes == 4 && (uint64_t)2 * n > d.scap) return hipErrorInvalidValue;
+  if (lanes != 2 && lanes != 4 && lanes != 8) return hipErrorInvalidValue;
+  if (lanes > 2 && (uint64_t)lanes / 2 * n > d.scap) return hipErrorInvalidValue;
   const dim3 grid((uint32_t)(((uint64_t)lanes * n + 255) / 256));
-  if (lanes == 4)
+  if (lanes == 8)
+    hipLaunchKernelGGL(cg_ed25519_msm_lanes<8>, grid, dim3(256), 0, s, d.status, d.pstat, d.digits, d.table, d.btab, n,
+                       d.scap, out_index, verdict);
+  else if (lanes == 4)
     hipLaunchKernelGGL(cg_ed25519_msm_lanes<4>, grid, dim3(256), 0, s, d.status, d.pstat, d.digits, d.table, d.btab, n,
                        d.scap, out_index, verdict);
   else

@@ -61,15 +61,22 @@ int cgh_half_scalars(const uint32_t* h, uint32_t* c0, uint32_t* c1, uint32_t* c1
   return (int)ed25519_half_scalars(h, c0, c1, *c1neg);
 }
 
-static ge_precomp g_btab[4][kBTabEntries];  // the device's shared tables k * 2^(64 t) B, built with the same code
-static int g_init;
+// the device's shared tables k * 2^(32 s) B (s = 0..7), built with the same code, each
+// on first use (the eight at kBWin 16 take a while on one host thread)
+static ge_precomp g_btab_store[kBTables][kBTabEntries];
+static int g_btab_built[kBTables];
+struct LazyBtab {
+  const ge_precomp* operator[](uint32_t s) const {
+    if (!g_btab_built[s]) {
+      for (uint32_t k = 0; k < (uint32_t)kBTabEntries; ++k) ed25519_btab_entry(g_btab_store[s][k], s, k);
+      g_btab_built[s] = 1;
+    }
+    return g_btab_store[s];
+  }
+};
+static const LazyBtab g_btab{};
 
-static void init_btab() {
-  if (g_init) return;
-  for (uint32_t t = 0; t < 4; ++t)
-    for (uint32_t k = 0; k < (uint32_t)kBTabEntries; ++k) ed25519_btab_entry(g_btab[t][k], t, k);
-  g_init = 1;
-}
+static void init_btab() {}
 
 // The three device phases in sequence (hash -> points -> msm) for one signature;
 // the digit count is the lane's own (on the device it is the wave maximum, which
@@ -137,54 +144,74 @@ int cgh_ed25519_verify_pair(const uint8_t* pk_bytes, const uint8_t* sig_bytes, u
   return ok[0] ? (int)V_ACCEPT : (int)V_REJECT;
 }
 
-// The four-lane latency mode: lane q = 2 h + u runs ed25519_msm_lane<4> over point
-// h (-A / R) taken to 2^(64 u) (ge_p3_dbl64, as cg_ed25519_points_lanes<4>), then the
-// lane sums with partner q ^ 1 and the combine with q ^ 2, in the kernel's order;
-// returns -1 if the four lanes disagree.
-int cgh_ed25519_verify_quad(const uint8_t* pk_bytes, const uint8_t* sig_bytes, uint32_t sig_len, const uint8_t* msg,
-                            uint32_t msg_len, uint32_t mode, uint32_t force_ndig) {
-  init_btab();
+// The four- and eight-lane latency modes: lane q = P h + u (P = LANES / 2) runs
+// ed25519_msm_lane<LANES> over point h (-A / R) taken to 2^(4 u D) (D = 32 / P digits per
+// part; ge_p3_dbl_n, as cg_ed25519_points_lanes), then the lane sums with partners
+// q ^ 1, q ^ 2, ... and the combine with q ^ (LANES / 2), in the kernel's order;
+// returns -1 if the lanes disagree.
+}  // extern "C"
+
+template <int LANES>
+static int verify_lanes(const uint8_t* pk_bytes, const uint8_t* sig_bytes, uint32_t sig_len, const uint8_t* msg,
+                        uint32_t msg_len, uint32_t mode, uint32_t force_ndig) {
+  constexpr int P = LANES / 2, D = 32 / P;
   uint32_t pk[8], sig[16] = {0};
   memcpy(pk, pk_bytes, 32);
   memcpy(sig, sig_bytes, sig_len < 64 ? sig_len : 64);
   uint32_t dig[kDigitWords], ndig, rneg;
   uint32_t pre = ed25519_hash_stage(pk, sig, sig_len, msg, msg_len, mode, dig, ndig, rneg);
-  ge_p3 P[4];
-  pre = ed25519_points_stage(pk, sig, pre, P[0], P[2]);
+  ge_p3 A, R;
+  pre = ed25519_points_stage(pk, sig, pre, A, R);
   if (pre != V_COMPUTE) return (int)pre;
-  P[1] = P[0];
-  P[3] = P[2];
-  ge_p3_dbl64(P[1]);
-  ge_p3_dbl64(P[3]);
-  static ge_cached tab[4][kATabEntries];
-  for (int q = 0; q < 4; ++q) ed25519_build_table(P[q], [&](int k, const ge_cached& c) { tab[q][k] = c; });
+  static ge_cached tab[LANES][kATabEntries];
+  for (int q = 0; q < LANES; ++q) {
+    ge_p3 pt = q / P ? R : A;
+    if (q % P) ge_p3_dbl_n(pt, 4 * D * (q % P));
+    ed25519_build_table(pt, [&](int k, const ge_cached& c) { tab[q][k] = c; });
+  }
   if (force_ndig > ndig) ndig = force_ndig;
-  ge_p1p1 t[4];
-  for (uint32_t q = 0; q < 4; ++q)
-    ed25519_msm_lane<ge_cached, 4>(
-        t[q], ndig, q, [&](int w) { return dig[w]; }, (q >> 1) ? rneg : 0u, [&](uint32_t k, ge_cached& c) { c = tab[q][k]; },
+  ge_p1p1 t[LANES];
+  for (uint32_t q = 0; q < LANES; ++q)
+    ed25519_msm_lane<ge_cached, LANES>(
+        t[q], ndig, q, [&](int w) { return dig[w]; }, (q / P) ? rneg : 0u, [&](uint32_t k, ge_cached& c) { c = tab[q][k]; },
         [&](const ge_cached& r, ge_cached& c) { c = r; }, [&](uint32_t tb, uint32_t k, ge_precomp& x) { x = g_btab[tb][k]; });
-  // a lane's xchg hands it the partner's p3 form of the partner's running sum
-  auto partner_of = [](const ge_p1p1& pt, ge_p3& x) { ge_p1p1_to_p3(x, pt); };
-  ge_p1p1 s[4];
-  for (int q = 0; q < 4; ++q) {  // level 1: q + (q ^ 1), both from the values before the swap
+  // a lane's xchg hands it the partner's p3 form of the partner's running sum; every
+  // level reads the values from before its swap
+  for (int m = 1; m < LANES / 2; m *= 2) {
+    ge_p1p1 s[LANES];
+    for (int q = 0; q < LANES; ++q) {
+      ge_p3 x;
+      ge_p1p1_to_p3(x, t[q ^ m]);
+      const fe* src[4] = {&x.X, &x.Y, &x.Z, &x.T};
+      int c = 0;
+      s[q] = t[q];
+      ed25519_lane_sum(s[q], [&](fe& v) { v = *src[c++]; });
+    }
+    for (int q = 0; q < LANES; ++q) t[q] = s[q];
+  }
+  uint32_t ok[LANES];
+  for (int q = 0; q < LANES; ++q) {  // the last level, with the identity test
     ge_p3 x;
-    partner_of(t[q ^ 1], x);
+    ge_p1p1_to_p3(x, t[q ^ (LANES / 2)]);
     const fe* src[4] = {&x.X, &x.Y, &x.Z, &x.T};
     int c = 0;
-    s[q] = t[q];
-    ed25519_lane_sum(s[q], [&](fe& v) { v = *src[c++]; });
+    ok[q] = ed25519_pair_combine(t[q], [&](fe& v) { v = *src[c++]; });
   }
-  uint32_t ok[4];
-  for (int q = 0; q < 4; ++q) {  // level 2: with q ^ 2, and the identity test
-    ge_p3 x;
-    partner_of(s[q ^ 2], x);
-    const fe* src[4] = {&x.X, &x.Y, &x.Z, &x.T};
-    int c = 0;
-    ok[q] = ed25519_pair_combine(s[q], [&](fe& v) { v = *src[c++]; });
-  }
-  if (ok[0] != ok[1] || ok[0] != ok[2] || ok[0] != ok[3]) return -1;
+  for (int q = 1; q < LANES; ++q)
+    if (ok[q] != ok[0]) return -1;
   return ok[0] ? (int)V_ACCEPT : (int)V_REJECT;
+}
+
+extern "C" {
+
+int cgh_ed25519_verify_quad(const uint8_t* pk_bytes, const uint8_t* sig_bytes, uint32_t sig_len, const uint8_t* msg,
+                            uint32_t msg_len, uint32_t mode, uint32_t force_ndig) {
+  return verify_lanes<4>(pk_bytes, sig_bytes, sig_len, msg, msg_len, mode, force_ndig);
+}
+
+int cgh_ed25519_verify_oct(const uint8_t* pk_bytes, const uint8_t* sig_bytes, uint32_t sig_len, const uint8_t* msg,
+                           uint32_t msg_len, uint32_t mode, uint32_t force_ndig) {
+  return verify_lanes<8>(pk_bytes, sig_bytes, sig_len, msg, msg_len, mode, force_ndig);
 }
 
 // The key-reuse path's phases (keyprep -> hash<REUSE> -> points_r -> msm_reuse) for

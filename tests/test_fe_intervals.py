@@ -405,13 +405,15 @@ def pair_combine(C, st):
         assert all(abs(a) < 1 << 29 and abs(b) < 1 << 29 for a, b in fe)
 
 
-def quad_combine(C, st):
-    """The four-lane combine: ed25519_lane_sum with lane q ^ 1 (its output, a cached
-    addition's p1p1, is the next level's input), then ed25519_pair_combine with q ^ 2."""
+def lanes_combine(C, st, levels):
+    """The four- / eight-lane combine: ed25519_lane_sum with lanes q ^ 1 (, q ^ 2) (each
+    output, a cached addition's p1p1, is the next level's input), then
+    ed25519_pair_combine; `levels` = the lane sums before it (1 or 2)."""
     src = p3_union(st["ADD"], st["MADD"])
-    own = to_p3(C, src)
-    s1 = add_cached(C, own, p3_to_cached(C, own))
-    own2 = to_p3(C, p3_union(src, s1))
+    for _ in range(levels):
+        own = to_p3(C, src)
+        src = p3_union(src, add_cached(C, own, p3_to_cached(C, own)))
+    own2 = to_p3(C, src)
     s = add_cached(C, own2, p3_to_cached(C, own2))
     for fe in (s[0], fe_sub(s[1], s[3])):
         assert all(abs(a) < 1 << 29 and abs(b) < 1 << 29 for a, b in fe)
@@ -424,13 +426,14 @@ def test_limb_bounds_hold_for_all_inputs():
     tab_a = lane_table(C, negate_p3(A))
     tab_r = lane_table(C, R)
     tab_k = key_tables(C, A)  # (covers 2^64 (-A) of the four-lane mode too)
-    tab_r64 = lane_table(C, dbl64(C, R))
+    tab_r64 = lane_table(C, dbl64(C, R))  # (any 2^n R of the latency mode's parts: the same fixed point)
     btab = btab_entry(C)
     # the balanced and key-reuse loops; the latency mode's lanes (ed25519_msm_lane) run
     # a subset of the same transitions (no ADD -> ADD), so their states are covered too
     st = msm_states(C, p3_union(tab_a, tab_k), p3_union(tab_r, tab_r64), btab)
     pair_combine(C, st)
-    quad_combine(C, st)
+    lanes_combine(C, st, 1)
+    lanes_combine(C, st, 2)
     # 19-scaled operands within int32 (|g| <= 113025455 = 1.684 * 2^26), f sides below
     # 2^28, columns below 2^62 (int64 has a factor 2 of headroom on top)
     assert C.max_g <= (2 ** 31 - 1) // 19

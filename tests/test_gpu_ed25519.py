@@ -465,20 +465,21 @@ def test_fused_points_msm_vs_oracle(gpu_ctx, oracle, golden_ed25519, monkeypatch
     assert np.array_equal(gpu_verdicts(gpu_ctx, w, mode), oracle_verdicts(oracle, w, mode))
 
 
-@pytest.mark.parametrize("lanes", [1, 2, 4])
+@pytest.mark.parametrize("lanes", [1, 2, 4, 8])
 @pytest.mark.parametrize("mode", [MODE_IS_VALID, MODE_DO_VERIFY])
 def test_latency_mode_on_and_off_vs_oracle(gpu_ctx, oracle, golden_ed25519, monkeypatch, lanes, mode):
-    """The latency mode (cg_ed25519_points_lanes / cg_ed25519_msm_lanes: two or four lanes
-    per signature, used for small pieces, CORDA_AMD_ED_PAIR_MAX / CORDA_AMD_ED_QUAD_MAX)
-    forced on for every size with 2 and with 4 lanes, and forced off: every golden class
+    """The latency mode (cg_ed25519_points_lanes / cg_ed25519_msm_lanes: two, four or eight
+    lanes per signature, used for small pieces, CORDA_AMD_ED_PAIR_MAX / _QUAD_MAX / _OCT_MAX)
+    forced on for every size with 2, 4 and 8 lanes, and forced off: every golden class
     and a mutated 4,096-signature batch (the serving size it is for) against the golden
     verdicts and the oracle, plus the forced (h, 1) fallback on every 3rd lane (64-window
     loops beside ~33-window ones in one wave).  The library's per-kernel counters confirm
     which MSM kernel ran."""
     from corda_amd._lib import DEBUG_FORCE_FULL_LENGTH
     monkeypatch.setenv("CORDA_AMD_ED_PAIR_MAX", "0" if lanes == 1 else "1000000")
-    monkeypatch.setenv("CORDA_AMD_ED_QUAD_MAX", "1000000" if lanes == 4 else "0")
-    msm = {1: "ed25519_msm", 2: "ed25519_msm_pair", 4: "ed25519_msm_quad"}[lanes]
+    monkeypatch.setenv("CORDA_AMD_ED_QUAD_MAX", "1000000" if lanes >= 4 else "0")
+    monkeypatch.setenv("CORDA_AMD_ED_OCT_MAX", "1000000" if lanes == 8 else "0")
+    msm = {1: "ed25519_msm", 2: "ed25519_msm_pair", 4: "ed25519_msm_quad", 8: "ed25519_msm_oct"}[lanes]
     gpu_ctx.set_profiling(True)
     gpu_ctx.reset_stats()
     g = golden_ed25519
@@ -500,6 +501,7 @@ def test_latency_mode_on_and_off_vs_oracle(gpu_ctx, oracle, golden_ed25519, monk
         assert np.array_equal(crypto.verify_packed(gpu_ctx, b, mode), exp_g)
     finally:
         gpu_ctx.set_debug(DEBUG_FORCE_FULL_LENGTH, 0)
-        launches = {k: gpu_ctx.kernel_stats(k)[1] for k in ("ed25519_msm", "ed25519_msm_pair", "ed25519_msm_quad")}
+        launches = {k: gpu_ctx.kernel_stats(k)[1]
+                    for k in ("ed25519_msm", "ed25519_msm_pair", "ed25519_msm_quad", "ed25519_msm_oct")}
         gpu_ctx.set_profiling(False)
     assert launches[msm] >= 4 and sum(launches.values()) == launches[msm], launches

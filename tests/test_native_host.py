@@ -34,7 +34,7 @@ def host():
                                           ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]
     lib.cgh_ed25519_verify_reuse.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p,
                                              ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]
-    for fn in ("cgh_ed25519_verify_pair", "cgh_ed25519_verify_quad"):
+    for fn in ("cgh_ed25519_verify_pair", "cgh_ed25519_verify_quad", "cgh_ed25519_verify_oct"):
         getattr(lib, fn).argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p,
                                      ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]
     return lib
@@ -230,7 +230,7 @@ def test_verify_random_mutations_vs_oracle(host, oracle):
                 oracle.oracle_ed25519_verify(p, sg, len(sg), m, len(m), 0)
 
 
-@pytest.mark.parametrize("fn", ["cgh_ed25519_verify_pair", "cgh_ed25519_verify_quad"])
+@pytest.mark.parametrize("fn", ["cgh_ed25519_verify_pair", "cgh_ed25519_verify_quad", "cgh_ed25519_verify_oct"])
 def test_verify_latency_lanes_golden_and_mutations(host, golden_ed25519, oracle, fn):
     """The latency mode's split of the MSM over two lanes (ed25519_msm_lane p = 0 / 1 +
     ed25519_pair_combine) and over four (ed25519_msm_lane<4> over the 64-bit halves and
@@ -275,7 +275,7 @@ def test_field_bounds_whole_pipeline(golden_ed25519, oracle):
     lib = ctypes.CDLL(so)
     lib.cgh_ed25519_verify_nd.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p,
                                           ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]
-    for fn in ("cgh_ed25519_verify_pair", "cgh_ed25519_verify_quad"):
+    for fn in ("cgh_ed25519_verify_pair", "cgh_ed25519_verify_quad", "cgh_ed25519_verify_oct"):
         getattr(lib, fn).argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p,
                                      ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]
     cases = [(bytes.fromhex(e["pk"]), bytes.fromhex(e["sig"]), bytes.fromhex(e["msg"]), e["is_valid"])
@@ -294,6 +294,7 @@ def test_field_bounds_whole_pipeline(golden_ed25519, oracle):
         if i % 2 == 0:  # the latency mode's two- and four-lane splits (their own operation sequences)
             assert lib.cgh_ed25519_verify_pair(pk, sig, len(sig), msg, len(msg), 0, nd) == exp
             assert lib.cgh_ed25519_verify_quad(pk, sig, len(sig), msg, len(msg), 0, nd) == exp
+            assert lib.cgh_ed25519_verify_oct(pk, sig, len(sig), msg, len(msg), 0, nd) == exp
     ml, lc = ctypes.c_int64(), ctypes.c_double()
     lib.cgh_bounds_report(ctypes.byref(ml), ctypes.byref(lc))
     # inputs stay below 1.69 * 2^26 (19 * limb fits int32), column sums far inside int64

@@ -34,7 +34,7 @@ SETTINGS = [
                      (8, 0.5, 0.5))
      for extra in ({}, {"CORDA_AMD_VERIFY_RING": "0"})]
 KEYS = ("CORDA_AMD_VERIFY_CHUNKS", "CORDA_AMD_VERIFY_MIN_CHUNK", "CORDA_AMD_VERIFY_HEAD", "CORDA_AMD_VERIFY_TAIL",
-        "CORDA_AMD_VERIFY_SERIAL", "CORDA_AMD_VERIFY_RING", "CORDA_AMD_ED_PAIR_MAX", "CORDA_AMD_ED_QUAD_MAX", "CORDA_AMD_VERIFY_ONE_DMA")
+        "CORDA_AMD_VERIFY_SERIAL", "CORDA_AMD_VERIFY_RING", "CORDA_AMD_ED_PAIR_MAX", "CORDA_AMD_ED_QUAD_MAX", "CORDA_AMD_ED_OCT_MAX", "CORDA_AMD_VERIFY_ONE_DMA")
 
 
 def h2d_rates(mb=256):
