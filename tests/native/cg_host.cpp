@@ -76,14 +76,11 @@ struct LazyBtab {
 };
 static const LazyBtab g_btab{};
 
-static void init_btab() {}
-
 // The three device phases in sequence (hash -> points -> msm) for one signature;
 // the digit count is the lane's own (on the device it is the wave maximum, which
 // only adds leading zero digits).  force_ndig > 0 overrides it.
 int cgh_ed25519_verify_nd(const uint8_t* pk_bytes, const uint8_t* sig_bytes, uint32_t sig_len, const uint8_t* msg,
                           uint32_t msg_len, uint32_t mode, uint32_t force_ndig, uint32_t full_length) {
-  init_btab();
   uint32_t pk[8], sig[16] = {0};
   memcpy(pk, pk_bytes, 32);
   memcpy(sig, sig_bytes, sig_len < 64 ? sig_len : 64);
@@ -114,7 +111,6 @@ int cgh_ed25519_verify(const uint8_t* pk_bytes, const uint8_t* sig_bytes, uint32
 // the two lanes disagree (they must not).
 int cgh_ed25519_verify_pair(const uint8_t* pk_bytes, const uint8_t* sig_bytes, uint32_t sig_len, const uint8_t* msg,
                             uint32_t msg_len, uint32_t mode, uint32_t force_ndig) {
-  init_btab();
   uint32_t pk[8], sig[16] = {0};
   memcpy(pk, pk_bytes, 32);
   memcpy(sig, sig_bytes, sig_len < 64 ? sig_len : 64);
@@ -219,7 +215,6 @@ int cgh_ed25519_verify_oct(const uint8_t* pk_bytes, const uint8_t* sig_bytes, ui
 // wave would cause; full_length forces this lane's own (h, 1) fallback.
 int cgh_ed25519_verify_reuse(const uint8_t* pk_bytes, const uint8_t* sig_bytes, uint32_t sig_len, const uint8_t* msg,
                              uint32_t msg_len, uint32_t mode, uint32_t wide, uint32_t full_length) {
-  init_btab();
   uint32_t pk[8], sig[16] = {0};
   memcpy(pk, pk_bytes, 32);
   memcpy(sig, sig_bytes, sig_len < 64 ? sig_len : 64);
