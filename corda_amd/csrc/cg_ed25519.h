@@ -494,7 +494,8 @@ CG_HD uint32_t ed25519_pair_combine(const ge_p1p1& t, Xchg&& xchg) {
 // [c1](+-R) with 16-digit chunks c0_t of c0's signed radix-16 digits (t = 0..3) and
 // |c1| < 2^66: 16 (or 17 when some lane's c1 needs a 17th digit) windows — ~64
 // doublings instead of ~130 — four per-key A tables (getA(t, k, .)), the lane's R
-// table, and 16-bit B windows over the four shared tables 2^(64 t) B (getB(2 t, k, .)).
+// table, and kBWin-bit B windows (16 on the device; 8 in the host bounds / sanitizer
+// builds) over the four shared tables 2^(64 t) B (getB(2 t, k, .)).
 // c3w (wave-uniform): chunk 3 is added in the c3w lowest windows only (its digits
 // are zero above; 16 for a fallback lane's 253-bit c0).  Returns 1 iff P is the
 // identity.
@@ -564,11 +565,11 @@ CG_HD uint32_t ed25519_msm_reuse(uint32_t c3w, uint32_t win17, const uint32_t di
         ge_add_cached(t, ge_identity_p3(), ca, nr ^ rneg);  // a 17th window: R comes first
       }
     }
-    if ((pos & 15) == 0 && pos < 64) {
-      constexpr uint32_t kHalf = 1u << 15;
+    if ((pos & (kBWin - 1)) == 0 && pos < 64) {  // (kBWin-bit fields, use order, top window first)
+      constexpr uint32_t kHalf = 1u << (kBWin - 1), kMask = (1u << kBWin) - 1;
       CG_NOUNROLL for (int c = 0; c < 4; ++c) {
-        const uint32_t e = (uint32_t)bt[0] & 0xffffu;
-        const uint64_t nx = bt[0] >> 16;
+        const uint32_t e = (uint32_t)bt[0] & kMask;
+        const uint64_t nx = bt[0] >> kBWin;
         bt[0] = bt[1];
         bt[1] = bt[2];
         bt[2] = bt[3];

@@ -144,7 +144,8 @@ class CopyPool {
 struct cg_ctx {
   int device = -1;
   uint32_t n_cu = 256;                  // compute units (hipDeviceProp)
-  uint32_t lds_per_cu = 160 * 1024;     // LDS bytes per CU on gfx950 (the only target cg_open accepts)
+  uint32_t lds_per_cu = 160 * 1024;     // LDS bytes per CU (hipDeviceProp; 160 KB on gfx950)
+  uint32_t lds_per_block = 160 * 1024;  // largest LDS request of one block (hipDeviceProp)
   hipStream_t stream = nullptr;
   hipStream_t copy_stream = nullptr;  // host-to-device uploads overlapped with `stream` (tx pipeline)
   hipStream_t hash_stream = nullptr;  // tx pipeline: Merkle ids of chunk k+1 beside chunk k's signatures
@@ -395,7 +396,8 @@ cg_status upload(cg_ctx* ctx, T** dst, const T* src, size_t count, const char* w
 
 // upload() of a host vector that dies before the copy runs: through the pinned
 // staging area when the tx pipeline has one active (the copy then never blocks the
-// host), else a plain upload followed by the caller's stream sync.
+// host), else a plain upload followed by the caller's stream sync — or, for a
+// MsgSrc::keep_raw batch (no sync), with the vector moved into the batch (idx_kept).
 cg_status upload_idx(cg_ctx* ctx, uint32_t** dst, const uint32_t* src, size_t count, const char* what) {
   const size_t bytes = (count * 4 + 255) & ~(size_t)255;
   if (!ctx->pin_active || ctx->pin_used + bytes > ctx->pin_cap) {
@@ -471,6 +473,10 @@ struct cg_batch {
   // engineVerify call); null in tx-pipeline batches, whose staging parse already sits
   // inside the pipeline's own timed run
   const void* raw_kept[3] = {nullptr, nullptr, nullptr};  // MsgSrc::keep_raw: staging's raw rows
+  // MsgSrc::keep_raw: the host index vectors the staging copies read (a plain
+  // hipMemcpyAsync when no pinned staging area is active), alive until the batch is freed
+  // after the caller's sync
+  std::vector<uint32_t> idx_kept[4];
   const uint8_t* arena_pending = nullptr;  // host arena still to upload (launch_verify, beside the points kernel)
   size_t arena_pending_bytes = 0;
   uint8_t* ec_rows[2] = {nullptr, nullptr};     // [ec[c].n][ec_sig_stride]
@@ -638,6 +644,8 @@ cg_status cg_open(int device, cg_ctx** out) {
   if (!ctx) return CG_E_OUT_OF_MEMORY;
   ctx->device = device;
   ctx->n_cu = (uint32_t)std::max(1, prop.multiProcessorCount);
+  if (prop.maxSharedMemoryPerMultiProcessor > 0) ctx->lds_per_cu = (uint32_t)prop.maxSharedMemoryPerMultiProcessor;
+  if (prop.sharedMemPerBlock > 0) ctx->lds_per_block = (uint32_t)prop.sharedMemPerBlock;
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
     delete ctx;
     return CG_E_DEVICE;
@@ -771,14 +779,18 @@ uint32_t ed_pair_max() {
 // too when every block fits on its own CU, else exactly half (two points blocks may
 // share a CU, a hash block never joins them) when that fits; otherwise nothing.
 // CORDA_AMD_ED_SPREAD_LDS=0 turns it off.  Sets d.spread_lds / d.spread_lds_hash.
-void ed_spread_lds(const cg_ctx* ctx, cg::Ed25519Dev& d, uint64_t points_blocks, uint64_t hash_blocks) {
+// n_cu: the CUs this piece may count on (inside the two-chunk verify pipeline the other
+// chunk's kernels hold about half the chip).
+void ed_spread_lds(const cg_ctx* ctx, cg::Ed25519Dev& d, uint64_t points_blocks, uint64_t hash_blocks,
+                   uint32_t n_cu) {
   const char* e = std::getenv("CORDA_AMD_ED_SPREAD_LDS");
   d.spread_lds = d.spread_lds_hash = 0;
   if (e && std::atoi(e) == 0) return;
   const uint32_t half = ctx->lds_per_cu / 2;
-  if (points_blocks + hash_blocks <= ctx->n_cu) {
+  if (half + 4096 > ctx->lds_per_block) return;  // a block cannot reserve more than half a CU
+  if (points_blocks + hash_blocks <= n_cu) {
     d.spread_lds = d.spread_lds_hash = half + 4096;
-  } else if ((points_blocks + 1) / 2 + hash_blocks <= ctx->n_cu) {
+  } else if ((points_blocks + 1) / 2 + hash_blocks <= n_cu) {
     d.spread_lds = half;
     d.spread_lds_hash = half + 4096;
   }
@@ -1047,13 +1059,18 @@ cg_status create_batch(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const ui
     }
   }
   // the host index vectors die here: wait for the copies that read them (unless every
-  // one went through the pinned staging area of an asynchronous tx-pipeline stage)
+  // one went through the pinned staging area of an asynchronous tx-pipeline stage, or
+  // the batch keeps them: keep_raw)
   if (m.keep_raw && raw_owned) {  // freed with the batch, after the caller's sync
     b->raw_kept[0] = pk_raw;
     b->raw_kept[1] = sig_raw;
     b->raw_kept[2] = sl_raw;
     pk_raw = sig_raw = nullptr;
     sl_raw = nullptr;
+  }
+  if (m.keep_raw) {  // no sync below: the copies may still read the index vectors
+    for (int c = 0; c < 3; ++c) b->idx_kept[c].swap(idx[c]);
+    b->idx_kept[3].swap(bad);
   }
   hipError_t e = ((m.async || m.keep_raw) && ctx->pin_fallbacks == fallbacks0) ? hipSuccess
                                                                                : hipStreamSynchronize(ctx->stream);
@@ -1220,6 +1237,18 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = 
       // prepared-batch verify (this call owns the streams): points beside hash on the idle copy stream
       hipStream_t pts = pts_stream ? pts_stream : (join_streams && ed_overlap_enabled() ? ctx->copy_stream : nullptr);
       if (split > 1) {
+        if (b->arena_pending) {  // every piece's hash kernel reads the arena: it goes up before the fork
+          {
+            Timed t(ctx, "h2d_arena", b->arena_pending_bytes);
+            CG_TRY(ctx,
+                   hipMemcpyAsync(b->arena, b->arena_pending, b->arena_pending_bytes, hipMemcpyHostToDevice,
+                                  ctx->stream),
+                   "upload arena");
+          }
+          b->arena_pending = nullptr;
+          CG_TRY(ctx, hipEventRecord(ctx->ev_arena, ctx->stream), "arena done");
+          CG_TRY(ctx, hipStreamWaitEvent(ctx->hash_stream, ctx->ev_arena, 0), "fork ed25519 split");
+        }
         CG_TRY(ctx, hipStreamWaitEvent(ctx->hash_stream, ctx->ev_fork, 0), "fork ed25519 split");
       }
       struct StreamBack {  // ctx->stream is the piece's lane inside the loop; restored on every exit
@@ -1257,7 +1286,9 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = 
         const bool pair = !b->ed_key_index && !fuse && cnt <= pair_max;  // latency mode
         // (quad_ok / oct_ok: one piece with 2 / 4 cnt scratch slots in its region)
         const uint32_t lanes = !pair ? 1u : oct_ok && split == 1 ? 8u : quad_ok && split == 1 ? 4u : 2u;
-        if (pair) ed_spread_lds(ctx, d, ((uint64_t)lanes * cnt + 255) / 256, (cnt + 255) / 256);
+        if (pair)
+          ed_spread_lds(ctx, d, ((uint64_t)lanes * cnt + 255) / 256, (cnt + 255) / 256,
+                        join_streams ? ctx->n_cu : std::max(1u, ctx->n_cu / 2));
         auto launch_points = [&](hipStream_t ps) -> cg_status {
           Timed t(ctx, lanes == 8   ? "ed25519_points_oct"
                        : lanes == 4 ? "ed25519_points_quad"

@@ -119,3 +119,87 @@ def ref_cert_cases():
                 dict(base, cls="ref_empty_msg", sig=sig, msg=b""),
                 dict(base, cls="ref_other_curve", scheme=5 - r["scheme"], sig=sig, msg=msg)]
     return out
+
+
+# (is_valid, do_verify) the structure of each reference-Ed25519 case implies; None = decided by the
+# restatement alone (i2p-specific rules A.6/A.7 and mixed-order keys: no reference artefact pins them)
+REF_ED_EXPECT = {"ref_sig": (0, 0), "ref_wrong_key": (1, 1), "ref_id_flip": (1, 1), "ref_sig0_inc": (1, 1),
+                 "ref_R_signflip": (1, 1), "ref_key_signflip": (1, 1), "ref_sig_len63": (2, 2),
+                 "ref_sig_len65": (2, 2), "ref_empty_msg": (1, 4), "ref_empty_sig": (2, 4),
+                 "ref_entropy_signed": (0, 0), "ref_S_plus_L": None, "ref_S_plus_kL": None,
+                 "ref_entropy_mixed_order": None}
+
+
+@pytest.fixture(scope="session")
+def ref_ed25519_cases():
+    """The reference's own Ed25519 artefacts (tests/golden/ref_ed25519_vectors.json, extracted by
+    make_ref_ed25519_vectors.py): the two signatures of the tutorial's verifiedTransactions dump
+    over its tx id (docs/source/tutorial-cordapp.rst:472-476) and mutants of them, every signature
+    under every other reference key, and signatures made with the two trade.json keys, which are
+    entropyToKeyPair(1)/(2) (Crypto.kt:733-739): over the tutorial id, 100 zero bytes and 1 KB
+    (CryptoUtilsTest.kt's shapes), plus E8-style mixed-order variants of those keys (a·B + T signed
+    with a).  Each case: dict(cls, pk, sig, msg); expected verdicts in REF_ED_EXPECT."""
+    import hashlib
+    import random
+
+    import ed25519_i2p as ED
+    g = load_golden("ref_ed25519_vectors.json")
+    keys = [bytes.fromhex(k["a"]) for k in g["keys"]]
+    out = []
+    for row in g["sigs"]:
+        a, sig, msg = bytes.fromhex(row["a"]), bytes.fromhex(row["sig"]), bytes.fromhex(row["msg"])
+        out.append(dict(cls="ref_sig", pk=a, sig=sig, msg=msg))
+        out += [dict(cls="ref_wrong_key", pk=k, sig=sig, msg=msg) for k in keys if k != a]
+        flip = bytearray(msg)
+        flip[5] ^= 0x01
+        bump = bytearray(sig)
+        bump[0] = (bump[0] + 1) & 0xFF
+        rsign = bytearray(sig)
+        rsign[31] ^= 0x80
+        ksign = bytearray(a)
+        ksign[31] ^= 0x80
+        s = int.from_bytes(sig[32:], "little")
+        out += [dict(cls="ref_id_flip", pk=a, sig=sig, msg=bytes(flip)),
+                dict(cls="ref_sig0_inc", pk=a, sig=bytes(bump), msg=msg),
+                dict(cls="ref_R_signflip", pk=a, sig=bytes(rsign), msg=msg),
+                dict(cls="ref_key_signflip", pk=bytes(ksign), sig=sig, msg=msg),
+                dict(cls="ref_sig_len63", pk=a, sig=sig[:63], msg=msg),
+                dict(cls="ref_sig_len65", pk=a, sig=sig + b"\0", msg=msg),
+                dict(cls="ref_empty_msg", pk=a, sig=sig, msg=b""),
+                dict(cls="ref_empty_sig", pk=a, sig=b"", msg=msg),
+                dict(cls="ref_S_plus_L", pk=a, sig=sig[:32] + (s + ED.L).to_bytes(32, "little"), msg=msg)]
+        out += [dict(cls="ref_S_plus_kL", pk=a, sig=sig[:32] + (s + k * ED.L).to_bytes(32, "little"), msg=msg)
+                for k in range(1, 16) if 2**255 <= s + k * ED.L < 2**256]
+    tutorial_id = bytes.fromhex(g["sigs"][0]["msg"])
+    rnd = random.Random(20170707)
+    tors = None
+    for k in g["keys"]:
+        if k["entropy_k"] is None:
+            continue
+        seed = ED.entropy_seed(k["entropy_k"])
+        for msg in (tutorial_id, bytes(100), rnd.randbytes(1024)):
+            pk, sig = ED.sign(seed, msg)
+            assert pk.hex() == k["a"]
+            out.append(dict(cls="ref_entropy_signed", pk=pk, sig=sig, msg=msg))
+        if tors is None:  # the order-8 subgroup, from a point of order 8L·k
+            y = 2
+            while True:
+                try:
+                    t = ED.scalarmult(ED.decode_point_i2p(y.to_bytes(32, "little")), ED.L)
+                except ED.KeyInvalid:
+                    y += 1
+                    continue
+                if not ED.point_equal(ED.scalarmult(t, 4), ED.IDENTITY):
+                    break
+                y += 1
+            tors = [ED.scalarmult(t, j) for j in range(8)]
+        a_sc, prefix, _ = ED.seed_to_keypair(seed)
+        for j in (1, 2, 4):  # torsion components of order 8, 4, 2
+            aenc = ED.encode_point(ED._add(ED.scalarmult(ED.BASE, a_sc), tors[j]))
+            for msg in (tutorial_id, rnd.randbytes(40)):
+                r = ED.sc_reduce(hashlib.sha512(prefix + msg).digest())
+                rb = ED.encode_point(ED.scalarmult(ED.BASE, r))
+                h = ED.sc_reduce(hashlib.sha512(rb + aenc + msg).digest())
+                out.append(dict(cls="ref_entropy_mixed_order", pk=aenc,
+                                sig=rb + ((r + h * a_sc) % ED.L).to_bytes(32, "little"), msg=msg))
+    return out

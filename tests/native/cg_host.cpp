@@ -62,17 +62,22 @@ int cgh_half_scalars(const uint32_t* h, uint32_t* c0, uint32_t* c1, uint32_t* c1
 }
 
 // the device's shared tables k * 2^(32 s) B (s = 0..7), built with the same code, each
-// on first use (the eight at kBWin 16 take a while on one host thread)
+// entry on first use (a verify touches ~16 of the 8 x 32,769; the sanitizer build runs
+// the same code ~10x slower, so whole tables would take minutes there)
 static ge_precomp g_btab_store[kBTables][kBTabEntries];
-static int g_btab_built[kBTables];
+static uint8_t g_btab_built[kBTables][kBTabEntries];
 struct LazyBtab {
-  const ge_precomp* operator[](uint32_t s) const {
-    if (!g_btab_built[s]) {
-      for (uint32_t k = 0; k < (uint32_t)kBTabEntries; ++k) ed25519_btab_entry(g_btab_store[s][k], s, k);
-      g_btab_built[s] = 1;
+  struct Row {
+    uint32_t s;
+    const ge_precomp& operator[](uint32_t k) const {
+      if (!g_btab_built[s][k]) {
+        ed25519_btab_entry(g_btab_store[s][k], s, k);
+        g_btab_built[s][k] = 1;
+      }
+      return g_btab_store[s][k];
     }
-    return g_btab_store[s];
-  }
+  };
+  Row operator[](uint32_t s) const { return Row{s}; }
 };
 static const LazyBtab g_btab{};
 
@@ -244,17 +249,27 @@ int cgh_half_scalars_reuse(const uint32_t* h, uint32_t* c0, uint32_t* c1, uint32
 // the device's shared generator tables (kGTabEntries affine points: k*G, and for
 // secp256k1 also k*2^128 G), built on the host with the same code
 template <class C>
-static const jpt* g_table(uint32_t t = 0) {
-  static jpt* tab[2] = {nullptr, nullptr};
-  if (!tab[t]) {
-    tab[t] = new jpt[kGTabEntries];
-    for (uint32_t k = 1; k < kGTabEntries; ++k) {
+struct LazyG {  // the device's G tables (t = 0: k G; t = 1: k 2^128 G), each entry on first use
+  uint32_t t;
+  const jpt& operator[](uint32_t k) const {
+    static jpt* tab[2] = {nullptr, nullptr};
+    static uint8_t* built[2] = {nullptr, nullptr};
+    if (!tab[t]) {
+      tab[t] = new jpt[kGTabEntries];
+      built[t] = new uint8_t[kGTabEntries]();
+    }
+    if (!built[t][k]) {
       ecdsa_g_entry<C>(k, tab[t][k].X, tab[t][k].Y, t);
       F26<C>::one(tab[t][k].Z);
       tab[t][k].inf = 0;
+      built[t][k] = 1;
     }
+    return tab[t][k];
   }
-  return tab[t];
+};
+template <class C>
+static LazyG<C> g_table(uint32_t t = 0) {
+  return LazyG<C>{t};
 }
 
 // secp256k1 joint multiplication exactly as cg_ecdsa_msm runs it (GLV split, the
@@ -266,8 +281,8 @@ static void joint_k1glv(jpt& acc, const uint32_t u1[8], const uint32_t u2[8], co
   recode_g(dg, u1);
   recode16_65(dk1, k1);
   recode16_65(dk2, k2);
-  const jpt* g0 = g_table<CurveK1>(0);
-  const jpt* g1 = g_table<CurveK1>(1);
+  const auto g0 = g_table<CurveK1>(0);
+  const auto g1 = g_table<CurveK1>(1);
   ecdsa_joint_glv(acc, nd, dk1, dk2, neg1, neg2, dg, [&](uint32_t k, jpt& p) { p = qtab[k]; },
                   [&](uint32_t t, uint32_t k, jpt& p) { p = t ? g1[k] : g0[k]; });
 }
@@ -275,7 +290,7 @@ static void joint_k1glv(jpt& acc, const uint32_t u1[8], const uint32_t u2[8], co
 template <class C>
 static int ecdsa_verify_host(const uint8_t* q_be, const uint8_t* sig, uint32_t sig_len, const uint8_t* msg,
                              uint32_t msg_len, uint32_t mode) {
-  const jpt* gtab = g_table<C>();
+  const auto gtab = g_table<C>();
   uint32_t qw[16], qx[8], qy[8], r[8], s[8], nn[8], u1[8], u2[8];
   memcpy(qw, q_be, 64);
   be_words_to_limbs(qx, qw);
@@ -372,7 +387,7 @@ template <class C>
 static int joint_host(const uint32_t* u1, const uint32_t* u2, const uint32_t* qx, const uint32_t* qy, uint32_t* out,
                       uint32_t force_nd) {
   jpt qtab[9], acc;
-  const jpt* gtab = g_table<C>();
+  const auto gtab = g_table<C>();
   ecdsa_q_table_affine<C>(qx, qy, [&](int k, const jpt& p) { qtab[k] = p; });
   if (C::kScheme == 2) {
     joint_k1glv(acc, u1, u2, qtab, force_nd);

@@ -266,8 +266,9 @@ def test_field_bounds_whole_pipeline(golden_ed25519, oracle):
     host build with 128-bit shadow column sums (-DCG_CHECK_BOUNDS traps when a
     column leaves +-2^62 or differs from the device formulation) runs the golden fixtures (incl.
     small-order / non-canonical points) and random + mutated signatures through all
-    three phases, forcing the full-length and padded-digit variants too (8-bit B
-    windows here: the same formulas, a 258-entry table instead of 65,538)."""
+    three phases, forcing the full-length and padded-digit variants too, and the latency
+    splits and the key-reuse path (8-bit B windows here: the same formulas, a 258-entry
+    table instead of 65,538)."""
     so = os.path.join(ROOT, "tests", "native", "libcg_host_bounds.so")
     src = os.path.join(ROOT, "tests", "native", "cg_host.cpp")
     subprocess.check_call(["g++", "-O1", "-std=c++17", "-shared", "-fPIC", "-DCG_CHECK_BOUNDS", "-DCG_ED_BWIN=8", "-I",
@@ -278,8 +279,10 @@ def test_field_bounds_whole_pipeline(golden_ed25519, oracle):
     for fn in ("cgh_ed25519_verify_pair", "cgh_ed25519_verify_quad", "cgh_ed25519_verify_oct"):
         getattr(lib, fn).argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p,
                                      ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]
+    lib.cgh_ed25519_verify_reuse.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p,
+                                             ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]
     cases = [(bytes.fromhex(e["pk"]), bytes.fromhex(e["sig"]), bytes.fromhex(e["msg"]), e["is_valid"])
-             for e in golden_ed25519]
+             for e in golden_ed25519 if len(bytes.fromhex(e["pk"])) == 32]
     rnd = random.Random(9)
     for _ in range(150):
         seed, msg = rnd.randbytes(32), rnd.randbytes(rnd.randint(0, 200))
@@ -295,6 +298,8 @@ def test_field_bounds_whole_pipeline(golden_ed25519, oracle):
             assert lib.cgh_ed25519_verify_pair(pk, sig, len(sig), msg, len(msg), 0, nd) == exp
             assert lib.cgh_ed25519_verify_quad(pk, sig, len(sig), msg, len(msg), 0, nd) == exp
             assert lib.cgh_ed25519_verify_oct(pk, sig, len(sig), msg, len(msg), 0, nd) == exp
+        else:  # the key-reuse path (per-key tables, 8-bit B windows over the four 2^(64 t) B tables)
+            assert lib.cgh_ed25519_verify_reuse(pk, sig, len(sig), msg, len(msg), 0, i % 4 == 1, i % 3 == 1) == exp
     ml, lc = ctypes.c_int64(), ctypes.c_double()
     lib.cgh_bounds_report(ctypes.byref(ml), ctypes.byref(lc))
     # inputs stay below 1.69 * 2^26 (19 * limb fits int32), column sums far inside int64

@@ -248,3 +248,50 @@ def test_ecdsa_reference_certificates(oracle, ref_cert_cases):
         if c["cls"] not in ("ref_sig0_inc", "ref_nonminimal_r", "ref_empty_msg"):
             assert OSSL.ecdsa_verify(c["scheme"], q, c["sig"], hashlib.sha256(c["msg"]).digest()) == (exp[0] == 0), \
                 c["cls"]
+
+
+def test_ed25519_reference_keys_and_signatures(oracle, ref_ed25519_cases):
+    """The Ed25519 oracle pinned by the reference's own artefacts (tests/golden/ref_ed25519_vectors.json):
+    * the Kryo wire keys decode (header corda\\0\\0\\1, SerializationScheme.kt:216; Kryo.kt:330-340) and
+      the two trade.json keys are reproduced byte for byte from entropyToKeyPair(1) / (2)
+      (Crypto.kt:733-739) by both the C restatement's signer path and the Python twin;
+    * the tutorial's two signatures over its tx id accept in the C restatement, the twin and OpenSSL,
+      under their signer's key only;
+    * every mutant gets the verdict its structure implies (REF_ED_EXPECT), in both restatements; the
+      S + L / S + kL / mixed-order rows (i2p rules A.6/A.7, torsion) are restatement-only and must
+      only agree between the two restatements."""
+    import base64
+    from conftest import REF_ED_EXPECT, load_golden
+    g = load_golden("ref_ed25519_vectors.json")
+    b58 = "123456789ABCDEFGHJKLMNPQRSTUVWXYZabcdefghijkmnopqrstuvwxyz"
+    for k in g["keys"]:
+        n = 0
+        for ch in k["base58"]:
+            n = n * 58 + b58.index(ch)
+        wire = n.to_bytes(43, "big")
+        assert wire.hex() == k["wire"] and wire[:8] == b"corda\0\0\1" and wire[10] == 32 and wire[11:].hex() == k["a"]
+        if k["entropy_k"] is not None:
+            seed = ED.entropy_seed(k["entropy_k"])
+            assert ED.seed_to_keypair(seed)[2].hex() == k["a"]
+            msg = b"reference key"
+            pk, sig = ED.sign(seed, msg)
+            assert OSSL.ed25519_sign(seed, msg) == sig and OSSL.ed25519_verify(pk, sig, msg)
+    assert sorted(k["entropy_k"] for k in g["keys"] if k["entropy_k"] is not None) == [1, 2]
+    assert {c["cls"] for c in ref_ed25519_cases} == set(REF_ED_EXPECT)
+    for c in ref_ed25519_cases:
+        pk, sig, msg = c["pk"], c["sig"], c["msg"]
+        got_c = tuple(oracle.oracle_ed25519_verify(pk, sig, len(sig), msg, len(msg), m) for m in (0, 1))
+        got_py = (ED.is_valid(pk, sig, msg), ED.do_verify(pk, sig, msg))
+        assert got_c == got_py, (c["cls"], got_c, got_py)
+        exp = REF_ED_EXPECT[c["cls"]]
+        if exp is not None:
+            assert got_c == exp, (c["cls"], got_c)
+            if len(sig) == 64 and msg:
+                assert OSSL.ed25519_verify(pk, sig, msg) == (exp[0] == 0), c["cls"]
+    # the E5 rows accept (i2p has no S < L check) and the mixed-order rows split on [h]T = O
+    assert all(c_ok == 0 for c_ok in (ED.is_valid(c["pk"], c["sig"], c["msg"]) for c in ref_ed25519_cases
+                                      if c["cls"] == "ref_S_plus_L"))
+    mixed = [ED.is_valid(c["pk"], c["sig"], c["msg"]) for c in ref_ed25519_cases
+             if c["cls"] == "ref_entropy_mixed_order"]
+    assert 0 in mixed and 1 in mixed
+    assert base64.b64encode(bytes.fromhex(g["sigs"][0]["sig"])).startswith(b"cRgJlF8c")
