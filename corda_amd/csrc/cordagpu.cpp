@@ -1129,7 +1129,7 @@ bool ed_overlap_enabled() {
 
 
 cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = true, uint32_t scratch_off = 0,
-                        hipStream_t pts_stream = nullptr, uint32_t scratch_lanes = 0) {
+                        hipStream_t pts_stream = nullptr, uint32_t scratch_lanes = 0, bool allow_lanes = true) {
   const size_t n = b->n;
   bool joins[2] = {false, false};
   cg_status st = CG_OK;
@@ -1283,7 +1283,7 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = 
           d.ktab = ctx->ed_ktab;
           d.kstat = ctx->ed_kstat;
         }
-        const bool pair = !b->ed_key_index && !fuse && cnt <= pair_max;  // latency mode
+        const bool pair = allow_lanes && !b->ed_key_index && !fuse && cnt <= pair_max;  // latency mode
         // (quad_ok / oct_ok: one piece with 2 / 4 cnt scratch slots in its region)
         const uint32_t lanes = !pair ? 1u : oct_ok && split == 1 ? 8u : quad_ok && split == 1 ? 4u : 2u;
         if (pair)
@@ -1681,6 +1681,12 @@ cg_status verify_pipeline(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
     }
     for (int c = 0; c < 3; ++c) max_cnt[c] = std::max(max_cnt[c], cnt[c]);
   }
+  // Latency lanes for pipeline chunks (CORDA_AMD_VERIFY_LANES=0/1 forces): a chunk's
+  // two / four / eight lanes per signature cost 1.4-1.7x the MSM instructions; they pay
+  // only when the call is bound by its copies (the extra work hides under the next
+  // chunk's upload and the last chunk's chain after the last byte is shorter).
+  bool lanes = true;
+  if (const char* e = std::getenv("CORDA_AMD_VERIFY_LANES")) lanes = std::atoi(e) != 0;
   // two chunks in flight need two disjoint scratch halves; chunks too large for that
   // (> kEdChunk Ed25519 lanes each) run one after the other on ctx->stream
   const bool dual = K > 1 && max_cnt[0] <= kEdChunk && !(std::getenv("CORDA_AMD_VERIFY_SERIAL"));
@@ -1759,7 +1765,7 @@ cg_status verify_pipeline(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
     if (dual && b->ed_key_index)
       CG_TRY(ctx, hipStreamWaitEvent(ctx->stream, done[L ^ 1], 0), "verify pipeline wait");
     st = launch_verify(ctx, b, mode, /*join_streams=*/false, dual ? (uint32_t)(L * max_cnt[0]) : 0, pts,
-                       dual ? max_cnt[0] : 0);
+                       dual ? max_cnt[0] : 0, lanes);
     if (st != CG_OK) return st;
     CG_TRY(ctx, hipEventRecord(done[L], ctx->stream), "verify pipeline record");
     if ((st = upload_through(k + 1 + ahead)) != CG_OK) return st;

@@ -215,3 +215,117 @@ class ShardBacklog:
         for pb in self.batches:
             pb.close()
         self.batches = []
+
+
+class ShardFailure(RuntimeError):
+    """No rank could verify some index range (every rank failed, or a rank failed again
+    on the range redistributed to it)."""
+
+
+def redistribute(bounds: list[int], failed: list[int], survivors: list[int]) -> dict[int, list[tuple[int, int]]]:
+    """Each failed rank's index range [b_f, b_f+1) re-split over the surviving ranks with
+    ``shard_bounds`` (32-aligned inside the range, so every piece owns whole bitmap words):
+    {survivor: [(lo, hi), ...]} in failed-rank order."""
+    plan: dict[int, list[tuple[int, int]]] = {s: [] for s in survivors}
+    for f in failed:
+        lo, hi = bounds[f], bounds[f + 1]
+        sub = shard_bounds(hi - lo, len(survivors))
+        for j, s in enumerate(survivors):
+            if sub[j + 1] > sub[j]:
+                plan[s].append((lo + sub[j], lo + sub[j + 1]))
+    return plan
+
+
+def _gather_status(code: int, world: int, device, group=None) -> list[int]:
+    import torch
+    import torch.distributed as dist
+    out = torch.zeros(world, dtype=torch.int32, device=device)
+    dist.all_gather_into_tensor(out, torch.tensor([code], dtype=torch.int32, device=device), group=group)
+    return [int(x) for x in out.cpu()]
+
+
+def verify_sharded_resilient(n: int, verify, group=None, device="cpu", bounds: list[int] | None = None):
+    """Sharded verification that survives a failing rank (SURVEY §5 "per-GPU error →
+    re-run that shard on the remaining GPUs"; the reference's analogue is the verifier
+    redistribution of VerifierTests.kt:74-100).
+
+    ``verify(lo, hi)`` verifies elements [lo, hi) on this rank's device and returns their
+    accept words (``pack_bits``, uint32); it raises ``_lib.CordaGpuError`` when the library
+    returns a status < 0 (device or allocation failure).  Steps:
+
+    1. every rank verifies its shard ``bounds[r]..bounds[r+1]`` (default ``shard_bounds``);
+    2. the ranks exchange one status word each (a world-sized all-gather);
+    3. each failed rank's range is re-split over the survivors (``redistribute``) and
+       verified there — a failed rank takes no further work, but stays in the collectives
+       so no rank blocks, and the caller exits it non-zero (nothing re-execs);
+    4. ONE bitmap all-gather of every rank's pieces (equal padded pieces, as
+       ``gather_ordered``), placed at word lo/32 of the index-ordered global bitmap.
+
+    Without failures this is ``gather_ordered`` plus the status word.  A second failure
+    during redistribution raises ``ShardFailure`` on every rank (they agree through a
+    second status exchange).  Returns (global bitmap as an int32 tensor on ``device``,
+    the failed ranks)."""
+    import torch
+    import torch.distributed as dist
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    bounds = bounds if bounds is not None else shard_bounds(n, world)
+    check_bounds(bounds, world)
+    pieces: list[tuple[int, int, np.ndarray]] = []
+
+    def attempt(lo, hi) -> int:
+        if hi == lo:
+            pieces.append((lo, hi, np.zeros(0, np.uint32)))
+            return 0
+        try:
+            w = np.asarray(verify(lo, hi), dtype=np.uint32)
+        except _lib.CordaGpuError as e:
+            return e.status if e.status != 0 else -1
+        if len(w) != (hi - lo + 31) // 32:
+            raise ValueError(f"verify({lo}, {hi}) returned {len(w)} words")
+        pieces.append((lo, hi, w))
+        return 0
+
+    status = _gather_status(attempt(bounds[rank], bounds[rank + 1]), world, device, group)
+    failed = [r for r in range(world) if status[r] != 0]
+    survivors = [r for r in range(world) if status[r] == 0]
+    plan: dict[int, list[tuple[int, int]]] = {}
+    if failed:
+        if not survivors:
+            raise ShardFailure(f"every rank failed (status {status})")
+        plan = redistribute(bounds, failed, survivors)
+        code = 0
+        for lo, hi in plan.get(rank, []) if rank in survivors else []:
+            code = code or attempt(lo, hi)
+        again = _gather_status(code, world, device, group)
+        if any(again):
+            raise ShardFailure(f"redistributed ranges failed again (status {again})")
+    layout = {r: ([(bounds[r], bounds[r + 1])] if status[r] == 0 else []) + plan.get(r, []) for r in range(world)}
+    nwords = {r: sum((hi - lo + 31) // 32 for lo, hi in layout[r]) for r in range(world)}
+    wmax = max(max(nwords.values()), 1)
+    local = torch.zeros(wmax, dtype=torch.int32, device=device)
+    pos = 0
+    for lo, hi, w in pieces:  # (appended in layout order: the own shard, then the plan's pieces)
+        local[pos:pos + len(w)] = torch.from_numpy(w.view(np.int32).copy()).to(device)
+        pos += len(w)
+    out = torch.empty(world * wmax, dtype=torch.int32, device=device)
+    dist.all_gather_into_tensor(out, local, group=group)
+    ordered = torch.zeros((bounds[-1] + 31) // 32, dtype=torch.int32, device=device)
+    for r in range(world):
+        at = r * wmax
+        for lo, hi in layout[r]:
+            k = (hi - lo + 31) // 32
+            ordered[lo // 32:lo // 32 + k] = out[at:at + k]
+            at += k
+    return ordered, failed
+
+
+def gpu_shard_verifier(ctx: _lib.Context, batch: PackedBatch, mode: int = _lib.MODE_IS_VALID):
+    """``verify(lo, hi)`` for ``verify_sharded_resilient`` on this rank's context: stages
+    elements [lo, hi) of ``batch`` (``slice_batch``) and verifies them through the C ABI."""
+    def verify(lo: int, hi: int) -> np.ndarray:
+        pb = PreparedBatch(ctx, slice_batch(batch, lo, hi))
+        try:
+            return pack_bits(pb.verify(mode) == _lib.ACCEPT)[:(hi - lo + 31) // 32]
+        finally:
+            pb.close()
+    return verify

@@ -169,3 +169,110 @@ def test_gather_ordered_uneven_shards(world, total):
     assert all(p.exitcode == 0 for p in procs)
     res = sorted(q.get(timeout=5) for _ in range(world))
     assert res == [(r, True) for r in range(world)]
+
+
+def _resilient_worker(rank, world, port, n, fail_ranks, fail_again, q):
+    """One rank of verify_sharded_resilient over gloo; verify() is the C oracle on the
+    rank's slice, and ranks in fail_ranks raise the error a failing cg_batch_verify
+    raises (CordaGpuError, status < 0).  fail_again: a survivor that also fails on its
+    redistributed piece.  Exit code 3 for a failed rank (the caller's contract)."""
+    import ctypes
+    import torch.distributed as dist
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tools", "datagen"))
+    from corda_amd import _lib
+    from corda_amd import dist as D
+    from corda_amd.crypto import PackedBatch
+    import datagen
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    code = 0
+    try:
+        w = datagen.add_ed25519_adversarial(datagen.make_batch(n, msg_bytes=40, seed=5, threads=2), 0.2, seed=6)
+        full = PackedBatch(w.n, w.scheme, w.pk, w.pk_stride, w.sig, w.sig_stride, w.sig_len, w.msg, w.msg_off,
+                           w.msg_len)
+        lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "liboracle.so"))
+        vp, sz = ctypes.c_void_p, ctypes.c_size_t
+        lib.oracle_verify_batch.argtypes = [vp, vp, sz, vp, sz, vp, vp, vp, vp, sz, ctypes.c_int, ctypes.c_int, vp]
+        P = lambda a: a.ctypes.data  # noqa: E731
+        calls = []
+
+        def verify(lo, hi):
+            calls.append((lo, hi))
+            if rank in fail_ranks or (rank == fail_again and len(calls) > 1):
+                raise _lib.CordaGpuError(-3, "injected allocation failure (CG_DEBUG_FAIL_ALLOC)")
+            s = D.slice_batch(full, lo, hi)
+            v = np.zeros(max(s.n, 1), np.uint8)
+            lib.oracle_verify_batch(P(s.scheme), P(s.pk), s.pk_stride, P(s.sig), s.sig_stride, P(s.sig_len),
+                                    P(s.msg), P(s.msg_off), P(s.msg_len), s.n, 0, 1, P(v))
+            return D.pack_bits(v[:s.n] == 0)
+
+        try:
+            glob, failed = D.verify_sharded_resilient(n, verify)
+        except D.ShardFailure:
+            q.put((rank, "ShardFailure", calls))
+            return
+        allv = np.zeros(n, np.uint8)
+        lib.oracle_verify_batch(P(full.scheme), P(full.pk), full.pk_stride, P(full.sig), full.sig_stride,
+                                P(full.sig_len), P(full.msg), P(full.msg_off), P(full.msg_len), n, 0, 2, P(allv))
+        ok = bool(np.array_equal(glob.numpy(), D.pack_bits(allv == 0).view(np.int32)))
+        q.put((rank, ok, failed, calls))
+        code = 3 if rank in failed else 0
+    finally:
+        dist.destroy_process_group()
+    if code:
+        os._exit(code)
+
+
+def _run_resilient(world, n, fail_ranks, fail_again=-1):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_resilient_worker, args=(r, world, port, n, fail_ranks, fail_again, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(180)
+    res = sorted((q.get(timeout=5) for _ in range(world)), key=lambda t: t[0])
+    return [p.exitcode for p in procs], res
+
+
+@pytest.mark.parametrize("world,n,fail", [(3, 3000, (1,)), (3, 2017, (2,)), (3, 4096 + 33, (0, 2)), (2, 777, ())])
+def test_shard_failure_redistributes_to_survivors(world, n, fail):
+    """verify_sharded_resilient at world 3 (and 2) over gloo with one or two ranks whose
+    verify fails (the CordaGpuError a cg_batch_verify returning < 0 raises, as
+    CG_DEBUG_FAIL_ALLOC injects on the GPU): each failed range is re-split over the
+    survivors, the gathered bitmap equals the oracle's for the whole batch on EVERY rank,
+    survivors verified their own shard plus their piece of each failed range (32-aligned),
+    and the failed ranks exit non-zero while the survivors exit 0."""
+    if not os.path.exists(os.path.join(ROOT, "oracle", "liboracle.so")):
+        pytest.skip("oracle not built")
+    codes, res = _run_resilient(world, n, set(fail))
+    assert [r[1] for r in res] == [True] * world, res
+    assert all(r[2] == list(fail) for r in res)
+    assert codes == [3 if r in fail else 0 for r in range(world)]
+    from corda_amd import dist as D
+    b = D.shard_bounds(n, world)
+    survivors = [r for r in range(world) if r not in fail]
+    plan = D.redistribute(b, list(fail), survivors)
+    covered = []
+    for r, _, _, calls in res:
+        if r in fail:
+            assert calls == [(b[r], b[r + 1])]
+        else:
+            assert calls == [(b[r], b[r + 1])] + plan[r]
+            covered += calls
+    covered.sort()
+    assert covered[0][0] == 0 and covered[-1][1] == n and all(x[1] == y[0] for x, y in zip(covered, covered[1:]))
+    assert all(lo % 32 == 0 for lo, _ in covered)
+
+
+def test_shard_failure_twice_raises_everywhere():
+    """A survivor that also fails on its redistributed piece: every rank raises
+    ShardFailure (they agree through the second status exchange; none blocks)."""
+    if not os.path.exists(os.path.join(ROOT, "oracle", "liboracle.so")):
+        pytest.skip("oracle not built")
+    codes, res = _run_resilient(3, 3000, {1}, fail_again=2)
+    assert [r[1] for r in res] == ["ShardFailure"] * 3 and codes == [0, 0, 0]

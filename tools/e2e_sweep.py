@@ -34,7 +34,8 @@ SETTINGS = [
                      (8, 0.5, 0.5))
      for extra in ({}, {"CORDA_AMD_VERIFY_RING": "0"})]
 KEYS = ("CORDA_AMD_VERIFY_CHUNKS", "CORDA_AMD_VERIFY_MIN_CHUNK", "CORDA_AMD_VERIFY_HEAD", "CORDA_AMD_VERIFY_TAIL",
-        "CORDA_AMD_VERIFY_SERIAL", "CORDA_AMD_VERIFY_RING", "CORDA_AMD_ED_PAIR_MAX", "CORDA_AMD_ED_QUAD_MAX", "CORDA_AMD_ED_OCT_MAX", "CORDA_AMD_VERIFY_ONE_DMA")
+        "CORDA_AMD_VERIFY_SERIAL", "CORDA_AMD_VERIFY_RING", "CORDA_AMD_ED_PAIR_MAX", "CORDA_AMD_ED_QUAD_MAX", "CORDA_AMD_ED_OCT_MAX", "CORDA_AMD_VERIFY_ONE_DMA",
+        "CORDA_AMD_VERIFY_LANES", "CORDA_AMD_VERIFY_POLICY")
 
 
 def h2d_rates(mb=256):
@@ -64,6 +65,7 @@ def main():
                     help="settings to try instead of the built-in list: ';'-separated, each ','-separated "
                          "VAR=value pairs ('' = library defaults), e.g. 'CORDA_AMD_VERIFY_HEAD=0.25;'")
     ap.add_argument("--pageable-only", action="store_true")
+    ap.add_argument("--msg-bytes", type=int, default=1024, help="message length (32: the production tx-id shape)")
     a = ap.parse_args()
     settings = SETTINGS if a.grid is None else [
         dict(kv.split("=", 1) for kv in g.split(",") if kv) for g in a.grid.split(";")]
@@ -71,7 +73,7 @@ def main():
     from corda_amd import Context, crypto
     from corda_amd._lib import ACCEPT, MODE_IS_VALID
     sizes = [int(x) for x in a.sizes.split(",")]
-    w = datagen.make_batch(max(sizes), msg_bytes=1024, seed=42, key_base=0, ref_seed_stride=4096)
+    w = datagen.make_batch(max(sizes), msg_bytes=a.msg_bytes, seed=42, key_base=0, ref_seed_stride=4096)
     res = {"h2d_GBps": h2d_rates(), "runs": a.runs, "rows": []}
     with Context(0) as ctx:
         for n in sizes:
@@ -95,7 +97,7 @@ def main():
                         crypto.verify_packed(ctx, b, MODE_IS_VALID)
                         ts.append(time.perf_counter() - t0)
                     p50 = statistics.median(ts) * 1e3
-                    row = {"n": n, "pinned": pinned, "setting": st, "p50_ms": round(p50, 3),
+                    row = {"n": n, "msg_bytes": a.msg_bytes, "pinned": pinned, "setting": st, "p50_ms": round(p50, 3),
                            "min_ms": round(min(ts) * 1e3, 3), "bytes": nbytes, "all_accept": ok,
                            "GBps": round(nbytes / (p50 / 1e3) / 1e9, 2)}
                     res["rows"].append(row)
