@@ -153,26 +153,15 @@ CG_HD uint32_t ge_frombytes_strict(ge_p3& h, const uint32_t w[8]) {
   return ge_frombytes_i2p(h, w) && ge_strict_check(h, w);
 }
 
-// Points phase: final pre-verdict and the decoded -A and R (both decodes run
-// together, their square roots interleaved).
+// Points phase: final pre-verdict and the decoded -A and R.
 CG_HD uint32_t ed25519_points_stage(const uint32_t pk[8], const uint32_t r[8], uint32_t pre, ge_p3& negA,
                                     ge_p3& R) {
   ge_p3 P[2];
   uint32_t ok[2];
-// CG_ED_PAIR_DECODE = 1 interleaves the two square roots (fe_pow22523_pair): more ILP
-// but 256 VGPRs with ~31 spilled; the two decodes one after the other need 234 and
-// spill nothing, and measured as fast or ~1 % faster with the points kernel running
-// beside the hash kernel (r03f A/B: 97.8 / 96.1 vs 96.8 / 95.2 M verifies/s).
-#ifndef CG_ED_PAIR_DECODE
-#define CG_ED_PAIR_DECODE 0
-#endif
-#if CG_ED_PAIR_DECODE
-  const uint32_t* const w[2] = {pk, r};
-  ge_frombytes_i2p_pair(P, w, ok);
-#else
+  // the two decodes one after the other: 234 VGPRs, no spill (interleaving their square
+  // roots needed 256 with ~31 spilled and measured equal or ~1 % slower, r03f / r04o)
   ok[0] = ge_frombytes_i2p(P[0], pk);
   ok[1] = ge_frombytes_i2p(P[1], r);
-#endif
   if (!ok[0]) return V_KEY_INVALID;
   if (pre != V_COMPUTE) return pre;
   if (!ok[1] || !ge_strict_check(P[1], r)) return V_REJECT;

@@ -654,42 +654,6 @@ CG_HD void fe_pow22523(fe& out, const fe& z) {
   fe_mul_f(out, t, z);    // z^(2^252 - 3)
 }
 
-// The same chains on two independent inputs in lockstep (the key and R decodes
-// of the points kernel): every step is an fe_pair, so the dependent squarings of
-// one chain interleave with the other's.
-CG_HD void fe_sqn_pair(fe& h0, const fe& f0, fe& h1, const fe& f1, int n) {
-  fe_pair(h0, FeSqF{f0}, h1, FeSqF{f1});
-  CG_NOUNROLL for (int i = 1; i < n; ++i) fe_pair(h0, FeSqF{h0}, h1, FeSqF{h1});
-}
-CG_HD void fe_mul_pair(fe& h0, const fe& f0, const fe& g0, fe& h1, const fe& f1, const fe& g1) {
-  fe_pair(h0, FeMulF{f0, g0}, h1, FeMulF{f1, g1});
-}
-CG_HD void fe_pow22523_pair(fe& out0, const fe& z0, fe& out1, const fe& z1) {
-  fe z2[2], z9[2], z11[2], t[2], a[2], b[2];
-  fe_sqn_pair(z2[0], z0, z2[1], z1, 1);
-  fe_sqn_pair(t[0], z2[0], t[1], z2[1], 2);
-  fe_mul_pair(z9[0], t[0], z0, z9[1], t[1], z1);
-  fe_mul_pair(z11[0], z9[0], z2[0], z11[1], z9[1], z2[1]);
-  fe_sqn_pair(t[0], z11[0], t[1], z11[1], 1);
-  fe_mul_pair(a[0], t[0], z9[0], a[1], t[1], z9[1]);      // 2^5 - 1
-  fe_sqn_pair(t[0], a[0], t[1], a[1], 5);
-  fe_mul_pair(a[0], t[0], a[0], a[1], t[1], a[1]);        // 2^10 - 1
-  fe_sqn_pair(t[0], a[0], t[1], a[1], 10);
-  fe_mul_pair(b[0], t[0], a[0], b[1], t[1], a[1]);        // 2^20 - 1
-  fe_sqn_pair(t[0], b[0], t[1], b[1], 20);
-  fe_mul_pair(t[0], t[0], b[0], t[1], t[1], b[1]);        // 2^40 - 1
-  fe_sqn_pair(t[0], t[0], t[1], t[1], 10);
-  fe_mul_pair(a[0], t[0], a[0], a[1], t[1], a[1]);        // 2^50 - 1
-  fe_sqn_pair(t[0], a[0], t[1], a[1], 50);
-  fe_mul_pair(b[0], t[0], a[0], b[1], t[1], a[1]);        // 2^100 - 1
-  fe_sqn_pair(t[0], b[0], t[1], b[1], 100);
-  fe_mul_pair(t[0], t[0], b[0], t[1], t[1], b[1]);        // 2^200 - 1
-  fe_sqn_pair(t[0], t[0], t[1], t[1], 50);
-  fe_mul_pair(t[0], t[0], a[0], t[1], t[1], a[1]);        // 2^250 - 1
-  fe_sqn_pair(t[0], t[0], t[1], t[1], 2);
-  fe_mul_pair(out0, t[0], z0, out1, t[1], z1);            // z^(2^252 - 3)
-}
-
 // Constants (limbs of the canonical values).
 #define CG_FE_D {{56195235, 13857412, 51736253, 6949390, 114729, 24766616, 60832955, 30306712, 48412415, 21499315}}
 #define CG_FE_D2 {{45281625, 27714825, 36363642, 13898781, 229458, 15978800, 54557047, 27058993, 29715967, 9444199}}

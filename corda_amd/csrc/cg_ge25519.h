@@ -206,46 +206,4 @@ CG_HD uint32_t ge_frombytes_i2p(ge_p3& h, const uint32_t w[8]) {
   return ok;
 }
 
-// ge_frombytes_i2p on two encodings at once (ok[i] as its return value), with
-// the two square-root exponentiations interleaved; branch-free.
-CG_HD void ge_frombytes_i2p_pair(ge_p3 h[2], const uint32_t* const w[2], uint32_t ok[2]) {
-  const fe d = CG_FE_D, sqrtm1 = CG_FE_SQRTM1;
-  fe u[2], v[2], v3[2], x[2], vxx[2], one;
-  fe_1(one);
-  CG_UNROLL for (int i = 0; i < 2; ++i) {
-    fe_frombytes(h[i].Y, w[i]);  // floor-shaped limbs (see ge_frombytes_i2p)
-    fe_1(h[i].Z);
-  }
-  fe_sqn_pair(u[0], h[0].Y, u[1], h[1].Y, 1);
-  fe_mul_pair(v[0], u[0], d, v[1], u[1], d);
-  CG_UNROLL for (int i = 0; i < 2; ++i) {
-    fe_sub(u[i], u[i], one);  // y^2 - 1
-    fe_add(v[i], v[i], one);  // d y^2 + 1
-  }
-  fe_sqn_pair(v3[0], v[0], v3[1], v[1], 1);
-  fe_mul_pair(v3[0], v3[0], v[0], v3[1], v3[1], v[1]);  // v^3
-  fe_sqn_pair(x[0], v3[0], x[1], v3[1], 1);
-  fe_mul_pair(x[0], x[0], v[0], x[1], x[1], v[1]);
-  fe_mul_pair(x[0], x[0], u[0], x[1], x[1], u[1]);      // u v^7
-  fe_pow22523_pair(x[0], x[0], x[1], x[1]);
-  fe_mul_pair(x[0], x[0], v3[0], x[1], x[1], v3[1]);
-  fe_mul_pair(x[0], x[0], u[0], x[1], x[1], u[1]);      // u v^3 (u v^7)^((p-5)/8)
-  fe_sqn_pair(vxx[0], x[0], vxx[1], x[1], 1);
-  fe_mul_pair(vxx[0], vxx[0], v[0], vxx[1], vxx[1], v[1]);
-  fe xi[2];
-  fe_mul_pair(xi[0], x[0], sqrtm1, xi[1], x[1], sqrtm1);
-  CG_UNROLL for (int i = 0; i < 2; ++i) {
-    fe check;
-    fe_sub(check, vxx[i], u[i]);
-    const uint32_t direct = fe_iszero(check);
-    fe_add(check, vxx[i], u[i]);
-    ok[i] = direct | fe_iszero(check);
-    fe_select(h[i].X, xi[i], x[i], direct);
-    fe negx;
-    fe_neg_p(negx, h[i].X);
-    fe_select(h[i].X, h[i].X, negx, fe_isnegative(h[i].X) ^ (w[i][7] >> 31));
-  }
-  fe_mul_pair(h[0].T, h[0].X, h[0].Y, h[1].T, h[1].X, h[1].Y);
-}
-
 }  // namespace cg

@@ -18,16 +18,11 @@
 //   msg_off[i] (u64, into the arena), msg_len[i]; scratch (`scap` = chunk):
 //   status[i] (verdict | digit count << 8 | R sign << 16), digits[w*scap+i]
 //   (24 words), and the per-signature tables entries 0..7 = k*(-A), 8..15 = k*R for
-//   k = 1..8 (cached points packed to 32 words = one 128-byte line, CG_ED_TAB_PACK)
+//   k = 1..8 (cached points packed to 32 words = one 128-byte line)
 //   lane-contiguous: table[(i*17 + e)*32 + w] (one pad entry: CG_ED_TAB_PAD), 2,176 B per
-//   lane; a zero digit reads one
-//   shared identity entry (CG_ED_TAB_NO0; with CG_ED_TAB_NO0=0 entries k = 0..8, 18
-//   per lane, as in round 2; CG_ED_TAB_PACK=0: 40 limbs, ten int4 quads per entry).
-//   CG_ED_TAB_SOA=1 lays them quad-major across lanes instead (int4
-//   table[(e*10 + q)*scap + i]: each of a wave's loads one contiguous 1 KB run, no
-//   over-fetch) — measured slower (r03c, one box: msm 7.11 -> 8.35 ms, points 2.47 ->
-//   3.9 ms per 1 M; an entry's ten quads sit scap * 16 B = 16 MB apart, ten pages per
-//   entry instead of one), so the lane-contiguous layout stays.
+//   lane; a zero digit reads one shared identity entry.  (Round 3 measured a
+//   quad-major layout across lanes — each wave load one contiguous 1 KB run — slower:
+//   msm 7.11 -> 8.35 ms, points 2.47 -> 3.9 ms per 1 M, an entry's quads 16 MB apart.)
 #include "cg_ed25519.h"
 #include "cg_kernels.h"
 
@@ -47,19 +42,13 @@ namespace {
 #define CG_MSM_R_WAVES 2
 #endif
 
-// CG_ED_TAB_PACK = 1: a table entry is its four coordinates as canonical 255-bit values
-// (8 words each): 128 B = one cache line per entry instead of 160 B over two or three;
-// the points kernel canonicalises on store, the MSM unpacks (floor-shaped limbs).
-#ifndef CG_ED_TAB_PACK
-#define CG_ED_TAB_PACK 1
-#endif
-constexpr int kTabLimbs = CG_ED_TAB_PACK ? 32 : 40;  // words per cached point: 4 fe x 8 packed / 10 limbs
-// CG_ED_TAB_NO0 = 1: the lane tables keep k = 1..8 only (16 entries, 2 KB per lane
-// packed); a zero digit reads one shared identity entry (L1 / L2 resident) instead.
-#ifndef CG_ED_TAB_NO0
-#define CG_ED_TAB_NO0 1
-#endif
-constexpr int kSlotsPerPoint = CG_ED_TAB_NO0 ? kATabEntries - 1 : kATabEntries;
+// A table entry is its four coordinates as canonical 255-bit values (8 words each):
+// 128 B = one cache line per entry (round 3: against 160 B of limbs over two or three
+// lines, MSM -2 %); the points kernel canonicalises on store, the MSM unpacks
+// (floor-shaped limbs).  The lane tables keep k = 1..8 only (16 entries, 2 KB per lane);
+// a zero digit reads one shared identity entry (L1 / L2 resident) instead (+1 %).
+constexpr int kTabLimbs = 32;  // words per cached point: 4 fe x 8 packed
+constexpr int kSlotsPerPoint = kATabEntries - 1;
 // CG_ED_TAB_PAD: unused entries after a lane's table, so the lane stride is not a
 // power of two: at 16 entries = 2 KB every lane of a wave writes into the same L2
 // channel and set, lines leave L2 before their eight 16-byte stores have merged and
@@ -71,24 +60,16 @@ constexpr int kSlotsPerPoint = CG_ED_TAB_NO0 ? kATabEntries - 1 : kATabEntries;
 constexpr int kLaneEntries = 2 * kSlotsPerPoint + CG_ED_TAB_PAD;
 constexpr int kBStride = 32;   // shared-table entry (precomputed point, 3 fe x 10 limbs) padded to one 128-byte line
 
-#ifndef CG_ED_TAB_SOA
-#define CG_ED_TAB_SOA 0
-#endif
-// A lane's view of the per-signature tables: entry k's quad q sits at
-// base[k * kstride + q * qstride].
+// A lane's view of the per-signature tables (lane-contiguous: a lane's entries are
+// consecutive lines; round 3 measured the quad-major alternative 17 % slower): entry
+// k's quad q sits at base[k * kTabLimbs / 4 + q].
 struct LaneTab {
   int4* base;
-  size_t kstride, qstride;
-  CG_DEV int4* entry(uint32_t k) const { return base + (size_t)k * kstride; }
+  CG_DEV int4* entry(uint32_t k) const { return base + (size_t)k * (kTabLimbs / 4); }
 };
-static_assert(!(CG_ED_TAB_NO0 && CG_ED_TAB_SOA), "CG_ED_TAB_NO0 needs the lane-contiguous layout");
 CG_DEV LaneTab lane_table(int32_t* table, uint32_t i, uint32_t scap) {
-#if CG_ED_TAB_SOA
-  return {reinterpret_cast<int4*>(table) + i, (size_t)(kTabLimbs / 4) * scap, scap};
-#else
   (void)scap;
-  return {reinterpret_cast<int4*>(table + (size_t)i * (kLaneEntries * kTabLimbs)), kTabLimbs / 4, 1};
-#endif
+  return {reinterpret_cast<int4*>(table + (size_t)i * (kLaneEntries * kTabLimbs))};
 }
 
 // Occupancy target of the hash kernel (0: the compiler's choice, 3 waves / SIMD at 138
@@ -133,18 +114,11 @@ __global__ __launch_bounds__(256) CG_HASH_ATTR void cg_ed25519_hash(const uint32
   CG_UNROLL for (int w = 0; w < kDigitWords; ++w) digits[(size_t)w * scap + i] = dig[w];
 }
 
-// The shared identity entry (1, 1, 1, 0) in the table's entry format (CG_ED_TAB_NO0).
-#if CG_ED_TAB_NO0 && CG_ED_TAB_PACK
+// The shared identity entry (1, 1, 1, 0) in the table's entry format.
 __device__ __attribute__((aligned(128))) const int4 g_ident_entry[kTabLimbs / 4] = {
     {1, 0, 0, 0}, {0, 0, 0, 0}, {1, 0, 0, 0}, {0, 0, 0, 0}, {1, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
-#elif CG_ED_TAB_NO0
-__device__ __attribute__((aligned(128))) const int4 g_ident_entry[kTabLimbs / 4] = {
-    {1, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 1, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {1, 0, 0, 0}, {0, 0, 0, 0},
-    {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
-#endif
 
-CG_DEV void store_cached(int4* dst, size_t qs, const ge_cached& c) {
-#if CG_ED_TAB_PACK
+CG_DEV void store_cached(int4* dst, const ge_cached& c) {
   uint32_t w[4][8];
   fe_tobytes(w[0], c.YplusX);
   fe_tobytes(w[1], c.YminusX);
@@ -152,80 +126,15 @@ CG_DEV void store_cached(int4* dst, size_t qs, const ge_cached& c) {
   fe_tobytes(w[3], c.T2d);
   CG_UNROLL for (int f = 0; f < 4; ++f)
     CG_UNROLL for (int h = 0; h < 2; ++h)
-      dst[(2 * f + h) * qs] = make_int4((int)w[f][4 * h], (int)w[f][4 * h + 1], (int)w[f][4 * h + 2], (int)w[f][4 * h + 3]);
-#else
-  int32_t v[kTabLimbs];
-  CG_UNROLL for (int l = 0; l < 10; ++l) {
-    v[l] = c.YplusX.v[l];
-    v[10 + l] = c.YminusX.v[l];
-    v[20 + l] = c.Z.v[l];
-    v[30 + l] = c.T2d.v[l];
-  }
-  CG_UNROLL for (int q = 0; q < kTabLimbs / 4; ++q)
-    dst[q * qs] = make_int4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
-#endif
-}
-
-CG_DEV void load_cached(const int4* src, size_t qs, ge_cached& c) {
-#if CG_ED_TAB_PACK
-  uint32_t w[4][8];
-  CG_UNROLL for (int f = 0; f < 4; ++f)
-    CG_UNROLL for (int h = 0; h < 2; ++h) {
-      const int4 x = src[(2 * f + h) * qs];
-      w[f][4 * h] = (uint32_t)x.x;
-      w[f][4 * h + 1] = (uint32_t)x.y;
-      w[f][4 * h + 2] = (uint32_t)x.z;
-      w[f][4 * h + 3] = (uint32_t)x.w;
-    }
-  fe_frombytes(c.YplusX, w[0]);
-  fe_frombytes(c.YminusX, w[1]);
-  fe_frombytes(c.Z, w[2]);
-  fe_frombytes(c.T2d, w[3]);
-#else
-  int32_t v[kTabLimbs];
-  CG_UNROLL for (int q = 0; q < kTabLimbs / 4; ++q) {
-    const int4 x = src[q * qs];
-    v[4 * q] = x.x;
-    v[4 * q + 1] = x.y;
-    v[4 * q + 2] = x.z;
-    v[4 * q + 3] = x.w;
-  }
-  CG_UNROLL for (int l = 0; l < 10; ++l) {
-    c.YplusX.v[l] = v[l];
-    c.YminusX.v[l] = v[10 + l];
-    c.Z.v[l] = v[20 + l];
-    c.T2d.v[l] = v[30 + l];
-  }
-#endif
-}
-
-// Entry k (0..8) of point p (0: -A, 1: R; a per-signature table holding R only uses
-// p = 0) of a lane's table: stored k for the full tables, k - 1 with CG_ED_TAB_NO0 (and
-// k = 0 reads the shared identity entry).
-CG_DEV void store_slot(const LaneTab& lt, int p, int k, const ge_cached& c) {
-  if (CG_ED_TAB_NO0 && k == 0) return;
-  store_cached(lt.entry(p * kSlotsPerPoint + k - CG_ED_TAB_NO0), lt.qstride, c);
-}
-CG_DEV void load_slot(const LaneTab& lt, int p, uint32_t k, ge_cached& c) {
-#if CG_ED_TAB_NO0
-  const int4* src = k ? lt.entry(p * kSlotsPerPoint + k - 1) : g_ident_entry;
-  load_cached(src, 1, c);
-#else
-  load_cached(lt.entry(p * kSlotsPerPoint + k), lt.qstride, c);
-#endif
+      dst[2 * f + h] = make_int4((int)w[f][4 * h], (int)w[f][4 * h + 1], (int)w[f][4 * h + 2], (int)w[f][4 * h + 3]);
 }
 
 // A table entry in its storage form (the MSM fetches the A entry of a window before
 // the window's doublings and unpacks it after them: 32 packed words live across the
 // doublings instead of 40 limbs).
-#if CG_ED_TAB_PACK && CG_ED_TAB_NO0
 struct RawEntry {
   int4 q[kTabLimbs / 4];
 };
-CG_DEV void fetch_slot(const LaneTab& lt, int p, uint32_t k, RawEntry& r) {
-  const int4* src = k ? lt.entry(p * kSlotsPerPoint + k - 1) : g_ident_entry;
-  CG_UNROLL for (int q = 0; q < kTabLimbs / 4; ++q) r.q[q] = src[q];
-}
 CG_DEV void unpack_entry(const RawEntry& r, ge_cached& c) {
   uint32_t w[4][8];
   CG_UNROLL for (int f = 0; f < 4; ++f)
@@ -241,11 +150,25 @@ CG_DEV void unpack_entry(const RawEntry& r, ge_cached& c) {
   fe_frombytes(c.Z, w[2]);
   fe_frombytes(c.T2d, w[3]);
 }
-#else
-using RawEntry = ge_cached;
-CG_DEV void fetch_slot(const LaneTab& lt, int p, uint32_t k, RawEntry& r) { load_slot(lt, p, k, r); }
-CG_DEV void unpack_entry(const RawEntry& r, ge_cached& c) { c = r; }
-#endif
+
+// Entry k (0..8) of point p (0: -A, 1: R; a per-signature table holding R only uses
+// p = 0) of a lane's table: stored at k - 1 (k = 0 reads the shared identity entry).
+CG_DEV void store_slot(const LaneTab& lt, int p, int k, const ge_cached& c) {
+  if (k == 0) return;
+  store_cached(lt.entry(p * kSlotsPerPoint + k - 1), c);
+}
+CG_DEV void fetch_slot(const LaneTab& lt, int p, uint32_t k, RawEntry& r) {
+  const int4* src = k ? lt.entry(p * kSlotsPerPoint + k - 1) : g_ident_entry;
+  CG_UNROLL for (int q = 0; q < kTabLimbs / 4; ++q) r.q[q] = src[q];
+}
+CG_DEV void load_entry(const int4* src, ge_cached& c) {
+  RawEntry r;
+  CG_UNROLL for (int q = 0; q < kTabLimbs / 4; ++q) r.q[q] = src[q];
+  unpack_entry(r, c);
+}
+CG_DEV void load_slot(const LaneTab& lt, int p, uint32_t k, ge_cached& c) {
+  load_entry(k ? lt.entry(p * kSlotsPerPoint + k - 1) : g_ident_entry, c);
+}
 
 #ifndef CG_POINTS_WAVES
 #define CG_POINTS_WAVES 2
@@ -292,7 +215,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_POINTS_W
   CG_UNROLL for (int w = 0; w < 8; ++w) pkw[w] = pk[(size_t)w * cap + e];
   int4* kt = key_table(ktab, j);
   kstat[j] = ed25519_key_tables(pkw, [&](int t, int k, const ge_cached& c) CG_LINLINE {
-    store_cached(kt + (t * kATabEntries + k) * (kTabLimbs / 4), 1, c);
+    store_cached(kt + (t * kATabEntries + k) * (kTabLimbs / 4), c);
   });
 }
 
@@ -364,76 +287,23 @@ CG_DEV void load_bentry(const int32_t* btab_g, uint32_t t, uint32_t k, ge_precom
   }
 }
 
-// Staging of the lane-table entries in the MSM loop (ed25519_msm's loadX / unpackX).
-//   registers (default): the A entry's packed words are fetched before a window's
-//     doublings and held across them; the R entry is loaded just before its addition.
-//   CG_MSM_LDS_A = 1: the A entry goes HBM -> LDS by LDS-DMA (global_load_lds_dwordx4,
-//     no VGPR destination) before the doublings and is read back (ds_read_b128) after
-//     them: 32 fewer VGPRs live across the doublings, 32 KB of LDS per 256-lane block.
-//   CG_MSM_LDS_R = 1 (with LDS_A): the R entry too, fetched at the same time (64 KB
-//     per block: at most 2 blocks per CU).
-// LDS image per wave and entry: [quad][lane] int4 — one DMA instruction writes 64
-// lanes x 16 B contiguously, so quad q of lane l sits at base + (q * 64 + l) * 16.
-#ifndef CG_MSM_LDS_A
-#define CG_MSM_LDS_A 0
-#endif
-#ifndef CG_MSM_LDS_R
-#define CG_MSM_LDS_R 0
-#endif
-static_assert(!CG_MSM_LDS_A || (CG_ED_TAB_PACK && CG_ED_TAB_NO0), "LDS staging needs the packed, identity-free tables");
-static_assert(!CG_MSM_LDS_R || CG_MSM_LDS_A, "CG_MSM_LDS_R needs CG_MSM_LDS_A");
-struct LdsSlot {};
+// Staging of the lane-table entries in the MSM loop (ed25519_msm's loadX / unpackX): the
+// A entry's packed words are fetched before a window's doublings and held across them;
+// the R entry is loaded just before its addition.  (Round 4 also staged them through
+// LDS by LDS-DMA — 3 waves / SIMD without spills — and measured no gain; removed.)
 struct LateSlot {
   uint32_t k;
 };
-#if CG_MSM_LDS_A
-constexpr int kMsmWavesPerBlock = 4;
-constexpr int kLdsEntries = CG_MSM_LDS_A + CG_MSM_LDS_R;
-// wbase: the wave's LDS image of one entry (a pointer into a __shared__ array)
-CG_DEV void lds_fetch(int4* wbase, const LaneTab& lt, int p, uint32_t k) {
-  const int4* src = k ? lt.entry(p * kSlotsPerPoint + k - 1) : g_ident_entry;
-#if defined(__HIP_DEVICE_COMPILE__)
-  CG_UNROLL for (int q = 0; q < kTabLimbs / 4; ++q)
-    __builtin_amdgcn_global_load_lds((const void*)(src + q),
-                                     (__attribute__((address_space(3))) void*)(wbase + q * 64), 16, 0, 0);
-#else
-  (void)wbase, (void)src;
-#endif
-}
-CG_DEV void lds_unpack(const int4* wbase, uint32_t lane, ge_cached& c) {
-  RawEntry r;
-  CG_UNROLL for (int q = 0; q < kTabLimbs / 4; ++q) r.q[q] = wbase[q * 64 + lane];
-  unpack_entry(r, c);
-}
-#endif
 
 CG_DEV uint32_t msm_lane(uint32_t ndig, const uint32_t* dig, uint32_t scap, uint32_t rneg, const LaneTab& lt,
                          const int32_t* btab_g) {
   auto getDig = [&](int w) CG_LINLINE { return dig[(size_t)w * scap]; };
   auto getB = [&](uint32_t t, uint32_t k, ge_precomp& p) CG_LINLINE { load_bentry(btab_g, t, k, p); };
-#if CG_MSM_LDS_A
-  __shared__ int4 s_ent[kMsmWavesPerBlock * kLdsEntries * (kTabLimbs / 4) * 64];
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  int4* wa = s_ent + (size_t)wave * kLdsEntries * (kTabLimbs / 4) * 64;
-  auto loadA = [&](uint32_t k, LdsSlot&) CG_LINLINE { lds_fetch(wa, lt, 0, k); };
-  auto unpackA = [&](LdsSlot&, ge_cached& c) CG_LINLINE { lds_unpack(wa, lane, c); };
-#if CG_MSM_LDS_R
-  int4* wr = wa + (kTabLimbs / 4) * 64;
-  auto loadR = [&](uint32_t k, LdsSlot&) CG_LINLINE { lds_fetch(wr, lt, 1, k); };
-  auto unpackR = [&](LdsSlot&, ge_cached& c) CG_LINLINE { lds_unpack(wr, lane, c); };
-  return ed25519_msm<LdsSlot, LdsSlot>(ndig, getDig, rneg, loadA, unpackA, loadR, unpackR, getB);
-#else
-  auto loadR = [&](uint32_t k, LateSlot& r) CG_LINLINE { r.k = k; };
-  auto unpackR = [&](LateSlot& r, ge_cached& c) CG_LINLINE { load_slot(lt, 1, r.k, c); };
-  return ed25519_msm<LdsSlot, LateSlot>(ndig, getDig, rneg, loadA, unpackA, loadR, unpackR, getB);
-#endif
-#else
   auto loadA = [&](uint32_t k, RawEntry& r) CG_LINLINE { fetch_slot(lt, 0, k, r); };
   auto unpackA = [&](const RawEntry& r, ge_cached& c) CG_LINLINE { unpack_entry(r, c); };
   auto loadR = [&](uint32_t k, LateSlot& r) CG_LINLINE { r.k = k; };
   auto unpackR = [&](LateSlot& r, ge_cached& c) CG_LINLINE { load_slot(lt, 1, r.k, c); };
   return ed25519_msm<RawEntry, LateSlot>(ndig, getDig, rneg, loadA, unpackA, loadR, unpackR, getB);
-#endif
 }
 
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_MSM_WAVES, CG_MSM_WAVES))) void cg_ed25519_msm(
@@ -647,7 +517,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_MSM_R_WA
   const uint32_t ok = ed25519_msm_reuse(
       c3w, win17, dig, ed_status_rneg(st),
       [&](uint32_t t, uint32_t k, ge_cached& c) CG_LINLINE {
-        load_cached(kt + (t * kATabEntries + k) * (kTabLimbs / 4), 1, c);
+        load_entry(kt + (t * kATabEntries + k) * (kTabLimbs / 4), c);
       },
       [&](uint32_t k, ge_cached& c) CG_LINLINE { load_slot(lt, 0, k, c); },
       [&](uint32_t t, uint32_t k, ge_precomp& p) CG_LINLINE { load_bentry(btab_g, t, k, p); });
@@ -660,7 +530,7 @@ namespace cg {
 
 size_t ed25519_table_bytes(uint32_t scap) { return (size_t)kLaneEntries * kTabLimbs * scap * sizeof(int32_t); }
 size_t ed25519_table_offset(uint32_t lanes) {  // int32 offset of lane `lanes` (the base of a sub-range's view)
-  return CG_ED_TAB_SOA ? (size_t)lanes * 4 : (size_t)kLaneEntries * kTabLimbs * lanes;
+  return (size_t)kLaneEntries * kTabLimbs * lanes;
 }
 size_t ed25519_digit_words() { return kDigitWords; }
 size_t ed25519_btab_words() { return (size_t)kBTables * kBTabEntries * kBStride; }
