@@ -105,6 +105,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--key-reuse", type=int, default=0,
                    help="ed25519/backlog/tx: draw signer keys from this many distinct keys (0 = all distinct)")
+    p.add_argument("--no-extra", action="store_true",
+                   help="ed25519 (N=1): skip the 32 B tx-id end-to-end record and the config-3 sub-record")
     p.add_argument("--dry-run", action="store_true",
                    help="launcher / barrier / all-gather logic over gloo on CPU, synthetic step (tests)")
     a = p.parse_args()
@@ -663,6 +665,70 @@ def run_ed25519(args, dist):
     return line
 
 
+def e2e_record_32b(args, dist, sizes=(4096, 65536, 262144)):
+    """End to end at the production message shape: 32-byte tx ids (WireTransaction.id,
+    WireTransaction.kt:39, signed over by TransactionWithSignatures.kt:58-62), host
+    buffers in the Ed25519-only caller layout (32-byte keys, 64-byte R||S rows, sig_len
+    only for ragged rows), pageable; p50 of --latency-runs calls and one profiled call's
+    spans per size; verdicts checked against the same batch staged in HBM."""
+    import datagen
+    from corda_amd import Context, crypto
+    from corda_amd._lib import MODE_IS_VALID
+    n = max(sizes)
+    w = datagen.make_batch(n, msg_bytes=32, seed=4242, key_base=1 << 36, threads=cpu_threads(), ref_seed_stride=4096)
+    if args.adversarial > 0:
+        w = datagen.add_ed25519_adversarial(w, frac=args.adversarial, seed=77)
+    tl_path = timeline_path(dist.rank)
+    out = {"msg_bytes": 32, "runs": args.latency_runs, "by_batch": {}, "spans": {},
+           "layout": "Ed25519-only host rows: pk_stride 32, sig_stride 64 (68 + sig_len for ragged E12 rows), "
+                     "scheme_id NULL; pageable numpy buffers; 1 % adversarial (E1-E12)"}
+    with Context(dist.local_rank) as ctx:
+        pb = crypto.PreparedBatch(ctx, crypto.PackedBatch(w.n, w.scheme, w.pk, w.pk_stride, w.sig, w.sig_stride,
+                                                          w.sig_len, w.msg, w.msg_off, w.msg_len))
+        ref = pb.verify(MODE_IS_VALID)
+        for m in sizes:
+            sub = w.subset(np.arange(m))
+            sl = sub.sig_len[:m].astype(np.uint32)
+            ragged = bool((sl != 64).any())
+            ss = max(64, (int(sl.max()) + 3) // 4 * 4) if ragged else 64
+            sg = np.zeros((m, ss), dtype=np.uint8)
+            sg[:, :min(ss, sub.sig_stride)] = sub.sig[:m, :min(ss, sub.sig_stride)]
+            sb = crypto.PackedBatch(m, None, np.ascontiguousarray(sub.pk[:, :32]), 32, sg, ss,
+                                    np.ascontiguousarray(sl) if ragged else None, sub.msg, sub.msg_off, sub.msg_len)
+            nbytes = sum(x.nbytes for x in (sb.pk, sb.sig, sb.msg_off, sb.msg_len)) + int(sb.msg_len.sum()) + \
+                (sl.nbytes if ragged else 0)
+            ok = bool(np.array_equal(crypto.verify_packed(ctx, sb, MODE_IS_VALID), ref[:m]))
+            ts = []
+            for _ in range(args.latency_runs):
+                t1 = time.perf_counter(); crypto.verify_packed(ctx, sb, MODE_IS_VALID); ts.append(time.perf_counter() - t1)
+            sp = statistics.median(ts)
+            out["by_batch"][m] = {"p50_ms": round(sp * 1e3, 3), "verifies_per_s": round(m / sp, 1), "bytes": nbytes,
+                                  "verdicts_match": ok}
+            sps = e2e_spans(ctx, lambda: crypto.verify_packed(ctx, sb, MODE_IS_VALID), tl_path)
+            out["spans"][m] = {k: v for k, v in (sps or {}).items() if k != "spans"}
+        dev = []
+        for _ in range(max(3, args.latency_runs // 3)):
+            t1 = time.perf_counter(); pb.verify(MODE_IS_VALID, want_verdicts=False); dev.append(time.perf_counter() - t1)
+        out["p50_device_ms"] = {n: round(statistics.median(dev) * 1e3, 3)}
+        pb.close()
+    return out
+
+
+def config3_subrecord(args, dist, per_curve=1 << 19):
+    """BASELINE config 3 at 2^19 signatures per curve (distinct keys, 1 KB messages, 1 %
+    adversarial), timed exactly as --workload ecdsa times it, summarised for the driver's
+    line; the full 2^20-per-curve run is --workload ecdsa."""
+    sub = argparse.Namespace(**vars(args))
+    sub.batch, sub.msg_bytes, sub.pool_set = per_curve, 1024, False
+    sub.steps, sub.warmup, sub.latency_runs, sub.no_cpu_baseline = 5, 2, 3, True
+    line = run_ecdsa(sub, dist)
+    r = line.get("roofline", {})
+    return {"metric": line["metric"], "value": line["value"], "unit": line["unit"], "ms_per_step": line["ms_per_step"],
+            "steps": sub.steps, "warmup": sub.warmup, "config": line["config"],
+            "roofline": {k: r.get(k) for k in ("kernel", "achieved", "peak", "frac", "avg_launch_ms", "units_per_launch")},
+            "kernels": line.get("kernels"), "checks": line.get("checks")}
+
+
 # ------------------------------------------------------------------ config 3
 def run_ecdsa(args, dist):
     import datagen
@@ -1090,6 +1156,12 @@ def main():
     run = run_dry if args.dry_run else {"ed25519": run_ed25519, "ecdsa": run_ecdsa, "tx": run_tx,
                                         "backlog": run_backlog, "ftx": run_ftx}[args.workload]
     line = run(args, dist)
+    if (args.workload == "ed25519" and not args.dry_run and dist.world == 1 and not args.no_extra
+            and not args.key_reuse and not args.batch and not args.msg_bytes):
+        # the driver's N = 1 line also carries the production tx-id shape end to end and a
+        # driver-observed config 3 (each from its own context, after the config-2 timing)
+        line["latency_32b"] = e2e_record_32b(args, dist)
+        line["config3"] = config3_subrecord(args, dist)
     if dist.rank == 0:
         line["kernel_src_hash"] = kernel_src_hash()
         print(json.dumps(line), flush=True)

@@ -35,7 +35,7 @@ SETTINGS = [
      for extra in ({}, {"CORDA_AMD_VERIFY_RING": "0"})]
 KEYS = ("CORDA_AMD_VERIFY_CHUNKS", "CORDA_AMD_VERIFY_MIN_CHUNK", "CORDA_AMD_VERIFY_HEAD", "CORDA_AMD_VERIFY_TAIL",
         "CORDA_AMD_VERIFY_SERIAL", "CORDA_AMD_VERIFY_RING", "CORDA_AMD_ED_PAIR_MAX", "CORDA_AMD_ED_QUAD_MAX", "CORDA_AMD_ED_OCT_MAX", "CORDA_AMD_VERIFY_ONE_DMA",
-        "CORDA_AMD_VERIFY_LANES", "CORDA_AMD_VERIFY_POLICY")
+        "CORDA_AMD_VERIFY_LANES", "CORDA_AMD_VERIFY_POLICY", "CORDA_AMD_COPY_THREADS", "CORDA_AMD_ARENA_BESIDE")
 
 
 def h2d_rates(mb=256):
@@ -66,7 +66,11 @@ def main():
                          "VAR=value pairs ('' = library defaults), e.g. 'CORDA_AMD_VERIFY_HEAD=0.25;'")
     ap.add_argument("--pageable-only", action="store_true")
     ap.add_argument("--msg-bytes", type=int, default=1024, help="message length (32: the production tx-id shape)")
+    ap.add_argument("--spans", action="store_true", help="also one profiled call per row: bench.e2e_spans")
     a = ap.parse_args()
+    if a.spans:
+        import tempfile
+        os.environ.setdefault("CORDA_AMD_TIMELINE", os.path.join(tempfile.gettempdir(), f"e2e_sweep_{os.getpid()}.txt"))
     settings = SETTINGS if a.grid is None else [
         dict(kv.split("=", 1) for kv in g.split(",") if kv) for g in a.grid.split(";")]
     import datagen
@@ -100,6 +104,13 @@ def main():
                     row = {"n": n, "msg_bytes": a.msg_bytes, "pinned": pinned, "setting": st, "p50_ms": round(p50, 3),
                            "min_ms": round(min(ts) * 1e3, 3), "bytes": nbytes, "all_accept": ok,
                            "GBps": round(nbytes / (p50 / 1e3) / 1e9, 2)}
+                    if a.spans:
+                        import bench
+                        sp = bench.e2e_spans(ctx, lambda: crypto.verify_packed(ctx, b, MODE_IS_VALID),
+                                             os.environ["CORDA_AMD_TIMELINE"])
+                        row["spans"] = {k: v for k, v in (sp or {}).items() if k != "spans"}
+                        row["kernels"] = {k: (v["count"], v["first_start_ms"], v["last_end_ms"], v["sum_ms"])
+                                          for k, v in (sp or {}).get("spans", {}).items()}
                     res["rows"].append(row)
                     print(json.dumps(row), flush=True)
                 if pinned:
