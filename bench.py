@@ -321,6 +321,31 @@ def e2e_spans(ctx, call, path):
     return out
 
 
+def host_share(ctx, call, runs):
+    """The host's share of a host-buffer call, without per-kernel profiling: each call
+    runs with only its "call" span on (cg_set_profiling 2: two HIP events, from the
+    library's entry on idle streams to the verdict download), so wall - GPU span is
+    the host work before the first GPU command and after the last one (staging copies,
+    the final sync's wake-up, frees, the Python wrapper).  Medians over `runs` calls."""
+    walls, gpus = [], []
+    ctx.set_profiling(2)
+    try:
+        for _ in range(runs):
+            ctx.reset_stats()
+            t0 = time.perf_counter()
+            call()
+            walls.append((time.perf_counter() - t0) * 1e3)
+            ms, launches, _ = ctx.kernel_stats("call")
+            if launches == 1:
+                gpus.append(ms)
+    finally:
+        ctx.set_profiling(False)
+    if not gpus:
+        return None
+    return {"wall_ms_p50": round(statistics.median(walls), 3), "gpu_call_ms_p50": round(statistics.median(gpus), 3),
+            "host_ms_p50": round(statistics.median([w - g for w, g in zip(walls, gpus)]), 3), "runs": len(gpus)}
+
+
 def kstats(ctx, names):
     out = {}
     for k in names:
@@ -539,6 +564,7 @@ def run_ed25519(args, dist):
 
     # p50 batch latency: device-only (resident batch) and end-to-end (H2D + kernels + D2H)
     lat_dev, lat_e2e, lat_small, lat_small_off, spans = [], [], {}, {}, {}
+    host_e2e = None
     e2e_bytes, e2e_ok, h2d_peak = 0, None, None
     e2e_n = min(n, 1 << 18)
     if rank == 0:
@@ -562,6 +588,7 @@ def run_ed25519(args, dist):
         for _ in range(args.latency_runs):
             t1 = time.perf_counter(); crypto.verify_packed(ctx, sb, MODE_IS_VALID); lat_e2e.append(time.perf_counter() - t1)
         spans[e2e_n] = e2e_spans(ctx, lambda: crypto.verify_packed(ctx, sb, MODE_IS_VALID), tl_path)
+        host_e2e = host_share(ctx, lambda: crypto.verify_packed(ctx, sb, MODE_IS_VALID), args.latency_runs)
         h2d_peak = pcie_h2d_peak_GBps(dist.local_rank)
         # serving-size batches (a notary's request queue): end-to-end p50 from host buffers,
         # with the latency mode (two lanes per signature for pieces <= CORDA_AMD_ED_PAIR_MAX)
@@ -585,6 +612,8 @@ def run_ed25519(args, dist):
                                 "verdicts_match": bool(np.array_equal(got2, verdict[:bn]))}
                     if env is None:
                         spans[bn] = e2e_spans(ctx, lambda: crypto.verify_packed(ctx, b2, MODE_IS_VALID), tl_path)
+                        dest[bn]["host_share"] = host_share(ctx, lambda: crypto.verify_packed(ctx, b2, MODE_IS_VALID),
+                                                            args.latency_runs)
                 finally:
                     if env is not None:
                         if prev is None:
@@ -649,6 +678,7 @@ def run_ed25519(args, dist):
                                    f"sig_len {'given (ragged E12 rows)' if sb.sig_len is not None else 'NULL'}; "
                                    "pageable numpy buffers") if lat_e2e else None,
                     "e2e_verdicts_match": e2e_ok if lat_e2e else None,
+                    "e2e_host_share": host_e2e,
                     "h2d_peak_GBps": h2d_peak if lat_e2e else None,
                     "e2e_pcie_frac": round(e2e_bytes / statistics.median(lat_e2e) / 1e9 / h2d_peak, 4)
                     if lat_e2e else None,
@@ -706,6 +736,8 @@ def e2e_record_32b(args, dist, sizes=(4096, 65536, 262144)):
                                   "verdicts_match": ok}
             sps = e2e_spans(ctx, lambda: crypto.verify_packed(ctx, sb, MODE_IS_VALID), tl_path)
             out["spans"][m] = {k: v for k, v in (sps or {}).items() if k != "spans"}
+            out["by_batch"][m]["host_share"] = host_share(ctx, lambda: crypto.verify_packed(ctx, sb, MODE_IS_VALID),
+                                                          args.latency_runs)
         dev = []
         for _ in range(max(3, args.latency_runs // 3)):
             t1 = time.perf_counter(); pb.verify(MODE_IS_VALID, want_verdicts=False); dev.append(time.perf_counter() - t1)

@@ -157,8 +157,9 @@ class Context:
         except Exception:
             pass
 
-    def set_profiling(self, on: bool):
-        self.check(self.lib.cg_set_profiling(self.h, 1 if on else 0))
+    def set_profiling(self, on):
+        """False / True, or 2: only each cg_verify_batch's "call" span (its GPU time)."""
+        self.check(self.lib.cg_set_profiling(self.h, 2 if on == 2 else 1 if on else 0))
 
     def kernel_stats(self, name: str):
         ms, launches, items = c_double(), c_uint64(), c_uint64()

@@ -22,6 +22,7 @@
 #include <algorithm>
 #include <array>
 #include <condition_variable>
+#include <functional>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -109,9 +110,30 @@ class CopyPool {
     work(g);  // the caller copies too
     done_.wait(g, [this] { return left_ == 0; });
   }
+  // Runs every function (the caller's thread takes part); returns when all are done.
+  void run_fns(const std::vector<std::function<void()>>& fns) {
+    std::unique_lock<std::mutex> g(m_);
+    tasks_.clear();
+    fns_ = &fns;
+    next_ = 0;
+    left_ = fns.size();
+    ++gen_;
+    cv_.notify_all();
+    work(g);
+    done_.wait(g, [this] { return left_ == 0; });
+    fns_ = nullptr;
+  }
+  size_t workers() const { return th_.size(); }
 
  private:
   void work(std::unique_lock<std::mutex>& g) {
+    while (fns_ && next_ < fns_->size()) {
+      const size_t t = next_++;
+      g.unlock();
+      (*fns_)[t]();
+      g.lock();
+      if (--left_ == 0) done_.notify_all();
+    }
     while (next_ < tasks_.size()) {
       const Piece t = tasks_[next_++];
       g.unlock();
@@ -134,6 +156,7 @@ class CopyPool {
   std::mutex m_;
   std::condition_variable cv_, done_;
   std::vector<Piece> tasks_;
+  const std::vector<std::function<void()>>* fns_ = nullptr;
   size_t next_ = 0, left_ = 0;
   uint64_t gen_ = 0;
   bool stop_ = false;
@@ -190,6 +213,10 @@ struct cg_ctx {
   size_t dl_pin_cap = 0;
   CopyPool* pool = nullptr;
   bool profiling = false;
+  // cg_set_profiling(ctx, 2): only the "call" span of each cg_verify_batch (two events
+  // per call, no per-kernel events, no timeline file): the GPU time of unprofiled-shape
+  // calls, so the host's share of a call's wall time can be measured
+  bool call_spans_only = false;
   // the "call" span of a profiled cg_verify_batch: begin recorded at entry (the
   // streams are idle then, so it marks the host's entry on the GPU clock), end after
   // the verdicts' D2H copy, just before the final sync (end_call_span)
@@ -197,6 +224,10 @@ struct cg_ctx {
   std::map<std::string, Stat> stats;
   std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending;
   std::vector<hipEvent_t> event_pool;
+  // ordering-only events (hipEventDisableTiming) of the host-buffer verify pipeline,
+  // reused across calls: creating and destroying ~10 per call cost host time after the
+  // final sync
+  std::vector<hipEvent_t> sync_event_pool;
   cg::EcdsaConsts* ec = nullptr;
   // device block cache: size -> free block; live block -> size
   std::multimap<size_t, void*> free_blocks;
@@ -227,6 +258,17 @@ cg_status hip_fail(cg_ctx* ctx, hipError_t e, const char* what) {
     hipError_t e_ = (expr);                               \
     if (e_ != hipSuccess) return hip_fail(ctx, e_, what); \
   } while (0)
+
+hipEvent_t take_sync_event(cg_ctx* ctx) {
+  if (!ctx->sync_event_pool.empty()) {
+    hipEvent_t e = ctx->sync_event_pool.back();
+    ctx->sync_event_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+  return e;
+}
 
 hipEvent_t take_event(cg_ctx* ctx) {
   if (!ctx->event_pool.empty()) {
@@ -264,7 +306,7 @@ struct Timed {
 };
 
 void begin_call_span(cg_ctx* ctx) {
-  if (!ctx->profiling || ctx->call_begin) return;
+  if (!(ctx->profiling || ctx->call_spans_only) || ctx->call_begin) return;
   ctx->call_begin = take_event(ctx);
   if (ctx->call_begin) (void)hipEventRecord(ctx->call_begin, ctx->stream);
 }
@@ -284,7 +326,7 @@ void collect_timings(cg_ctx* ctx) {
   // CORDA_AMD_TIMELINE=<file>: every timed span of the call appended as
   // "name items start_ms end_ms" relative to the call's first span (tools/timeline.py)
   static const char* tl_path = std::getenv("CORDA_AMD_TIMELINE");
-  if (tl_path && !ctx->pending.empty()) {
+  if (tl_path && ctx->profiling && !ctx->pending.empty()) {
     if (FILE* f = std::fopen(tl_path, "a")) {
       const hipEvent_t ref = ctx->pending.front().second.first;
       std::fprintf(f, "# call\n");
@@ -479,6 +521,12 @@ struct cg_batch {
   std::vector<uint32_t> idx_kept[4];
   const uint8_t* arena_pending = nullptr;  // host arena still to upload (launch_verify, beside the points kernel)
   size_t arena_pending_bytes = 0;
+  // host msg_off / msg_len still to upload with the arena (an all-Ed25519 in-order batch:
+  // only the hash kernel reads them); ed_msg_off / ed_msg_len then alias msg_off_all /
+  // msg_len_all instead of being gathered copies
+  const uint64_t* meta_pending_off = nullptr;
+  const uint32_t* meta_pending_len = nullptr;
+  bool ed_meta_alias = false;
   uint8_t* ec_rows[2] = {nullptr, nullptr};     // [ec[c].n][ec_sig_stride]
   uint32_t* ec_row_len[2] = {nullptr, nullptr};  // [ec[c].n], or null: every row is ec_sig_stride long
   size_t ec_sig_stride = 0;
@@ -499,8 +547,10 @@ void batch_free(cg_ctx* ctx, cg_batch* b) {
   dfree(ctx, b->ed_pk);
   dfree(ctx, b->ed_sig);
   dfree(ctx, b->ed_sig_len);
-  dfree(ctx, b->ed_msg_off);
-  dfree(ctx, b->ed_msg_len);
+  if (!b->ed_meta_alias) {
+    dfree(ctx, b->ed_msg_off);
+    dfree(ctx, b->ed_msg_len);
+  }
   dfree(ctx, b->ed_key_index);
   dfree(ctx, b->ed_key_first);
   dfree(ctx, b->bad_index);
@@ -551,8 +601,23 @@ cg_status check_inputs(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const ui
   if (!m.dev && (!m.off_host || !m.len_host)) return fail(ctx, CG_E_INVALID_ARGUMENT, "null input pointer");
   if (!m.dev && m.bytes > 0 && !m.host) return fail(ctx, CG_E_INVALID_ARGUMENT, "null message arena");
   bool has_ed = false, has_ec = false;
+  if (!scheme_id) {  // all Ed25519: only the arena bounds, in a branch-free (vectorised) pass
+    if (m.off_host) {
+      const uint64_t* off = m.off_host;
+      const uint32_t* len = m.len_host;
+      const uint64_t bytes = m.bytes;
+      uint32_t bad = 0;
+      for (size_t i = 0; i < n; ++i) bad |= (uint32_t)(off[i] > bytes) | (uint32_t)((uint64_t)len[i] > bytes - off[i]);
+      for (size_t i = 0; bad && i < n; ++i)
+        if (off[i] > bytes || len[i] > bytes - off[i])
+          return fail(ctx, CG_E_INVALID_ARGUMENT, "message out of arena bounds at element " + std::to_string(i));
+    }
+    if (pk_stride < 32 || sig_stride < 64)
+      return fail(ctx, CG_E_INVALID_ARGUMENT, "Ed25519 needs pk_stride >= 32 and sig_stride >= 64");
+    return CG_OK;
+  }
   for (size_t i = 0; i < n; ++i) {
-    const uint8_t s = scheme_id ? scheme_id[i] : CG_SCHEME_EDDSA_ED25519_SHA512;
+    const uint8_t s = scheme_id[i];
     // off > bytes || len > bytes - off: the sum off + len could wrap for a huge off
     if (m.off_host && (m.off_host[i] > m.bytes || m.len_host[i] > m.bytes - m.off_host[i]))
       return fail(ctx, CG_E_INVALID_ARGUMENT, "message out of arena bounds at element " + std::to_string(i));
@@ -700,6 +765,7 @@ void cg_close(cg_ctx* ctx) {
     ctx->live_blocks.clear();
     release_cached(ctx);
     for (hipEvent_t e : ctx->event_pool) (void)hipEventDestroy(e);
+    for (hipEvent_t e : ctx->sync_event_pool) (void)hipEventDestroy(e);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     if (ctx->copy_stream) (void)hipStreamDestroy(ctx->copy_stream);
     if (ctx->hash_stream) (void)hipStreamDestroy(ctx->hash_stream);
@@ -932,7 +998,8 @@ cg_status create_batch(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const ui
   std::vector<uint32_t> bad;     // flagged CG_SCHEME_FLAG_KEY_INVALID
   debug_throw_point(ctx);
   bool ed_identity = true;
-  for (size_t i = 0; i < n; ++i) {
+  size_t n_ed = 0;  // Ed25519 elements (idx[0] stays empty when they are the whole batch in order)
+  for (size_t i = 0; scheme_id && i < n; ++i) {
     const uint8_t s = scheme_id ? scheme_id[i] : CG_SCHEME_EDDSA_ED25519_SHA512;
     if (s & CG_SCHEME_FLAG_KEY_INVALID) {
       bad.push_back((uint32_t)i);
@@ -945,7 +1012,10 @@ cg_status create_batch(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const ui
       idx[2].push_back((uint32_t)i);
     }
   }
-  if (idx[0].size() != n) ed_identity = false;
+  // scheme_id NULL: every element is Ed25519, in order — no index vector (an O(n) loop
+  // of push_backs was ~0.1-0.2 ms of host time before the first copy at 2^18 elements)
+  n_ed = scheme_id ? idx[0].size() : n;
+  if (n_ed != n) ed_identity = false;
   const size_t nwords = (n + 31) / 32;
   const uint64_t fallbacks0 = ctx->pin_fallbacks;
   if (m.verdict_dev) {
@@ -966,8 +1036,12 @@ cg_status create_batch(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const ui
     // one-chunk host verify of an Ed25519-only batch: the message arena goes up later,
     // from launch_verify, once the points kernel (which needs only keys and R) is
     // running — the copy then overlaps it (no ECDSA kernel reads the arena earlier)
-    const bool defer_arena = m.keep_raw && m.bytes && idx[1].empty() && idx[2].empty() && !idx[0].empty();
-    Timed t(ctx, "h2d_stage", (defer_arena ? 0 : m.bytes) + 12 * n +
+    const bool defer_arena = m.keep_raw && m.bytes && idx[1].empty() && idx[2].empty() && n_ed;
+    // ... and, when every element is Ed25519 in order, its offsets / lengths too: the
+    // points kernel starts after the key and signature rows alone (r05: 2^18 x 32 B ids
+    // spent ~0.85 ms in copies before the first kernel)
+    const bool defer_meta = defer_arena && ed_identity && bad.empty();
+    Timed t(ctx, "h2d_stage", (defer_arena ? 0 : m.bytes) + (defer_meta ? 0 : 12 * n) +
                                   (raw_owned ? n * (pk_stride + sig_stride + (sig_len ? 4 : 0)) : 0));
     if (defer_arena) {
       b->arena_pending = m.host;
@@ -978,8 +1052,16 @@ cg_status create_batch(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const ui
     }
     const hipError_t e = hipMemsetAsync(b->arena + m.bytes, 0, 16, ctx->stream);
     if (e != hipSuccess) return bail(hip_fail(ctx, e, "pad arena"));
-    if ((st = upload(ctx, &b->msg_off_all, m.off_host, n, "upload msg_off")) != CG_OK) return bail(st);
-    if ((st = upload(ctx, &b->msg_len_all, m.len_host, n, "upload msg_len")) != CG_OK) return bail(st);
+    if (defer_meta) {
+      if ((st = dalloc(ctx, &b->msg_off_all, n, "alloc msg_off")) != CG_OK ||
+          (st = dalloc(ctx, &b->msg_len_all, n, "alloc msg_len")) != CG_OK)
+        return bail(st);
+      b->meta_pending_off = m.off_host;
+      b->meta_pending_len = m.len_host;
+    } else {
+      if ((st = upload(ctx, &b->msg_off_all, m.off_host, n, "upload msg_off")) != CG_OK) return bail(st);
+      if ((st = upload(ctx, &b->msg_len_all, m.len_host, n, "upload msg_len")) != CG_OK) return bail(st);
+    }
     if (raw_owned) {
       if ((st = upload(ctx, &pk_raw, pk, n * pk_stride, "upload pk")) != CG_OK) return bail(st);
       if ((st = upload(ctx, &sig_raw, sig, n * sig_stride, "upload sig")) != CG_OK) return bail(st);
@@ -1007,24 +1089,31 @@ cg_status create_batch(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const ui
   {
     Timed t(ctx, "stage", n);
     // Ed25519 subset -> SoA
-    const uint32_t ne = (uint32_t)idx[0].size();
+    const uint32_t ne = (uint32_t)n_ed;
     b->n_ed = ne;
     if (ne) {
       if (!ed_identity && (st = upload_idx(ctx, &b->ed_index, idx[0].data(), ne, "upload ed index")) != CG_OK)
         return bail(st);
+      b->ed_meta_alias = b->meta_pending_off != nullptr;
+      if (b->ed_meta_alias) {  // (identity order: the gathered copies would equal them)
+        b->ed_msg_off = b->msg_off_all;
+        b->ed_msg_len = b->msg_len_all;
+      }
       if ((st = dalloc(ctx, &b->ed_pk, (size_t)8 * ne, "alloc ed pk")) != CG_OK ||
           (st = dalloc(ctx, &b->ed_sig, (size_t)16 * ne, "alloc ed sig")) != CG_OK ||
           (st = dalloc(ctx, &b->ed_sig_len, ne, "alloc ed sig_len")) != CG_OK ||
-          (st = dalloc(ctx, &b->ed_msg_off, ne, "alloc ed msg_off")) != CG_OK ||
-          (st = dalloc(ctx, &b->ed_msg_len, ne, "alloc ed msg_len")) != CG_OK)
+          (!b->ed_meta_alias && (st = dalloc(ctx, &b->ed_msg_off, ne, "alloc ed msg_off")) != CG_OK) ||
+          (!b->ed_meta_alias && (st = dalloc(ctx, &b->ed_msg_len, ne, "alloc ed msg_len")) != CG_OK))
         return bail(st);
       hipError_t e = cg::launch_gather_words(pk_raw, pk_stride, 0, 8, b->ed_index, ne, ne, b->ed_pk, ctx->stream);
       if (e == hipSuccess)
         e = cg::launch_gather_words(sig_raw, sig_stride, 0, 16, b->ed_index, ne, ne, b->ed_sig, ctx->stream);
       if (e == hipSuccess)
         e = cg::launch_gather_u32(sl_raw, b->ed_index, ne, b->ed_sig_len, (uint32_t)sig_stride, ctx->stream);
-      if (e == hipSuccess) e = cg::launch_gather_u64(b->msg_off_all, b->ed_index, ne, b->ed_msg_off, ctx->stream);
-      if (e == hipSuccess) e = cg::launch_gather_u32(b->msg_len_all, b->ed_index, ne, b->ed_msg_len, 0, ctx->stream);
+      if (e == hipSuccess && !b->ed_meta_alias)
+        e = cg::launch_gather_u64(b->msg_off_all, b->ed_index, ne, b->ed_msg_off, ctx->stream);
+      if (e == hipSuccess && !b->ed_meta_alias)
+        e = cg::launch_gather_u32(b->msg_len_all, b->ed_index, ne, b->ed_msg_len, 0, ctx->stream);
       if (e != hipSuccess) return bail(hip_fail(ctx, e, "stage ed25519"));
       if ((st = stage_key_dedupe(ctx, b, pk, pk_stride, idx[0])) != CG_OK) return bail(st);
     }
@@ -1244,8 +1333,16 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = 
                    hipMemcpyAsync(b->arena, b->arena_pending, b->arena_pending_bytes, hipMemcpyHostToDevice,
                                   ctx->stream),
                    "upload arena");
+            if (b->meta_pending_off) {
+              CG_TRY(ctx, hipMemcpyAsync(b->msg_off_all, b->meta_pending_off, b->n * 8, hipMemcpyHostToDevice,
+                                         ctx->stream), "upload msg_off");
+              CG_TRY(ctx, hipMemcpyAsync(b->msg_len_all, b->meta_pending_len, b->n * 4, hipMemcpyHostToDevice,
+                                         ctx->stream), "upload msg_len");
+            }
           }
           b->arena_pending = nullptr;
+          b->meta_pending_off = nullptr;
+          b->meta_pending_len = nullptr;
           CG_TRY(ctx, hipEventRecord(ctx->ev_arena, ctx->stream), "arena done");
           CG_TRY(ctx, hipStreamWaitEvent(ctx->hash_stream, ctx->ev_arena, 0), "fork ed25519 split");
         }
@@ -1308,7 +1405,8 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = 
         auto upload_pending_arena = [&](bool beside) -> cg_status {
           if (!b->arena_pending) return CG_OK;
           const char* ab = std::getenv("CORDA_AMD_ARENA_BESIDE");
-          hipStream_t as = beside && split == 1 && b->arena_pending_bytes >= ((size_t)6 << 20) &&
+          const size_t pending = b->arena_pending_bytes + (b->meta_pending_off ? (size_t)12 * b->n : 0);
+          hipStream_t as = beside && split == 1 && pending >= ((size_t)6 << 20) &&
                                    !(ab && std::atoi(ab) == 0)
                                ? ctx->hash_stream
                                : ctx->stream;
@@ -1316,8 +1414,16 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = 
             Timed t(ctx, "h2d_arena", b->arena_pending_bytes, as);
             CG_TRY(ctx, hipMemcpyAsync(b->arena, b->arena_pending, b->arena_pending_bytes, hipMemcpyHostToDevice, as),
                    "upload arena");
+            if (b->meta_pending_off) {
+              CG_TRY(ctx, hipMemcpyAsync(b->msg_off_all, b->meta_pending_off, b->n * 8, hipMemcpyHostToDevice, as),
+                     "upload msg_off");
+              CG_TRY(ctx, hipMemcpyAsync(b->msg_len_all, b->meta_pending_len, b->n * 4, hipMemcpyHostToDevice, as),
+                     "upload msg_len");
+            }
           }
           b->arena_pending = nullptr;
+          b->meta_pending_off = nullptr;
+          b->meta_pending_len = nullptr;
           if (as != ctx->stream) {
             CG_TRY(ctx, hipEventRecord(ctx->ev_arena, as), "arena done");
             CG_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_arena, 0), "wait arena");
@@ -1423,7 +1529,7 @@ struct VerifyRun {
     for (cg_batch* b : batches) batch_free(ctx, b);
     batches.clear();
     for (hipEvent_t e : ev)
-      if (e) (void)hipEventDestroy(e);
+      if (e) ctx->sync_event_pool.push_back(e);  // (idle after the syncs above)
     ev.clear();
     for (const void* p : {(const void*)arena, (const void*)rows, (const void*)verdict, (const void*)bitmap}) dfree(ctx, p);
     arena = rows = verdict = nullptr;
@@ -1436,13 +1542,26 @@ struct VerifyRun {
 // regular one (a small first chunk starts the kernels early, a small last one
 // shortens what runs after the last byte).  CORDA_AMD_VERIFY_CHUNKS / _MIN_CHUNK /
 // _HEAD / _TAIL override (tuning, tests).
-std::vector<size_t> verify_chunk_bounds(size_t n) {
+// A host-buffer call is copy-bound when its bytes take longer over PCIe than its
+// Ed25519 kernels take on the device: ~50 GB/s against ~9.5 ns per verify (105 M/s), i.e.
+// above ~475 bytes per element (1 KB messages: 1,132 B; 32 B tx ids: 140 B).  A
+// compute-bound call gains nothing from chunking its copies: its chunks' kernels,
+// which the pipeline runs two at a time, each pay a serial chain and the host staging
+// of the first chunk delays the first kernel.  CORDA_AMD_VERIFY_POLICY=0 restores the
+// copy-bound chunking for every call (A/B).
+bool verify_copy_bound(size_t n, size_t msg_bytes, size_t row_bytes) {
+  if (const char* e = std::getenv("CORDA_AMD_VERIFY_POLICY"))
+    if (std::atoi(e) == 0) return true;
+  return n && (double)msg_bytes / (double)n + (double)row_bytes > 475.0;
+}
+
+std::vector<size_t> verify_chunk_bounds(size_t n, bool copy_bound = true) {
   // head 0.25: the host stages the first chunk's pageable bytes before any DMA can
-  // start (r04d spans: 0.37 ms at 0.5); tail 0.4: the last chunk — the only one whose
-  // kernels run after the last byte — stays within the latency mode (kEdPairMaxDefault)
-  // for 2^18-element calls
+  // start (r04d spans: 0.37 ms at 0.5); tail 0.25: the last chunk — the only one whose
+  // kernels run after the last byte — runs in the four-lane latency mode for 2^18-element
+  // calls (r05 sweeps, 2^18 x 1 KB: 6.89-6.91 ms against 6.98-7.05 at 0.4)
   size_t kmax = 8, min_chunk = 32768;
-  double head = 0.25, tail = 0.4;
+  double head = 0.25, tail = 0.25;
   if (const char* e = std::getenv("CORDA_AMD_VERIFY_CHUNKS")) kmax = std::max(1, std::atoi(e));
   if (const char* e = std::getenv("CORDA_AMD_VERIFY_MIN_CHUNK")) min_chunk = std::max(1, std::atoi(e));
   if (const char* e = std::getenv("CORDA_AMD_VERIFY_HEAD")) head = std::min(2.0, std::max(0.05, std::atof(e)));
@@ -1450,7 +1569,8 @@ std::vector<size_t> verify_chunk_bounds(size_t n) {
   // below 2^17 elements one chunk is fastest (r03b sweep, 65,536 x 1 KB pageable: 2.38 ms
   // as one chunk, 2.70 ms as two: every chunk adds a serial ~0.7 ms kernel chain)
   const bool tuned = std::getenv("CORDA_AMD_VERIFY_MIN_CHUNK") || std::getenv("CORDA_AMD_VERIFY_CHUNKS");
-  const size_t whole = tuned ? 0 : (size_t)1 << 17;
+  // a compute-bound call runs as one chunk up to 2^20 elements (r05 sweeps, 32 B ids)
+  const size_t whole = tuned ? 0 : (size_t)1 << (copy_bound ? 17 : 20);
   const size_t K = n < whole ? 1 : std::max<size_t>(1, std::min<size_t>(kmax, n / min_chunk));
   std::vector<size_t> b(K + 1, 0);
   std::vector<double> w(K, 1.0);
@@ -1546,7 +1666,8 @@ cg_status verify_pipeline(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
       (st = dalloc(ctx, &r.bitmap, (n + 31) / 32, "alloc bitmap")) != CG_OK)
     return st;
   r.ev.assign(K, nullptr);
-  for (hipEvent_t& e : r.ev) CG_TRY(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming), "verify pipeline event");
+  for (hipEvent_t& e : r.ev)
+    if (!(e = take_sync_event(ctx))) return fail(ctx, CG_E_DEVICE, "verify pipeline event");
   // the arena's 16-byte tail pad (kernels' vector loads may run past a message end)
   CG_TRY(ctx, hipMemsetAsync(r.arena + msg_bytes, 0, 16, ctx->copy_stream), "pad arena");
   // Chunk k's upload: the arena bytes its messages reach beyond what earlier chunks
@@ -1555,10 +1676,6 @@ cg_status verify_pipeline(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
   // End of the arena prefix each chunk's messages reach (clamped: a chunk's offsets are
   // checked against the arena before its copy goes out).
   std::vector<uint64_t> aend(K + 1, 0);
-  for (size_t k = 0, u = 0; k < K; ++k) {
-    for (size_t i = cb[k]; i < cb[k + 1]; ++i) u = std::max<uint64_t>(u, clamped_end(msg_off[i], msg_len[i], msg_bytes));
-    aend[k + 1] = u;
-  }
   // Pinned inputs: the copies are asynchronous.  Pageable inputs go through the
   // context's two page-locked ring slots, filled by the copy workers (chunk k+1's
   // slot while chunk k's DMA runs; a slot is reused once chunk k-2's copies are done);
@@ -1568,6 +1685,38 @@ cg_status verify_pipeline(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
                       host_is_pinned(msg_off) && host_is_pinned(msg_len) && host_is_pinned(sig_len);
   bool ring = !pinned && K > 1;
   if (const char* e = std::getenv("CORDA_AMD_VERIFY_RING")) ring = ring && std::atoi(e) != 0;
+  if (ring && !ctx->pool) {
+    int workers = 7;
+    if (const char* e = std::getenv("CORDA_AMD_COPY_THREADS")) workers = std::max(0, std::atoi(e) - 1);
+    ctx->pool = new CopyPool(workers);
+  }
+  // arena end of each chunk's messages (a prefix scan over every element: on the copy
+  // workers when they exist — one thread needed ~0.2 ms of host time before the first
+  // DMA at 2^18 elements)
+  {
+    std::vector<uint64_t> cmax(K, 0);
+    auto scan = [&](size_t lo, size_t hi, uint64_t* out) {
+      for (size_t k = 0; k < K; ++k) {
+        uint64_t u = 0;
+        const size_t a = std::max(lo, cb[k]), z = std::min(hi, cb[k + 1]);
+        for (size_t i = a; i < z; ++i) u = std::max<uint64_t>(u, clamped_end(msg_off[i], msg_len[i], msg_bytes));
+        out[k] = std::max(out[k], u);
+      }
+    };
+    const size_t parts = ctx->pool && n >= 65536 ? ctx->pool->workers() + 1 : 1;
+    std::vector<std::vector<uint64_t>> part(parts, std::vector<uint64_t>(K, 0));
+    if (parts > 1) {
+      std::vector<std::function<void()>> fns;
+      for (size_t t = 0; t < parts; ++t)
+        fns.push_back([&, t] { scan(n * t / parts, n * (t + 1) / parts, part[t].data()); });
+      ctx->pool->run_fns(fns);
+    } else {
+      scan(0, n, part[0].data());
+    }
+    for (size_t t = 0; t < parts; ++t)
+      for (size_t k = 0; k < K; ++k) cmax[k] = std::max(cmax[k], part[t][k]);
+    for (size_t k = 0; k < K; ++k) aend[k + 1] = std::max(aend[k], cmax[k]);
+  }
   const size_t row_bytes = 12 + pk_stride + sig_stride + (sig_len ? 4 : 0);
   size_t slot = 0;
   for (size_t k = 0; k < K; ++k)
@@ -1600,11 +1749,6 @@ cg_status verify_pipeline(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
       }
     }
     ring = ctx->ring_cap >= slot;
-    if (ring && !ctx->pool) {
-      int workers = 7;
-      if (const char* e = std::getenv("CORDA_AMD_COPY_THREADS")) workers = std::max(0, std::atoi(e) - 1);
-      ctx->pool = new CopyPool(workers);
-    }
   }
   const char* od = std::getenv("CORDA_AMD_VERIFY_ONE_DMA");
   const bool one_dma = !od || std::atoi(od) != 0;
@@ -1658,7 +1802,8 @@ cg_status verify_pipeline(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
   // Asynchronous copies (pinned or staged) run one chunk ahead of the kernels, so the
   // copy engine never waits for the host; a copy that holds the host goes after the
   // previous chunk's kernels are enqueued, so they run beside it.
-  const size_t ahead = (pinned || ring) ? 2 : 1;
+  size_t ahead = (pinned || ring) ? 2 : 1;
+  if (const char* e = std::getenv("CORDA_AMD_VERIFY_AHEAD")) ahead = (size_t)std::max(1, std::atoi(e));
   size_t uploaded = 0;  // chunks whose copies are enqueued
   auto upload_through = [&](size_t k) -> cg_status {  // enqueue copies of chunks < min(k, K)
     for (; uploaded < std::min(k, K); ++uploaded) {
@@ -1672,8 +1817,8 @@ cg_status verify_pipeline(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
   // an earlier chunk's kernels still use.
   uint32_t max_cnt[3] = {0, 0, 0};
   for (size_t k = 0; k < K; ++k) {
-    uint32_t cnt[3] = {0, 0, 0};
-    for (size_t i = cb[k]; i < cb[k + 1]; ++i) {
+    uint32_t cnt[3] = {scheme_id ? 0u : (uint32_t)(cb[k + 1] - cb[k]), 0, 0};
+    for (size_t i = cb[k]; scheme_id && i < cb[k + 1]; ++i) {
       const uint8_t sc = scheme_id ? scheme_id[i] : CG_SCHEME_EDDSA_ED25519_SHA512;
       if (sc == CG_SCHEME_EDDSA_ED25519_SHA512) ++cnt[0];
       else if (sc == CG_SCHEME_ECDSA_SECP256K1_SHA256) ++cnt[1];
@@ -1728,14 +1873,10 @@ cg_status verify_pipeline(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
     ~StreamRestore() { c->stream = main; }
   } restore{ctx, ctx->stream};
   hipEvent_t done[2] = {nullptr, nullptr};  // the latest chunk's end on each lane
-  struct EvFree {
-    hipEvent_t* e;
-    ~EvFree() {
-      for (int i = 0; i < 2; ++i)
-        if (e[i]) (void)hipEventDestroy(e[i]);
-    }
-  } ev_free{done};
-  for (hipEvent_t& e : done) CG_TRY(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming), "verify pipeline event");
+  for (hipEvent_t& e : done) {
+    if (!(e = take_sync_event(ctx))) return fail(ctx, CG_E_DEVICE, "verify pipeline event");
+    r.ev.push_back(e);  // returned to the pool by VerifyRun::release, after the syncs
+  }
   for (size_t k = 0; k < K; ++k) {
     const size_t lo = cb[k], hi = cb[k + 1];
     if ((st = upload_through(k + 1)) != CG_OK) return st;  // (chunk k's own copy, if not yet)
@@ -1845,7 +1986,8 @@ cg_status cg_verify_batch(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
       c->call_begin = nullptr;
     }
   } call_span_end{ctx};
-  const std::vector<size_t> cb = verify_chunk_bounds(n);
+  const std::vector<size_t> cb =
+      verify_chunk_bounds(n, verify_copy_bound(n, msg_bytes, 12 + pk_stride + sig_stride + (sig_len ? 4 : 0)));
   if (cb.size() == 2) {  // one chunk: stage, then verify, with one host sync at the end
     MsgSrc m;
     m.host = msg;
@@ -1953,7 +2095,8 @@ cg_status cg_set_profiling(cg_ctx* ctx, int enable) {
   CG_API_BEGIN
   if (!ctx) return CG_E_INVALID_ARGUMENT;
   collect_timings(ctx);
-  ctx->profiling = enable != 0;
+  ctx->profiling = enable == 1;
+  ctx->call_spans_only = enable == 2;
   return CG_OK;
   CG_API_END(ctx)
 }

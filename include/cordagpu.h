@@ -291,6 +291,8 @@ cg_status cg_release_cached(cg_ctx* ctx);
  * profiling is enabled.  Names: "ed25519_hash", "ed25519_points", "ed25519_msm",
  * "ecdsa_k1_prep", "ecdsa_k1_msm", "ecdsa_r1_prep", "ecdsa_r1_msm", "der_parse",
  * "merkle_leaf", "merkle_tree", "pmt_eval", "composite_eval", "stage".
+ * enable: 0 off, 1 every span, 2 only the "call" span of each cg_verify_batch (its
+ * GPU time from entry to the verdict download; two events per call).
  */
 cg_status cg_set_profiling(cg_ctx* ctx, int enable);
 cg_status cg_kernel_stats(cg_ctx* ctx, const char* kernel, double* total_ms, uint64_t* launches,

@@ -578,3 +578,37 @@ def test_one_chunk_verify_split_pieces_vs_oracle(gpu_ctx, oracle, monkeypatch, s
         got = gpu_verdicts(gpu_ctx, w, mode)
         assert (got[~adv] == ACCEPT).all(), np.flatnonzero(got[~adv] != ACCEPT)[:10]
         assert np.array_equal(got[check], oracle_verdicts(oracle, w.subset(check), mode))
+
+
+@pytest.mark.parametrize("n,reverse", [(160_000, True), (20_000, False)])
+def test_compute_bound_one_chunk_deferred_offsets_vs_oracle(gpu_ctx, oracle, n, reverse):
+    """A compute-bound host-buffer call (32-byte tx ids: ~140 B per element) runs as ONE chunk
+    up to 2^20 elements, and for an Ed25519-only in-order batch its offsets and lengths go
+    up with the arena, after the key and signature rows (the points kernel starts first;
+    the hash kernel reads them through the batch's own arrays).  Arena in reverse element
+    order (offsets far from monotone), ragged E12 rows with sig_len, 20 % mutated, both
+    modes, against the oracle; the larger call's deferred copy (>= 6 MB) runs beside the
+    points kernel."""
+    w = datagen.add_ed25519_adversarial(datagen.make_batch(n, msg_bytes=32, seed=101, key_base=1_700_000),
+                                        frac=0.2, seed=31)
+    ln = w.msg_len[:n].astype(np.uint64)
+    off = w.msg_off[:n].astype(np.uint64)
+    if reverse:
+        new_off = np.zeros(n, np.uint64)
+        new_off[::-1] = np.concatenate([[0], np.cumsum(ln[::-1])[:-1]]).astype(np.uint64)
+        arena = np.zeros(int(ln.sum()) + 1, np.uint8)
+        for i in range(n):
+            arena[int(new_off[i]):int(new_off[i] + ln[i])] = w.msg[int(off[i]):int(off[i] + ln[i])]
+    else:
+        new_off, arena = off, w.msg
+    sl = w.sig_len[:n].astype(np.uint32)
+    sg = np.zeros((n, 68), np.uint8)
+    sg[:, :min(68, w.sig_stride)] = w.sig[:n, :min(68, w.sig_stride)]
+    b = crypto.PackedBatch(n, None, np.ascontiguousarray(w.pk[:n, :32]), 32, sg, 68, sl, arena, new_off, w.msg_len[:n])
+    ow = datagen.Workload(n, w.scheme, w.pk, w.pk_stride, w.sig, w.sig_stride, w.sig_len, arena, new_off,
+                          w.msg_len)
+    for mode in (MODE_IS_VALID, MODE_DO_VERIFY):
+        exp = oracle_verdicts(oracle, ow, mode)
+        got = crypto.verify_packed(gpu_ctx, b, mode)
+        bad = np.flatnonzero(got != exp)
+        assert bad.size == 0, [(w.classes[i], int(got[i]), int(exp[i])) for i in bad[:10]]
