@@ -32,6 +32,12 @@ struct Ed25519Dev {
   // latency mode: dynamic LDS each points / hash block reserves (0: none), so that the
   // two kernels' few blocks, running side by side, land on different CUs
   uint32_t spread_lds = 0, spread_lds_hash = 0;
+  // points kernels of a one-chunk call: read the key and R words straight from the raw
+  // element-major rows (word w of element i at rows[i * stride_words + w]) instead of the
+  // staged SoA arrays, so it need not wait for the staging kernels (null: SoA)
+  const uint32_t* pk_rows = nullptr;
+  const uint32_t* sig_rows = nullptr;
+  uint32_t pk_row_words = 0, sig_row_words = 0;
 };
 
 size_t ed25519_btab_words();

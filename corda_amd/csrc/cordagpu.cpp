@@ -185,6 +185,7 @@ struct cg_ctx {
   hipEvent_t ev_split = nullptr;  // prepared-batch verify: the Ed25519 pieces on hash_stream are done
   hipEvent_t ev_pts_in = nullptr, ev_pts_done = nullptr;  // Ed25519 points kernel beside the hash kernel
   hipEvent_t ev_arena = nullptr;  // one-chunk verify: the deferred arena copy (on hash_stream) is done
+  hipEvent_t ev_rows = nullptr;   // one-chunk verify: the raw key / signature rows are on the device
   std::string err;
   int32_t* btab = nullptr;
   // Ed25519 chunk scratch
@@ -527,6 +528,14 @@ struct cg_batch {
   const uint64_t* meta_pending_off = nullptr;
   const uint32_t* meta_pending_len = nullptr;
   bool ed_meta_alias = false;
+  // one-chunk verify of an all-Ed25519 in-order batch: ctx->ev_rows marks the raw rows'
+  // arrival (raw_kept[0..1], word strides below), so a latency-mode points kernel can
+  // read them without waiting for the staging kernels
+  bool rows_event = false;
+  uint32_t raw_pk_words = 0, raw_sig_words = 0;
+  // early points (early_points_parts): the balanced points kernels already run on
+  // ctx->copy_stream and ctx->ev_pts_done marks their end
+  bool points_early = false;
   uint8_t* ec_rows[2] = {nullptr, nullptr};     // [ec[c].n][ec_sig_stride]
   uint32_t* ec_row_len[2] = {nullptr, nullptr};  // [ec[c].n], or null: every row is ec_sig_stride long
   size_t ec_sig_stride = 0;
@@ -725,7 +734,8 @@ cg_status cg_open(int device, cg_ctx** out) {
       hipEventCreateWithFlags(&ctx->ev_split, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_pts_in, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_pts_done, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&ctx->ev_arena, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&ctx->ev_arena, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->ev_rows, hipEventDisableTiming) != hipSuccess) {
     cg_close(ctx);
     return CG_E_DEVICE;
   }
@@ -772,7 +782,7 @@ void cg_close(cg_ctx* ctx) {
     if (ctx->ec_stream[1] && ctx->ec_stream[1] != ctx->ec_stream[0]) (void)hipStreamDestroy(ctx->ec_stream[1]);
     if (ctx->ec_stream[0]) (void)hipStreamDestroy(ctx->ec_stream[0]);
     for (hipEvent_t e : {ctx->ev_fork, ctx->ev_join[0], ctx->ev_join[1], ctx->ev_keys, ctx->ev_split, ctx->ev_pts_in,
-                         ctx->ev_pts_done, ctx->ev_arena})
+                         ctx->ev_pts_done, ctx->ev_arena, ctx->ev_rows})
       if (e) (void)hipEventDestroy(e);
     if (ctx->pin) (void)hipHostFree(ctx->pin);
     for (uint8_t* r : ctx->ring)
@@ -873,6 +883,32 @@ uint32_t ed_oct_max() {
   return e ? (uint32_t)std::max(0, std::atoi(e)) : kEdOctMaxDefault;
 }
 
+bool ed_fuse_enabled() {
+  const char* e = std::getenv("CORDA_AMD_ED_FUSE");
+  return e && std::atoi(e) != 0;
+}
+
+bool ed_overlap_enabled() {
+  const char* e = std::getenv("CORDA_AMD_ED_OVERLAP");
+  return !e || std::atoi(e) != 0;
+}
+
+// Early points: a one-chunk verify of an all-Ed25519 in-order batch on the balanced path
+// uploads its key and signature rows in up to this many parts of at least kEarlyPartMin
+// signatures, and each part's points kernel starts on copy_stream, reading the raw rows,
+// as soon as that part has landed — the copy of the next part runs beside it (r05 spans,
+// 2^18 x 32 B: rows copy ~0.55 ms, then the points kernel ~0.63 ms, both ahead of the
+// MSM; r05g: 4 parts 3.24 -> 2.92 ms).  Smaller parts lose: a points kernel of 32,768
+// signatures (128 blocks) takes as long as one of 65,536, and the extra pageable copies
+// cost ~0.1 ms (r05g: 65,536 in two parts 0.98 -> 1.10 ms).  CORDA_AMD_EARLY_POINTS
+// overrides the part count (0 or 1: off).  launch_verify then only joins those kernels
+// (cg_batch::points_early).
+constexpr uint32_t kEarlyPartMin = 65536;
+uint32_t early_points_parts() {
+  const char* e = std::getenv("CORDA_AMD_EARLY_POINTS");
+  return e ? (uint32_t)std::min(8, std::max(0, std::atoi(e))) : 4u;
+}
+
 bool key_reuse_mode(uint32_t n, uint32_t n_keys) {
   const int forced = key_reuse_forced();
   if (forced >= 0) return forced == 1;
@@ -901,8 +937,9 @@ bool key_sample_suggests_reuse(const uint8_t* pk, size_t pk_stride, const std::v
   return (uint64_t)repeats * ne >= (uint64_t)kSample * kSample * 2;
 }
 
+// sample: key_sample_suggests_reuse's answer when the caller already has it (-1: unknown)
 cg_status stage_key_dedupe(cg_ctx* ctx, cg_batch* b, const uint8_t* pk, size_t pk_stride,
-                           const std::vector<uint32_t>& idx0) {
+                           const std::vector<uint32_t>& idx0, int sample = -1) {
   const uint32_t ne = b->n_ed;
   const int forced = key_reuse_forced();
   if (forced == 0 || (ne < 64 && forced != 1)) return CG_OK;
@@ -910,7 +947,7 @@ cg_status stage_key_dedupe(cg_ctx* ctx, cg_batch* b, const uint8_t* pk, size_t p
   // per-key table build (~190 doublings, one wave per 64 keys) would be the longest
   // chain of the call, and the exact count is a host round trip
   if (forced != 1 && ne <= ed_pair_max()) return CG_OK;
-  if (forced != 1 && !key_sample_suggests_reuse(pk, pk_stride, idx0, ne)) return CG_OK;
+  if (forced != 1 && !(sample >= 0 ? sample == 1 : key_sample_suggests_reuse(pk, pk_stride, idx0, ne))) return CG_OK;
   uint32_t tsize = 1;
   while (tsize < 2 * ne) tsize <<= 1;
   uint32_t *table = nullptr, *slot_of = nullptr, *owner = nullptr, *counter = nullptr;
@@ -989,6 +1026,7 @@ cg_status create_batch(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const ui
   };
   auto bail = [&](cg_status s) {
     (void)hipStreamSynchronize(ctx->stream);
+    if (b->points_early) (void)hipStreamSynchronize(ctx->copy_stream);
     free_raw();
     batch_free(ctx, b);
     return s;
@@ -998,6 +1036,7 @@ cg_status create_batch(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const ui
   std::vector<uint32_t> bad;     // flagged CG_SCHEME_FLAG_KEY_INVALID
   debug_throw_point(ctx);
   bool ed_identity = true;
+  int key_sample = -1;  // key_sample_suggests_reuse's answer, once asked
   size_t n_ed = 0;  // Ed25519 elements (idx[0] stays empty when they are the whole batch in order)
   for (size_t i = 0; scheme_id && i < n; ++i) {
     const uint8_t s = scheme_id ? scheme_id[i] : CG_SCHEME_EDDSA_ED25519_SHA512;
@@ -1063,8 +1102,58 @@ cg_status create_batch(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const ui
       if ((st = upload(ctx, &b->msg_len_all, m.len_host, n, "upload msg_len")) != CG_OK) return bail(st);
     }
     if (raw_owned) {
-      if ((st = upload(ctx, &pk_raw, pk, n * pk_stride, "upload pk")) != CG_OK) return bail(st);
-      if ((st = upload(ctx, &sig_raw, sig, n * sig_stride, "upload sig")) != CG_OK) return bail(st);
+      const bool rows_direct =
+          m.keep_raw && ed_identity && bad.empty() && pk_stride % 4 == 0 && sig_stride % 4 == 0 && ctx->ev_rows;
+      uint32_t parts = 0;
+      if (rows_direct && n > ed_pair_max() && n <= kEdChunk && !ed_fuse_enabled() && ed_overlap_enabled() &&
+          !std::getenv("CORDA_AMD_ED_SPLIT")) {
+        const int forced = key_reuse_forced();
+        if (forced == 0 || (forced != 1 && !key_sample_suggests_reuse(pk, pk_stride, idx[0], (uint32_t)n))) {
+          key_sample = 0;
+          parts = std::min<uint32_t>(early_points_parts(), (uint32_t)(n / kEarlyPartMin));
+        }
+      }
+      if (parts > 1) {
+        if ((st = ensure_ed_scratch(ctx, (uint32_t)n)) != CG_OK ||
+            (st = dalloc(ctx, &pk_raw, n * pk_stride, "alloc pk")) != CG_OK ||
+            (st = dalloc(ctx, &sig_raw, n * sig_stride, "alloc sig")) != CG_OK)
+          return bail(st);
+        for (uint32_t p = 0; p < parts; ++p) {  // part boundaries: whole 256-lane blocks
+          const size_t lo = (size_t)(((uint64_t)n * p / parts) & ~(uint64_t)255);
+          const size_t hi = p + 1 == parts ? n : (size_t)(((uint64_t)n * (p + 1) / parts) & ~(uint64_t)255);
+          hipError_t e2 = hipMemcpyAsync(pk_raw + lo * pk_stride, pk + lo * pk_stride, (hi - lo) * pk_stride,
+                                         hipMemcpyHostToDevice, ctx->stream);
+          if (e2 == hipSuccess)
+            e2 = hipMemcpyAsync(sig_raw + lo * sig_stride, sig + lo * sig_stride, (hi - lo) * sig_stride,
+                                hipMemcpyHostToDevice, ctx->stream);
+          if (e2 == hipSuccess) e2 = hipEventRecord(ctx->ev_rows, ctx->stream);
+          if (e2 == hipSuccess) e2 = hipStreamWaitEvent(ctx->copy_stream, ctx->ev_rows, 0);
+          if (e2 != hipSuccess) return bail(hip_fail(ctx, e2, "upload rows"));
+          b->points_early = true;  // (from here on copy_stream may hold work: bail syncs it)
+          cg::Ed25519Dev d;
+          d.cap = (uint32_t)n;
+          d.scap = ctx->ed_scap;
+          d.pk_rows = reinterpret_cast<const uint32_t*>(pk_raw + lo * pk_stride);
+          d.sig_rows = reinterpret_cast<const uint32_t*>(sig_raw + lo * sig_stride);
+          d.pk_row_words = (uint32_t)(pk_stride / 4);
+          d.sig_row_words = (uint32_t)(sig_stride / 4);
+          d.pstat = ctx->ed_status + ctx->ed_scap + lo;
+          d.table = ctx->ed_table + cg::ed25519_table_offset((uint32_t)lo);
+          Timed t(ctx, "ed25519_points", hi - lo, ctx->copy_stream);
+          e2 = cg::launch_ed25519_points(d, (uint32_t)(hi - lo), ctx->copy_stream);
+          if (e2 != hipSuccess) return bail(hip_fail(ctx, e2, "launch ed25519_points"));
+        }
+        const hipError_t e2 = hipEventRecord(ctx->ev_pts_done, ctx->copy_stream);
+        if (e2 != hipSuccess) return bail(hip_fail(ctx, e2, "points done"));
+      } else {
+        if ((st = upload(ctx, &pk_raw, pk, n * pk_stride, "upload pk")) != CG_OK) return bail(st);
+        if ((st = upload(ctx, &sig_raw, sig, n * sig_stride, "upload sig")) != CG_OK) return bail(st);
+        if (rows_direct && hipEventRecord(ctx->ev_rows, ctx->stream) == hipSuccess) {
+          b->rows_event = true;
+          b->raw_pk_words = (uint32_t)(pk_stride / 4);
+          b->raw_sig_words = (uint32_t)(sig_stride / 4);
+        }
+      }
       if (sig_len && (st = upload(ctx, &sl_raw, sig_len, n, "upload sig_len")) != CG_OK) return bail(st);
     }
   }
@@ -1115,7 +1204,7 @@ cg_status create_batch(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const ui
       if (e == hipSuccess && !b->ed_meta_alias)
         e = cg::launch_gather_u32(b->msg_len_all, b->ed_index, ne, b->ed_msg_len, 0, ctx->stream);
       if (e != hipSuccess) return bail(hip_fail(ctx, e, "stage ed25519"));
-      if ((st = stage_key_dedupe(ctx, b, pk, pk_stride, idx[0])) != CG_OK) return bail(st);
+      if ((st = stage_key_dedupe(ctx, b, pk, pk_stride, idx[0], key_sample)) != CG_OK) return bail(st);
     }
     for (int c = 0; c < 2; ++c) {
       const std::vector<uint32_t>& ix = idx[1 + c];
@@ -1206,15 +1295,7 @@ cg_status join_ecdsa_streams(cg_ctx* ctx) {
 // Ed25519 points kernels beside the hash kernels on `pts_stream` (null: after them on
 // the same stream); CORDA_AMD_ED_OVERLAP=0 turns it off.
 // CORDA_AMD_ED_FUSE=1: the balanced path's points and MSM kernels as one kernel
-bool ed_fuse_enabled() {
-  const char* e = std::getenv("CORDA_AMD_ED_FUSE");
-  return e && std::atoi(e) != 0;
-}
-
-bool ed_overlap_enabled() {
-  const char* e = std::getenv("CORDA_AMD_ED_OVERLAP");
-  return !e || std::atoi(e) != 0;
-}
+// (ed_fuse_enabled, above create_batch)
 
 
 cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = true, uint32_t scratch_off = 0,
@@ -1348,6 +1429,14 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = 
         }
         CG_TRY(ctx, hipStreamWaitEvent(ctx->hash_stream, ctx->ev_fork, 0), "fork ed25519 split");
       }
+      // create_batch's early points kernels cover the whole batch as one balanced piece;
+      // any other plan recomputes them, after they are done
+      const bool early = b->points_early && pts && !fuse && split == 1 && !b->ed_key_index && b->n_ed <= span &&
+                         !(allow_lanes && b->n_ed <= pair_max);
+      if (b->points_early && !early) {
+        CG_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_pts_done, 0), "join early points");
+        if (split > 1) CG_TRY(ctx, hipStreamWaitEvent(ctx->hash_stream, ctx->ev_pts_done, 0), "join early points");
+      }
       struct StreamBack {  // ctx->stream is the piece's lane inside the loop; restored on every exit
         cg_ctx* c;
         hipStream_t main;
@@ -1445,11 +1534,29 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = 
           base += cnt;
           continue;
         }
-        if (pts) {
+        if (early) {  // points already running on copy_stream since the rows' arrival
+          if ((s2 = upload_pending_arena(true)) != CG_OK) return s2;
+          {
+            Timed t(ctx, "ed25519_hash", cnt);
+            CG_TRY(ctx, cg::launch_ed25519_hash(d, cnt, (uint32_t)mode, ctx->stream), "launch ed25519_hash");
+          }
+          CG_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_pts_done, 0), "join points");
+        } else if (pts) {
           // the points kernel needs only the rows (ready where this lane stands now):
-          // it runs on pts beside the hash kernel, and the MSM waits for both
-          CG_TRY(ctx, hipEventRecord(ctx->ev_pts_in, ctx->stream), "fork points");
-          CG_TRY(ctx, hipStreamWaitEvent(pts, ctx->ev_pts_in, 0), "fork points");
+          // it runs on pts beside the hash kernel, and the MSM waits for both.  In a
+          // one-chunk call it reads the raw rows and waits only for their copy, not for
+          // the staging kernels (r05 spans: 4,096 x 1 KB ~0.05 ms, 65,536 x 32 B ~0.05 ms)
+          hipEvent_t in = ctx->ev_pts_in;
+          if (b->rows_event && !b->ed_key_index && split == 1 && base == 0 && cnt == b->n_ed) {
+            d.pk_rows = static_cast<const uint32_t*>(b->raw_kept[0]);
+            d.sig_rows = static_cast<const uint32_t*>(b->raw_kept[1]);
+            d.pk_row_words = b->raw_pk_words;
+            d.sig_row_words = b->raw_sig_words;
+            in = ctx->ev_rows;
+          } else {
+            CG_TRY(ctx, hipEventRecord(ctx->ev_pts_in, ctx->stream), "fork points");
+          }
+          CG_TRY(ctx, hipStreamWaitEvent(pts, in, 0), "fork points");
           if (keys_pending && piece == 0) CG_TRY(ctx, hipStreamWaitEvent(pts, ctx->ev_keys, 0), "wait keyprep");
           if ((s2 = launch_points(pts)) != CG_OK) return s2;
           CG_TRY(ctx, hipEventRecord(ctx->ev_pts_done, pts), "points done");
@@ -1963,6 +2070,7 @@ void cg_batch_destroy(cg_ctx* ctx, cg_batch* b) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
+    if (b && b->points_early) (void)hipStreamSynchronize(ctx->copy_stream);  // (a verify that never joined them)
     batch_free(ctx, b);
   } catch (...) {
     api_guard_fail(ctx);

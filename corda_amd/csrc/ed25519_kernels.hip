@@ -173,17 +173,19 @@ CG_DEV void load_slot(const LaneTab& lt, int p, uint32_t k, ge_cached& c) {
 #ifndef CG_POINTS_WAVES
 #define CG_POINTS_WAVES 2
 #endif
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_POINTS_WAVES, 8))) void cg_ed25519_points(const uint32_t* __restrict__ pk,
-                                                         const uint32_t* __restrict__ sig, uint32_t n, uint32_t cap,
-                                                         uint32_t scap, uint32_t* __restrict__ pstat,
-                                                         int32_t* __restrict__ table) {
+// Inputs: word w of element i at pk[i * pk_es + w * pk_ws] (and sig likewise): the staged
+// SoA arrays (es 1, ws cap) or the raw rows of a one-chunk call (es = row stride in words,
+// ws 1), which lets the kernel start before the staging kernels (Ed25519Dev::pk_rows).
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_POINTS_WAVES, 8))) void cg_ed25519_points(
+    const uint32_t* __restrict__ pk, const uint32_t* __restrict__ sig, uint32_t n, uint32_t pk_es, uint32_t pk_ws,
+    uint32_t sig_es, uint32_t sig_ws, uint32_t scap, uint32_t* __restrict__ pstat, int32_t* __restrict__ table) {
   CG_WAVE_PRIO(1);
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint32_t pkw[8], rw[8];
   CG_UNROLL for (int w = 0; w < 8; ++w) {
-    pkw[w] = pk[(size_t)w * cap + i];
-    rw[w] = sig[(size_t)w * cap + i];
+    pkw[w] = pk[(size_t)i * pk_es + (size_t)w * pk_ws];
+    rw[w] = sig[(size_t)i * sig_es + (size_t)w * sig_ws];
   }
   // independent of the hash kernel (it may run beside it): the points verdict alone
   // (KEY_INVALID / REJECT for a bad R / COMPUTE); the MSM merges it with the hash's
@@ -414,17 +416,20 @@ struct LaneOf {
 };
 
 template <int LANES>
+// Inputs: word k of element i at pk[i * pk_es + k * pk_ws] (and sig likewise): the staged
+// SoA arrays (es 1, ws cap) or the raw rows (es = the row stride in words, ws 1).
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_POINTS_WAVES, 8))) void cg_ed25519_points_lanes(
-    const uint32_t* __restrict__ pk, const uint32_t* __restrict__ sig, uint32_t n, uint32_t cap, uint32_t scap,
-    uint32_t* __restrict__ pstat, int32_t* __restrict__ table) {
+    const uint32_t* __restrict__ pk, const uint32_t* __restrict__ sig, uint32_t n, uint32_t pk_es, uint32_t pk_ws,
+    uint32_t sig_es, uint32_t sig_ws, uint32_t scap, uint32_t* __restrict__ pstat, int32_t* __restrict__ table) {
   CG_WAVE_PRIO(1);
   const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t i = l / LANES, q = l % LANES;
   const LaneOf<LANES> lo(i, q);
   if (i >= n) return;
-  const uint32_t* src = lo.h ? sig : pk;  // R is words 0..7 of the signature rows
+  const uint32_t* src = lo.h ? sig + (size_t)i * sig_es : pk + (size_t)i * pk_es;  // R: words 0..7 of the signature
+  const uint32_t ws = lo.h ? sig_ws : pk_ws;
   uint32_t w[8];
-  CG_UNROLL for (int k = 0; k < 8; ++k) w[k] = src[(size_t)k * cap + i];
+  CG_UNROLL for (int k = 0; k < 8; ++k) w[k] = src[(size_t)k * ws];
   ge_p3 P;
   uint32_t ok = ge_frombytes_i2p(P, w);
   if (lo.h) {
@@ -566,9 +571,12 @@ hipError_t launch_ed25519_points(const Ed25519Dev& d, uint32_t n, hipStream_t s)
   if (d.key_index)
     hipLaunchKernelGGL(cg_ed25519_points_r, dim3((n + 255) / 256), dim3(256), 0, s, d.sig, n, d.cap, d.scap,
                        d.key_index, d.kstat, d.pstat, d.table);
+  else if (d.pk_rows && d.sig_rows)
+    hipLaunchKernelGGL(cg_ed25519_points, dim3((n + 255) / 256), dim3(256), 0, s, d.pk_rows, d.sig_rows, n,
+                       d.pk_row_words, 1u, d.sig_row_words, 1u, d.scap, d.pstat, d.table);
   else
-    hipLaunchKernelGGL(cg_ed25519_points, dim3((n + 255) / 256), dim3(256), 0, s, d.pk, d.sig, n, d.cap, d.scap,
-                       d.pstat, d.table);
+    hipLaunchKernelGGL(cg_ed25519_points, dim3((n + 255) / 256), dim3(256), 0, s, d.pk, d.sig, n, 1u, d.cap, 1u, d.cap,
+                       d.scap, d.pstat, d.table);
   return hipGetLastError();
 }
 
@@ -586,15 +594,20 @@ hipError_t launch_ed25519_points_lanes(const Ed25519Dev& d, uint32_t n, uint32_t
   // four / eight lanes: tables in scratch slots [0, lanes / 2 n) of this view (the caller sized scap for it)
   if (lanes > 2 && (uint64_t)lanes / 2 * n > d.scap) return hipErrorInvalidValue;
   const dim3 grid((uint32_t)(((uint64_t)lanes * n + 255) / 256));
+  const bool rows = d.pk_rows && d.sig_rows;
+  const uint32_t* pk = rows ? d.pk_rows : d.pk;
+  const uint32_t* sig = rows ? d.sig_rows : d.sig;
+  const uint32_t pk_es = rows ? d.pk_row_words : 1u, pk_ws = rows ? 1u : d.cap;
+  const uint32_t sig_es = rows ? d.sig_row_words : 1u, sig_ws = rows ? 1u : d.cap;
   if (lanes == 8)
-    hipLaunchKernelGGL(cg_ed25519_points_lanes<8>, grid, dim3(256), d.spread_lds, s, d.pk, d.sig, n, d.cap, d.scap, d.pstat,
-                       d.table);
+    hipLaunchKernelGGL(cg_ed25519_points_lanes<8>, grid, dim3(256), d.spread_lds, s, pk, sig, n, pk_es, pk_ws, sig_es,
+                       sig_ws, d.scap, d.pstat, d.table);
   else if (lanes == 4)
-    hipLaunchKernelGGL(cg_ed25519_points_lanes<4>, grid, dim3(256), d.spread_lds, s, d.pk, d.sig, n, d.cap, d.scap, d.pstat,
-                       d.table);
+    hipLaunchKernelGGL(cg_ed25519_points_lanes<4>, grid, dim3(256), d.spread_lds, s, pk, sig, n, pk_es, pk_ws, sig_es,
+                       sig_ws, d.scap, d.pstat, d.table);
   else
-    hipLaunchKernelGGL(cg_ed25519_points_lanes<2>, grid, dim3(256), d.spread_lds, s, d.pk, d.sig, n, d.cap, d.scap, d.pstat,
-                       d.table);
+    hipLaunchKernelGGL(cg_ed25519_points_lanes<2>, grid, dim3(256), d.spread_lds, s, pk, sig, n, pk_es, pk_ws, sig_es,
+                       sig_ws, d.scap, d.pstat, d.table);
   return hipGetLastError();
 }
 

@@ -580,15 +580,20 @@ def test_one_chunk_verify_split_pieces_vs_oracle(gpu_ctx, oracle, monkeypatch, s
         assert np.array_equal(got[check], oracle_verdicts(oracle, w.subset(check), mode))
 
 
-@pytest.mark.parametrize("n,reverse", [(160_000, True), (20_000, False)])
-def test_compute_bound_one_chunk_deferred_offsets_vs_oracle(gpu_ctx, oracle, n, reverse):
+@pytest.mark.parametrize("n,reverse,early", [(160_000, True, None), (160_000, False, "0"), (20_000, False, None)])
+def test_compute_bound_one_chunk_deferred_offsets_vs_oracle(gpu_ctx, oracle, monkeypatch, n, reverse, early):
     """A compute-bound host-buffer call (32-byte tx ids: ~140 B per element) runs as ONE chunk
     up to 2^20 elements, and for an Ed25519-only in-order batch its offsets and lengths go
-    up with the arena, after the key and signature rows (the points kernel starts first;
-    the hash kernel reads them through the batch's own arrays).  Arena in reverse element
-    order (offsets far from monotone), ragged E12 rows with sig_len, 20 % mutated, both
-    modes, against the oracle; the larger call's deferred copy (>= 6 MB) runs beside the
-    points kernel."""
+    up with the arena, after the key and signature rows (the points kernel starts first,
+    reading the raw 68-byte signature rows; the hash kernel reads the offsets through the
+    batch's own arrays).  160,000 signatures: the rows go up in two parts (65,536-aligned
+    boundary at 79,872) with each part's points kernel started on its arrival (early
+    points; early="0": one upload, one points kernel on the raw rows).  Arena in reverse
+    element order (offsets far from monotone), ragged E12 rows with sig_len, 20 % mutated,
+    both modes, against the oracle; the larger call's deferred copy (>= 6 MB) runs beside
+    the points kernel."""
+    if early is not None:
+        monkeypatch.setenv("CORDA_AMD_EARLY_POINTS", early)
     w = datagen.add_ed25519_adversarial(datagen.make_batch(n, msg_bytes=32, seed=101, key_base=1_700_000),
                                         frac=0.2, seed=31)
     ln = w.msg_len[:n].astype(np.uint64)

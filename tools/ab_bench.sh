@@ -12,7 +12,7 @@ for rep in $(seq 1 ${AB_REPS:-2}); do
     if [[ $v == *%* ]]; then IFS=% read -r -a envs <<< "${v#*%}"; fi
     if [ "$lib" = new ]; then unset CORDA_AMD_LIB; else export CORDA_AMD_LIB=$PWD/abvar/libcg_$lib.so; fi
     tag=${v//[%=]/_}
-    env "${envs[@]}" timeout -k 10 200 python -u bench.py --steps 10 --warmup 2 --no-cpu-baseline --latency-runs 1 \
+    env "${envs[@]}" timeout -k 10 200 python -u bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-extra --latency-runs 1 \
       $AB_ARGS > gpurun_out/ab_$tag.log 2>&1
     python -c "import json; d=json.loads(open('gpurun_out/ab_$tag.log').read().splitlines()[-1]); print('$v', d['value'], {k:v['avg_launch_ms'] for k,v in d['kernels'].items()})" >> gpurun_out/ab.txt
   done

@@ -89,7 +89,7 @@ def main():
                 if pinned:
                     ctx.register_host(b.pk, b.sig, b.msg, b.msg_off, b.msg_len)
                 for st in settings:
-                    for k in KEYS:
+                    for k in set(KEYS).union(*settings):
                         os.environ.pop(k, None)
                     os.environ.update(st)
                     for _ in range(3):
@@ -115,7 +115,7 @@ def main():
                     print(json.dumps(row), flush=True)
                 if pinned:
                     ctx.unregister_host(b.pk, b.sig, b.msg, b.msg_off, b.msg_len)
-    for k in KEYS:
+    for k in set(KEYS).union(*settings):
         os.environ.pop(k, None)
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
     with open(a.out, "w") as f:

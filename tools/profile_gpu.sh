@@ -12,7 +12,7 @@ export TMPDIR=/tmp
 export CORDA_AMD_ED_OVERLAP=0
 O=$GRAFT_REPO_ROOT/gpurun_out/prof_$TAG
 mkdir -p "$O"
-ARGS="bench.py --steps 3 --warmup 1 --no-cpu-baseline --latency-runs 1 ${BENCH_EXTRA:-}"
+ARGS="bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-extra --latency-runs 1 ${BENCH_EXTRA:-}"
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/trace" -o trace -- python3 $ARGS > "$O/trace.log" 2>&1
 timeout -s KILL 180 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VMEM_RD SQ_INSTS_LDS GRBM_GUI_ACTIVE --output-format csv -d "$O/p1" -o p1 -- python3 $ARGS > "$O/p1.log" 2>&1
 timeout -s KILL 180 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_VMEM_WR SQ_INSTS_VALU_INT64 GRBM_COUNT --output-format csv -d "$O/p2" -o p2 -- python3 $ARGS > "$O/p2.log" 2>&1
