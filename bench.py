@@ -274,7 +274,7 @@ def timeline_path(rank):
     return os.environ["CORDA_AMD_TIMELINE"]
 
 
-def e2e_spans(ctx, call, path):
+def e2e_spans(ctx, call, path, timeline=False):
     """Where one host-buffer call's time goes: the call runs once with the library's
     HIP-event spans on, and its timeline group (times relative to the 'call' span's
     begin, recorded at the library's entry on idle streams) is summarised: the call's
@@ -309,6 +309,8 @@ def e2e_spans(ctx, call, path):
     h2d = [v for k, v in spans.items() if k.startswith("h2d")]
     kern = [v for k, v in spans.items() if k.startswith("ed25519") or k == "stage"]
     out = {"wall_ms": round(wall, 3), "call_gpu_ms": call_ms, "spans": spans}
+    if timeline:  # every span, in start order
+        out["timeline"] = [(n, round(a, 3), round(b, 3)) for n, a, b in sorted(rows, key=lambda r: r[1])]
     if h2d:
         out["host_pre_ms"] = round(min(v["first_start_ms"] for v in h2d), 3)
         out["h2d_end_ms"] = round(max(v["last_end_ms"] for v in h2d), 3)

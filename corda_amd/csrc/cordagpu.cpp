@@ -95,11 +95,12 @@ class CopyPool {
     cv_.notify_all();
     for (auto& t : th_) t.join();
   }
-  // Copies every piece (split into ~1 MB tasks); returns when all are done.
+  // Copies every piece (split into 256 KB tasks: a 12 MB slice is then ~48 tasks over
+  // the 8 threads, not 12 tasks in two uneven rounds); returns when all are done.
   void run(const std::vector<Piece>& pieces) {
     std::unique_lock<std::mutex> g(m_);
     tasks_.clear();
-    constexpr size_t kTask = 1u << 20;
+    constexpr size_t kTask = 256u << 10;
     for (const Piece& p : pieces)
       for (size_t o = 0; o < p.bytes; o += kTask)
         tasks_.push_back({(char*)p.dst + o, (const char*)p.src + o, std::min(kTask, p.bytes - o)});
@@ -1684,6 +1685,20 @@ std::vector<size_t> verify_chunk_bounds(size_t n, bool copy_bound = true) {
   if (K > 1) {
     w[0] = head;
     w[K - 1] = tail;
+    // CORDA_AMD_VERIFY_TAPER="a,b,..." (or "a:b:..."): the weights of the last chunks, the last one last
+    // (overrides the tail weight)
+    if (const char* e = std::getenv("CORDA_AMD_VERIFY_TAPER")) {
+      std::vector<double> t;
+      for (const char* q = e; *q;) {
+        char* end = nullptr;
+        const double v = std::strtod(q, &end);
+        if (end == q) break;
+        t.push_back(std::min(2.0, std::max(0.05, v)));
+        q = (*end == ',' || *end == ':') ? end + 1 : end;
+      }
+      if (t.size() < K)  // (the head keeps its weight)
+        for (size_t i = 0; i < t.size(); ++i) w[K - t.size() + i] = t[i];
+    }
   }
   double wsum = 0;
   for (double x : w) wsum += x;
@@ -1859,6 +1874,9 @@ cg_status verify_pipeline(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
   }
   const char* od = std::getenv("CORDA_AMD_VERIFY_ONE_DMA");
   const bool one_dma = !od || std::atoi(od) != 0;
+  // staging slice size (ring only); CORDA_AMD_VERIFY_SLICE_KB overrides (0: whole chunks)
+  size_t slice_bytes = (size_t)12 << 20;
+  if (const char* e = std::getenv("CORDA_AMD_VERIFY_SLICE_KB")) slice_bytes = (size_t)std::max(0, std::atoi(e)) << 10;
   auto enqueue_upload = [&](size_t k) -> cg_status {
     const size_t lo = cb[k], hi = cb[k + 1];
     // the chunk's inputs are checked just before they go out (the host scan then
@@ -1891,14 +1909,43 @@ cg_status verify_pipeline(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
       std::vector<CopyPool::Piece> staged = {{slot, msg + aend[k], abytes}};
       for (size_t i = 1; i < pieces.size(); ++i)
         staged.push_back({slot + rows0 + (size_t)(static_cast<uint8_t*>(pieces[i].dst) - rb), pieces[i].src, pieces[i].bytes});
-      ctx->pool->run(staged);
-      if (one_dma) {
-        pieces = {{r.arena + aend[k], slot, abytes}, {rb, slot + rows0, cr.bytes}};
-      } else {  // (A/B: one DMA per array, as before)
-        for (size_t i = 0; i < pieces.size(); ++i) pieces[i].src = staged[i].dst;
+      if (one_dma && slice_bytes) {
+        // staged in slices, each slice's DMA issued as soon as it is in the slot (the
+        // first one small): the first DMA starts after ~2 MB of host copying instead of
+        // the whole head chunk's, and the copy engine never waits for a whole chunk's
+        // staging (r05j timeline, 2^18 x 1 KB: first DMA at 0.17-0.22 ms, then 0.13-0.28
+        // ms idle after the head while the next chunk was staged)
+        const size_t total = rows0 + cr.bytes;
+        Timed t(ctx, "h2d_verify", (aend[k + 1] - aend[k]) + (hi - lo) * row_bytes, cs);
+        for (size_t x = 0, y; x < total; x = y) {
+          y = std::min(total, (x + (k == 0 && x == 0 ? std::min(slice_bytes, (size_t)2 << 20) : slice_bytes) + 4095) &
+                                  ~(size_t)4095);
+          std::vector<CopyPool::Piece> part;
+          for (const CopyPool::Piece& q : staged) {
+            const size_t qa = (size_t)(static_cast<uint8_t*>(q.dst) - slot), a = std::max(x, qa);
+            const size_t z = std::min(y, qa + q.bytes);
+            if (a < z) part.push_back({slot + a, static_cast<const uint8_t*>(q.src) + (a - qa), z - a});
+          }
+          ctx->pool->run(part);
+          if (x < abytes)
+            CG_TRY(ctx, hipMemcpyAsync(r.arena + aend[k] + x, slot + x, std::min(y, abytes) - x, hipMemcpyHostToDevice, cs),
+                   "upload chunk");
+          if (y > rows0) {
+            const size_t a = std::max(x, rows0);
+            CG_TRY(ctx, hipMemcpyAsync(rb + (a - rows0), slot + a, y - a, hipMemcpyHostToDevice, cs), "upload chunk");
+          }
+        }
+        pieces.clear();
+      } else {
+        ctx->pool->run(staged);
+        if (one_dma) {
+          pieces = {{r.arena + aend[k], slot, abytes}, {rb, slot + rows0, cr.bytes}};
+        } else {  // (A/B: one DMA per array, as before)
+          for (size_t i = 0; i < pieces.size(); ++i) pieces[i].src = staged[i].dst;
+        }
       }
     }
-    {
+    if (!pieces.empty()) {
       Timed t(ctx, "h2d_verify", (aend[k + 1] - aend[k]) + (hi - lo) * row_bytes, cs);
       for (const CopyPool::Piece& p : pieces)
         if (p.bytes) CG_TRY(ctx, hipMemcpyAsync(p.dst, p.src, p.bytes, hipMemcpyHostToDevice, cs), "upload chunk");

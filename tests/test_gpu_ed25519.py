@@ -291,6 +291,7 @@ def test_key_reuse_prepared_batch_bitmap(gpu_ctx, oracle, key_reuse):
 
 @pytest.mark.parametrize("chunks,min_chunk,tail,variant", [("9", "700", "0.3", "default"), ("3", "1", "1.0", "default"),
                                                           ("9", "700", "0.3", "one_dma_off"),
+                                                          ("9", "700", "0.3", "slices_taper"),
                                                           ("4", "700", "0.4", "pinned_in")])
 def test_host_verify_pipeline_small_chunks_vs_oracle(gpu_ctx, oracle, monkeypatch, chunks, min_chunk, tail, variant):
     """cg_verify_batch's pipeline (chunk k's upload on the copy stream beside chunk k-1's
@@ -299,8 +300,11 @@ def test_host_verify_pipeline_small_chunks_vs_oracle(gpu_ctx, oracle, monkeypatc
     unsupported scheme id and wrong-length keys — whose arena is packed in REVERSE element
     order (the first chunk's messages sit at the end, so its prefix is the whole arena),
     in both modes, verdicts and accept bitmap against the oracle.  Variants: each staged
-    chunk's rows as one DMA (default) or one per array (CORDA_AMD_VERIFY_ONE_DMA=0), and
-    page-locked inputs (cg_register_host: no staging ring, direct DMAs; the pageable
+    chunk's rows as one DMA per staging slice (default: 12 MB slices, so one here) or one
+    per array (CORDA_AMD_VERIFY_ONE_DMA=0); 4 KB staging slices, one DMA each
+    (CORDA_AMD_VERIFY_SLICE_KB=4: slices straddle the arena / rows boundary of the slot)
+    with the last chunks tapered
+    (CORDA_AMD_VERIFY_TAPER=0.5,0.25,0.125); and page-locked inputs (cg_register_host: no staging ring, direct DMAs; the pageable
     verdict buffers then come back through the bounce buffer)."""
     from corda_amd import dist as D
     from corda_amd._lib import KEY_INVALID, UNSUPPORTED
@@ -309,6 +313,9 @@ def test_host_verify_pipeline_small_chunks_vs_oracle(gpu_ctx, oracle, monkeypatc
     monkeypatch.setenv("CORDA_AMD_VERIFY_TAIL", tail)
     if variant == "one_dma_off":
         monkeypatch.setenv("CORDA_AMD_VERIFY_ONE_DMA", "0")
+    if variant == "slices_taper":
+        monkeypatch.setenv("CORDA_AMD_VERIFY_SLICE_KB", "4")
+        monkeypatch.setenv("CORDA_AMD_VERIFY_TAPER", "0.5,0.25,0.125")
     sch = np.random.default_rng(12).choice(np.array([2, 3, 4, 4, 4], np.uint8), size=5200)
     w = datagen.make_batch(len(sch), msg_bytes=70, scheme=sch, seed=23, key_base=620_000)
     w = datagen.add_ecdsa_adversarial(w, frac=0.2, seed=4)
@@ -580,20 +587,21 @@ def test_one_chunk_verify_split_pieces_vs_oracle(gpu_ctx, oracle, monkeypatch, s
         assert np.array_equal(got[check], oracle_verdicts(oracle, w.subset(check), mode))
 
 
-@pytest.mark.parametrize("n,reverse,early", [(160_000, True, None), (160_000, False, "0"), (20_000, False, None)])
-def test_compute_bound_one_chunk_deferred_offsets_vs_oracle(gpu_ctx, oracle, monkeypatch, n, reverse, early):
+@pytest.mark.parametrize("n,reverse,env", [(160_000, True, ""), (160_000, False, "CORDA_AMD_EARLY_POINTS=0"),
+                                           (20_000, False, "")])
+def test_compute_bound_one_chunk_deferred_offsets_vs_oracle(gpu_ctx, oracle, monkeypatch, n, reverse, env):
     """A compute-bound host-buffer call (32-byte tx ids: ~140 B per element) runs as ONE chunk
     up to 2^20 elements, and for an Ed25519-only in-order batch its offsets and lengths go
     up with the arena, after the key and signature rows (the points kernel starts first,
     reading the raw 68-byte signature rows; the hash kernel reads the offsets through the
     batch's own arrays).  160,000 signatures: the rows go up in two parts (65,536-aligned
     boundary at 79,872) with each part's points kernel started on its arrival (early
-    points; early="0": one upload, one points kernel on the raw rows).  Arena in reverse
-    element order (offsets far from monotone), ragged E12 rows with sig_len, 20 % mutated,
-    both modes, against the oracle; the larger call's deferred copy (>= 6 MB) runs beside
-    the points kernel."""
-    if early is not None:
-        monkeypatch.setenv("CORDA_AMD_EARLY_POINTS", early)
+    points; EARLY_POINTS=0: one upload, one points kernel on the raw rows).  Arena in
+    reverse element order (offsets far from monotone), ragged E12 rows with sig_len, 20 %
+    mutated, both modes, against the oracle; the larger call's deferred copy (>= 6 MB)
+    runs beside the points kernel."""
+    for kv in filter(None, env.split(",")):
+        monkeypatch.setenv(*kv.split("=", 1))
     w = datagen.add_ed25519_adversarial(datagen.make_batch(n, msg_bytes=32, seed=101, key_base=1_700_000),
                                         frac=0.2, seed=31)
     ln = w.msg_len[:n].astype(np.uint64)

@@ -67,6 +67,7 @@ def main():
     ap.add_argument("--pageable-only", action="store_true")
     ap.add_argument("--msg-bytes", type=int, default=1024, help="message length (32: the production tx-id shape)")
     ap.add_argument("--spans", action="store_true", help="also one profiled call per row: bench.e2e_spans")
+    ap.add_argument("--timeline", action="store_true", help="with --spans: every span of that call, in start order")
     a = ap.parse_args()
     if a.spans:
         import tempfile
@@ -107,8 +108,10 @@ def main():
                     if a.spans:
                         import bench
                         sp = bench.e2e_spans(ctx, lambda: crypto.verify_packed(ctx, b, MODE_IS_VALID),
-                                             os.environ["CORDA_AMD_TIMELINE"])
-                        row["spans"] = {k: v for k, v in (sp or {}).items() if k != "spans"}
+                                             os.environ["CORDA_AMD_TIMELINE"], timeline=a.timeline)
+                        row["spans"] = {k: v for k, v in (sp or {}).items() if k not in ("spans", "timeline")}
+                        if a.timeline:
+                            row["timeline"] = (sp or {}).get("timeline")
                         row["kernels"] = {k: (v["count"], v["first_start_ms"], v["last_end_ms"], v["sum_ms"])
                                           for k, v in (sp or {}).get("spans", {}).items()}
                     res["rows"].append(row)
