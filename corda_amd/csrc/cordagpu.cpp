@@ -163,6 +163,51 @@ class CopyPool {
   bool stop_ = false;
 };
 
+// One long-lived helper thread: runs posted jobs in order.  Its HIP device is set
+// once, when it starts (the verify pipeline's upload thread: a thread created per call
+// cost ~0.05-0.07 ms before the first copy, r05p spans).
+class JobThread {
+ public:
+  explicit JobThread(int device) : th_([this, device] {
+    (void)hipSetDevice(device);
+    loop();
+  }) {}
+  ~JobThread() {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    th_.join();
+  }
+  void post(std::function<void()> f) {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      q_.push_back(std::move(f));
+    }
+    cv_.notify_all();
+  }
+
+ private:
+  void loop() {
+    std::unique_lock<std::mutex> g(m_);
+    for (;;) {
+      cv_.wait(g, [&] { return stop_ || !q_.empty(); });
+      if (q_.empty()) return;  // (stop_)
+      std::function<void()> f = std::move(q_.front());
+      q_.erase(q_.begin());
+      g.unlock();
+      f();
+      g.lock();
+    }
+  }
+  std::mutex m_;
+  std::condition_variable cv_;
+  std::vector<std::function<void()>> q_;
+  bool stop_ = false;
+  std::thread th_;  // (last: started once the members above exist)
+};
+
 }  // namespace
 
 struct cg_ctx {
@@ -214,6 +259,7 @@ struct cg_ctx {
   uint8_t* dl_pin = nullptr;
   size_t dl_pin_cap = 0;
   CopyPool* pool = nullptr;
+  JobThread* uploader = nullptr;  // the verify pipeline's upload thread (created on first use)
   bool profiling = false;
   // cg_set_profiling(ctx, 2): only the "call" span of each cg_verify_batch (two events
   // per call, no per-kernel events, no timeline file): the GPU time of unprofiled-shape
@@ -789,6 +835,7 @@ void cg_close(cg_ctx* ctx) {
     for (uint8_t* r : ctx->ring)
       if (r) (void)hipHostFree(r);
     if (ctx->dl_pin) (void)hipHostFree(ctx->dl_pin);
+    delete ctx->uploader;
     delete ctx->pool;
     delete ctx;
   } catch (...) {
@@ -1798,15 +1845,18 @@ cg_status verify_pipeline(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
   // End of the arena prefix each chunk's messages reach (clamped: a chunk's offsets are
   // checked against the arena before its copy goes out).
   std::vector<uint64_t> aend(K + 1, 0);
-  // Pinned inputs: the copies are asynchronous.  Pageable inputs go through the
-  // context's two page-locked ring slots, filled by the copy workers (chunk k+1's
-  // slot while chunk k's DMA runs; a slot is reused once chunk k-2's copies are done);
-  // without the ring (CORDA_AMD_VERIFY_RING=0, or no page-locked memory) a pageable
-  // copy holds the calling thread for its duration.
+  // Pinned inputs: the copies are asynchronous.  Pageable inputs go up as the runtime's
+  // own pageable copies (they hold the issuing thread: the upload thread below), or with
+  // CORDA_AMD_VERIFY_RING=1 through the context's two page-locked ring slots, filled by
+  // the copy workers (chunk k+1's slot while chunk k's DMA runs; a slot is reused once
+  // chunk k-2's copies are done).  The ring was the default until r05: it is as fast
+  // where the host's memcpy runs at ~90 GB/s, but it is bound by it, and on three of five
+  // r05 boxes the staging ran at 35-50 GB/s (2^18 x 1 KB: 7.5-9.8 ms against 6.9-7.5 for
+  // the runtime's copies on the same boxes; r05l/o/p sweeps).
   const bool pinned = host_is_pinned(msg) && host_is_pinned(pk) && host_is_pinned(sig) &&
                       host_is_pinned(msg_off) && host_is_pinned(msg_len) && host_is_pinned(sig_len);
-  bool ring = !pinned && K > 1;
-  if (const char* e = std::getenv("CORDA_AMD_VERIFY_RING")) ring = ring && std::atoi(e) != 0;
+  bool ring = false;
+  if (const char* e = std::getenv("CORDA_AMD_VERIFY_RING")) ring = !pinned && K > 1 && std::atoi(e) != 0;
   if (ring && !ctx->pool) {
     int workers = 7;
     if (const char* e = std::getenv("CORDA_AMD_COPY_THREADS")) workers = std::max(0, std::atoi(e) - 1);
@@ -1877,19 +1927,21 @@ cg_status verify_pipeline(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
   // staging slice size (ring only); CORDA_AMD_VERIFY_SLICE_KB overrides (0: whole chunks)
   size_t slice_bytes = (size_t)12 << 20;
   if (const char* e = std::getenv("CORDA_AMD_VERIFY_SLICE_KB")) slice_bytes = (size_t)std::max(0, std::atoi(e)) << 10;
-  auto enqueue_upload = [&](size_t k) -> cg_status {
+  // the chunk's inputs are checked just before they go out (the host scan then
+  // overlaps the earlier chunks' copies and kernels); an error ends the call
+  auto check_chunk = [&](size_t k) -> cg_status {
     const size_t lo = cb[k], hi = cb[k + 1];
-    // the chunk's inputs are checked just before they go out (the host scan then
-    // overlaps the earlier chunks' copies and kernels); an error ends the call
     MsgSrc mc;
     mc.host = msg;
     mc.bytes = msg_bytes;
     mc.off_host = msg_off + lo;
     mc.len_host = msg_len + lo;
-    cg_status cst = check_inputs(ctx, hi - lo, scheme_id ? scheme_id + lo : nullptr, pk + lo * pk_stride, pk_stride,
-                                 sig + lo * sig_stride, sig_stride, sig_len ? sig_len + lo : nullptr, mc);
-    if (cst != CG_OK) return cst;
-    // (device destination, host source, bytes) of the chunk: its arena piece and rows
+    return check_inputs(ctx, hi - lo, scheme_id ? scheme_id + lo : nullptr, pk + lo * pk_stride, pk_stride,
+                        sig + lo * sig_stride, sig_stride, sig_len ? sig_len + lo : nullptr, mc);
+  };
+  // (device destination, host source, bytes) of chunk k: its arena piece and rows
+  auto chunk_pieces = [&](size_t k) {
+    const size_t lo = cb[k], hi = cb[k + 1];
     const ChunkRows cr(hi - lo, pk_stride, sig_stride, sig_len);
     uint8_t* const rb = r.rows + rows_at[k];
     std::vector<CopyPool::Piece> pieces = {
@@ -1899,10 +1951,21 @@ cg_status verify_pipeline(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
         {rb + cr.pk, pk + lo * pk_stride, (hi - lo) * pk_stride},
         {rb + cr.sig, sig + lo * sig_stride, (hi - lo) * sig_stride}};
     if (sig_len) pieces.push_back({rb + cr.sl, sig_len + lo, (hi - lo) * 4});
+    return pieces;
+  };
+  // Issues chunk k's copies on the copy stream and records ev[k] (and the profiling span
+  // events a / b when given): ring staging or direct copies.  Touches no context state
+  // but the ring and the copy workers, so the upload thread can run it.
+  auto issue_chunk = [&](size_t k, hipEvent_t a, hipEvent_t b) -> hipError_t {
+    const size_t lo = cb[k], hi = cb[k + 1];
+    const ChunkRows cr(hi - lo, pk_stride, sig_stride, sig_len);
+    uint8_t* const rb = r.rows + rows_at[k];
+    std::vector<CopyPool::Piece> pieces = chunk_pieces(k);
     hipStream_t cs = ctx->copy_stream;
+    hipError_t e = hipSuccess;
     if (ring) {  // stage into slot k % 2 (free once chunk k-2's copies are done)
       uint8_t* slot = ctx->ring[k & 1];
-      if (k >= 2) CG_TRY(ctx, hipEventSynchronize(r.ev[k - 2]), "verify ring wait");
+      if (k >= 2 && (e = hipEventSynchronize(r.ev[k - 2])) != hipSuccess) return e;
       // the slot: the arena piece, then the rows in their device layout, so the rows
       // go up in one DMA (each extra DMA costs ~9 us of engine time, r04 ubench)
       const size_t abytes = (size_t)(aend[k + 1] - aend[k]), rows0 = (abytes + 255) & ~(size_t)255;
@@ -1916,25 +1979,25 @@ cg_status verify_pipeline(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
         // staging (r05j timeline, 2^18 x 1 KB: first DMA at 0.17-0.22 ms, then 0.13-0.28
         // ms idle after the head while the next chunk was staged)
         const size_t total = rows0 + cr.bytes;
-        Timed t(ctx, "h2d_verify", (aend[k + 1] - aend[k]) + (hi - lo) * row_bytes, cs);
-        for (size_t x = 0, y; x < total; x = y) {
+        if (a) (void)hipEventRecord(a, cs);
+        for (size_t x = 0, y; x < total && e == hipSuccess; x = y) {
           y = std::min(total, (x + (k == 0 && x == 0 ? std::min(slice_bytes, (size_t)2 << 20) : slice_bytes) + 4095) &
                                   ~(size_t)4095);
           std::vector<CopyPool::Piece> part;
           for (const CopyPool::Piece& q : staged) {
-            const size_t qa = (size_t)(static_cast<uint8_t*>(q.dst) - slot), a = std::max(x, qa);
+            const size_t qa = (size_t)(static_cast<uint8_t*>(q.dst) - slot), a2 = std::max(x, qa);
             const size_t z = std::min(y, qa + q.bytes);
-            if (a < z) part.push_back({slot + a, static_cast<const uint8_t*>(q.src) + (a - qa), z - a});
+            if (a2 < z) part.push_back({slot + a2, static_cast<const uint8_t*>(q.src) + (a2 - qa), z - a2});
           }
           ctx->pool->run(part);
           if (x < abytes)
-            CG_TRY(ctx, hipMemcpyAsync(r.arena + aend[k] + x, slot + x, std::min(y, abytes) - x, hipMemcpyHostToDevice, cs),
-                   "upload chunk");
-          if (y > rows0) {
-            const size_t a = std::max(x, rows0);
-            CG_TRY(ctx, hipMemcpyAsync(rb + (a - rows0), slot + a, y - a, hipMemcpyHostToDevice, cs), "upload chunk");
+            e = hipMemcpyAsync(r.arena + aend[k] + x, slot + x, std::min(y, abytes) - x, hipMemcpyHostToDevice, cs);
+          if (e == hipSuccess && y > rows0) {
+            const size_t a2 = std::max(x, rows0);
+            e = hipMemcpyAsync(rb + (a2 - rows0), slot + a2, y - a2, hipMemcpyHostToDevice, cs);
           }
         }
+        if (b && e == hipSuccess) (void)hipEventRecord(b, cs);
         pieces.clear();
       } else {
         ctx->pool->run(staged);
@@ -1946,26 +2009,112 @@ cg_status verify_pipeline(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
       }
     }
     if (!pieces.empty()) {
-      Timed t(ctx, "h2d_verify", (aend[k + 1] - aend[k]) + (hi - lo) * row_bytes, cs);
+      if (a) (void)hipEventRecord(a, cs);
       for (const CopyPool::Piece& p : pieces)
-        if (p.bytes) CG_TRY(ctx, hipMemcpyAsync(p.dst, p.src, p.bytes, hipMemcpyHostToDevice, cs), "upload chunk");
+        if (e == hipSuccess && p.bytes) e = hipMemcpyAsync(p.dst, p.src, p.bytes, hipMemcpyHostToDevice, cs);
+      if (b && e == hipSuccess) (void)hipEventRecord(b, cs);
     }
-    CG_TRY(ctx, hipEventRecord(r.ev[k], cs), "verify pipeline record");
-    return CG_OK;
+    if (e == hipSuccess) e = hipEventRecord(r.ev[k], cs);
+    return e;
+  };
+  auto chunk_span = [&](size_t k, hipEvent_t a, hipEvent_t b) {  // (a profiling span of chunk k's copies)
+    if (!a || !b) return;
+    ctx->pending.push_back({"h2d_verify", {a, b}});
+    ctx->stats["h2d_verify"].items += (aend[k + 1] - aend[k]) + (cb[k + 1] - cb[k]) * row_bytes;
+  };
+  auto enqueue_upload = [&](size_t k) -> cg_status {
+    cg_status cst = check_chunk(k);
+    if (cst != CG_OK) return cst;
+    hipEvent_t a = ctx->profiling ? take_event(ctx) : nullptr, b = ctx->profiling ? take_event(ctx) : nullptr;
+    const hipError_t e = issue_chunk(k, a, b);
+    chunk_span(k, a, b);
+    return e == hipSuccess ? CG_OK : hip_fail(ctx, e, "upload chunk");
   };
   // Asynchronous copies (pinned or staged) run one chunk ahead of the kernels, so the
   // copy engine never waits for the host; a copy that holds the host goes after the
   // previous chunk's kernels are enqueued, so they run beside it.
-  size_t ahead = (pinned || ring) ? 2 : 1;
-  if (const char* e = std::getenv("CORDA_AMD_VERIFY_AHEAD")) ahead = (size_t)std::max(1, std::atoi(e));
-  size_t uploaded = 0;  // chunks whose copies are enqueued
+
+  size_t uploaded = 0;  // chunks whose copies are enqueued (and inputs checked)
+  // The upload thread (pageable inputs): every chunk's copies — the ring staging and its
+  // DMAs, or the runtime's own pageable copies, which hold the issuing thread for their
+  // duration — are issued on a helper thread, chunk after chunk, so the calling thread
+  // only checks inputs and enqueues kernels, each chunk's as soon as its copies are
+  // issued.  On the calling thread the copy engine idled between chunks while it
+  // enqueued the kernels (r05n, no ring: 0.05-0.15 ms per chunk), and with the ring the
+  // last chunks' kernels went out late whenever the host copies ran slow (1.5 ms of
+  // kernels after the last byte against 0.8 at best).  CORDA_AMD_VERIFY_UPLOAD_THREAD=0
+  // keeps the uploads on the calling thread.  `issued` counts the chunks whose ev[k] is
+  // recorded.
+  bool thread_up = !pinned && K > 1;
+  if (const char* e = std::getenv("CORDA_AMD_VERIFY_UPLOAD_THREAD")) thread_up = thread_up && std::atoi(e) != 0;
+  // (with the upload thread the calling thread waits only for the chunk it launches next)
+  size_t ahead = thread_up ? 0 : (pinned || ring) ? 2 : 1;
+  if (const char* e = std::getenv("CORDA_AMD_VERIFY_AHEAD"))
+    if (!thread_up) ahead = (size_t)std::max(1, std::atoi(e));
+  struct Uploader {
+    std::mutex m;
+    std::condition_variable cv;
+    size_t issued = 0;
+    bool started = false, stop = false, finished = false;
+    hipError_t err = hipSuccess;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> spans;  // (profiling) per chunk, pre-taken
+    void finish() {  // stop the job (if still running) and wait for its end
+      std::unique_lock<std::mutex> g(m);
+      if (!started) return;
+      stop = true;
+      cv.wait(g, [&] { return finished; });
+      started = false;
+    }
+  } up;
+  struct UploaderJoin {
+    Uploader& u;
+    ~UploaderJoin() { u.finish(); }
+  } up_join{up};
   auto upload_through = [&](size_t k) -> cg_status {  // enqueue copies of chunks < min(k, K)
     for (; uploaded < std::min(k, K); ++uploaded) {
-      cg_status s2 = enqueue_upload(uploaded);
+      if (!thread_up) {
+        cg_status s2 = enqueue_upload(uploaded);
+        if (s2 != CG_OK) return s2;
+        continue;
+      }
+      cg_status s2 = check_chunk(uploaded);
       if (s2 != CG_OK) return s2;
+      std::unique_lock<std::mutex> g(up.m);
+      up.cv.wait(g, [&] { return up.issued > uploaded || up.err != hipSuccess; });
+      if (up.issued <= uploaded) return hip_fail(ctx, up.err, "upload chunk");
     }
     return CG_OK;
   };
+  if (thread_up) {
+    if (ctx->profiling) {
+      up.spans.resize(K, {nullptr, nullptr});
+      for (auto& sp : up.spans) sp = {take_event(ctx), take_event(ctx)};
+    }
+    try {
+      if (!ctx->uploader) ctx->uploader = new JobThread(ctx->device);
+      up.started = true;
+      ctx->uploader->post([&] {
+        hipError_t e = hipSuccess;
+        for (size_t k = 0; k < K && e == hipSuccess; ++k) {
+          {
+            std::lock_guard<std::mutex> g(up.m);
+            if (up.stop) break;
+          }
+          e = up.spans.empty() ? issue_chunk(k, nullptr, nullptr) : issue_chunk(k, up.spans[k].first, up.spans[k].second);
+          std::lock_guard<std::mutex> g(up.m);
+          if (e == hipSuccess) ++up.issued;
+          else up.err = e;
+          up.cv.notify_all();
+        }
+        std::lock_guard<std::mutex> g(up.m);
+        up.finished = true;
+        up.cv.notify_all();
+      });
+    } catch (...) {  // (a thread that cannot be created: std::system_error)
+      up.started = false;
+      return fail(ctx, CG_E_DEVICE, "verify upload thread");
+    }
+  }
   if ((st = upload_through(ahead)) != CG_OK) return st;
   // Scratch sized for the largest chunk first, so no chunk regrows (frees) a buffer
   // an earlier chunk's kernels still use.
@@ -2069,6 +2218,10 @@ cg_status verify_pipeline(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
   if (dual) CG_TRY(ctx, hipStreamWaitEvent(ctx->stream, done[1], 0), "verify pipeline join");
   if ((st = join_ecdsa_streams(ctx)) != CG_OK) return st;
   CG_TRY(ctx, cg::launch_verdict_bitmap(r.verdict, (uint32_t)n, r.bitmap, ctx->stream), "launch bitmap");
+  if (up.started) {  // (every chunk is issued by now)
+    up.finish();
+    for (size_t k = 0; k < up.spans.size(); ++k) chunk_span(k, up.spans[k].first, up.spans[k].second);
+  }
   return CG_OK;
 }
 

@@ -292,6 +292,8 @@ def test_key_reuse_prepared_batch_bitmap(gpu_ctx, oracle, key_reuse):
 @pytest.mark.parametrize("chunks,min_chunk,tail,variant", [("9", "700", "0.3", "default"), ("3", "1", "1.0", "default"),
                                                           ("9", "700", "0.3", "one_dma_off"),
                                                           ("9", "700", "0.3", "slices_taper"),
+                                                          ("9", "700", "0.3", "upload_on_caller"),
+                                                          ("9", "700", "0.3", "ring"),
                                                           ("4", "700", "0.4", "pinned_in")])
 def test_host_verify_pipeline_small_chunks_vs_oracle(gpu_ctx, oracle, monkeypatch, chunks, min_chunk, tail, variant):
     """cg_verify_batch's pipeline (chunk k's upload on the copy stream beside chunk k-1's
@@ -299,20 +301,28 @@ def test_host_verify_pipeline_small_chunks_vs_oracle(gpu_ctx, oracle, monkeypatc
     from 12 repeated signers (the key-reuse path inside a chunk), secp256k1, P-256, an
     unsupported scheme id and wrong-length keys — whose arena is packed in REVERSE element
     order (the first chunk's messages sit at the end, so its prefix is the whole arena),
-    in both modes, verdicts and accept bitmap against the oracle.  Variants: each staged
-    chunk's rows as one DMA per staging slice (default: 12 MB slices, so one here) or one
-    per array (CORDA_AMD_VERIFY_ONE_DMA=0); 4 KB staging slices, one DMA each
-    (CORDA_AMD_VERIFY_SLICE_KB=4: slices straddle the arena / rows boundary of the slot)
-    with the last chunks tapered
-    (CORDA_AMD_VERIFY_TAPER=0.5,0.25,0.125); and page-locked inputs (cg_register_host: no staging ring, direct DMAs; the pageable
-    verdict buffers then come back through the bounce buffer)."""
+    in both modes, verdicts and accept bitmap against the oracle.  Variants: the default
+    (the runtime's pageable copies, issued by the upload thread); the page-locked staging
+    ring instead (CORDA_AMD_VERIFY_RING=1), with each staged chunk's rows as one DMA per
+    staging slice (12 MB slices, so one here) or one per array (CORDA_AMD_VERIFY_ONE_DMA=0)
+    or 4 KB staging slices, one DMA each (CORDA_AMD_VERIFY_SLICE_KB=4: slices straddle the
+    arena / rows boundary of the slot) with the last chunks tapered
+    (CORDA_AMD_VERIFY_TAPER=0.5,0.25,0.125); the uploads issued on the calling thread
+    (CORDA_AMD_VERIFY_UPLOAD_THREAD=0); and page-locked inputs (cg_register_host: direct
+    DMAs; the pageable verdict buffers then come back through the bounce buffer)."""
     from corda_amd import dist as D
     from corda_amd._lib import KEY_INVALID, UNSUPPORTED
     monkeypatch.setenv("CORDA_AMD_VERIFY_CHUNKS", chunks)
     monkeypatch.setenv("CORDA_AMD_VERIFY_MIN_CHUNK", min_chunk)
     monkeypatch.setenv("CORDA_AMD_VERIFY_TAIL", tail)
+    if variant in ("one_dma_off", "slices_taper"):  # (ring staging options)
+        monkeypatch.setenv("CORDA_AMD_VERIFY_RING", "1")
     if variant == "one_dma_off":
         monkeypatch.setenv("CORDA_AMD_VERIFY_ONE_DMA", "0")
+    if variant == "upload_on_caller":
+        monkeypatch.setenv("CORDA_AMD_VERIFY_UPLOAD_THREAD", "0")
+    if variant == "ring":
+        monkeypatch.setenv("CORDA_AMD_VERIFY_RING", "1")
     if variant == "slices_taper":
         monkeypatch.setenv("CORDA_AMD_VERIFY_SLICE_KB", "4")
         monkeypatch.setenv("CORDA_AMD_VERIFY_TAPER", "0.5,0.25,0.125")
