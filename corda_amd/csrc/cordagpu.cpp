@@ -1857,7 +1857,8 @@ cg_status verify_pipeline(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
                       host_is_pinned(msg_off) && host_is_pinned(msg_len) && host_is_pinned(sig_len);
   bool ring = false;
   if (const char* e = std::getenv("CORDA_AMD_VERIFY_RING")) ring = !pinned && K > 1 && std::atoi(e) != 0;
-  if (ring && !ctx->pool) {
+  // the copy workers: the ring's host copies, and the arena-end scan below
+  if (!ctx->pool && (ring || n >= 65536)) {
     int workers = 7;
     if (const char* e = std::getenv("CORDA_AMD_COPY_THREADS")) workers = std::max(0, std::atoi(e) - 1);
     ctx->pool = new CopyPool(workers);
