@@ -197,7 +197,10 @@ class JobThread {
       std::function<void()> f = std::move(q_.front());
       q_.erase(q_.begin());
       g.unlock();
-      f();
+      try {
+        f();
+      } catch (...) {  // (a job reports its own failures; nothing unwinds out of the thread)
+      }
       g.lock();
     }
   }
@@ -2101,7 +2104,12 @@ cg_status verify_pipeline(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
             std::lock_guard<std::mutex> g(up.m);
             if (up.stop) break;
           }
-          e = up.spans.empty() ? issue_chunk(k, nullptr, nullptr) : issue_chunk(k, up.spans[k].first, up.spans[k].second);
+          try {  // (nothing may unwind out of the thread: a host allocation failure ends the uploads)
+            e = up.spans.empty() ? issue_chunk(k, nullptr, nullptr)
+                                 : issue_chunk(k, up.spans[k].first, up.spans[k].second);
+          } catch (...) {
+            e = hipErrorOutOfMemory;
+          }
           std::lock_guard<std::mutex> g(up.m);
           if (e == hipSuccess) ++up.issued;
           else up.err = e;

@@ -597,9 +597,9 @@ def test_one_chunk_verify_split_pieces_vs_oracle(gpu_ctx, oracle, monkeypatch, s
         assert np.array_equal(got[check], oracle_verdicts(oracle, w.subset(check), mode))
 
 
-@pytest.mark.parametrize("n,reverse,env", [(160_000, True, ""), (160_000, False, "CORDA_AMD_EARLY_POINTS=0"),
-                                           (20_000, False, "")])
-def test_compute_bound_one_chunk_deferred_offsets_vs_oracle(gpu_ctx, oracle, monkeypatch, n, reverse, env):
+@pytest.mark.parametrize("n,reverse,env,msg_bytes", [(160_000, True, "", 32), (160_000, False, "CORDA_AMD_EARLY_POINTS=0", 32),
+                                                     (20_000, False, "", 32), (6_000, True, "", 1024)])
+def test_compute_bound_one_chunk_deferred_offsets_vs_oracle(gpu_ctx, oracle, monkeypatch, n, reverse, env, msg_bytes):
     """A compute-bound host-buffer call (32-byte tx ids: ~140 B per element) runs as ONE chunk
     up to 2^20 elements, and for an Ed25519-only in-order batch its offsets and lengths go
     up with the arena, after the key and signature rows (the points kernel starts first,
@@ -609,10 +609,11 @@ def test_compute_bound_one_chunk_deferred_offsets_vs_oracle(gpu_ctx, oracle, mon
     points; EARLY_POINTS=0: one upload, one points kernel on the raw rows).  Arena in
     reverse element order (offsets far from monotone), ragged E12 rows with sig_len, 20 %
     mutated, both modes, against the oracle; the larger call's deferred copy (>= 6 MB)
-    runs beside the points kernel."""
+    runs beside the points kernel.  6,000 x 1 KB: a copy-bound call below the pipeline's
+    threshold, one chunk in the four-lane latency mode, its 6 MB arena deferred."""
     for kv in filter(None, env.split(",")):
         monkeypatch.setenv(*kv.split("=", 1))
-    w = datagen.add_ed25519_adversarial(datagen.make_batch(n, msg_bytes=32, seed=101, key_base=1_700_000),
+    w = datagen.add_ed25519_adversarial(datagen.make_batch(n, msg_bytes=msg_bytes, seed=101, key_base=1_700_000),
                                         frac=0.2, seed=31)
     ln = w.msg_len[:n].astype(np.uint64)
     off = w.msg_off[:n].astype(np.uint64)
