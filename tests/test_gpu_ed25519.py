@@ -610,7 +610,7 @@ def test_compute_bound_one_chunk_deferred_offsets_vs_oracle(gpu_ctx, oracle, mon
     reverse element order (offsets far from monotone), ragged E12 rows with sig_len, 20 %
     mutated, both modes, against the oracle; the larger call's deferred copy (>= 6 MB)
     runs beside the points kernel.  6,000 x 1 KB: a copy-bound call below the pipeline's
-    threshold, one chunk in the four-lane latency mode, its 6 MB arena deferred."""
+    threshold, one chunk in the eight-lane latency mode, its 6 MB arena deferred."""
     for kv in filter(None, env.split(",")):
         monkeypatch.setenv(*kv.split("=", 1))
     w = datagen.add_ed25519_adversarial(datagen.make_batch(n, msg_bytes=msg_bytes, seed=101, key_base=1_700_000),
