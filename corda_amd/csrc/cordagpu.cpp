@@ -1735,20 +1735,6 @@ std::vector<size_t> verify_chunk_bounds(size_t n, bool copy_bound = true) {
   if (K > 1) {
     w[0] = head;
     w[K - 1] = tail;
-    // CORDA_AMD_VERIFY_TAPER="a,b,..." (or "a:b:..."): the weights of the last chunks, the last one last
-    // (overrides the tail weight)
-    if (const char* e = std::getenv("CORDA_AMD_VERIFY_TAPER")) {
-      std::vector<double> t;
-      for (const char* q = e; *q;) {
-        char* end = nullptr;
-        const double v = std::strtod(q, &end);
-        if (end == q) break;
-        t.push_back(std::min(2.0, std::max(0.05, v)));
-        q = (*end == ',' || *end == ':') ? end + 1 : end;
-      }
-      if (t.size() < K)  // (the head keeps its weight)
-        for (size_t i = 0; i < t.size(); ++i) w[K - t.size() + i] = t[i];
-    }
   }
   double wsum = 0;
   for (double x : w) wsum += x;

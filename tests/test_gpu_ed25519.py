@@ -291,7 +291,7 @@ def test_key_reuse_prepared_batch_bitmap(gpu_ctx, oracle, key_reuse):
 
 @pytest.mark.parametrize("chunks,min_chunk,tail,variant", [("9", "700", "0.3", "default"), ("3", "1", "1.0", "default"),
                                                           ("9", "700", "0.3", "one_dma_off"),
-                                                          ("9", "700", "0.3", "slices_taper"),
+                                                          ("9", "700", "0.3", "small_slices"),
                                                           ("9", "700", "0.3", "upload_on_caller"),
                                                           ("9", "700", "0.3", "ring"),
                                                           ("4", "700", "0.4", "pinned_in")])
@@ -306,8 +306,7 @@ def test_host_verify_pipeline_small_chunks_vs_oracle(gpu_ctx, oracle, monkeypatc
     ring instead (CORDA_AMD_VERIFY_RING=1), with each staged chunk's rows as one DMA per
     staging slice (12 MB slices, so one here) or one per array (CORDA_AMD_VERIFY_ONE_DMA=0)
     or 4 KB staging slices, one DMA each (CORDA_AMD_VERIFY_SLICE_KB=4: slices straddle the
-    arena / rows boundary of the slot) with the last chunks tapered
-    (CORDA_AMD_VERIFY_TAPER=0.5,0.25,0.125); the uploads issued on the calling thread
+    arena / rows boundary of the slot); the uploads issued on the calling thread
     (CORDA_AMD_VERIFY_UPLOAD_THREAD=0); and page-locked inputs (cg_register_host: direct
     DMAs; the pageable verdict buffers then come back through the bounce buffer)."""
     from corda_amd import dist as D
@@ -315,7 +314,7 @@ def test_host_verify_pipeline_small_chunks_vs_oracle(gpu_ctx, oracle, monkeypatc
     monkeypatch.setenv("CORDA_AMD_VERIFY_CHUNKS", chunks)
     monkeypatch.setenv("CORDA_AMD_VERIFY_MIN_CHUNK", min_chunk)
     monkeypatch.setenv("CORDA_AMD_VERIFY_TAIL", tail)
-    if variant in ("one_dma_off", "slices_taper"):  # (ring staging options)
+    if variant in ("one_dma_off", "small_slices"):  # (ring staging options)
         monkeypatch.setenv("CORDA_AMD_VERIFY_RING", "1")
     if variant == "one_dma_off":
         monkeypatch.setenv("CORDA_AMD_VERIFY_ONE_DMA", "0")
@@ -323,9 +322,8 @@ def test_host_verify_pipeline_small_chunks_vs_oracle(gpu_ctx, oracle, monkeypatc
         monkeypatch.setenv("CORDA_AMD_VERIFY_UPLOAD_THREAD", "0")
     if variant == "ring":
         monkeypatch.setenv("CORDA_AMD_VERIFY_RING", "1")
-    if variant == "slices_taper":
+    if variant == "small_slices":
         monkeypatch.setenv("CORDA_AMD_VERIFY_SLICE_KB", "4")
-        monkeypatch.setenv("CORDA_AMD_VERIFY_TAPER", "0.5,0.25,0.125")
     sch = np.random.default_rng(12).choice(np.array([2, 3, 4, 4, 4], np.uint8), size=5200)
     w = datagen.make_batch(len(sch), msg_bytes=70, scheme=sch, seed=23, key_base=620_000)
     w = datagen.add_ecdsa_adversarial(w, frac=0.2, seed=4)
