@@ -15,12 +15,9 @@
 #include "cg_mp256.h"
 #include "cg_sha256.h"
 
-// CG_EC_FUSE = 1: the Y3 outputs of the doubling (a = -3) and of the addition, each a
-// difference of two products, are one column chain with one Montgomery reduction
-// instead of two products reduced separately (~88 instructions less each).
-#ifndef CG_EC_FUSE
-#define CG_EC_FUSE 1
-#endif
+// The Y3 outputs of the doubling (a = -3) and of the addition, each a difference of two
+// products, are one column chain with one Montgomery reduction instead of two products
+// reduced separately (~88 instructions less each).
 
 namespace cg {
 
@@ -126,17 +123,8 @@ CG_HD void ec_dbl(jpt& r, const jpt& p) {
     f26_sub(z3, z3, gamma);
     f26_sub(z3, z3, delta);  // c 3, left unnormalised: Z feeds only products (<= 4 x 4)
     f26_sub(t0, t0, x3);  // 4 beta - X3: c 5
-#if CG_EC_FUSE
     f26_mul_sub_sq<C>(y3, alpha, t0, gamma, 8);  // alpha t0 - 8 gamma^2, one reduction: 3 x 5 + 8 x 1 x 1
     f26_norm<C>(y3);
-#else
-    f26_pair<C>(y3, F26Mul{alpha, t0}, t3, F26Sqr{gamma});  // 3 x 5, 1 x 1
-    f26_add(t3, t3, t3);
-    f26_add(t3, t3, t3);
-    f26_add(t3, t3, t3);  // 8 gamma^2
-    f26_sub(y3, y3, t3);
-    f26_norm<C>(y3);  // c 9
-#endif
   } else {
     // dbl-2009-l (a = 0)
     f26 A, B, Cc, D, E, F, y2;
@@ -201,14 +189,8 @@ CG_HD void ec_add(jpt& r, const jpt& p, const jpt& q, uint32_t q_skip) {
   f26_sub(x3, x3, v);
   f26_norm<C>(x3);       // c 4
   f26_sub(t, v, x3);     // c 2
-#if CG_EC_FUSE
   f26_mul_sub_mul<C>(y3, rr, t, s1, hhh);  // rr t - s1 hhh, one reduction: 2 x 2 + 1 x 1
   f26_norm<C>(y3);
-#else
-  f26_pair<C>(y3, F26Mul{rr, t}, t, F26Mul{s1, hhh});  // 2 x 2, 1 x 1
-  f26_sub(y3, y3, t);
-  f26_norm<C>(y3);       // c 2
-#endif
   const uint32_t hz = f26_iszero<C>(h);
   jpt out;
   out.X = x3;

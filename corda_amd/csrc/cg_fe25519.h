@@ -118,32 +118,7 @@ CG_HD int32_t fe_pin(int32_t x) {
 // m * x pinned as 32 bits (m = 2, 4, 8: v_lshlrev_b32; 19: v_mul_lo_u32).  A/B r02:
 // doublings through v_add_u32 x, x (a 2-cycle op, v_lshlrev_b32 takes 4) measured
 // 0.8 % slower as inline asm (it broke the interleaving of the mad chains).
-// CG_FE_ADD_SCALE = 1: the power-of-two scalings as chains of v_add_u32 x, x (2 cycles
-// each; v_lshlrev_b32 takes 4), emitted as asm so LLVM does not fold them back into a
-// shift.
-#ifndef CG_FE_ADD_SCALE
-#define CG_FE_ADD_SCALE 0
-#endif
-CG_HD int32_t fe_scale(int32_t x, int m, bool g_side = false) {
-#if defined(__HIP_DEVICE_COMPILE__) && CG_FE_ADD_SCALE
-  if (m == 2) {
-    int32_t r;
-    asm("v_add_u32 %0, %1, %1" : "=v"(r) : "v"(x));
-    return r;
-  }
-  if (m == 4) {
-    int32_t r;
-    asm("v_add_u32 %0, %1, %1\n\tv_add_u32 %0, %0, %0" : "=&v"(r) : "v"(x));
-    return r;
-  }
-  if (m == 8) {
-    int32_t r;
-    asm("v_add_u32 %0, %1, %1\n\tv_add_u32 %0, %0, %0\n\tv_add_u32 %0, %0, %0" : "=&v"(r) : "v"(x));
-    return r;
-  }
-#endif
-  return fe_pin(CG_SCALE(x, m, g_side));
-}
+CG_HD int32_t fe_scale(int32_t x, int m, bool g_side = false) { return fe_pin(CG_SCALE(x, m, g_side)); }
 
 // Signed carry chain (round-to-nearest) on 64-bit column sums -> reduced limbs.
 // With rounding carries c = (t + 2^(w-1)) >> w, the residue t - c*2^w is exactly
@@ -193,14 +168,11 @@ CG_HD int64_t fe_pin64(int64_t x) {
 // acc + a * b as one v_mad_i64_i32 kept in the chain's order.
 CG_HD int64_t fe_mad(int64_t acc, int32_t a, int32_t b) { return fe_pin64(acc + (int64_t)a * b); }
 
-// CG_FE_ASM_COL = 1: every column of a product (or of 2 / 3 interleaved products) is one
+// On the device every column of a product (or of 2 / 3 interleaved products) is one
 // inline-asm statement of v_mad_i64_i32 (cg_fe_asm.h, generated by tools/gen_fe_asm.py).
 // With the per-mad barrier above, LLVM pads each read of a barrier-defined register by
 // the very next VALU instruction with an s_nop (an asm might be a transcendental op):
 // ~500 s_nops in the MSM kernel, none inside a column statement.
-#ifndef CG_FE_ASM_COL
-#define CG_FE_ASM_COL 1
-#endif
 
 template <typename Op>
 CG_HD FeColOps fe_col_ops(const Op& op, int k) {
@@ -218,7 +190,7 @@ CG_HD FeColOps fe_col_ops(const Op& op, int k) {
 // One column of 1 / 2 / 3 chains as one asm statement; false when no generated shape
 // fits (the caller then runs the C chain).  n is a compile-time constant here.
 CG_HD bool fe_col_asm(int64_t& c0, const FeColOps& x0) {
-#if defined(__HIP_DEVICE_COMPILE__) && CG_FE_ASM_COL
+#if defined(__HIP_DEVICE_COMPILE__)
   if (x0.n == 10) return fe_asm_col1_10(c0, x0), true;
   if (x0.n == 6) return fe_asm_col1_6(c0, x0), true;
   if (x0.n == 5) return fe_asm_col1_5(c0, x0), true;
@@ -228,7 +200,7 @@ CG_HD bool fe_col_asm(int64_t& c0, const FeColOps& x0) {
   return false;
 }
 CG_HD bool fe_col_asm(int64_t& c0, const FeColOps& x0, int64_t& c1, const FeColOps& x1) {
-#if defined(__HIP_DEVICE_COMPILE__) && CG_FE_ASM_COL
+#if defined(__HIP_DEVICE_COMPILE__)
   if (x0.n == 10 && x1.n == 10) return fe_asm_col2_10(c0, c1, x0, x1), true;
   if (x0.n == 6 && x1.n == 6) return fe_asm_col2_6(c0, c1, x0, x1), true;
   if (x0.n == 5 && x1.n == 5) return fe_asm_col2_5(c0, c1, x0, x1), true;
@@ -238,7 +210,7 @@ CG_HD bool fe_col_asm(int64_t& c0, const FeColOps& x0, int64_t& c1, const FeColO
 }
 CG_HD bool fe_col_asm(int64_t& c0, const FeColOps& x0, int64_t& c1, const FeColOps& x1, int64_t& c2,
                       const FeColOps& x2) {
-#if defined(__HIP_DEVICE_COMPILE__) && CG_FE_ASM_COL
+#if defined(__HIP_DEVICE_COMPILE__)
   if (x0.n == 10 && x1.n == 10 && x2.n == 10) return fe_asm_col3_10(c0, c1, c2, x0, x1, x2), true;
 #endif
   (void)c0, (void)x0, (void)c1, (void)x1, (void)c2, (void)x2;
@@ -247,7 +219,7 @@ CG_HD bool fe_col_asm(int64_t& c0, const FeColOps& x0, int64_t& c1, const FeColO
 
 CG_HD bool fe_col_asm(int64_t& c0, const FeColOps& x0, int64_t& c1, const FeColOps& x1, int64_t& c2,
                       const FeColOps& x2, int64_t& c3, const FeColOps& x3) {
-#if defined(__HIP_DEVICE_COMPILE__) && CG_FE_ASM_COL
+#if defined(__HIP_DEVICE_COMPILE__)
   if (x0.n == 10 && x1.n == 10 && x2.n == 10 && x3.n == 10)
     return fe_asm_col4_10(c0, c1, c2, c3, x0, x1, x2, x3), true;
   if (x0.n == 6 && x1.n == 6 && x2.n == 6 && x3.n == 6) return fe_asm_col4_6(c0, c1, c2, c3, x0, x1, x2, x3), true;

@@ -47,9 +47,6 @@ size_t ed25519_digit_words();
 hipError_t launch_ed25519_btab_build(int32_t* btab, hipStream_t s);
 hipError_t launch_ed25519_hash(const Ed25519Dev& d, uint32_t n, uint32_t mode, hipStream_t s);
 hipError_t launch_ed25519_points(const Ed25519Dev& d, uint32_t n, hipStream_t s);
-// points + MSM fused (balanced path only: d.key_index must be null)
-hipError_t launch_ed25519_points_msm(const Ed25519Dev& d, uint32_t n, const uint32_t* out_index, uint8_t* verdict,
-                                     hipStream_t s);
 size_t ed25519_key_table_bytes(uint32_t n_keys);
 hipError_t launch_ed25519_keyprep(const Ed25519Dev& d, const uint32_t* key_first, uint32_t n_keys, hipStream_t s);
 // Key dedupe at staging: key_index[i] = dense id of element i's 32-byte key among the

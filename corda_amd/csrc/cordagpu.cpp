@@ -934,11 +934,6 @@ uint32_t ed_oct_max() {
   return e ? (uint32_t)std::max(0, std::atoi(e)) : kEdOctMaxDefault;
 }
 
-bool ed_fuse_enabled() {
-  const char* e = std::getenv("CORDA_AMD_ED_FUSE");
-  return e && std::atoi(e) != 0;
-}
-
 bool ed_overlap_enabled() {
   const char* e = std::getenv("CORDA_AMD_ED_OVERLAP");
   return !e || std::atoi(e) != 0;
@@ -1156,7 +1151,7 @@ cg_status create_batch(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const ui
       const bool rows_direct =
           m.keep_raw && ed_identity && bad.empty() && pk_stride % 4 == 0 && sig_stride % 4 == 0 && ctx->ev_rows;
       uint32_t parts = 0;
-      if (rows_direct && n > ed_pair_max() && n <= kEdChunk && !ed_fuse_enabled() && ed_overlap_enabled() &&
+      if (rows_direct && n > ed_pair_max() && n <= kEdChunk && ed_overlap_enabled() &&
           !std::getenv("CORDA_AMD_ED_SPLIT")) {
         const int forced = key_reuse_forced();
         if (forced == 0 || (forced != 1 && !key_sample_suggests_reuse(pk, pk_stride, idx[0], (uint32_t)n))) {
@@ -1345,8 +1340,6 @@ cg_status join_ecdsa_streams(cg_ctx* ctx) {
 // two chunks at once on disjoint halves); the four-lane latency mode needs 2 n_ed.
 // Ed25519 points kernels beside the hash kernels on `pts_stream` (null: after them on
 // the same stream); CORDA_AMD_ED_OVERLAP=0 turns it off.
-// CORDA_AMD_ED_FUSE=1: the balanced path's points and MSM kernels as one kernel
-// (ed_fuse_enabled, above create_batch)
 
 
 cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = true, uint32_t scratch_off = 0,
@@ -1431,11 +1424,10 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = 
       }
     }
     if (b->n_ed) {
-      const bool fuse = ed_fuse_enabled();
       const uint32_t pair_max = ed_pair_max();
       // four lanes per signature: tables in 2 n_ed scratch slots — grown for it only where
       // this call owns the whole scratch; inside a pipeline only if its region has room
-      const bool quad_want = !b->ed_key_index && !fuse && b->n_ed <= std::min(pair_max, ed_quad_max());
+      const bool quad_want = !b->ed_key_index && b->n_ed <= std::min(pair_max, ed_quad_max());
       const bool oct_want = quad_want && b->n_ed <= ed_oct_max();
       cg_status s2 = ensure_ed_scratch(
           ctx, quad_want && join_streams && scratch_off == 0 ? (oct_want ? 4 : 2) * b->n_ed : b->n_ed);
@@ -1482,7 +1474,7 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = 
       }
       // create_batch's early points kernels cover the whole batch as one balanced piece;
       // any other plan recomputes them, after they are done
-      const bool early = b->points_early && pts && !fuse && split == 1 && !b->ed_key_index && b->n_ed <= span &&
+      const bool early = b->points_early && pts && split == 1 && !b->ed_key_index && b->n_ed <= span &&
                          !(allow_lanes && b->n_ed <= pair_max);
       if (b->points_early && !early) {
         CG_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_pts_done, 0), "join early points");
@@ -1520,7 +1512,7 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = 
           d.ktab = ctx->ed_ktab;
           d.kstat = ctx->ed_kstat;
         }
-        const bool pair = allow_lanes && !b->ed_key_index && !fuse && cnt <= pair_max;  // latency mode
+        const bool pair = allow_lanes && !b->ed_key_index && cnt <= pair_max;  // latency mode
         // (quad_ok / oct_ok: one piece with 2 / 4 cnt scratch slots in its region)
         const uint32_t lanes = !pair ? 1u : oct_ok && split == 1 ? 8u : quad_ok && split == 1 ? 4u : 2u;
         if (pair)
@@ -1570,21 +1562,6 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = 
           }
           return CG_OK;
         };
-        if (fuse && !b->ed_key_index) {  // points + MSM as one kernel after the hash kernel
-          cg_status s3 = upload_pending_arena(false);
-          if (s3 != CG_OK) return s3;
-          {
-            Timed t(ctx, "ed25519_hash", cnt);
-            CG_TRY(ctx, cg::launch_ed25519_hash(d, cnt, (uint32_t)mode, ctx->stream), "launch ed25519_hash");
-          }
-          Timed t(ctx, "ed25519_points_msm", cnt);
-          CG_TRY(ctx,
-                 cg::launch_ed25519_points_msm(d, cnt, b->ed_index ? b->ed_index + base : nullptr,
-                                               b->ed_index ? b->verdict : b->verdict + base, ctx->stream),
-                 "launch ed25519_points_msm");
-          base += cnt;
-          continue;
-        }
         if (early) {  // points already running on copy_stream since the rows' arrival
           if ((s2 = upload_pending_arena(true)) != CG_OK) return s2;
           {

@@ -34,10 +34,7 @@ namespace {
 #ifndef CG_MSM_WAVES
 #define CG_MSM_WAVES 2
 #endif
-// the same for the fused points + MSM kernel and the key-reuse MSM
-#ifndef CG_PM_WAVES
-#define CG_PM_WAVES 2
-#endif
+// the same for the key-reuse MSM
 #ifndef CG_MSM_R_WAVES
 #define CG_MSM_R_WAVES 2
 #endif
@@ -326,53 +323,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_MSM_WAVE
     return;
   }
   const uint32_t* dig = digits + i;
-#if CG_MSM_FAKE_TABLE  // timing experiment only (wrong verdicts): every lane reads lane 0's tables
-  const LaneTab lt = lane_table(const_cast<int32_t*>(table), 0, scap);
-#else
   const LaneTab lt = lane_table(const_cast<int32_t*>(table), i, scap);
-#endif
-  const uint32_t ok = msm_lane(ndig, dig, scap, ed_status_rneg(st), lt, btab_g);
-  verdict[dst] = ok ? (uint8_t)V_ACCEPT : (uint8_t)V_REJECT;
-}
-
-
-// Points + MSM in one kernel (CORDA_AMD_ED_FUSE=1): each lane decodes A and R, writes
-// its tables and reads them straight back in its MSM — the reads then hit the L2 / MALL
-// lines the same CU just wrote instead of HBM (the two-kernel form writes the whole
-// batch's ~2.4-3 GB of tables before the first read).  Same verdict merge as the
-// separate kernels.
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_PM_WAVES, CG_PM_WAVES))) void cg_ed25519_pm(
-    const uint32_t* __restrict__ pk, const uint32_t* __restrict__ sig, const uint32_t* __restrict__ status,
-    const uint32_t* __restrict__ digits, int32_t* __restrict__ table, const int32_t* __restrict__ btab_g, uint32_t n,
-    uint32_t cap, uint32_t scap, const uint32_t* __restrict__ out_index, uint8_t* __restrict__ verdict) {
-  CG_WAVE_PRIO(0);
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  const bool in = i < n;
-  const uint32_t st = in ? status[i] : 0u;
-  uint32_t v = V_REJECT;
-  const LaneTab lt = lane_table(table, in ? i : 0u, scap);
-  if (in) {
-    uint32_t pkw[8], rw[8];
-    CG_UNROLL for (int w = 0; w < 8; ++w) {
-      pkw[w] = pk[(size_t)w * cap + i];
-      rw[w] = sig[(size_t)w * cap + i];
-    }
-    ge_p3 negA, R;
-    v = ed_merge_verdict(st, ed25519_points_stage(pkw, rw, V_COMPUTE, negA, R));
-    if (v == V_COMPUTE) {
-      ed25519_build_table(negA, [&](int k, const ge_cached& c) { store_slot(lt, 0, k, c); });
-      ed25519_build_table(R, [&](int k, const ge_cached& c) { store_slot(lt, 1, k, c); });
-    }
-  }
-  const bool live = in && v == V_COMPUTE;
-  const uint32_t ndig = wave_max(live ? ed_status_ndig(st) : 0u);
-  if (!in) return;
-  const uint32_t dst = out_index ? out_index[i] : i;
-  if (!live) {
-    verdict[dst] = (uint8_t)v;
-    return;
-  }
-  const uint32_t* dig = digits + i;
   const uint32_t ok = msm_lane(ndig, dig, scap, ed_status_rneg(st), lt, btab_g);
   verdict[dst] = ok ? (uint8_t)V_ACCEPT : (uint8_t)V_REJECT;
 }
@@ -577,14 +528,6 @@ hipError_t launch_ed25519_points(const Ed25519Dev& d, uint32_t n, hipStream_t s)
   else
     hipLaunchKernelGGL(cg_ed25519_points, dim3((n + 255) / 256), dim3(256), 0, s, d.pk, d.sig, n, 1u, d.cap, 1u, d.cap,
                        d.scap, d.pstat, d.table);
-  return hipGetLastError();
-}
-
-hipError_t launch_ed25519_points_msm(const Ed25519Dev& d, uint32_t n, const uint32_t* out_index, uint8_t* verdict,
-                                     hipStream_t s) {
-  if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(cg_ed25519_pm, dim3((n + 255) / 256), dim3(256), 0, s, d.pk, d.sig, d.status, d.digits, d.table,
-                     d.btab, n, d.cap, d.scap, out_index, verdict);
   return hipGetLastError();
 }
 

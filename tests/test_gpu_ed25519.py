@@ -464,22 +464,6 @@ def test_prepared_batch_split_and_overlap_vs_oracle(gpu_ctx, oracle, monkeypatch
     pb.close()
 
 
-@pytest.mark.parametrize("mode", [MODE_IS_VALID, MODE_DO_VERIFY])
-def test_fused_points_msm_vs_oracle(gpu_ctx, oracle, golden_ed25519, monkeypatch, mode):
-    """CORDA_AMD_ED_FUSE=1 (points + MSM as one kernel, each lane reading back the tables it
-    just wrote): every golden class plus a random 25 %-mutated batch, against the oracle and
-    the golden verdicts."""
-    monkeypatch.setenv("CORDA_AMD_ED_FUSE", "1")
-    g = golden_ed25519
-    b = crypto.pack(crypto.EDDSA_ED25519_SHA512, [bytes.fromhex(e["pk"]) for e in g],
-                    [bytes.fromhex(e["sig"]) for e in g], [bytes.fromhex(e["msg"]) for e in g])
-    key = "is_valid" if mode == MODE_IS_VALID else "do_verify"
-    assert np.array_equal(crypto.verify_packed(gpu_ctx, b, mode), np.array([e[key] for e in g], dtype=np.uint8))
-    w = datagen.add_ed25519_adversarial(datagen.make_batch(5000, msg_bytes=77, seed=61, key_base=900_000),
-                                        frac=0.25, seed=7)
-    assert np.array_equal(gpu_verdicts(gpu_ctx, w, mode), oracle_verdicts(oracle, w, mode))
-
-
 @pytest.mark.parametrize("lanes", [1, 2, 4, 8])
 @pytest.mark.parametrize("mode", [MODE_IS_VALID, MODE_DO_VERIFY])
 def test_latency_mode_on_and_off_vs_oracle(gpu_ctx, oracle, golden_ed25519, monkeypatch, lanes, mode):
