@@ -267,23 +267,16 @@ CG_HD void recode16_65(uint32_t packed[9], const uint32_t k[8]) {
   packed[8] = carry + 8;
 }
 
-// Width of the fixed-base windows over G (bits).  16: one shared table of 2^15 + 1
-// affine points k*G per curve (2.1 MB, built on the device, read from L2) and 17
-// mixed additions per verify; 4: eight points in LDS and 65 mixed additions.
-#ifndef CG_EC_GWIN
-#define CG_EC_GWIN 16
-#endif
-constexpr int kGWin = CG_EC_GWIN;
+// Width of the fixed-base windows over G (bits): one shared table of 2^15 + 1 affine
+// points k*G per curve (2.1 MB, built on the device, read from L2) and 17 mixed
+// additions per verify (4-bit windows over eight points in LDS took 65; round 1).
+constexpr int kGWin = 16;
 constexpr uint32_t kGTabEntries = (1u << (kGWin - 1)) + 1;  // k*G, k = 0 .. 2^(kGWin-1)
 
-// Digits of u1 for the G table: kGWin = 4 -> recode16_65; kGWin = 16 -> 16 signed
-// radix-2^16 digits d in [-2^15, 2^15) stored as e = d + 2^15, two per word (digit
-// 2w in the low half of word w), and the top digit (0 or 1) in word 8.
+// Digits of u1 for the G table: 16 signed radix-2^16 digits d in [-2^15, 2^15) stored
+// as e = d + 2^15, two per word (digit 2w in the low half of word w), and the top
+// digit (0 or 1) in word 8.
 CG_HD void recode_g(uint32_t out[9], const uint32_t k[8]) {
-  if (kGWin == 4) {
-    recode16_65(out, k);
-    return;
-  }
   uint32_t carry = 0;
   CG_UNROLL for (int w = 0; w < 8; ++w) {
     const uint32_t lo = (k[w] & 0xffffu) + carry;
@@ -345,12 +338,9 @@ CG_HD uint32_t ecdsa_prep(const uint32_t qx[8], const uint32_t qy[8], uint32_t d
 }
 
 // P = u1 G + u2 Q from the packed digits; getQ(k, jpt&) loads affine k*Q (k = 1..8),
-// getG(k, jpt&) loads affine k*G (k = 1 .. 2^(kGWin-1)).
-// CG_EC_PREFETCH = 1: the window's Q and G entries are loaded before its four
-// doublings (their load latency hidden under them; +40 VGPRs held across).
-#ifndef CG_EC_PREFETCH
-#define CG_EC_PREFETCH 1
-#endif
+// getG(k, jpt&) loads affine k*G (k = 1 .. 2^(kGWin-1)).  The window's Q and G entries
+// are loaded before its four doublings (their load latency hidden under them; +40
+// VGPRs held across).
 
 template <class C, typename GetQ, typename GetG>
 CG_HD void ecdsa_joint(jpt& acc, uint32_t d1[9], uint32_t d2[9], GetQ&& getQ, GetG&& getG) {
@@ -358,26 +348,13 @@ CG_HD void ecdsa_joint(jpt& acc, uint32_t d1[9], uint32_t d2[9], GetQ&& getQ, Ge
   CG_UNROLL for (int i = 0; i < 10; ++i) { acc.X.v[i] = 0; acc.Y.v[i] = 0; acc.Z.v[i] = 0; }
   acc.inf = 1;
   CG_NOUNROLL for (int i = 64; i >= 0; --i) {
-#if !CG_EC_PREFETCH
-    if (i != 64) {
-      CG_NOUNROLL for (int k = 0; k < 4; ++k) ec_dbl<C>(acc, acc);
-    }
-#endif
     const uint32_t eq = i == 64 ? (d2[8] & 15) : (d2[7] >> 28);  // digit of u2 (Q)
-    uint32_t eg = 0, has_g = 1;                                   // digit of u1 (G)
-    if (kGWin == 4) {
-      eg = i == 64 ? (d1[8] & 15) : (d1[7] >> 28);
-    } else {
-      has_g = (i & 3) == 0;  // one 16-bit digit every fourth position
-      eg = i == 64 ? d1[8] : d1[7] >> 16;
-    }
+    const uint32_t has_g = (i & 3) == 0;                          // one 16-bit digit of u1 (G)
+    const uint32_t eg = i == 64 ? d1[8] : d1[7] >> 16;            //   every fourth position
     if (i != 64) {
       CG_UNROLL for (int w = 7; w > 0; --w) d2[w] = d2[w] << 4 | d2[w - 1] >> 28;
       d2[0] <<= 4;
-      if (kGWin == 4) {
-        CG_UNROLL for (int w = 7; w > 0; --w) d1[w] = d1[w] << 4 | d1[w - 1] >> 28;
-        d1[0] <<= 4;
-      } else if (has_g) {
+      if (has_g) {
         CG_UNROLL for (int w = 7; w > 0; --w) d1[w] = d1[w] << 16 | d1[w - 1] >> 16;
         d1[0] <<= 16;
       }
@@ -385,15 +362,11 @@ CG_HD void ecdsa_joint(jpt& acc, uint32_t d1[9], uint32_t d2[9], GetQ&& getQ, Ge
     constexpr uint32_t kHalf = 1u << (kGWin - 1);
     const uint32_t nq = eq < 8, aq = nq ? 8 - eq : eq - 8;
     const uint32_t ng = eg < kHalf, ag = ng ? kHalf - eg : eg - kHalf;
-#if CG_EC_PREFETCH
     getQ(aq == 0 ? 1u : aq, t);
     if (has_g) getG(ag == 0 ? 1u : ag, tg);
     if (i != 64) {
       CG_NOUNROLL for (int k = 0; k < 4; ++k) ec_dbl<C>(acc, acc);
     }
-#else
-    getQ(aq == 0 ? 1u : aq, t);
-#endif
     // Q part
     {
       f26 ny;
@@ -404,9 +377,6 @@ CG_HD void ecdsa_joint(jpt& acc, uint32_t d1[9], uint32_t d2[9], GetQ&& getQ, Ge
     }
     // G part (affine)
     if (has_g) {
-#if !CG_EC_PREFETCH
-      getG(ag == 0 ? 1u : ag, tg);
-#endif
       f26 ny;
       f26_neg(ny, tg.Y);
       f26_select(tg.Y, tg.Y, ny, ng);

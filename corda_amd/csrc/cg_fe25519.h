@@ -502,22 +502,11 @@ template <typename A, typename B, typename C, typename D>
 CG_HD void fe_quad(fe& h0, const A& a, fe& h1, const B& b, fe& h2, const C& c, fe& h3, const D& d) {
   fe_fold_quad(h0, fe_op(a), h1, fe_op(b), h2, fe_op(c), h3, fe_op(d));
 }
-// CG_FE_QUAD = 1: the point formulas run their four independent products as one
-// 4-chain group instead of two pairs: more ILP at 2 waves/SIMD (a dependent
-// v_mad_i64_i32 chain issues at 31.8 T lane-ops/s with 2 chains per wave, 33.5 T with 4:
+// The point formulas run their four independent products as one 4-chain group (fe_quad)
+// instead of two pairs: more ILP at 2 waves/SIMD (a dependent v_mad_i64_i32 chain issues
+// at 31.8 T lane-ops/s with 2 chains per wave, 33.5 T with 4:
 // profiles/r03f_mad_latency.json), more live registers (MSM 175 -> 208 VGPRs, still 2
 // waves, no spills).  r03h A/B: MSM 6.92-6.93 vs 6.98-7.04 ms per 1 M.
-#ifndef CG_FE_QUAD
-#define CG_FE_QUAD 1
-#endif
-// Per formula (register pressure differs: p1p1 -> p3 shares its operands between the
-// four products, the doubling's squarings and the cached addition's products do not).
-#ifndef CG_FE_QUAD_DBL
-#define CG_FE_QUAD_DBL CG_FE_QUAD
-#endif
-#ifndef CG_FE_QUAD_ADD
-#define CG_FE_QUAD_ADD CG_FE_QUAD
-#endif
 
 // h = f * g, f^2, 2 f^2 (rounding carries: limbs |h_k| <= 2^(w-1) + small)
 CG_HD void fe_mul(fe& h, const fe& f, const fe& g) { fe_one(h, FeMul{f, g}); }

@@ -103,13 +103,10 @@ CG_HD int32_t f26_kpin(int32_t x) {
 
 // 64-bit column accumulator barrier (see fe_pin64 in cg_fe25519.h): keeps a column
 // chain in source order, the carry as the first mad's addend.
-// CG_F26_PIN64 = 0 drops the barrier (A/B: LLVM may then reassociate the chains; every
-// barrier-defined register costs an s_nop before its next VALU read).
-#ifndef CG_F26_PIN64
-#define CG_F26_PIN64 1
-#endif
+// (Without it LLVM may reassociate the chains; every barrier-defined register costs an
+// s_nop before its next VALU read.)
 CG_HD int64_t f26_pin64(int64_t x) {
-#if defined(__HIP_DEVICE_COMPILE__) && CG_F26_PIN64
+#if defined(__HIP_DEVICE_COMPILE__)
   asm("" : "+v"(x));
 #endif
   return x;

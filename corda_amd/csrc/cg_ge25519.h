@@ -45,18 +45,10 @@ CG_HD void ge_p1p1_to_p2(ge_p2& r, const ge_p1p1& p) {
 // rounding carries (the input of ge_madd).
 template <bool Z_ROUND = false>
 CG_HD void ge_p1p1_to_p3(ge_p3& r, const ge_p1p1& p) {
-#if CG_FE_QUAD
   if (Z_ROUND)
     fe_quad(r.X, FeMulF{p.X, p.T}, r.Y, FeMulF{p.Z, p.Y}, r.Z, FeMul{p.Z, p.T}, r.T, FeMulF{p.X, p.Y});
   else
     fe_quad(r.X, FeMulF{p.X, p.T}, r.Y, FeMulF{p.Z, p.Y}, r.Z, FeMulF{p.Z, p.T}, r.T, FeMulF{p.X, p.Y});
-#else
-  fe_pair(r.X, FeMulF{p.X, p.T}, r.Y, FeMulF{p.Z, p.Y});
-  if (Z_ROUND)
-    fe_pair(r.Z, FeMul{p.Z, p.T}, r.T, FeMulF{p.X, p.Y});
-  else
-    fe_pair(r.Z, FeMulF{p.Z, p.T}, r.T, FeMulF{p.X, p.Y});
-#endif
 }
 
 // (Y+X, Y-X, Z, 2dT) of a p3 point (the decoded keys / R, the B table builder).
@@ -88,12 +80,7 @@ template <bool ADD_READY = false>
 CG_HD void ge_p2_dbl(ge_p1p1& r, const ge_p2& p) {
   fe s, xx, yy, zz2, ss;
   fe_add_p(s, p.X, p.Y);
-#if CG_FE_QUAD_DBL
   fe_quad(xx, FeSqF{p.X}, yy, FeSqF{p.Y}, zz2, FeSq2{p.Z}, ss, FeSqF{s});
-#else
-  fe_pair(xx, FeSqF{p.X}, yy, FeSqF{p.Y});
-  fe_pair(zz2, FeSq2{p.Z}, ss, FeSqF{s});
-#endif
   if (ADD_READY)
     fe_add_p(r.Y, yy, xx);
   else
@@ -130,12 +117,7 @@ CG_HD void ge_add_cached(ge_p1p1& r, const ge_p3& p, const ge_cached& q, uint32_
   fe_cneg(t2d, q.T2d, neg);
   fe_add(a, p.Y, p.X);
   fe_sub(b, p.Y, p.X);
-#if CG_FE_QUAD_ADD
   fe_quad(A, FeMulF{a, qa}, B, FeMulF{b, qb}, C, FeMulF{t2d, p.T}, D2, FeMul2F{p.Z, q.Z});  // D2 = 2 Z Zq
-#else
-  fe_pair(A, FeMulF{a, qa}, B, FeMulF{b, qb});
-  fe_pair(C, FeMulF{t2d, p.T}, D2, FeMul2F{p.Z, q.Z});  // D2 = 2 Z Zq
-#endif
   fe_sub(r.X, A, B);
   fe_add_p(r.Y, A, B);
   fe_add_p(r.Z, D2, C);

@@ -412,30 +412,6 @@ CG_DEV uint32_t ecdsa_prep_b_lane(const uint32_t* rs, uint32_t i, uint32_t n, ui
   return aux;
 }
 
-// Phase 1b as its own kernel (CG_EC_FOLD_PREPB = 0): digits to HBM for the MSM.
-template <class C>
-__global__ __launch_bounds__(256) void cg_ecdsa_prep_b(const uint32_t* __restrict__ rs, uint32_t n, uint32_t cap,
-                                                       uint32_t scap, uint32_t* __restrict__ status,
-                                                       const uint32_t* __restrict__ ework,
-                                                       const uint32_t* __restrict__ leaf_n,
-                                                       const uint32_t* __restrict__ leaf_p,
-                                                       uint32_t* __restrict__ digits, const uint32_t* __restrict__ qjac,
-                                                       uint32_t* __restrict__ qtab, uint32_t glv_full_mod,
-                                                       uint32_t index_base) {
-  CG_WAVE_PRIO(2);
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n || status[i] != 0xff) return;
-  uint32_t d1[9], d2[9], d3[9];
-  const uint32_t aux = ecdsa_prep_b_lane<C>(rs, i, n, cap, scap, ework, leaf_n, leaf_p, qjac, qtab,
-                                            glv_full_mod != 0 && (index_base + i) % glv_full_mod == 0, d1, d2, d3);
-  status[i] = 0xff | aux << 8;
-  CG_UNROLL for (int k = 0; k < 9; ++k) {
-    digits[(size_t)k * scap + i] = d1[k];
-    digits[(size_t)(9 + k) * scap + i] = d2[k];
-    if constexpr (C::kScheme == 2) digits[(size_t)(18 + k) * scap + i] = d3[k];
-  }
-}
-
 // Two waves per SIMD (<= 256 VGPRs); the GLV loop keeps one add site per formula
 // (rolled slot loops) so it fits without scratch spills.
 template <class C>
@@ -446,13 +422,10 @@ constexpr int ecdsa_msm_waves_min() { return CG_ECDSA_MSM_WAVES; }
 template <class C>
 constexpr int ecdsa_msm_waves_max() { return 8; }
 
-// CG_EC_FOLD_PREPB = 1 (default): prep_b's work runs as the MSM kernel's prologue
+// Phase 1b (prep_b: the scalars' digits, the Q table) runs as the MSM kernel's prologue
 // (ecdsa_prep_b_lane; digits stay in registers).  As a kernel of its own it was
 // latency-bound (r03g2 PMC: 0.19 / 0.14 of peak, 74-79 % of wave cycles waiting on
 // its loads); in the prologue those waits overlap the other MSM waves' arithmetic.
-#ifndef CG_EC_FOLD_PREPB
-#define CG_EC_FOLD_PREPB 1
-#endif
 template <class C>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ecdsa_msm_waves_min<C>(), ecdsa_msm_waves_max<C>())))
 void cg_ecdsa_msm(const uint32_t* __restrict__ rs,
@@ -471,23 +444,12 @@ void cg_ecdsa_msm(const uint32_t* __restrict__ rs,
   uint32_t st = i < n ? status[i] : 0u;
   const bool live = i < n && (st & 0xff) == 0xff;
   uint32_t d1[9], d2[9], d3[9];
-#if CG_EC_FOLD_PREPB
   (void)digits;
   if (live) {
     const uint32_t aux = ecdsa_prep_b_lane<C>(rs, i, n, cap, scap, ework, leaf_n, leaf_p, qjac, qtab,
                                               glv_full_mod != 0 && (index_base + i) % glv_full_mod == 0, d1, d2, d3);
     st = 0xff | aux << 8;
   }
-#else
-  (void)ework, (void)leaf_n, (void)leaf_p, (void)qjac, (void)glv_full_mod, (void)index_base;
-  if (live) {
-    CG_UNROLL for (int w = 0; w < 9; ++w) {
-      d1[w] = digits[(size_t)w * scap + i];
-      d2[w] = digits[(size_t)(9 + w) * scap + i];
-      d3[w] = C::kScheme == 2 ? digits[(size_t)(18 + w) * scap + i] : 0u;
-    }
-  }
-#endif
   // secp256k1: every lane of the wave walks the longest split scalar's digits
   const uint32_t nd = C::kScheme == 2 ? wave_max_u32(live ? (st >> 8) & 0xff : 0u) : 0u;
   if (i >= n) return;
@@ -642,11 +604,6 @@ hipError_t launch_prep(const EcdsaBatch& b, EcdsaConsts* cc, uint32_t base, uint
   hipLaunchKernelGGL(cg_inv_roots<C>, dim3(1), dim3(128), 0, s, c->inv + vn[ln], c->invp + vp[lp]);
   launch_inv_down<InvN<C>>(c->inv, vn, tn, mn, ln, s);
   launch_inv_down<InvP<C>>(c->invp, vp, tp, mp, lp, s);
-#if !CG_EC_FOLD_PREPB
-  hipLaunchKernelGGL(cg_ecdsa_prep_b<C>, grid_for(cnt), dim3(256), 0, s, b.rs + base, cnt, b.n, c->scap, c->status,
-                     c->ework, c->inv + vn[0], c->invp + vp[0], c->digits, c->qjac, c->qtab, cc->glv_full_mod,
-                     base);
-#endif
   return hipGetLastError();
 }
 

@@ -618,3 +618,40 @@ def test_compute_bound_one_chunk_deferred_offsets_vs_oracle(gpu_ctx, oracle, mon
         got = crypto.verify_packed(gpu_ctx, b, mode)
         bad = np.flatnonzero(got != exp)
         assert bad.size == 0, [(w.classes[i], int(got[i]), int(exp[i])) for i in bad[:10]]
+
+
+@pytest.mark.parametrize("upload_thread", ["1", "0"])
+def test_pipeline_errors_then_recovery(gpu_ctx, oracle, monkeypatch, upload_thread):
+    """A chunked host-buffer call (forced into six chunks) whose fifth chunk holds a message
+    outside the arena returns CG_E_INVALID_ARGUMENT: the chunk's inputs are checked on the
+    calling thread before its kernels go out, the upload thread (CORDA_AMD_VERIFY_UPLOAD_THREAD)
+    is stopped and joined, the call's streams drained.  Then allocation failures injected at
+    the k-th device allocation (CG_DEBUG_FAIL_ALLOC) return CG_E_OUT_OF_MEMORY (or, past the
+    call's last allocation, nothing).  After every failure the same context verifies the
+    intact batch against the oracle."""
+    from corda_amd._lib import DEBUG_FAIL_ALLOC, CordaGpuError
+    monkeypatch.setenv("CORDA_AMD_VERIFY_CHUNKS", "6")
+    monkeypatch.setenv("CORDA_AMD_VERIFY_MIN_CHUNK", "500")
+    monkeypatch.setenv("CORDA_AMD_VERIFY_UPLOAD_THREAD", upload_thread)
+    n = 4000
+    w = datagen.add_ed25519_adversarial(datagen.make_batch(n, msg_bytes=96, seed=77, key_base=1_900_000),
+                                        frac=0.2, seed=13)
+    mk = lambda off: crypto.PackedBatch(n, None, np.ascontiguousarray(w.pk[:n, :32]), 32, np.ascontiguousarray(
+        w.sig[:n, :w.sig_stride]), w.sig_stride, w.sig_len[:n].astype(np.uint32), w.msg, off, w.msg_len[:n])
+    good = mk(w.msg_off[:n].astype(np.uint64))
+    exp = oracle_verdicts(oracle, w, MODE_IS_VALID)
+    assert np.array_equal(crypto.verify_packed(gpu_ctx, good, MODE_IS_VALID), exp)
+    off = w.msg_off[:n].astype(np.uint64).copy()
+    off[3400] = np.uint64(len(w.msg))  # (chunk 5 of 6) past the arena's end
+    with pytest.raises(CordaGpuError):
+        crypto.verify_packed(gpu_ctx, mk(off), MODE_IS_VALID)
+    assert np.array_equal(crypto.verify_packed(gpu_ctx, good, MODE_IS_VALID), exp)
+    for k in (1, 2, 4, 7, 11, 16, 24):
+        gpu_ctx.set_debug(DEBUG_FAIL_ALLOC, k)
+        try:
+            crypto.verify_packed(gpu_ctx, good, MODE_IS_VALID)
+        except CordaGpuError:
+            pass
+        finally:
+            gpu_ctx.set_debug(DEBUG_FAIL_ALLOC, 0)
+        assert np.array_equal(crypto.verify_packed(gpu_ctx, good, MODE_IS_VALID), exp), k
