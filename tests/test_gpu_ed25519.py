@@ -655,4 +655,3 @@ def test_pipeline_errors_then_recovery(gpu_ctx, oracle, monkeypatch, upload_thre
         finally:
             gpu_ctx.set_debug(DEBUG_FAIL_ALLOC, 0)
         assert np.array_equal(crypto.verify_packed(gpu_ctx, good, MODE_IS_VALID), exp), k
-
