@@ -655,3 +655,19 @@ def test_pipeline_errors_then_recovery(gpu_ctx, oracle, monkeypatch, upload_thre
         finally:
             gpu_ctx.set_debug(DEBUG_FAIL_ALLOC, 0)
         assert np.array_equal(crypto.verify_packed(gpu_ctx, good, MODE_IS_VALID), exp), k
+
+
+@pytest.mark.parametrize("n,msg_bytes", [(1, 32), (63, 1024), (65, 32), (257, 1024), (40_001, 32), (65_537, 32),
+                                         (131_073, 32), (131_073, 1024), (262_145, 1024), ((1 << 20) + 1, 32)])
+def test_host_verify_plan_boundaries_vs_oracle(gpu_ctx, oracle, n, msg_bytes):
+    """cg_verify_batch from pageable host buffers at sizes one past each plan boundary:
+    the latency-mode thresholds (40,000), the early-points part size (65,536), the
+    pipeline's start for copy-bound calls (2^17) and for compute-bound ones (2^20: 2^20 + 1
+    32-byte ids run as eight chunks), and small ragged calls; 32 B ids and 1 KB messages, 2 %
+    mutated, every verdict against the oracle."""
+    w = datagen.add_ed25519_adversarial(datagen.make_batch(n, msg_bytes=msg_bytes, seed=n % 1000 + 5,
+                                                           key_base=3_000_000 + n % 7919), frac=0.02, seed=29)
+    exp = oracle_verdicts(oracle, w, MODE_IS_VALID)
+    got = gpu_verdicts(gpu_ctx, w, MODE_IS_VALID)
+    bad = np.flatnonzero(got != exp)
+    assert bad.size == 0, [(w.classes[i], int(got[i]), int(exp[i])) for i in bad[:10]]
