@@ -47,6 +47,9 @@ size_t ed25519_digit_words();
 hipError_t launch_ed25519_btab_build(int32_t* btab, hipStream_t s);
 hipError_t launch_ed25519_hash(const Ed25519Dev& d, uint32_t n, uint32_t mode, hipStream_t s);
 hipError_t launch_ed25519_points(const Ed25519Dev& d, uint32_t n, hipStream_t s);
+// the points phase in two halves over raw rows (d.pk_rows / d.sig_rows): half 0 -A, then
+// half 1 R, on one stream (half 1 reads half 0's pstat)
+hipError_t launch_ed25519_points_half(const Ed25519Dev& d, int half, uint32_t n, hipStream_t s);
 size_t ed25519_key_table_bytes(uint32_t n_keys);
 hipError_t launch_ed25519_keyprep(const Ed25519Dev& d, const uint32_t* key_first, uint32_t n_keys, hipStream_t s);
 // Key dedupe at staging: key_index[i] = dense id of element i's 32-byte key among the

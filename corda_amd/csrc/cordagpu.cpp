@@ -950,6 +950,14 @@ bool ed_overlap_enabled() {
 // overrides the part count (0 or 1: off).  launch_verify then only joins those kernels
 // (cg_batch::points_early).
 constexpr uint32_t kEarlyPartMin = 65536;
+// Split points: a one-chunk call on the balanced path below the early-points sizes
+// uploads the key rows first and decodes the keys (cg_ed25519_points_half<0>) beside the
+// signature rows' copy, then R (<1>): after the last row only half of the points phase is
+// left.  CORDA_AMD_SPLIT_POINTS=0 turns it off.
+bool split_points_enabled() {
+  const char* e = std::getenv("CORDA_AMD_SPLIT_POINTS");
+  return !e || std::atoi(e) != 0;
+}
 uint32_t early_points_parts() {
   const char* e = std::getenv("CORDA_AMD_EARLY_POINTS");
   return e ? (uint32_t)std::min(8, std::max(0, std::atoi(e))) : 4u;
@@ -1151,15 +1159,44 @@ cg_status create_batch(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const ui
       const bool rows_direct =
           m.keep_raw && ed_identity && bad.empty() && pk_stride % 4 == 0 && sig_stride % 4 == 0 && ctx->ev_rows;
       uint32_t parts = 0;
+      bool split_points = false;
       if (rows_direct && n > ed_pair_max() && n <= kEdChunk && ed_overlap_enabled() &&
           !std::getenv("CORDA_AMD_ED_SPLIT")) {
         const int forced = key_reuse_forced();
         if (forced == 0 || (forced != 1 && !key_sample_suggests_reuse(pk, pk_stride, idx[0], (uint32_t)n))) {
           key_sample = 0;
           parts = std::min<uint32_t>(early_points_parts(), (uint32_t)(n / kEarlyPartMin));
+          split_points = parts <= 1 && split_points_enabled();
         }
       }
-      if (parts > 1) {
+      if (split_points) {  // the A half beside the signatures' copy (split_points_enabled)
+        if ((st = ensure_ed_scratch(ctx, (uint32_t)n)) != CG_OK ||
+            (st = dalloc(ctx, &pk_raw, n * pk_stride, "alloc pk")) != CG_OK ||
+            (st = dalloc(ctx, &sig_raw, n * sig_stride, "alloc sig")) != CG_OK)
+          return bail(st);
+        cg::Ed25519Dev d;
+        d.cap = (uint32_t)n;
+        d.scap = ctx->ed_scap;
+        d.pk_rows = reinterpret_cast<const uint32_t*>(pk_raw);
+        d.sig_rows = reinterpret_cast<const uint32_t*>(sig_raw);
+        d.pk_row_words = (uint32_t)(pk_stride / 4);
+        d.sig_row_words = (uint32_t)(sig_stride / 4);
+        d.pstat = ctx->ed_status + ctx->ed_scap;
+        d.table = ctx->ed_table;
+        for (int half = 0; half < 2; ++half) {
+          hipError_t e2 = half ? hipMemcpyAsync(sig_raw, sig, n * sig_stride, hipMemcpyHostToDevice, ctx->stream)
+                               : hipMemcpyAsync(pk_raw, pk, n * pk_stride, hipMemcpyHostToDevice, ctx->stream);
+          if (e2 == hipSuccess) e2 = hipEventRecord(ctx->ev_rows, ctx->stream);
+          if (e2 == hipSuccess) e2 = hipStreamWaitEvent(ctx->copy_stream, ctx->ev_rows, 0);
+          if (e2 != hipSuccess) return bail(hip_fail(ctx, e2, "upload rows"));
+          b->points_early = true;  // (from here on copy_stream may hold work: bail syncs it)
+          Timed t(ctx, half ? "ed25519_points_r" : "ed25519_points_a", n, ctx->copy_stream);
+          e2 = cg::launch_ed25519_points_half(d, half, (uint32_t)n, ctx->copy_stream);
+          if (e2 != hipSuccess) return bail(hip_fail(ctx, e2, "launch ed25519_points"));
+        }
+        const hipError_t e2 = hipEventRecord(ctx->ev_pts_done, ctx->copy_stream);
+        if (e2 != hipSuccess) return bail(hip_fail(ctx, e2, "points done"));
+      } else if (parts > 1) {
         if ((st = ensure_ed_scratch(ctx, (uint32_t)n)) != CG_OK ||
             (st = dalloc(ctx, &pk_raw, n * pk_stride, "alloc pk")) != CG_OK ||
             (st = dalloc(ctx, &sig_raw, n * sig_stride, "alloc sig")) != CG_OK)

@@ -195,6 +195,36 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_POINTS_W
   ed25519_build_table(R, [&](int k, const ge_cached& c) { store_slot(lt, 1, k, c); });
 }
 
+// The points phase in two halves (one-chunk host-buffer calls: the key rows land before
+// the signature rows, so the A half runs beside the signatures' copy): HALF 0 decodes -A
+// into point 0 of lane slot i and writes pstat[i] (KEY_INVALID / COMPUTE); HALF 1, ordered
+// after it on the same stream, decodes R (strict) into point 1 unless the key already
+// failed and writes REJECT / COMPUTE — together the verdict and tables of
+// ed25519_points_stage.  rows: word w of element i at rows[i * es + w].
+template <int HALF>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_POINTS_WAVES, 8))) void cg_ed25519_points_half(
+    const uint32_t* __restrict__ rows, uint32_t n, uint32_t es, uint32_t scap, uint32_t* __restrict__ pstat,
+    int32_t* __restrict__ table) {
+  CG_WAVE_PRIO(1);
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (HALF == 1 && pstat[i] != V_COMPUTE) return;
+  uint32_t w[8];
+  CG_UNROLL for (int k = 0; k < 8; ++k) w[k] = rows[(size_t)i * es + k];
+  ge_p3 P;
+  uint32_t ok = ge_frombytes_i2p(P, w);
+  if (HALF == 1) {
+    ok = ok && ge_strict_check(P, w);
+  } else {
+    fe_neg_p(P.X, P.X);  // -A kept floor-shaped, as ed25519_points_stage
+    fe_neg_p(P.T, P.T);
+  }
+  pstat[i] = ok ? V_COMPUTE : HALF ? V_REJECT : V_KEY_INVALID;
+  if (!ok) return;
+  const LaneTab lt = lane_table(table, i, scap);
+  ed25519_build_table(P, [&](int k, const ge_cached& c) { store_slot(lt, HALF, k, c); });
+}
+
 // Key-reuse path, once per distinct key and verify call: decode A and build its
 // four tables k * 2^(64 t) (-A) (lane-contiguous, kKeyEntries entries per key).
 constexpr int kKeyEntries = 4 * kATabEntries;
@@ -514,6 +544,17 @@ hipError_t launch_ed25519_keyprep(const Ed25519Dev& d, const uint32_t* key_first
   if (n_keys == 0) return hipSuccess;
   hipLaunchKernelGGL(cg_ed25519_keyprep, dim3((n_keys + 255) / 256), dim3(256), 0, s, d.pk, d.cap, key_first, n_keys,
                      const_cast<int32_t*>(d.ktab), const_cast<uint32_t*>(d.kstat));
+  return hipGetLastError();
+}
+
+hipError_t launch_ed25519_points_half(const Ed25519Dev& d, int half, uint32_t n, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  if (half == 0)
+    hipLaunchKernelGGL(cg_ed25519_points_half<0>, dim3((n + 255) / 256), dim3(256), 0, s, d.pk_rows, n,
+                       d.pk_row_words, d.scap, d.pstat, d.table);
+  else
+    hipLaunchKernelGGL(cg_ed25519_points_half<1>, dim3((n + 255) / 256), dim3(256), 0, s, d.sig_rows, n,
+                       d.sig_row_words, d.scap, d.pstat, d.table);
   return hipGetLastError();
 }
 

@@ -580,6 +580,8 @@ def test_one_chunk_verify_split_pieces_vs_oracle(gpu_ctx, oracle, monkeypatch, s
 
 
 @pytest.mark.parametrize("n,reverse,env,msg_bytes", [(160_000, True, "", 32), (160_000, False, "CORDA_AMD_EARLY_POINTS=0", 32),
+                                                     (160_000, True, "CORDA_AMD_EARLY_POINTS=0,CORDA_AMD_SPLIT_POINTS=0", 32),
+                                                     (50_000, True, "", 32),
                                                      (20_000, False, "", 32), (6_000, True, "", 1024)])
 def test_compute_bound_one_chunk_deferred_offsets_vs_oracle(gpu_ctx, oracle, monkeypatch, n, reverse, env, msg_bytes):
     """A compute-bound host-buffer call (32-byte tx ids: ~140 B per element) runs as ONE chunk
@@ -588,7 +590,9 @@ def test_compute_bound_one_chunk_deferred_offsets_vs_oracle(gpu_ctx, oracle, mon
     reading the raw 68-byte signature rows; the hash kernel reads the offsets through the
     batch's own arrays).  160,000 signatures: the rows go up in two parts (65,536-aligned
     boundary at 79,872) with each part's points kernel started on its arrival (early
-    points; EARLY_POINTS=0: one upload, one points kernel on the raw rows).  Arena in
+    points).  Below that (50,000, and 160,000 with EARLY_POINTS=0) the key rows go up first
+    and the keys are decoded beside the signature rows' copy, then R (split points;
+    SPLIT_POINTS=0: one points kernel on the raw rows after both copies).  Arena in
     reverse element order (offsets far from monotone), ragged E12 rows with sig_len, 20 %
     mutated, both modes, against the oracle; the larger call's deferred copy (>= 6 MB)
     runs beside the points kernel.  6,000 x 1 KB: a copy-bound call below the pipeline's
