@@ -27,6 +27,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <new>
 #include <string>
@@ -578,6 +579,22 @@ struct cg_batch {
   const uint64_t* meta_pending_off = nullptr;
   const uint32_t* meta_pending_len = nullptr;
   bool ed_meta_alias = false;
+  // async arena (async_arena_enabled): the deferred arena and offsets / lengths go up from
+  // the upload thread on hash_stream while the calling thread copies the rows; ctx->ev_arena
+  // is recorded after them once `done`
+  struct ArenaJob {
+    std::mutex m;
+    std::condition_variable cv;
+    bool done = false;
+    hipError_t err = hipSuccess;
+    hipEvent_t span[2] = {nullptr, nullptr};  // (profiling: the copies' h2d_arena span)
+    size_t bytes = 0;
+    void wait() {
+      std::unique_lock<std::mutex> g(m);
+      cv.wait(g, [&] { return done; });
+    }
+  };
+  std::unique_ptr<ArenaJob> arena_job;
   // one-chunk verify of an all-Ed25519 in-order batch: ctx->ev_rows marks the raw rows'
   // arrival (raw_kept[0..1], word strides below), so a latency-mode points kernel can
   // read them without waiting for the staging kernels
@@ -595,6 +612,10 @@ namespace {
 
 void batch_free(cg_ctx* ctx, cg_batch* b) {
   if (!b) return;
+  if (b->arena_job) {  // (a call that ended before launch_verify joined the arena copy)
+    b->arena_job->wait();
+    (void)hipStreamSynchronize(ctx->hash_stream);
+  }
   if (b->verdict_owned) dfree(ctx, b->verdict);
   dfree(ctx, b->bitmap);
   if (b->arena_owned) dfree(ctx, b->arena);
@@ -950,6 +971,17 @@ bool ed_overlap_enabled() {
 // overrides the part count (0 or 1: off).  launch_verify then only joins those kernels
 // (cg_batch::points_early).
 constexpr uint32_t kEarlyPartMin = 65536;
+// Async arena: a one-chunk call's deferred arena (and offsets / lengths) of at least
+// kAsyncArenaMin bytes goes up from the upload thread while the calling thread copies the
+// key and signature rows, instead of after them — below the early-points sizes, whose row
+// parts it would slow (r05x: 65,536 x 1 KB 2.19 -> 2.11 ms, 16,384 x 1 KB 0.79 -> 0.77;
+// but 4,096 x 1 KB 0.47 -> 0.56, the thread hand-off, and 2^17-2^18 x 32 B +0.05-0.15).
+// CORDA_AMD_ASYNC_ARENA=0 turns it off.
+constexpr size_t kAsyncArenaMin = (size_t)8 << 20;
+bool async_arena_enabled() {
+  const char* e = std::getenv("CORDA_AMD_ASYNC_ARENA");
+  return !e || std::atoi(e) != 0;
+}
 // Split points: a one-chunk call on the balanced path below the early-points sizes
 // uploads the key rows first and decodes the keys (cg_ed25519_points_half<0>) beside the
 // signature rows' copy, then R (<1>): after the last row only half of the points phase is
@@ -1091,6 +1123,7 @@ cg_status create_batch(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const ui
   debug_throw_point(ctx);
   bool ed_identity = true;
   int key_sample = -1;  // key_sample_suggests_reuse's answer, once asked
+  bool meta_deferred = false;  // offsets / lengths go up after create_batch (launch_verify or the upload thread)
   size_t n_ed = 0;  // Ed25519 elements (idx[0] stays empty when they are the whole batch in order)
   for (size_t i = 0; scheme_id && i < n; ++i) {
     const uint8_t s = scheme_id ? scheme_id[i] : CG_SCHEME_EDDSA_ED25519_SHA512;
@@ -1134,6 +1167,7 @@ cg_status create_batch(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const ui
     // points kernel starts after the key and signature rows alone (r05: 2^18 x 32 B ids
     // spent ~0.85 ms in copies before the first kernel)
     const bool defer_meta = defer_arena && ed_identity && bad.empty();
+    meta_deferred = defer_meta;
     Timed t(ctx, "h2d_stage", (defer_arena ? 0 : m.bytes) + (defer_meta ? 0 : 12 * n) +
                                   (raw_owned ? n * (pk_stride + sig_stride + (sig_len ? 4 : 0)) : 0));
     if (defer_arena) {
@@ -1154,6 +1188,45 @@ cg_status create_batch(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const ui
     } else {
       if ((st = upload(ctx, &b->msg_off_all, m.off_host, n, "upload msg_off")) != CG_OK) return bail(st);
       if ((st = upload(ctx, &b->msg_len_all, m.len_host, n, "upload msg_len")) != CG_OK) return bail(st);
+    }
+    if (defer_arena && m.bytes >= kAsyncArenaMin && n < 2 * (size_t)kEarlyPartMin && async_arena_enabled() &&
+        !std::getenv("CORDA_AMD_ED_SPLIT")) {
+      try {
+        if (!ctx->uploader) ctx->uploader = new JobThread(ctx->device);
+        b->arena_job.reset(new cg_batch::ArenaJob());
+        cg_batch::ArenaJob* job = b->arena_job.get();
+        uint8_t* arena = b->arena;
+        uint64_t* off_d = b->msg_off_all;
+        uint32_t* len_d = b->msg_len_all;
+        const uint64_t* off_h = b->meta_pending_off;
+        const uint32_t* len_h = b->meta_pending_len;
+        const uint8_t* host = m.host;
+        const size_t bytes = m.bytes;
+        hipStream_t hs = ctx->hash_stream;
+        hipEvent_t ev = ctx->ev_arena;
+        job->bytes = bytes;
+        if (ctx->profiling) {
+          job->span[0] = take_event(ctx);
+          job->span[1] = take_event(ctx);
+        }
+        ctx->uploader->post([=] {
+          if (job->span[0]) (void)hipEventRecord(job->span[0], hs);
+          hipError_t e2 = hipMemcpyAsync(arena, host, bytes, hipMemcpyHostToDevice, hs);
+          if (e2 == hipSuccess && off_h) e2 = hipMemcpyAsync(off_d, off_h, n * 8, hipMemcpyHostToDevice, hs);
+          if (e2 == hipSuccess && len_h) e2 = hipMemcpyAsync(len_d, len_h, n * 4, hipMemcpyHostToDevice, hs);
+          if (e2 == hipSuccess && job->span[1]) (void)hipEventRecord(job->span[1], hs);
+          if (e2 == hipSuccess) e2 = hipEventRecord(ev, hs);
+          std::lock_guard<std::mutex> g(job->m);
+          job->err = e2;
+          job->done = true;
+          job->cv.notify_all();
+        });
+        b->arena_pending = nullptr;
+        b->meta_pending_off = nullptr;
+        b->meta_pending_len = nullptr;
+      } catch (...) {  // (no thread: the copies stay deferred to launch_verify)
+        b->arena_job.reset();
+      }
     }
     if (raw_owned) {
       const bool rows_direct =
@@ -1266,7 +1339,7 @@ cg_status create_batch(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const ui
     if (ne) {
       if (!ed_identity && (st = upload_idx(ctx, &b->ed_index, idx[0].data(), ne, "upload ed index")) != CG_OK)
         return bail(st);
-      b->ed_meta_alias = b->meta_pending_off != nullptr;
+      b->ed_meta_alias = meta_deferred;  // (the offsets / lengths are not on the device yet: no gather)
       if (b->ed_meta_alias) {  // (identity order: the gathered copies would equal them)
         b->ed_msg_off = b->msg_off_all;
         b->ed_msg_len = b->msg_len_all;
@@ -1572,6 +1645,18 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = 
         // cross-stream wait cost more than the copy's head start, +0.01 ms).
         // CORDA_AMD_ARENA_BESIDE=0 keeps it on ctx->stream.
         auto upload_pending_arena = [&](bool beside) -> cg_status {
+          if (b->arena_job) {  // issued by the upload thread: the hash kernel waits for ev_arena
+            b->arena_job->wait();
+            const hipError_t e2 = b->arena_job->err;
+            if (b->arena_job->span[0] && b->arena_job->span[1]) {
+              ctx->pending.push_back({"h2d_arena", {b->arena_job->span[0], b->arena_job->span[1]}});
+              ctx->stats["h2d_arena"].items += b->arena_job->bytes;
+            }
+            b->arena_job.reset();
+            CG_TRY(ctx, e2, "upload arena");
+            CG_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_arena, 0), "wait arena");
+            return CG_OK;
+          }
           if (!b->arena_pending) return CG_OK;
           const char* ab = std::getenv("CORDA_AMD_ARENA_BESIDE");
           const size_t pending = b->arena_pending_bytes + (b->meta_pending_off ? (size_t)12 * b->n : 0);

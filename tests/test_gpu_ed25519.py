@@ -582,7 +582,8 @@ def test_one_chunk_verify_split_pieces_vs_oracle(gpu_ctx, oracle, monkeypatch, s
 @pytest.mark.parametrize("n,reverse,env,msg_bytes", [(160_000, True, "", 32), (160_000, False, "CORDA_AMD_EARLY_POINTS=0", 32),
                                                      (160_000, True, "CORDA_AMD_EARLY_POINTS=0,CORDA_AMD_SPLIT_POINTS=0", 32),
                                                      (50_000, True, "", 32),
-                                                     (20_000, False, "", 32), (6_000, True, "", 1024)])
+                                                     (20_000, False, "", 32), (6_000, True, "", 1024),
+                                                     (12_000, True, "", 1024), (12_000, False, "CORDA_AMD_ASYNC_ARENA=0", 1024)])
 def test_compute_bound_one_chunk_deferred_offsets_vs_oracle(gpu_ctx, oracle, monkeypatch, n, reverse, env, msg_bytes):
     """A compute-bound host-buffer call (32-byte tx ids: ~140 B per element) runs as ONE chunk
     up to 2^20 elements, and for an Ed25519-only in-order batch its offsets and lengths go
@@ -596,7 +597,9 @@ def test_compute_bound_one_chunk_deferred_offsets_vs_oracle(gpu_ctx, oracle, mon
     reverse element order (offsets far from monotone), ragged E12 rows with sig_len, 20 %
     mutated, both modes, against the oracle; the larger call's deferred copy (>= 6 MB)
     runs beside the points kernel.  6,000 x 1 KB: a copy-bound call below the pipeline's
-    threshold, one chunk in the eight-lane latency mode, its 6 MB arena deferred."""
+    threshold, one chunk in the eight-lane latency mode, its 6 MB arena deferred; 12,000 x 1 KB (12 MB)
+    the same with the arena and its offsets / lengths issued from the upload thread beside
+    the row copies (async arena; ASYNC_ARENA=0: after them)."""
     for kv in filter(None, env.split(",")):
         monkeypatch.setenv(*kv.split("=", 1))
     w = datagen.add_ed25519_adversarial(datagen.make_batch(n, msg_bytes=msg_bytes, seed=101, key_base=1_700_000),
