@@ -51,6 +51,9 @@ constexpr uint32_t kEdSplitMin = 65536;
 // 32,768 1.51 -> 1.37 ms with it, 65,536 2.21 -> 2.36 ms (slower: two waves per SIMD
 // already), so the crossover lies between 32k and 64k signatures
 constexpr uint32_t kEdPairMaxDefault = 40000;
+// ... for a one-chunk host-buffer call, by its bytes per element (verify_copy_bound)
+constexpr uint32_t kEdPairMaxCopyBound = 32768;
+constexpr uint32_t kEdPairMaxCompute = 20480;
 // ... and up to this size with four lanes per signature (the scalars' 64-bit halves
 // over 2^64-multiple tables: ~64 doublings per lane instead of ~128)
 constexpr uint32_t kEdQuadMaxDefault = 32768;
@@ -600,6 +603,7 @@ struct cg_batch {
   // read them without waiting for the staging kernels
   bool rows_event = false;
   uint32_t raw_pk_words = 0, raw_sig_words = 0;
+  uint32_t pair_max = 0;  // latency-mode threshold of this batch (MsgSrc::pair_max; 0: the default)
   // early points (early_points_parts): the balanced points kernels already run on
   // ctx->copy_stream and ctx->ev_pts_done marks their end
   bool points_early = false;
@@ -670,6 +674,7 @@ struct MsgSrc {
   // one-chunk cg_verify_batch: the raw rows stay with the batch (freed by batch_free
   // after the call's final sync) instead of a host sync at the end of staging
   bool keep_raw = false;
+  uint32_t pair_max = 0;  // the batch's latency-mode threshold (0: kEdPairMaxDefault)
 };
 
 cg_status check_inputs(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const uint8_t* pk, size_t pk_stride,
@@ -914,10 +919,11 @@ int key_reuse_forced() {
 
 // Latency mode (ed25519_kernels.hip cg_ed25519_points_lanes / _msm_lanes: two lanes per
 // signature) for Ed25519 pieces of at most this many signatures on the balanced path;
-// CORDA_AMD_ED_PAIR_MAX overrides (0: never).
-uint32_t ed_pair_max() {
+// CORDA_AMD_ED_PAIR_MAX overrides (0: never).  call_default: the batch's own threshold
+// (cg_batch::pair_max; a one-chunk host-buffer call sets it by its bytes per element).
+uint32_t ed_pair_max(uint32_t call_default = 0) {
   const char* e = std::getenv("CORDA_AMD_ED_PAIR_MAX");
-  return e ? (uint32_t)std::max(0, std::atoi(e)) : kEdPairMaxDefault;
+  return e ? (uint32_t)std::max(0, std::atoi(e)) : call_default ? call_default : kEdPairMaxDefault;
 }
 // Latency mode: the hash and points kernels run side by side with a few blocks each,
 // and the dispatcher packs those blocks onto the same CUs, where they slow each other
@@ -1032,7 +1038,7 @@ cg_status stage_key_dedupe(cg_ctx* ctx, cg_batch* b, const uint8_t* pk, size_t p
   // automatic mode and a batch the latency mode will verify: the key-reuse path's
   // per-key table build (~190 doublings, one wave per 64 keys) would be the longest
   // chain of the call, and the exact count is a host round trip
-  if (forced != 1 && ne <= ed_pair_max()) return CG_OK;
+  if (forced != 1 && ne <= ed_pair_max(b->pair_max)) return CG_OK;
   if (forced != 1 && !(sample >= 0 ? sample == 1 : key_sample_suggests_reuse(pk, pk_stride, idx0, ne))) return CG_OK;
   uint32_t tsize = 1;
   while (tsize < 2 * ne) tsize <<= 1;
@@ -1097,6 +1103,7 @@ cg_status create_batch(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const ui
   cg_batch* b = new (std::nothrow) cg_batch();
   if (!b) return fail(ctx, CG_E_OUT_OF_MEMORY, "host alloc");
   b->n = n;
+  b->pair_max = m.pair_max;
   // raw element-major inputs (temporary)
   uint8_t *pk_raw = nullptr, *sig_raw = nullptr;
   uint32_t* sl_raw = nullptr;
@@ -1233,7 +1240,7 @@ cg_status create_batch(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const ui
           m.keep_raw && ed_identity && bad.empty() && pk_stride % 4 == 0 && sig_stride % 4 == 0 && ctx->ev_rows;
       uint32_t parts = 0;
       bool split_points = false;
-      if (rows_direct && n > ed_pair_max() && n <= kEdChunk && ed_overlap_enabled() &&
+      if (rows_direct && n > ed_pair_max(b->pair_max) && n <= kEdChunk && ed_overlap_enabled() &&
           !std::getenv("CORDA_AMD_ED_SPLIT")) {
         const int forced = key_reuse_forced();
         if (forced == 0 || (forced != 1 && !key_sample_suggests_reuse(pk, pk_stride, idx[0], (uint32_t)n))) {
@@ -1534,7 +1541,7 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = 
       }
     }
     if (b->n_ed) {
-      const uint32_t pair_max = ed_pair_max();
+      const uint32_t pair_max = ed_pair_max(b->pair_max);
       // four lanes per signature: tables in 2 n_ed scratch slots — grown for it only where
       // this call owns the whole scratch; inside a pipeline only if its region has room
       const bool quad_want = !b->ed_key_index && b->n_ed <= std::min(pair_max, ed_quad_max());
@@ -2388,8 +2395,8 @@ cg_status cg_verify_batch(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
       c->call_begin = nullptr;
     }
   } call_span_end{ctx};
-  const std::vector<size_t> cb =
-      verify_chunk_bounds(n, verify_copy_bound(n, msg_bytes, 12 + pk_stride + sig_stride + (sig_len ? 4 : 0)));
+  const bool copy_bound = verify_copy_bound(n, msg_bytes, 12 + pk_stride + sig_stride + (sig_len ? 4 : 0));
+  const std::vector<size_t> cb = verify_chunk_bounds(n, copy_bound);
   if (cb.size() == 2) {  // one chunk: stage, then verify, with one host sync at the end
     MsgSrc m;
     m.host = msg;
@@ -2397,6 +2404,10 @@ cg_status cg_verify_batch(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
     m.off_host = msg_off;
     m.len_host = msg_len;
     m.keep_raw = true;
+    // latency mode only up to where it beats the balanced path with split points (r05z:
+    // 32 B ids 24,576 0.84 vs 0.81 ms, 40,000 0.97 vs 0.83; 1 KB 32,768 1.21 vs 1.33, 40,000
+    // 1.65 vs 1.49)
+    m.pair_max = copy_bound ? kEdPairMaxCopyBound : kEdPairMaxCompute;
     cg_batch* b = nullptr;
     cg_status st = create_batch(ctx, n, scheme_id, pk, pk_stride, sig, sig_stride, sig_len, m, &b);
     if (st != CG_OK) return st;
