@@ -38,6 +38,12 @@ struct Ed25519Dev {
   const uint32_t* pk_rows = nullptr;
   const uint32_t* sig_rows = nullptr;
   uint32_t pk_row_words = 0, sig_row_words = 0;
+  // balanced MSM with its lanes grouped by digit count (launch_ed25519_bucket; null: in
+  // index order): order[c * scap + k] = the k-th lane of class c (0: >= 34 digits, 1: 33,
+  // 2: 32); order_count: four words per 1,024-lane block (its class sizes; the class
+  // totals in words 3, 7, 11), at most n words
+  uint32_t* order = nullptr;
+  uint32_t* order_count = nullptr;
 };
 
 size_t ed25519_btab_words();
@@ -60,6 +66,11 @@ hipError_t launch_key_dedupe(const uint32_t* pk, uint32_t n, uint32_t cap, uint3
                              uint32_t* key_first, hipStream_t s);
 hipError_t launch_ed25519_msm(const Ed25519Dev& d, uint32_t n, const uint32_t* out_index, uint8_t* verdict,
                               hipStream_t s);
+// Before a grouped balanced MSM (d.order set; n >= 3,072): one lane per element merges
+// the hash and points verdicts — writes the final verdict of every lane the MSM need not
+// run — and places each live lane in its digit-count class (index order within a class).
+hipError_t launch_ed25519_bucket(const Ed25519Dev& d, uint32_t n, const uint32_t* out_index, uint8_t* verdict,
+                                 hipStream_t s);
 // Latency mode (lanes = 2 or 4 lanes per signature, balanced path only: d.key_index
 // null): the points phase (pstat byte 4i + q: lane q's point verdict) and the MSM.
 // lanes = 4 keeps its tables in scratch slots [0, 2n) of the view: the caller sizes

@@ -62,6 +62,8 @@ constexpr uint32_t kEdQuadMaxDefault = 32768;
 // against four lanes, 8,192 +0.07 ms — past ~7,280 signatures the eight-lane points
 // blocks and the hash blocks no longer get a CU each (ed_spread_lds)
 constexpr uint32_t kEdOctMaxDefault = 7168;
+// grouped balanced MSM (cg_ed25519_bucket) from this many signatures per piece
+constexpr uint32_t kEdBucketMinDefault = 16384;
 constexpr uint32_t kEdSplitDefault = 1;  // r03d A/B: 2 or 4 pieces measured no faster (95-96 M/s either way)
 
 struct Stat {
@@ -525,8 +527,10 @@ cg_status ensure_ed_scratch(cg_ctx* ctx, uint32_t need, uint32_t limit = kEdChun
   ctx->ed_table = nullptr;
   ctx->ed_scap = 0;
   cg_status st;
-  // status words of the hash phase [0, want) and of the points phase [want, 2 want)
-  if ((st = dalloc(ctx, &ctx->ed_status, 2 * (size_t)want, "alloc ed25519 status")) != CG_OK) return st;
+  // status words of the hash phase [0, want) and of the points phase [want, 2 want), the
+  // grouped MSM's three lane classes [(2 + c) want, (3 + c) want) and its block counts
+  // [5 want, 6 want) (a piece uses fewer words than lanes, from its first lane on)
+  if ((st = dalloc(ctx, &ctx->ed_status, 6 * (size_t)want, "alloc ed25519 status")) != CG_OK) return st;
   if ((st = dalloc(ctx, &ctx->ed_digits, cg::ed25519_digit_words() * want, "alloc ed25519 digits")) != CG_OK) return st;
   if ((st = dalloc(ctx, (uint8_t**)&ctx->ed_table, cg::ed25519_table_bytes(want), "alloc ed25519 table")) != CG_OK)
     return st;
@@ -959,6 +963,14 @@ uint32_t ed_quad_max() {
 uint32_t ed_oct_max() {
   const char* e = std::getenv("CORDA_AMD_ED_OCT_MAX");
   return e ? (uint32_t)std::max(0, std::atoi(e)) : kEdOctMaxDefault;
+}
+
+// Balanced MSM pieces of at least this many signatures run over lanes grouped by digit
+// count (cg_ed25519_bucket); CORDA_AMD_ED_BUCKET_MIN overrides (0: never).
+uint32_t ed_bucket_min() {
+  const char* e = std::getenv("CORDA_AMD_ED_BUCKET_MIN");
+  const int v = e ? std::atoi(e) : (int)kEdBucketMinDefault;
+  return v > 0 ? (uint32_t)v : UINT32_MAX;
 }
 
 bool ed_overlap_enabled() {
@@ -1630,6 +1642,11 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = 
           d.kstat = ctx->ed_kstat;
         }
         const bool pair = allow_lanes && !b->ed_key_index && cnt <= pair_max;  // latency mode
+        // balanced MSM over lanes grouped by digit count
+        if (!pair && !b->ed_key_index && cnt >= std::max<uint32_t>(ed_bucket_min(), 4096)) {
+          d.order = ctx->ed_status + 2 * (size_t)ctx->ed_scap + soff;
+          d.order_count = ctx->ed_status + 5 * (size_t)ctx->ed_scap + soff;
+        }
         // (quad_ok / oct_ok: one piece with 2 / 4 cnt scratch slots in its region)
         const uint32_t lanes = !pair ? 1u : oct_ok && split == 1 ? 8u : quad_ok && split == 1 ? 4u : 2u;
         if (pair)
@@ -1733,11 +1750,15 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = 
             CG_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_keys, 0), "wait keyprep");
           if ((s2 = launch_points(ctx->stream)) != CG_OK) return s2;
         }
+        const uint32_t* oi = b->ed_index ? b->ed_index + base : nullptr;
+        uint8_t* vd = b->ed_index ? b->verdict : b->verdict + base;
+        if (d.order) {
+          Timed t(ctx, "ed25519_bucket", cnt);
+          CG_TRY(ctx, cg::launch_ed25519_bucket(d, cnt, oi, vd, ctx->stream), "launch ed25519_bucket");
+        }
         {
           Timed t(ctx, lanes == 8 ? "ed25519_msm_oct" : lanes == 4 ? "ed25519_msm_quad" : pair ? "ed25519_msm_pair" : "ed25519_msm",
                   cnt);
-          const uint32_t* oi = b->ed_index ? b->ed_index + base : nullptr;
-          uint8_t* vd = b->ed_index ? b->verdict : b->verdict + base;
           CG_TRY(ctx,
                  pair ? cg::launch_ed25519_msm_lanes(d, cnt, lanes, oi, vd, ctx->stream)
                       : cg::launch_ed25519_msm(d, cnt, oi, vd, ctx->stream),

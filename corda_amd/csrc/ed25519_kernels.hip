@@ -335,18 +335,32 @@ CG_DEV uint32_t msm_lane(uint32_t ndig, const uint32_t* dig, uint32_t scap, uint
   return ed25519_msm<RawEntry, LateSlot>(ndig, getDig, rneg, loadA, unpackA, loadR, unpackR, getB);
 }
 
+// Lane j of a grouped MSM (order != null): the classes' lanes back to back (class 0, the
+// longest, dispatched first), from the counts the bucket kernel left; past the last class
+// the lane has nothing to do (its verdict, if any, the bucket kernel wrote).
+CG_DEV uint32_t grouped_lane(uint32_t j, const uint32_t* __restrict__ order, const uint32_t* __restrict__ count,
+                             uint32_t scap, bool& in) {
+  const uint32_t n0 = count[3], n01 = n0 + count[7], all = n01 + count[11];  // cg_ed25519_bucket_scatter
+  in = j < all;
+  const size_t k = j < n0 ? j : j < n01 ? (size_t)scap + (j - n0) : 2 * (size_t)scap + (j - n01);
+  return in ? order[k] : 0u;
+}
+
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_MSM_WAVES, CG_MSM_WAVES))) void cg_ed25519_msm(
-    const uint32_t* __restrict__ sig, const uint32_t* __restrict__ status, const uint32_t* __restrict__ pstat,
-    const uint32_t* __restrict__ digits, const int32_t* __restrict__ table, const int32_t* __restrict__ btab_g,
-    uint32_t n, uint32_t cap, uint32_t scap, const uint32_t* __restrict__ out_index, uint8_t* __restrict__ verdict) {
+    const uint32_t* __restrict__ status, const uint32_t* __restrict__ pstat, const uint32_t* __restrict__ digits,
+    const int32_t* __restrict__ table, const int32_t* __restrict__ btab_g, uint32_t n, uint32_t scap,
+    const uint32_t* __restrict__ order, const uint32_t* __restrict__ order_count,
+    const uint32_t* __restrict__ out_index, uint8_t* __restrict__ verdict) {
   CG_WAVE_PRIO(0);
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t st = i < n ? status[i] : 0u;
-  const uint32_t v = i < n ? ed_merge_verdict(st, pstat[i]) : 0u;
-  const bool live = i < n && v == V_COMPUTE;
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  bool in = j < n;
+  const uint32_t i = order ? grouped_lane(j, order, order_count, scap, in) : j;
+  const uint32_t st = in ? status[i] : 0u;
+  const uint32_t v = in ? ed_merge_verdict(st, pstat[i]) : 0u;
+  const bool live = in && v == V_COMPUTE;
   // every lane of the wave walks the same bit positions: the longest scalar sets the length
   const uint32_t ndig = wave_max(live ? ed_status_ndig(st) : 0u);
-  if (i >= n) return;
+  if (!in) return;
   const uint32_t dst = out_index ? out_index[i] : i;
   if (!live) {
     verdict[dst] = (uint8_t)v;
@@ -358,6 +372,98 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CG_MSM_WAVE
   verdict[dst] = ok ? (uint8_t)V_ACCEPT : (uint8_t)V_REJECT;
 }
 
+// Lanes grouped by digit count for the balanced MSM (round 6).  The MSM's loop length is
+// the wave's largest digit count; in index order ~23 % of waves hold one of the 0.4 % of
+// lanes with 34 digits and none runs fewer than 33 (32 for 34 % of lanes): grouping cuts
+// the windows per lane from 33.2 to 32.7 (profiles/r06_digit_hist.json).  Two passes
+// over 1,024-lane blocks, no atomics (a first version appended every wave's lanes with
+// one atomicAdd per wave and class on three words: +0.6 ms per 1 M, r06a), and the order
+// within a class is the index order:
+//   cg_ed25519_bucket_count    lanes the MSM need not run (hash or points verdict final)
+//                              get their verdict; the block's class sizes -> blk[4 b + c]
+//   cg_ed25519_bucket_scatter  block b sums the sizes of blocks < b (at most a few
+//                              thousand words), places its live lanes in their classes;
+//                              the last block writes the class totals to blk[4 c + 3]
+// Class of a lane: 0 >= 34 digits, 1: 33, 2: 32, 3: not live.
+constexpr uint32_t kBucketBlock = 1024;
+CG_DEV uint32_t bucket_class(const uint32_t* __restrict__ status, const uint32_t* __restrict__ pstat, uint32_t i,
+                             uint32_t n, uint32_t& v) {
+  const bool in = i < n;
+  const uint32_t st = in ? status[i] : 0u;
+  v = in ? ed_merge_verdict(st, pstat[i]) : 0u;
+  const uint32_t nd = ed_status_ndig(st);
+  return !(in && v == V_COMPUTE) ? 3u : nd >= 34u ? 0u : nd == 33u ? 1u : 2u;
+}
+
+__global__ __launch_bounds__(kBucketBlock) void cg_ed25519_bucket_count(const uint32_t* __restrict__ status,
+                                                                        const uint32_t* __restrict__ pstat, uint32_t n,
+                                                                        uint32_t* __restrict__ blk,
+                                                                        const uint32_t* __restrict__ out_index,
+                                                                        uint8_t* __restrict__ verdict) {
+  CG_WAVE_PRIO(1);
+  __shared__ uint32_t part[kBucketBlock / 64][3];
+  const uint32_t i = blockIdx.x * kBucketBlock + threadIdx.x, wv = threadIdx.x / 64;
+  uint32_t v;
+  const uint32_t cls = bucket_class(status, pstat, i, n, v);
+  if (i < n && cls == 3u) verdict[out_index ? out_index[i] : i] = (uint8_t)v;
+  CG_UNROLL for (uint32_t c = 0; c < 3; ++c) {
+    const uint32_t k = (uint32_t)__popcll(__ballot(cls == c));
+    if ((threadIdx.x & 63u) == 0) part[wv][c] = k;
+  }
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    uint32_t t = 0;
+    CG_UNROLL for (uint32_t w = 0; w < kBucketBlock / 64; ++w) t += part[w][threadIdx.x];
+    blk[4 * blockIdx.x + threadIdx.x] = t;
+  }
+}
+
+__global__ __launch_bounds__(kBucketBlock) void cg_ed25519_bucket_scatter(const uint32_t* __restrict__ status,
+                                                                          const uint32_t* __restrict__ pstat,
+                                                                          uint32_t n, uint32_t scap,
+                                                                          uint32_t* __restrict__ blk,
+                                                                          uint32_t* __restrict__ order) {
+  CG_WAVE_PRIO(1);
+  __shared__ uint32_t part[kBucketBlock / 64][3];
+  __shared__ uint32_t base[3];
+  const uint32_t b = blockIdx.x, wv = threadIdx.x / 64, lane = threadIdx.x & 63u;
+  // this block's class offsets: the sizes of the blocks before it (the last block also
+  // adds its own: the totals the MSM reads)
+  const uint32_t upto = b + 1 == gridDim.x ? b + 1 : b;
+  uint32_t s[3] = {0, 0, 0};
+  for (uint32_t k = threadIdx.x; k < upto; k += kBucketBlock)
+    CG_UNROLL for (uint32_t c = 0; c < 3; ++c) s[c] += blk[4 * k + c];
+  CG_UNROLL for (uint32_t c = 0; c < 3; ++c) {
+    CG_UNROLL for (int o = 32; o >= 1; o >>= 1) s[c] += (uint32_t)__shfl_xor((int)s[c], o, 64);
+    if (lane == 0) part[wv][c] = s[c];
+  }
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    uint32_t t = 0;
+    CG_UNROLL for (uint32_t w = 0; w < kBucketBlock / 64; ++w) t += part[w][threadIdx.x];
+    if (b + 1 == gridDim.x) {  // totals, then back to this block's own offsets
+      blk[4 * threadIdx.x + 3] = t;
+      t -= blk[4 * b + threadIdx.x];
+    }
+    base[threadIdx.x] = t;
+  }
+  __syncthreads();
+  const uint32_t i = b * kBucketBlock + threadIdx.x;
+  uint32_t v;
+  const uint32_t cls = bucket_class(status, pstat, i, n, v);
+  const uint64_t below = lane ? (~0ull >> (64u - lane)) : 0ull;
+  uint64_t m[3];
+  CG_UNROLL for (uint32_t c = 0; c < 3; ++c) {
+    m[c] = __ballot(cls == c);
+    if (lane == 0) part[wv][c] = (uint32_t)__popcll(m[c]);
+  }
+  __syncthreads();
+  if (cls < 3u) {
+    uint32_t off = base[cls];
+    for (uint32_t w = 0; w < wv; ++w) off += part[w][cls];
+    order[(size_t)cls * scap + off + (uint32_t)__popcll(m[cls] & below)] = i;
+  }
+}
 
 // ---------------------------------------------------------------- latency mode
 // Small batches (a notary's request queue: ValidatingNotaryFlow.kt:34-40) leave most
@@ -620,8 +726,20 @@ hipError_t launch_ed25519_msm(const Ed25519Dev& d, uint32_t n, const uint32_t* o
     hipLaunchKernelGGL(cg_ed25519_msm_r, dim3((n + 255) / 256), dim3(256), 0, s, d.status, d.pstat, d.digits, d.table,
                        d.ktab, d.key_index, d.btab, n, d.scap, out_index, verdict);
   else
-    hipLaunchKernelGGL(cg_ed25519_msm, dim3((n + 255) / 256), dim3(256), 0, s, d.sig, d.status, d.pstat, d.digits,
-                       d.table, d.btab, n, d.cap, d.scap, out_index, verdict);
+    hipLaunchKernelGGL(cg_ed25519_msm, dim3((n + 255) / 256), dim3(256), 0, s, d.status, d.pstat, d.digits, d.table,
+                       d.btab, n, d.scap, d.order, d.order_count, out_index, verdict);
+  return hipGetLastError();
+}
+
+hipError_t launch_ed25519_bucket(const Ed25519Dev& d, uint32_t n, const uint32_t* out_index, uint8_t* verdict,
+                                 hipStream_t s) {
+  // the class totals live in the 4th words of the first three block entries
+  if (!d.order || !d.order_count || d.key_index || n < 3 * kBucketBlock) return hipErrorInvalidValue;
+  const dim3 grid((n + kBucketBlock - 1) / kBucketBlock);
+  hipLaunchKernelGGL(cg_ed25519_bucket_count, grid, dim3(kBucketBlock), 0, s, d.status, d.pstat, n, d.order_count,
+                     out_index, verdict);
+  hipLaunchKernelGGL(cg_ed25519_bucket_scatter, grid, dim3(kBucketBlock), 0, s, d.status, d.pstat, n, d.scap,
+                     d.order_count, d.order);
   return hipGetLastError();
 }
 

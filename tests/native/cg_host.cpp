@@ -106,6 +106,18 @@ int cgh_ed25519_verify_nd(const uint8_t* pk_bytes, const uint8_t* sig_bytes, uin
   return ok ? (int)V_ACCEPT : (int)V_REJECT;
 }
 
+// The hash phase's digit count (status bits 8-15) and digit words of one signature
+// (tools/digit_hist.py, tests: the count must equal 1 + the highest nonzero digit).
+uint32_t cgh_ed25519_hash_ndig(const uint8_t* pk_bytes, const uint8_t* sig_bytes, const uint8_t* msg, uint32_t msg_len,
+                               uint32_t* dig_out) {
+  uint32_t pk[8], sig[16], dig[kDigitWords], ndig, rneg;
+  memcpy(pk, pk_bytes, 32);
+  memcpy(sig, sig_bytes, 64);
+  const uint32_t pre = ed25519_hash_stage(pk, sig, 64, msg, msg_len, MODE_IS_VALID, dig, ndig, rneg);
+  if (dig_out) memcpy(dig_out, dig, sizeof dig);
+  return pre == V_COMPUTE ? ndig : 0u;
+}
+
 int cgh_ed25519_verify(const uint8_t* pk_bytes, const uint8_t* sig_bytes, uint32_t sig_len, const uint8_t* msg,
                        uint32_t msg_len, uint32_t mode) {
   return cgh_ed25519_verify_nd(pk_bytes, sig_bytes, sig_len, msg, msg_len, mode, 0, 0);

@@ -223,6 +223,44 @@ def test_forced_full_length_fallback_vs_oracle(gpu_ctx, oracle, golden_ed25519, 
         gpu_ctx.set_debug(DEBUG_FORCE_FULL_LENGTH, 0)
 
 
+@pytest.mark.parametrize("bucket_min", ["0", "1", None])
+@pytest.mark.parametrize("mixed", [False, True])
+def test_grouped_msm_vs_oracle(gpu_ctx, oracle, golden_ed25519, monkeypatch, bucket_min, mixed):
+    """The balanced MSM over lanes grouped by digit count (cg_ed25519_bucket; round 6)
+    against the oracle: off ('0'), from 4,096 signatures ('1'), and
+    the default threshold (every piece of at least 4,096 grouped with '1').  Latency lanes off so the balanced MSM runs; every 97th lane
+    takes the 64-digit (h, 1) fallback, so class 0 holds long lanes; 30 % mutations put
+    hash- and points-phase verdicts (written by the bucket kernel) among them; the mixed
+    batch scatters the Ed25519 verdicts through the scheme partition's index."""
+    from corda_amd._lib import DEBUG_FORCE_FULL_LENGTH
+    monkeypatch.setenv("CORDA_AMD_ED_PAIR_MAX", "0")
+    if bucket_min is not None:
+        monkeypatch.setenv("CORDA_AMD_ED_BUCKET_MIN", bucket_min)
+    g = golden_ed25519
+    gb = crypto.pack(crypto.EDDSA_ED25519_SHA512, [bytes.fromhex(e["pk"]) for e in g],
+                     [bytes.fromhex(e["sig"]) for e in g], [bytes.fromhex(e["msg"]) for e in g])
+    n = 40_000
+    scheme = 4
+    if mixed:
+        scheme = np.random.default_rng(3).choice(np.array([4, 4, 4, 2, 3], np.uint8), size=n)
+    w = datagen.make_batch(n, msg_bytes=48, scheme=scheme, seed=31, key_base=4_400)
+    w = datagen.add_ed25519_adversarial(w, frac=0.3, seed=13)
+    gpu_ctx.set_debug(DEBUG_FORCE_FULL_LENGTH, 97)
+    try:
+        for mode, key in ((MODE_IS_VALID, "is_valid"), (MODE_DO_VERIFY, "do_verify")):
+            v = crypto.verify_packed(gpu_ctx, gb, mode)
+            exp = np.array([e[key] for e in g], dtype=np.uint8)
+            bad = np.flatnonzero(v != exp)
+            assert bad.size == 0, [(g[i]["cls"], int(v[i]), int(exp[i])) for i in bad[:10]]
+            got = gpu_verdicts(gpu_ctx, w, mode)
+            want = oracle_verdicts(oracle, w, mode)
+            bad = np.flatnonzero(got != want)
+            assert bad.size == 0, (bad[:10].tolist(), got[bad[:10]].tolist(), want[bad[:10]].tolist())
+        assert (got == ACCEPT).sum() > n // 3
+    finally:
+        gpu_ctx.set_debug(DEBUG_FORCE_FULL_LENGTH, 0)
+
+
 @pytest.fixture
 def key_reuse(monkeypatch, request):
     """CORDA_AMD_KEY_REUSE: '1' forces the key-reuse path, '0' the balanced one,

@@ -166,6 +166,32 @@ def test_half_scalars_property(host):
             assert (C0, C1) == (h, 1)
 
 
+def test_hash_digit_count_is_exact(host):
+    """The hash phase's digit count (the balanced MSM's loop length and its grouping
+    class) is 1 + the highest nonzero signed radix-16 digit of c0 or |c1|, at least 32,
+    and the digits recode c0 and |c1| exactly (round 6: exact count instead of the
+    bit-length bound; a count one short would drop a digit and reject valid signatures,
+    which test_verify_random_vs_oracle catches on the lanes' own counts)."""
+    host.cgh_ed25519_hash_ndig.restype = ctypes.c_uint32
+    host.cgh_ed25519_hash_ndig.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32,
+                                           ctypes.c_void_p]
+    rnd = random.Random(11)
+    dig = (ctypes.c_uint32 * 24)()
+    seen = set()
+
+    def digits(words):
+        return [((words[j >> 3] >> (4 * (j & 7))) & 15) - 8 for j in range(64)]
+
+    for _ in range(3000):
+        r = rnd.randbytes(128)
+        nd = host.cgh_ed25519_hash_ndig(r[:32], r[32:96], r[96:], 32, dig)
+        d0, d1 = digits(dig[0:8]), digits(dig[8:16])
+        top = max([j for j in range(64) if d0[j] or d1[j]] + [-1]) + 1
+        assert nd == max(32, top)
+        seen.add(nd)
+    assert {32, 33} <= seen and max(seen) <= 35
+
+
 def _half_scalars_euclid(h, tb_bits=128, c1_bits=252):
     def cost(l0, l1):
         return max(l0, l1) if tb_bits == 128 else (1000 if l1 > c1_bits else l0)
