@@ -106,7 +106,7 @@ def parse():
     p.add_argument("--key-reuse", type=int, default=0,
                    help="ed25519/backlog/tx: draw signer keys from this many distinct keys (0 = all distinct)")
     p.add_argument("--no-extra", action="store_true",
-                   help="ed25519 (N=1): skip the 32 B tx-id end-to-end record and the config-3 sub-record")
+                   help="ed25519 (N=1): skip the 32 B tx-id end-to-end record and the config-3 / config-4 sub-records")
     p.add_argument("--dry-run", action="store_true",
                    help="launcher / barrier / all-gather logic over gloo on CPU, synthetic step (tests)")
     a = p.parse_args()
@@ -748,19 +748,41 @@ def e2e_record_32b(args, dist, sizes=(4096, 65536, 262144)):
     return out
 
 
-def config3_subrecord(args, dist, per_curve=1 << 19):
-    """BASELINE config 3 at 2^19 signatures per curve (distinct keys, 1 KB messages, 1 %
-    adversarial), timed exactly as --workload ecdsa times it, summarised for the driver's
-    line; the full 2^20-per-curve run is --workload ecdsa."""
+def _subrecord(line, sub):
+    """A workload's own JSON line, carried inside the driver's N = 1 line (its timing
+    settings stated beside it)."""
+    keep = ("metric", "value", "unit", "ms_per_step", "config", "roofline", "path_roofline", "kernels",
+            "signatures_per_s", "merkle_kernels", "cpu_baseline", "checks", "latency")
+    out = {k: line[k] for k in keep if k in line}
+    out.update({"steps": sub.steps, "warmup": sub.warmup})
+    return out
+
+
+def config3_subrecord(args, dist, per_curve=1 << 20):
+    """BASELINE config 3 at its stated size — 1,048,576 ECDSA_SECP256K1_SHA256 +
+    1,048,576 ECDSA_SECP256R1_SHA256, distinct keys, 1 KB messages, 1 % adversarial
+    (D1-D8) — timed exactly as --workload ecdsa times it, with its own VALU roofline
+    (the slower curve's MSM against profiles/pmc_ecdsa.json) and CPU baseline (the C
+    BC-exact port on a 65,536-signature sample, verdicts compared)."""
     sub = argparse.Namespace(**vars(args))
     sub.batch, sub.msg_bytes, sub.pool_set = per_curve, 1024, False
-    sub.steps, sub.warmup, sub.latency_runs, sub.no_cpu_baseline = 5, 2, 3, True
-    line = run_ecdsa(sub, dist)
-    r = line.get("roofline", {})
-    return {"metric": line["metric"], "value": line["value"], "unit": line["unit"], "ms_per_step": line["ms_per_step"],
-            "steps": sub.steps, "warmup": sub.warmup, "config": line["config"],
-            "roofline": {k: r.get(k) for k in ("kernel", "achieved", "peak", "frac", "avg_launch_ms", "units_per_launch")},
-            "kernels": line.get("kernels"), "checks": line.get("checks")}
+    sub.steps, sub.warmup, sub.latency_runs = 5, 2, 3
+    sub.no_cpu_baseline, sub.cpu_sample = args.no_cpu_baseline, 65536
+    return _subrecord(run_ecdsa(sub, dist), sub)
+
+
+def config4_subrecord(args, dist, n_tx=1 << 20):
+    """BASELINE config 4 at its stated size — 1,048,576 SignedTransactions (trader-demo /
+    loadtest shapes, 70/15/15 % Ed25519/R1/K1 signatures over the recomputed 32 B ids, 1 %
+    tampered), host buffers in, per-tx first failing signature out — timed exactly as
+    --workload tx times it, with its PCIe roofline (host-to-device bytes per step against
+    the box's measured pinned copy rate) and CPU baseline (the C port's tx ids + per-
+    signature verify on a 32,768-tx sample, ids and first-bad indices compared)."""
+    sub = argparse.Namespace(**vars(args))
+    sub.batch, sub.pool, sub.pool_set, sub.msg_bytes, sub.key_reuse = n_tx, 131072, False, None, 0
+    sub.steps, sub.warmup = 5, 2
+    sub.no_cpu_baseline, sub.cpu_sample = args.no_cpu_baseline, 32768
+    return _subrecord(run_tx(sub, dist), sub)
 
 
 # ------------------------------------------------------------------ config 3
@@ -1192,10 +1214,12 @@ def main():
     line = run(args, dist)
     if (args.workload == "ed25519" and not args.dry_run and dist.world == 1 and not args.no_extra
             and not args.key_reuse and not args.batch and not args.msg_bytes):
-        # the driver's N = 1 line also carries the production tx-id shape end to end and a
-        # driver-observed config 3 (each from its own context, after the config-2 timing)
+        # the driver's N = 1 line also carries the production tx-id shape end to end and
+        # driver-observed configs 3 and 4 at their BASELINE sizes (each from its own
+        # context, after the config-2 timing)
         line["latency_32b"] = e2e_record_32b(args, dist)
         line["config3"] = config3_subrecord(args, dist)
+        line["config4"] = config4_subrecord(args, dist)
     if dist.rank == 0:
         line["kernel_src_hash"] = kernel_src_hash()
         print(json.dumps(line), flush=True)
