@@ -217,6 +217,10 @@ class ShardBacklog:
         self.batches = []
 
 
+# status word of a rank whose verify raised something other than CordaGpuError
+STATUS_EXCEPTION = -1000
+
+
 class ShardFailure(RuntimeError):
     """No rank could verify some index range (every rank failed, or a rank failed again
     on the range redistributed to it)."""
@@ -263,14 +267,18 @@ def verify_sharded_resilient(n: int, verify, group=None, device="cpu", bounds: l
 
     Without failures this is ``gather_ordered`` plus the status word.  A second failure
     during redistribution raises ``ShardFailure`` on every rank (they agree through a
-    second status exchange).  Returns (global bitmap as an int32 tensor on ``device``,
-    the failed ranks)."""
+    second status exchange).  Any other exception ``verify`` raises on a rank (a wrong word
+    count, ``MemoryError``, a torch / HIP ``RuntimeError``) fails that rank the same way —
+    status ``STATUS_EXCEPTION``, its range redistributed — and is re-raised on that rank
+    only after the last collective, so no rank is left waiting in one.  Returns (global
+    bitmap as an int32 tensor on ``device``, the failed ranks)."""
     import torch
     import torch.distributed as dist
     world, rank = dist.get_world_size(group), dist.get_rank(group)
     bounds = bounds if bounds is not None else shard_bounds(n, world)
     check_bounds(bounds, world)
     pieces: list[tuple[int, int, np.ndarray]] = []
+    kept: list[BaseException] = []
 
     def attempt(lo, hi) -> int:
         if hi == lo:
@@ -278,12 +286,21 @@ def verify_sharded_resilient(n: int, verify, group=None, device="cpu", bounds: l
             return 0
         try:
             w = np.asarray(verify(lo, hi), dtype=np.uint32)
+            if len(w) != (hi - lo + 31) // 32:
+                raise ValueError(f"verify({lo}, {hi}) returned {len(w)} words")
         except _lib.CordaGpuError as e:
             return e.status if e.status != 0 else -1
-        if len(w) != (hi - lo + 31) // 32:
-            raise ValueError(f"verify({lo}, {hi}) returned {len(w)} words")
+        except Exception as e:  # noqa: BLE001 — kept, re-raised after the collectives
+            kept.append(e)
+            return STATUS_EXCEPTION
         pieces.append((lo, hi, w))
         return 0
+
+    def reraise_kept(exc: BaseException | None = None):
+        if kept:
+            raise kept[0] from exc
+        if exc is not None:
+            raise exc
 
     status = _gather_status(attempt(bounds[rank], bounds[rank + 1]), world, device, group)
     failed = [r for r in range(world) if status[r] != 0]
@@ -291,14 +308,14 @@ def verify_sharded_resilient(n: int, verify, group=None, device="cpu", bounds: l
     plan: dict[int, list[tuple[int, int]]] = {}
     if failed:
         if not survivors:
-            raise ShardFailure(f"every rank failed (status {status})")
+            reraise_kept(ShardFailure(f"every rank failed (status {status})"))
         plan = redistribute(bounds, failed, survivors)
         code = 0
         for lo, hi in plan.get(rank, []) if rank in survivors else []:
             code = code or attempt(lo, hi)
         again = _gather_status(code, world, device, group)
         if any(again):
-            raise ShardFailure(f"redistributed ranges failed again (status {again})")
+            reraise_kept(ShardFailure(f"redistributed ranges failed again (status {again})"))
     layout = {r: ([(bounds[r], bounds[r + 1])] if status[r] == 0 else []) + plan.get(r, []) for r in range(world)}
     nwords = {r: sum((hi - lo + 31) // 32 for lo, hi in layout[r]) for r in range(world)}
     wmax = max(max(nwords.values()), 1)
@@ -316,6 +333,7 @@ def verify_sharded_resilient(n: int, verify, group=None, device="cpu", bounds: l
             k = (hi - lo + 31) // 32
             ordered[lo // 32:lo // 32 + k] = out[at:at + k]
             at += k
+    reraise_kept()  # this rank's own exception, now that every collective is done
     return ordered, failed
 
 

@@ -171,7 +171,7 @@ def test_gather_ordered_uneven_shards(world, total):
     assert res == [(r, True) for r in range(world)]
 
 
-def _resilient_worker(rank, world, port, n, fail_ranks, fail_again, q):
+def _resilient_worker(rank, world, port, n, fail_ranks, fail_again, q, fail_kind="gpu"):
     """One rank of verify_sharded_resilient over gloo; verify() is the C oracle on the
     rank's slice, and ranks in fail_ranks raise the error a failing cg_batch_verify
     raises (CordaGpuError, status < 0).  fail_again: a survivor that also fails on its
@@ -201,18 +201,28 @@ def _resilient_worker(rank, world, port, n, fail_ranks, fail_again, q):
         def verify(lo, hi):
             calls.append((lo, hi))
             if rank in fail_ranks or (rank == fail_again and len(calls) > 1):
-                raise _lib.CordaGpuError(-3, "injected allocation failure (CG_DEBUG_FAIL_ALLOC)")
+                if fail_kind == "runtime":
+                    raise RuntimeError("HIP error: injected")
+                if fail_kind != "words":
+                    raise _lib.CordaGpuError(-3, "injected allocation failure (CG_DEBUG_FAIL_ALLOC)")
             s = D.slice_batch(full, lo, hi)
             v = np.zeros(max(s.n, 1), np.uint8)
             lib.oracle_verify_batch(P(s.scheme), P(s.pk), s.pk_stride, P(s.sig), s.sig_stride, P(s.sig_len),
                                     P(s.msg), P(s.msg_off), P(s.msg_len), s.n, 0, 1, P(v))
-            return D.pack_bits(v[:s.n] == 0)
+            words = D.pack_bits(v[:s.n] == 0)
+            return words[:-1] if fail_kind == "words" and rank in fail_ranks else words
 
         try:
             glob, failed = D.verify_sharded_resilient(n, verify)
         except D.ShardFailure:
             q.put((rank, "ShardFailure", calls))
             return
+        except (RuntimeError, ValueError) as e:  # the rank's own verify exception, after the collectives
+            q.put((rank, type(e).__name__, calls))
+            q.close()
+            q.join_thread()  # flushed before the hard exit
+            dist.destroy_process_group()
+            os._exit(3)
         allv = np.zeros(n, np.uint8)
         lib.oracle_verify_batch(P(full.scheme), P(full.pk), full.pk_stride, P(full.sig), full.sig_stride,
                                 P(full.sig_len), P(full.msg), P(full.msg_off), P(full.msg_len), n, 0, 2, P(allv))
@@ -225,11 +235,11 @@ def _resilient_worker(rank, world, port, n, fail_ranks, fail_again, q):
         os._exit(code)
 
 
-def _run_resilient(world, n, fail_ranks, fail_again=-1):
+def _run_resilient(world, n, fail_ranks, fail_again=-1, fail_kind="gpu"):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_resilient_worker, args=(r, world, port, n, fail_ranks, fail_again, q))
+    procs = [ctx.Process(target=_resilient_worker, args=(r, world, port, n, fail_ranks, fail_again, q, fail_kind))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -276,3 +286,17 @@ def test_shard_failure_twice_raises_everywhere():
         pytest.skip("oracle not built")
     codes, res = _run_resilient(3, 3000, {1}, fail_again=2)
     assert [r[1] for r in res] == ["ShardFailure"] * 3 and codes == [0, 0, 0]
+
+
+@pytest.mark.parametrize("kind,exc", [("runtime", "RuntimeError"), ("words", "ValueError")])
+def test_shard_failure_other_exceptions_do_not_block(kind, exc):
+    """A rank whose verify raises something other than CordaGpuError — a torch / HIP
+    RuntimeError, or a wrong accept-word count (ValueError) — fails like a device
+    failure: its range goes to the survivors, who get the oracle's bitmap, and the
+    rank re-raises its own exception only after the last collective (no rank blocks)."""
+    if not os.path.exists(os.path.join(ROOT, "oracle", "liboracle.so")):
+        pytest.skip("oracle not built")
+    codes, res = _run_resilient(3, 3000, {1}, fail_kind=kind)
+    assert res[0][1] is True and res[2][1] is True and res[0][2] == [1] and res[2][2] == [1], res
+    assert res[1][1] == exc, res
+    assert codes == [0, 3, 0]
