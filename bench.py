@@ -146,6 +146,7 @@ def launch_ranks(args) -> int | None:
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env))
     rc = 0
     alive = list(procs)
+    stop_at = None
     while alive:
         for p in list(alive):
             code = p.poll()
@@ -154,8 +155,13 @@ def launch_ranks(args) -> int | None:
             alive.remove(p)
             if code != 0 and rc == 0:
                 rc = code if code > 0 else 1
+                stop_at = time.monotonic() + 30
                 for q in alive:  # a dead rank leaves the others waiting in a collective
                     q.terminate()
+        if stop_at is not None and time.monotonic() > stop_at:
+            for q in alive:  # one that ignored SIGTERM (e.g. inside a GPU call)
+                q.kill()
+            stop_at = None
         time.sleep(0.2)
     return rc
 
@@ -172,10 +178,21 @@ def host_cpu_model():
 
 
 def cpu_threads():
-    # the GPU box grants this process a 16-CPU share even though nproc shows the machine
+    """Host threads for this rank's datagen / CPU baseline: the box's CPU share (it grants
+    a 16-CPU share even though nproc shows the machine; OMP_NUM_THREADS says so) divided
+    over the ranks on this node, so 8 ranks do not oversubscribe it 8x."""
     env = os.environ.get("OMP_NUM_THREADS")
-    n = int(env) if env and env.isdigit() else (os.cpu_count() or 1)
-    return max(1, min(n, 16))
+    share = max(1, min(int(env) if env and env.isdigit() else (os.cpu_count() or 1), 16))
+    local = os.environ.get("LOCAL_WORLD_SIZE") or os.environ.get("WORLD_SIZE") or "1"
+    return max(1, share // max(1, int(local) if local.isdigit() else 1))
+
+
+def dist_timeout_s() -> float:
+    """Bound on every collective (and the process-group rendezvous): a rank that hangs
+    makes the others fail with an error instead of waiting forever, so the launcher
+    sees a non-zero exit and stops the rest.  Datagen happens before the first barrier
+    and takes well under a minute per rank; CORDA_AMD_DIST_TIMEOUT_S overrides."""
+    return float(os.environ.get("CORDA_AMD_DIST_TIMEOUT_S", "600"))
 
 
 def oracle_lib():
@@ -214,13 +231,17 @@ class Dist:
         self.device = "cpu" if cpu else "cuda"
         self.d = None
         if self.world > 1:
+            import datetime
+
             import torch
             import torch.distributed as dist
+            timeout = datetime.timedelta(seconds=dist_timeout_s())
             if cpu:
-                dist.init_process_group("gloo")
+                dist.init_process_group("gloo", timeout=timeout)
             else:
                 torch.cuda.set_device(self.local_rank)
-                dist.init_process_group("nccl", device_id=torch.device("cuda", self.local_rank))
+                # RCCL: the watchdog aborts a collective past `timeout` and fails the process
+                dist.init_process_group("nccl", device_id=torch.device("cuda", self.local_rank), timeout=timeout)
             self.d = dist
 
     def sync(self):
@@ -459,6 +480,8 @@ def run_dry(args, dist):
     from corda_amd import dist as D
     if os.environ.get("CORDA_AMD_DRY_FAIL_RANK") == str(dist.rank):
         sys.exit(3)  # tests: a failing rank must fail the launcher
+    if os.environ.get("CORDA_AMD_DRY_HANG_RANK") == str(dist.rank):
+        time.sleep(3600)  # tests: a hung rank — the others' collectives time out, the launcher fails
     backlog = args.workload == "backlog"
     total = (args.batch or 100_000_000) if backlog else (args.batch or 4096) * dist.world
     bounds = D.shard_bounds(total, dist.world)

@@ -26,7 +26,7 @@ def _run(args, env, timeout=180):
                           timeout=timeout, cwd="/tmp")
 
 
-@pytest.mark.parametrize("n", [2, 3])
+@pytest.mark.parametrize("n", [2, 3, 8])
 def test_launcher_spawns_n_gloo_ranks(n):
     r = _run(["--gpus", str(n), "--dry-run", "--steps", "3", "--warmup", "1", "--batch", "1000"], _env())
     assert r.returncode == 0, r.stderr[-2000:]
@@ -48,6 +48,32 @@ def test_world_size_mismatch_is_refused():
 def test_failing_rank_fails_the_launcher():
     r = _run(["--gpus", "2", "--dry-run", "--steps", "2"], _env(CORDA_AMD_DRY_FAIL_RANK="1"), timeout=240)
     assert r.returncode != 0
+
+
+def test_hung_rank_times_out_at_world_8():
+    """One of 8 ranks hangs before its first collective: the others' collectives hit the
+    process-group timeout (CORDA_AMD_DIST_TIMEOUT_S, the same bound bench.py puts on RCCL)
+    and fail, the launcher stops the hung rank and exits non-zero — no stall."""
+    import time
+    t0 = time.monotonic()
+    r = _run(["--gpus", "8", "--dry-run", "--steps", "2"],
+             _env(CORDA_AMD_DRY_HANG_RANK="5", CORDA_AMD_DIST_TIMEOUT_S="8"), timeout=240)
+    assert r.returncode != 0
+    assert time.monotonic() - t0 < 120
+    assert not [x for x in r.stdout.splitlines() if x.startswith("{")]
+
+
+def test_cpu_thread_budget_per_rank(monkeypatch):
+    """Datagen / CPU-baseline threads: the 16-CPU share split over the node's ranks."""
+    sys.path.insert(0, ROOT)
+    import bench
+    monkeypatch.setenv("OMP_NUM_THREADS", "16")
+    for world, want in ((None, 16), ("1", 16), ("2", 8), ("8", 2), ("32", 1)):
+        monkeypatch.delenv("LOCAL_WORLD_SIZE", raising=False)
+        monkeypatch.delenv("WORLD_SIZE", raising=False)
+        if world:
+            monkeypatch.setenv("LOCAL_WORLD_SIZE", world)
+        assert bench.cpu_threads() == want
 
 
 def test_single_rank_dry_run_without_launcher():

@@ -152,7 +152,7 @@ def _gather_worker(rank, world, port, total, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,total", [(3, 100_003), (3, 96), (2, 33)])
+@pytest.mark.parametrize("world,total", [(3, 100_003), (3, 96), (2, 33), (8, 100_003), (8, 1000), (8, 100)])
 def test_gather_ordered_uneven_shards(world, total):
     """ShardBacklog.allgather's collective (dist.gather_ordered) at world 3 with uneven
     32-aligned shards: one all_gather_into_tensor of equal padded pieces, then every rank's
