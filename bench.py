@@ -285,6 +285,7 @@ def timed(dist, ctx, step, steps, warmup):
 ED_PREP_KERNELS = ("ed25519_hash", "ed25519_points")
 ED_KERNELS = [*ED_PREP_KERNELS, "ed25519_msm"]
 ED_REUSE_KERNELS = ["ed25519_keyprep"]  # the key-reuse path only (distinct keys decoded once per verify)
+ED_AUX_KERNELS = ["ed25519_bucket"]  # the grouped MSM's two lane-classing kernels (one span)
 
 
 def timeline_path(rank):
@@ -556,29 +557,20 @@ def run_ed25519(args, dist):
             dist.d.all_gather_into_tensor(gathered, bitmap_dev)  # C1: verdict-bitmap all-gather over RCCL
 
     elapsed = timed(dist, ctx, step, args.steps, args.warmup)
-    ks = kstats(ctx, ED_KERNELS + ED_REUSE_KERNELS)
+    ks = kstats(ctx, ED_KERNELS + ED_REUSE_KERNELS + ED_AUX_KERNELS)
     # In the timed step the points kernel runs beside the hash kernel (CORDA_AMD_ED_OVERLAP) and a
     # split batch runs as pieces on two streams, so those HIP-event spans overlap: the per-kernel
     # times and the roofline come from 3 extra steps with both off (each kernel alone over the
     # whole batch); the timed step's own spans are kept as kernels_in_step.
     ks_step = ks
-    prev = {k: os.environ.get(k) for k in ("CORDA_AMD_ED_SPLIT", "CORDA_AMD_ED_OVERLAP")}
-    os.environ["CORDA_AMD_ED_SPLIT"] = "1"
-    os.environ["CORDA_AMD_ED_OVERLAP"] = "0"
-    try:
+    with ctx.options(ED_SPLIT=1, ED_OVERLAP=0):  # (cg_set_option: this context only)
         ctx.set_profiling(True)
         ctx.reset_stats()
         for _ in range(3):
             step()
-        ks = kstats(ctx, ED_KERNELS + ED_REUSE_KERNELS)
+        ks = kstats(ctx, ED_KERNELS + ED_REUSE_KERNELS + ED_AUX_KERNELS)
         ctx.set_profiling(False)
-    finally:
-        for k, v in prev.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
-    split_note = ("kernels / roofline: 3 extra steps with CORDA_AMD_ED_SPLIT=1 CORDA_AMD_ED_OVERLAP=0 (each kernel "
+    split_note = ("kernels / roofline: 3 extra steps with the options CORDA_AMD_ED_SPLIT=1 CORDA_AMD_ED_OVERLAP=0 (each kernel "
                   "alone over the whole batch); kernels_in_step: the timed steps' own spans (points beside hash)")
 
     # verdict check (outside the timed region): untouched elements must accept
@@ -625,9 +617,8 @@ def run_ed25519(args, dist):
             b2 = crypto.PackedBatch(s2.n, s2.scheme, s2.pk, s2.pk_stride, s2.sig, s2.sig_stride, s2.sig_len,
                                     s2.msg, s2.msg_off, s2.msg_len)
             for dest, env in ((lat_small, None), (lat_small_off, "0")):
-                prev = os.environ.get("CORDA_AMD_ED_PAIR_MAX")
                 if env is not None:
-                    os.environ["CORDA_AMD_ED_PAIR_MAX"] = env
+                    ctx.set_option("CORDA_AMD_ED_PAIR_MAX", env)
                 try:
                     got2 = crypto.verify_packed(ctx, b2, MODE_IS_VALID)
                     ts = []
@@ -641,10 +632,7 @@ def run_ed25519(args, dist):
                                                             args.latency_runs)
                 finally:
                     if env is not None:
-                        if prev is None:
-                            os.environ.pop("CORDA_AMD_ED_PAIR_MAX", None)
-                        else:
-                            os.environ["CORDA_AMD_ED_PAIR_MAX"] = prev
+                        ctx.set_option("CORDA_AMD_ED_PAIR_MAX", None)
 
     value = n * world * args.steps / elapsed
     model = OP_MODEL["ed25519_1kb" if msg_bytes > 32 else "ed25519_32b"]
@@ -1144,9 +1132,9 @@ def run_backlog(args, dist):
     p = datagen.make_batch(pool, msg_bytes=msg_bytes, seed=42 + rank, key_base=(2 << 32) + rank * pool,
                            threads=cpu_threads(), key_reuse=args.key_reuse)
     t_gen = time.perf_counter() - t_gen
-    if not args.key_reuse:  # config 5 has distinct keys: the tiling's repeats must not reach the key-reuse path
-        os.environ["CORDA_AMD_KEY_REUSE"] = "0"
     ctx = Context(dist.local_rank)
+    if not args.key_reuse:  # config 5 has distinct keys: the tiling's repeats must not reach the key-reuse path
+        ctx.set_option("CORDA_AMD_KEY_REUSE", 0)
     adv_ok = [True]
     first = {}
     t_stage = time.perf_counter()

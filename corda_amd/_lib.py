@@ -32,7 +32,7 @@ COMPOSITE_LEAF, COMPOSITE_NODE, COMPOSITE_INVALID = 0, 1, 0x80
 TX_OK, TX_NO_SIGNATURES, TX_NO_COMPONENTS, TX_SIGNATURES_MISSING = -1, -2, -3, -4
 # cg_set_debug options (test hooks)
 DEBUG_FORCE_FULL_LENGTH, DEBUG_FAIL_ALLOC, DEBUG_THROW, DEBUG_FORCE_GLV_FALLBACK = 1, 2, 3, 4
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 # exported symbols and their prototypes: (restype, argtypes)
 _u8p, _u32p, _u64p, _i32p = POINTER(c_uint8), POINTER(c_uint32), POINTER(c_uint64), POINTER(ctypes.c_int32)
@@ -70,6 +70,7 @@ PROTOTYPES = {
     "cg_kernel_stats": (c_int, [c_void_p, c_char_p, POINTER(c_double), POINTER(c_uint64), POINTER(c_uint64)]),
     "cg_reset_stats": (c_int, [c_void_p]),
     "cg_set_debug": (c_int, [c_void_p, c_int, ctypes.c_int64]),
+    "cg_set_option": (c_int, [c_void_p, c_char_p, c_char_p]),
 }
 
 _lib = None
@@ -174,6 +175,29 @@ class Context:
         """Test hooks (cg_set_debug): forced full-length Ed25519 scalars, injected
         allocation failures, an injected exception."""
         self.check(self.lib.cg_set_debug(self.h, option, value))
+
+    def set_option(self, key: str, value=None):
+        """One run-time option of this context (cg_set_option): a
+        CORDA_AMD_* knob, read from the environment only at cg_open.  value None: unset
+        (the library default)."""
+        self.check(self.lib.cg_set_option(self.h, key.encode(), None if value is None else str(value).encode()))
+
+    def options(self, **kv):
+        """Context manager: set options (CORDA_AMD_ prefix optional) for a block, unset
+        them afterwards."""
+        import contextlib
+
+        @contextlib.contextmanager
+        def scope():
+            keys = [k if k.startswith("CORDA_AMD_") else "CORDA_AMD_" + k for k in kv]
+            try:
+                for k, v in zip(keys, kv.values()):
+                    self.set_option(k, v)
+                yield self
+            finally:
+                for k in keys:
+                    self.set_option(k, None)
+        return scope()
 
     def register_host(self, *arrays):
         """Page-locks numpy arrays the caller will pass again (cg_register_host)."""

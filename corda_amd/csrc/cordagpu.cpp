@@ -39,32 +39,15 @@
 #include "cg_ecdsa_api.h"
 #include "cg_kernels.h"
 #include "cg_merkle_api.h"
+#include "cg_plan.h"
 
 namespace {
 
-constexpr uint32_t kEdChunk = 1u << 21;  // Ed25519 scratch chunk (elements)
-// cg_batch_verify of a large Ed25519 subset: pieces on two streams (launch_verify);
-// CORDA_AMD_ED_SPLIT overrides the count, pieces stay >= kEdSplitMin elements
-constexpr uint32_t kEdSplitMin = 65536;
-// Ed25519 pieces up to this size run in the latency mode (two lanes per signature):
-// r04f/r04g sweeps (host-buffer verify p50, 1 KB messages): 16,384 1.13 -> 1.02 ms,
-// 32,768 1.51 -> 1.37 ms with it, 65,536 2.21 -> 2.36 ms (slower: two waves per SIMD
-// already), so the crossover lies between 32k and 64k signatures
-constexpr uint32_t kEdPairMaxDefault = 40000;
-// ... for a one-chunk host-buffer call, by its bytes per element (verify_copy_bound)
-constexpr uint32_t kEdPairMaxCopyBound = 32768;
-constexpr uint32_t kEdPairMaxCompute = 20480;
-// ... and up to this size with four lanes per signature (the scalars' 64-bit halves
-// over 2^64-multiple tables: ~64 doublings per lane instead of ~128)
-constexpr uint32_t kEdQuadMaxDefault = 32768;
-// ... and up to this size with eight (32-bit parts over 2^(32 u)-multiple tables: ~32
-// doublings per lane): r04ap, 1 KB messages, 2,048-6,144 signatures -0.012..0.015 ms
-// against four lanes, 8,192 +0.07 ms — past ~7,280 signatures the eight-lane points
-// blocks and the hash blocks no longer get a CU each (ed_spread_lds)
-constexpr uint32_t kEdOctMaxDefault = 7168;
-// grouped balanced MSM (cg_ed25519_bucket) from this many signatures per piece
-constexpr uint32_t kEdBucketMinDefault = 16384;
-constexpr uint32_t kEdSplitDefault = 1;  // r03d A/B: 2 or 4 pieces measured no faster (95-96 M/s either way)
+using cg::kAsyncArenaMin;
+using cg::kEarlyPartMin;
+using cg::kEdChunk;
+using cg::kEdSplitDefault;
+using cg::kEdSplitMin;
 
 struct Stat {
   double ms = 0;
@@ -221,6 +204,7 @@ class JobThread {
 
 struct cg_ctx {
   int device = -1;
+  cg::Options opts;  // the CORDA_AMD_* knobs: environment snapshot at cg_open, cg_set_option
   uint32_t n_cu = 256;                  // compute units (hipDeviceProp)
   uint32_t lds_per_cu = 160 * 1024;     // LDS bytes per CU (hipDeviceProp; 160 KB on gfx950)
   uint32_t lds_per_block = 160 * 1024;  // largest LDS request of one block (hipDeviceProp)
@@ -382,7 +366,7 @@ void end_call_span(cg_ctx* ctx) {
 void collect_timings(cg_ctx* ctx) {
   // CORDA_AMD_TIMELINE=<file>: every timed span of the call appended as
   // "name items start_ms end_ms" relative to the call's first span (tools/timeline.py)
-  static const char* tl_path = std::getenv("CORDA_AMD_TIMELINE");
+  const char* tl_path = ctx->opts.str(cg::OPT_TIMELINE);
   if (tl_path && ctx->profiling && !ctx->pending.empty()) {
     if (FILE* f = std::fopen(tl_path, "a")) {
       const hipEvent_t ref = ctx->pending.front().second.first;
@@ -797,6 +781,7 @@ cg_status cg_open(int device, cg_ctx** out) {
   cg_ctx* ctx = new (std::nothrow) cg_ctx();
   if (!ctx) return CG_E_OUT_OF_MEMORY;
   ctx->device = device;
+  ctx->opts.from_env();  // the CORDA_AMD_* knobs, read once (cg_set_option changes them later)
   ctx->n_cu = (uint32_t)std::max(1, prop.multiProcessorCount);
   if (prop.maxSharedMemoryPerMultiProcessor > 0) ctx->lds_per_cu = (uint32_t)prop.maxSharedMemoryPerMultiProcessor;
   if (prop.sharedMemPerBlock > 0) ctx->lds_per_block = (uint32_t)prop.sharedMemPerBlock;
@@ -912,23 +897,14 @@ cg_status cg_release_cached(cg_ctx* ctx) {
 
 namespace {
 
+// The knobs of a context (cg_plan.h: each a pure function of ctx->opts, the environment
+// snapshot of cg_open plus cg_set_option).
 // Key-reuse decision (CORDA_AMD_KEY_REUSE: 0 never, 1 always, else automatic):
 // the per-key path pays a decode and four 9-entry tables (~190 doublings) per
 // distinct key and saves ~70 doublings, the A decode and the A table per
 // signature, so it wins once keys repeat a few times; automatic = n / n_keys >= 8.
-int key_reuse_forced() {
-  const char* e = std::getenv("CORDA_AMD_KEY_REUSE");
-  return e && (e[0] == '0' || e[0] == '1') ? e[0] - '0' : -1;
-}
-
-// Latency mode (ed25519_kernels.hip cg_ed25519_points_lanes / _msm_lanes: two lanes per
-// signature) for Ed25519 pieces of at most this many signatures on the balanced path;
-// CORDA_AMD_ED_PAIR_MAX overrides (0: never).  call_default: the batch's own threshold
-// (cg_batch::pair_max; a one-chunk host-buffer call sets it by its bytes per element).
-uint32_t ed_pair_max(uint32_t call_default = 0) {
-  const char* e = std::getenv("CORDA_AMD_ED_PAIR_MAX");
-  return e ? (uint32_t)std::max(0, std::atoi(e)) : call_default ? call_default : kEdPairMaxDefault;
-}
+int key_reuse_forced(const cg_ctx* ctx) { return cg::key_reuse_forced(ctx->opts); }
+uint32_t ed_pair_max(const cg_ctx* ctx, uint32_t call_default = 0) { return cg::ed_pair_max(ctx->opts, call_default); }
 // Latency mode: the hash and points kernels run side by side with a few blocks each,
 // and the dispatcher packs those blocks onto the same CUs, where they slow each other
 // (4,096 signatures: hash 0.16 -> 0.26 ms beside the points kernel, r04r spans).  The
@@ -941,9 +917,8 @@ uint32_t ed_pair_max(uint32_t call_default = 0) {
 // chunk's kernels hold about half the chip).
 void ed_spread_lds(const cg_ctx* ctx, cg::Ed25519Dev& d, uint64_t points_blocks, uint64_t hash_blocks,
                    uint32_t n_cu) {
-  const char* e = std::getenv("CORDA_AMD_ED_SPREAD_LDS");
   d.spread_lds = d.spread_lds_hash = 0;
-  if (e && std::atoi(e) == 0) return;
+  if (!ctx->opts.on(cg::OPT_ED_SPREAD_LDS, true)) return;
   const uint32_t half = ctx->lds_per_cu / 2;
   if (half + 4096 > ctx->lds_per_block) return;  // a block cannot reserve more than half a CU
   if (points_blocks + hash_blocks <= n_cu) {
@@ -953,68 +928,10 @@ void ed_spread_lds(const cg_ctx* ctx, cg::Ed25519Dev& d, uint64_t points_blocks,
     d.spread_lds_hash = half + 4096;
   }
 }
-// Four lanes per signature for latency-mode pieces of at most this many signatures;
-// CORDA_AMD_ED_QUAD_MAX overrides (0: never).
-uint32_t ed_quad_max() {
-  const char* e = std::getenv("CORDA_AMD_ED_QUAD_MAX");
-  return e ? (uint32_t)std::max(0, std::atoi(e)) : kEdQuadMaxDefault;
-}
-// Eight lanes per signature up to this many; CORDA_AMD_ED_OCT_MAX overrides (0: never).
-uint32_t ed_oct_max() {
-  const char* e = std::getenv("CORDA_AMD_ED_OCT_MAX");
-  return e ? (uint32_t)std::max(0, std::atoi(e)) : kEdOctMaxDefault;
-}
+bool ed_overlap_enabled(const cg_ctx* ctx) { return cg::ed_overlap_enabled(ctx->opts); }
 
-// Balanced MSM pieces of at least this many signatures run over lanes grouped by digit
-// count (cg_ed25519_bucket); CORDA_AMD_ED_BUCKET_MIN overrides (0: never).
-uint32_t ed_bucket_min() {
-  const char* e = std::getenv("CORDA_AMD_ED_BUCKET_MIN");
-  const int v = e ? std::atoi(e) : (int)kEdBucketMinDefault;
-  return v > 0 ? (uint32_t)v : UINT32_MAX;
-}
-
-bool ed_overlap_enabled() {
-  const char* e = std::getenv("CORDA_AMD_ED_OVERLAP");
-  return !e || std::atoi(e) != 0;
-}
-
-// Early points: a one-chunk verify of an all-Ed25519 in-order batch on the balanced path
-// uploads its key and signature rows in up to this many parts of at least kEarlyPartMin
-// signatures, and each part's points kernel starts on copy_stream, reading the raw rows,
-// as soon as that part has landed — the copy of the next part runs beside it (r05 spans,
-// 2^18 x 32 B: rows copy ~0.55 ms, then the points kernel ~0.63 ms, both ahead of the
-// MSM; r05g: 4 parts 3.24 -> 2.92 ms).  Smaller parts lose: a points kernel of 32,768
-// signatures (128 blocks) takes as long as one of 65,536, and the extra pageable copies
-// cost ~0.1 ms (r05g: 65,536 in two parts 0.98 -> 1.10 ms).  CORDA_AMD_EARLY_POINTS
-// overrides the part count (0 or 1: off).  launch_verify then only joins those kernels
-// (cg_batch::points_early).
-constexpr uint32_t kEarlyPartMin = 65536;
-// Async arena: a one-chunk call's deferred arena (and offsets / lengths) of at least
-// kAsyncArenaMin bytes goes up from the upload thread while the calling thread copies the
-// key and signature rows, instead of after them — below the early-points sizes, whose row
-// parts it would slow (r05x: 65,536 x 1 KB 2.19 -> 2.11 ms, 16,384 x 1 KB 0.79 -> 0.77;
-// but 4,096 x 1 KB 0.47 -> 0.56, the thread hand-off, and 2^17-2^18 x 32 B +0.05-0.15).
-// CORDA_AMD_ASYNC_ARENA=0 turns it off.
-constexpr size_t kAsyncArenaMin = (size_t)8 << 20;
-bool async_arena_enabled() {
-  const char* e = std::getenv("CORDA_AMD_ASYNC_ARENA");
-  return !e || std::atoi(e) != 0;
-}
-// Split points: a one-chunk call on the balanced path below the early-points sizes
-// uploads the key rows first and decodes the keys (cg_ed25519_points_half<0>) beside the
-// signature rows' copy, then R (<1>): after the last row only half of the points phase is
-// left.  CORDA_AMD_SPLIT_POINTS=0 turns it off.
-bool split_points_enabled() {
-  const char* e = std::getenv("CORDA_AMD_SPLIT_POINTS");
-  return !e || std::atoi(e) != 0;
-}
-uint32_t early_points_parts() {
-  const char* e = std::getenv("CORDA_AMD_EARLY_POINTS");
-  return e ? (uint32_t)std::min(8, std::max(0, std::atoi(e))) : 4u;
-}
-
-bool key_reuse_mode(uint32_t n, uint32_t n_keys) {
-  const int forced = key_reuse_forced();
+bool key_reuse_mode(const cg_ctx* ctx, uint32_t n, uint32_t n_keys) {
+  const int forced = key_reuse_forced(ctx);
   if (forced >= 0) return forced == 1;
   return n_keys > 0 && (uint64_t)n_keys * 8 <= n;
 }
@@ -1045,12 +962,12 @@ bool key_sample_suggests_reuse(const uint8_t* pk, size_t pk_stride, const std::v
 cg_status stage_key_dedupe(cg_ctx* ctx, cg_batch* b, const uint8_t* pk, size_t pk_stride,
                            const std::vector<uint32_t>& idx0, int sample = -1) {
   const uint32_t ne = b->n_ed;
-  const int forced = key_reuse_forced();
+  const int forced = key_reuse_forced(ctx);
   if (forced == 0 || (ne < 64 && forced != 1)) return CG_OK;
   // automatic mode and a batch the latency mode will verify: the key-reuse path's
   // per-key table build (~190 doublings, one wave per 64 keys) would be the longest
   // chain of the call, and the exact count is a host round trip
-  if (forced != 1 && ne <= ed_pair_max(b->pair_max)) return CG_OK;
+  if (forced != 1 && ne <= ed_pair_max(ctx, b->pair_max)) return CG_OK;
   if (forced != 1 && !(sample >= 0 ? sample == 1 : key_sample_suggests_reuse(pk, pk_stride, idx0, ne))) return CG_OK;
   uint32_t tsize = 1;
   while (tsize < 2 * ne) tsize <<= 1;
@@ -1076,7 +993,7 @@ cg_status stage_key_dedupe(cg_ctx* ctx, cg_batch* b, const uint8_t* pk, size_t p
   if (e == hipSuccess) e = hipMemcpyAsync(&n_keys, counter, 4, hipMemcpyDeviceToHost, ctx->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
   if (e != hipSuccess) return done(hip_fail(ctx, e, "key dedupe"));
-  if (!key_reuse_mode(ne, n_keys)) {
+  if (!key_reuse_mode(ctx, ne, n_keys)) {
     dfree(ctx, b->ed_key_index);
     dfree(ctx, b->ed_key_first);
     b->ed_key_index = b->ed_key_first = nullptr;
@@ -1178,14 +1095,34 @@ cg_status create_batch(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const ui
     b->meta_owned = false;
   } else {
     if ((st = dalloc(ctx, &b->arena, m.bytes + 16, "alloc arena")) != CG_OK) return bail(st);
-    // one-chunk host verify of an Ed25519-only batch: the message arena goes up later,
-    // from launch_verify, once the points kernel (which needs only keys and R) is
-    // running — the copy then overlaps it (no ECDSA kernel reads the arena earlier)
-    const bool defer_arena = m.keep_raw && m.bytes && idx[1].empty() && idx[2].empty() && n_ed;
-    // ... and, when every element is Ed25519 in order, its offsets / lengths too: the
-    // points kernel starts after the key and signature rows alone (r05: 2^18 x 32 B ids
-    // spent ~0.85 ms in copies before the first kernel)
-    const bool defer_meta = defer_arena && ed_identity && bad.empty();
+    // A one-chunk host verify (m.keep_raw) follows its plan (cg_plan.h plan_verify, from
+    // the call's shape as the partition above found it; the key sample only when a
+    // choice hinges on it).  An Ed25519-only batch: the message arena goes up later, from
+    // launch_verify, once the points kernel (which needs only keys and R) is running —
+    // the copy then overlaps it (no ECDSA kernel reads the arena earlier); when every
+    // element is Ed25519 in order, its offsets / lengths too: the points kernel starts
+    // after the key and signature rows alone (r05: 2^18 x 32 B ids spent ~0.85 ms in
+    // copies before the first kernel).
+    cg::VerifyPlan plan;
+    if (m.keep_raw) {
+      cg::VerifyShape shape;
+      shape.n = n;
+      shape.n_ed = n_ed;
+      shape.msg_bytes = m.bytes;
+      shape.pk_stride = pk_stride;
+      shape.sig_stride = sig_stride;
+      shape.sig_len = sig_len != nullptr;
+      shape.ecdsa = !idx[1].empty() || !idx[2].empty();
+      shape.ed_in_order = ed_identity && bad.empty();
+      plan = cg::plan_verify(shape, ctx->opts);
+      if (plan.needs_key_sample) {
+        shape.keys_repeat = key_sample_suggests_reuse(pk, pk_stride, idx[0], (uint32_t)n_ed) ? 1 : 0;
+        key_sample = shape.keys_repeat;
+        plan = cg::plan_verify(shape, ctx->opts);
+      }
+    }
+    const bool defer_arena = plan.defer_arena;
+    const bool defer_meta = plan.defer_meta;
     meta_deferred = defer_meta;
     Timed t(ctx, "h2d_stage", (defer_arena ? 0 : m.bytes) + (defer_meta ? 0 : 12 * n) +
                                   (raw_owned ? n * (pk_stride + sig_stride + (sig_len ? 4 : 0)) : 0));
@@ -1208,8 +1145,7 @@ cg_status create_batch(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const ui
       if ((st = upload(ctx, &b->msg_off_all, m.off_host, n, "upload msg_off")) != CG_OK) return bail(st);
       if ((st = upload(ctx, &b->msg_len_all, m.len_host, n, "upload msg_len")) != CG_OK) return bail(st);
     }
-    if (defer_arena && m.bytes >= kAsyncArenaMin && n < 2 * (size_t)kEarlyPartMin && async_arena_enabled() &&
-        !std::getenv("CORDA_AMD_ED_SPLIT")) {
+    if (plan.async_arena) {
       try {
         if (!ctx->uploader) ctx->uploader = new JobThread(ctx->device);
         b->arena_job.reset(new cg_batch::ArenaJob());
@@ -1248,19 +1184,9 @@ cg_status create_batch(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const ui
       }
     }
     if (raw_owned) {
-      const bool rows_direct =
-          m.keep_raw && ed_identity && bad.empty() && pk_stride % 4 == 0 && sig_stride % 4 == 0 && ctx->ev_rows;
-      uint32_t parts = 0;
-      bool split_points = false;
-      if (rows_direct && n > ed_pair_max(b->pair_max) && n <= kEdChunk && ed_overlap_enabled() &&
-          !std::getenv("CORDA_AMD_ED_SPLIT")) {
-        const int forced = key_reuse_forced();
-        if (forced == 0 || (forced != 1 && !key_sample_suggests_reuse(pk, pk_stride, idx[0], (uint32_t)n))) {
-          key_sample = 0;
-          parts = std::min<uint32_t>(early_points_parts(), (uint32_t)(n / kEarlyPartMin));
-          split_points = parts <= 1 && split_points_enabled();
-        }
-      }
+      const bool rows_direct = plan.rows_direct && ctx->ev_rows;
+      const uint32_t parts = rows_direct ? plan.early_parts : 0;
+      const bool split_points = rows_direct && plan.split_points;
       if (split_points) {  // the A half beside the signatures' copy (split_points_enabled)
         if ((st = ensure_ed_scratch(ctx, (uint32_t)n)) != CG_OK ||
             (st = dalloc(ctx, &pk_raw, n * pk_stride, "alloc pk")) != CG_OK ||
@@ -1553,11 +1479,11 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = 
       }
     }
     if (b->n_ed) {
-      const uint32_t pair_max = ed_pair_max(b->pair_max);
+      const uint32_t pair_max = ed_pair_max(ctx, b->pair_max);
       // four lanes per signature: tables in 2 n_ed scratch slots — grown for it only where
       // this call owns the whole scratch; inside a pipeline only if its region has room
-      const bool quad_want = !b->ed_key_index && b->n_ed <= std::min(pair_max, ed_quad_max());
-      const bool oct_want = quad_want && b->n_ed <= ed_oct_max();
+      const bool quad_want = !b->ed_key_index && b->n_ed <= std::min(pair_max, cg::ed_quad_max(ctx->opts));
+      const bool oct_want = quad_want && b->n_ed <= cg::ed_oct_max(ctx->opts);
       cg_status s2 = ensure_ed_scratch(
           ctx, quad_want && join_streams && scratch_off == 0 ? (oct_want ? 4 : 2) * b->n_ed : b->n_ed);
       if (s2 != CG_OK) return s2;
@@ -1572,13 +1498,21 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = 
       uint32_t split = 1;
       if (join_streams && b->n_ed >= 2 * kEdSplitMin && b->n_ed <= span) {
         split = kEdSplitDefault;
-        if (const char* e = std::getenv("CORDA_AMD_ED_SPLIT")) split = (uint32_t)std::max(1, std::atoi(e));
+        if (ctx->opts.has(cg::OPT_ED_SPLIT)) split = (uint32_t)std::max(1, ctx->opts.i(cg::OPT_ED_SPLIT, 1));
         split = std::min<uint32_t>(split, b->n_ed / kEdSplitMin);
       }
       hipStream_t ed_lane[2] = {ctx->stream, ctx->hash_stream};
       // prepared-batch verify (this call owns the streams): points beside hash on the idle copy stream
-      hipStream_t pts = pts_stream ? pts_stream : (join_streams && ed_overlap_enabled() ? ctx->copy_stream : nullptr);
+      hipStream_t pts = pts_stream ? pts_stream : (join_streams && ed_overlap_enabled(ctx) ? ctx->copy_stream : nullptr);
       if (split > 1) {
+        if (b->arena_job) {  // (never with split pieces: cg_plan.h's static_assert; kept safe anyway)
+          b->arena_job->wait();
+          const hipError_t e2 = b->arena_job->err;
+          b->arena_job.reset();
+          CG_TRY(ctx, e2, "upload arena");
+          CG_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_arena, 0), "wait arena");
+          CG_TRY(ctx, hipStreamWaitEvent(ctx->hash_stream, ctx->ev_arena, 0), "wait arena");
+        }
         if (b->arena_pending) {  // every piece's hash kernel reads the arena: it goes up before the fork
           {
             Timed t(ctx, "h2d_arena", b->arena_pending_bytes);
@@ -1643,7 +1577,7 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = 
         }
         const bool pair = allow_lanes && !b->ed_key_index && cnt <= pair_max;  // latency mode
         // balanced MSM over lanes grouped by digit count
-        if (!pair && !b->ed_key_index && cnt >= std::max<uint32_t>(ed_bucket_min(), 4096)) {
+        if (!pair && !b->ed_key_index && cnt >= cg::ed_bucket_min(ctx->opts)) {
           d.order = ctx->ed_status + 2 * (size_t)ctx->ed_scap + soff;
           d.order_count = ctx->ed_status + 5 * (size_t)ctx->ed_scap + soff;
         }
@@ -1682,10 +1616,9 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = 
             return CG_OK;
           }
           if (!b->arena_pending) return CG_OK;
-          const char* ab = std::getenv("CORDA_AMD_ARENA_BESIDE");
           const size_t pending = b->arena_pending_bytes + (b->meta_pending_off ? (size_t)12 * b->n : 0);
           hipStream_t as = beside && split == 1 && pending >= ((size_t)6 << 20) &&
-                                   !(ab && std::atoi(ab) == 0)
+                                   ctx->opts.on(cg::OPT_ARENA_BESIDE, true)
                                ? ctx->hash_stream
                                : ctx->stream;
           {
@@ -1822,58 +1755,7 @@ struct VerifyRun {
   }
 };
 
-// Chunk boundaries of an n-element host batch: K = n / min_chunk chunks (at most
-// kmax), 64-aligned (whole waves); the first is `head` and the last `tail` times a
-// regular one (a small first chunk starts the kernels early, a small last one
-// shortens what runs after the last byte).  CORDA_AMD_VERIFY_CHUNKS / _MIN_CHUNK /
-// _HEAD / _TAIL override (tuning, tests).
-// A host-buffer call is copy-bound when its bytes take longer over PCIe than its
-// Ed25519 kernels take on the device: ~50 GB/s against ~9.5 ns per verify (105 M/s), i.e.
-// above ~475 bytes per element (1 KB messages: 1,132 B; 32 B tx ids: 140 B).  A
-// compute-bound call gains nothing from chunking its copies: its chunks' kernels,
-// which the pipeline runs two at a time, each pay a serial chain and the host staging
-// of the first chunk delays the first kernel.  CORDA_AMD_VERIFY_POLICY=0 restores the
-// copy-bound chunking for every call (A/B).
-bool verify_copy_bound(size_t n, size_t msg_bytes, size_t row_bytes) {
-  if (const char* e = std::getenv("CORDA_AMD_VERIFY_POLICY"))
-    if (std::atoi(e) == 0) return true;
-  return n && (double)msg_bytes / (double)n + (double)row_bytes > 475.0;
-}
-
-std::vector<size_t> verify_chunk_bounds(size_t n, bool copy_bound = true) {
-  // head 0.25: the host stages the first chunk's pageable bytes before any DMA can
-  // start (r04d spans: 0.37 ms at 0.5); tail 0.25: the last chunk — the only one whose
-  // kernels run after the last byte — runs in the four-lane latency mode for 2^18-element
-  // calls (r05 sweeps, 2^18 x 1 KB: 6.89-6.91 ms against 6.98-7.05 at 0.4)
-  size_t kmax = 8, min_chunk = 32768;
-  double head = 0.25, tail = 0.25;
-  if (const char* e = std::getenv("CORDA_AMD_VERIFY_CHUNKS")) kmax = std::max(1, std::atoi(e));
-  if (const char* e = std::getenv("CORDA_AMD_VERIFY_MIN_CHUNK")) min_chunk = std::max(1, std::atoi(e));
-  if (const char* e = std::getenv("CORDA_AMD_VERIFY_HEAD")) head = std::min(2.0, std::max(0.05, std::atof(e)));
-  if (const char* e = std::getenv("CORDA_AMD_VERIFY_TAIL")) tail = std::min(2.0, std::max(0.05, std::atof(e)));
-  // below 2^17 elements one chunk is fastest (r03b sweep, 65,536 x 1 KB pageable: 2.38 ms
-  // as one chunk, 2.70 ms as two: every chunk adds a serial ~0.7 ms kernel chain)
-  const bool tuned = std::getenv("CORDA_AMD_VERIFY_MIN_CHUNK") || std::getenv("CORDA_AMD_VERIFY_CHUNKS");
-  // a compute-bound call runs as one chunk up to 2^20 elements (r05 sweeps, 32 B ids)
-  const size_t whole = tuned ? 0 : (size_t)1 << (copy_bound ? 17 : 20);
-  const size_t K = n < whole ? 1 : std::max<size_t>(1, std::min<size_t>(kmax, n / min_chunk));
-  std::vector<size_t> b(K + 1, 0);
-  std::vector<double> w(K, 1.0);
-  if (K > 1) {
-    w[0] = head;
-    w[K - 1] = tail;
-  }
-  double wsum = 0;
-  for (double x : w) wsum += x;
-  double acc = 0;
-  for (size_t k = 1; k < K; ++k) {
-    acc += w[k - 1];
-    b[k] = std::min(n, (size_t)((double)n * acc / wsum) / 64 * 64);
-  }
-  b[K] = n;
-  for (size_t k = 1; k <= K; ++k) b[k] = std::max(b[k], b[k - 1]);
-  return b;
-}
+// (copy-bound vs compute-bound calls and their chunk bounds: cg_plan.h plan_verify)
 
 // Page-locked host memory (cg_register_host, hipHostMalloc): a copy from it is truly
 // asynchronous.  A pageable copy is staged by the runtime and holds the calling thread.
@@ -1972,11 +1854,11 @@ cg_status verify_pipeline(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
   const bool pinned = host_is_pinned(msg) && host_is_pinned(pk) && host_is_pinned(sig) &&
                       host_is_pinned(msg_off) && host_is_pinned(msg_len) && host_is_pinned(sig_len);
   bool ring = false;
-  if (const char* e = std::getenv("CORDA_AMD_VERIFY_RING")) ring = !pinned && K > 1 && std::atoi(e) != 0;
+  if (ctx->opts.has(cg::OPT_VERIFY_RING)) ring = !pinned && K > 1 && ctx->opts.on(cg::OPT_VERIFY_RING, false);
   // the copy workers: the ring's host copies, and the arena-end scan below
   if (!ctx->pool && (ring || n >= 65536)) {
     int workers = 7;
-    if (const char* e = std::getenv("CORDA_AMD_COPY_THREADS")) workers = std::max(0, std::atoi(e) - 1);
+    if (ctx->opts.has(cg::OPT_COPY_THREADS)) workers = std::max(0, ctx->opts.i(cg::OPT_COPY_THREADS, 8) - 1);
     ctx->pool = new CopyPool(workers);
   }
   // arena end of each chunk's messages (a prefix scan over every element: on the copy
@@ -2016,7 +1898,7 @@ cg_status verify_pipeline(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
     // more — e.g. an arena packed in reverse element order, whose first chunk's prefix
     // is the whole arena — copies its pageable buffers synchronously instead.
     size_t cap_mb = 256;
-    if (const char* e = std::getenv("CORDA_AMD_RING_MAX_MB")) cap_mb = (size_t)std::max(1, std::atoi(e));
+    if (ctx->opts.has(cg::OPT_RING_MAX_MB)) cap_mb = (size_t)std::max(1, ctx->opts.i(cg::OPT_RING_MAX_MB, 256));
     if (slot > (cap_mb << 20)) ring = false;
   }
   if (ring) {
@@ -2039,11 +1921,10 @@ cg_status verify_pipeline(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
     }
     ring = ctx->ring_cap >= slot;
   }
-  const char* od = std::getenv("CORDA_AMD_VERIFY_ONE_DMA");
-  const bool one_dma = !od || std::atoi(od) != 0;
+  const bool one_dma = ctx->opts.on(cg::OPT_VERIFY_ONE_DMA, true);
   // staging slice size (ring only); CORDA_AMD_VERIFY_SLICE_KB overrides (0: whole chunks)
   size_t slice_bytes = (size_t)12 << 20;
-  if (const char* e = std::getenv("CORDA_AMD_VERIFY_SLICE_KB")) slice_bytes = (size_t)std::max(0, std::atoi(e)) << 10;
+  if (ctx->opts.has(cg::OPT_VERIFY_SLICE_KB)) slice_bytes = (size_t)std::max(0, ctx->opts.i(cg::OPT_VERIFY_SLICE_KB, 0)) << 10;
   // the chunk's inputs are checked just before they go out (the host scan then
   // overlaps the earlier chunks' copies and kernels); an error ends the call
   auto check_chunk = [&](size_t k) -> cg_status {
@@ -2163,11 +2044,10 @@ cg_status verify_pipeline(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
   // keeps the uploads on the calling thread.  `issued` counts the chunks whose ev[k] is
   // recorded.
   bool thread_up = !pinned && K > 1;
-  if (const char* e = std::getenv("CORDA_AMD_VERIFY_UPLOAD_THREAD")) thread_up = thread_up && std::atoi(e) != 0;
+  thread_up = thread_up && ctx->opts.on(cg::OPT_VERIFY_UPLOAD_THREAD, true);
   // (with the upload thread the calling thread waits only for the chunk it launches next)
   size_t ahead = thread_up ? 0 : (pinned || ring) ? 2 : 1;
-  if (const char* e = std::getenv("CORDA_AMD_VERIFY_AHEAD"))
-    if (!thread_up) ahead = (size_t)std::max(1, std::atoi(e));
+  if (ctx->opts.has(cg::OPT_VERIFY_AHEAD) && !thread_up) ahead = (size_t)std::max(1, ctx->opts.i(cg::OPT_VERIFY_AHEAD, 1));
   struct Uploader {
     std::mutex m;
     std::condition_variable cv;
@@ -2256,10 +2136,10 @@ cg_status verify_pipeline(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
   // only when the call is bound by its copies (the extra work hides under the next
   // chunk's upload and the last chunk's chain after the last byte is shorter).
   bool lanes = true;
-  if (const char* e = std::getenv("CORDA_AMD_VERIFY_LANES")) lanes = std::atoi(e) != 0;
+  lanes = ctx->opts.on(cg::OPT_VERIFY_LANES, lanes);
   // two chunks in flight need two disjoint scratch halves; chunks too large for that
   // (> kEdChunk Ed25519 lanes each) run one after the other on ctx->stream
-  const bool dual = K > 1 && max_cnt[0] <= kEdChunk && !(std::getenv("CORDA_AMD_VERIFY_SERIAL"));
+  const bool dual = K > 1 && max_cnt[0] <= kEdChunk && !ctx->opts.has(cg::OPT_VERIFY_SERIAL);
   if (max_cnt[0] &&
       (st = ensure_ed_scratch(ctx, dual ? 2 * max_cnt[0] : max_cnt[0], dual ? 2 * kEdChunk : kEdChunk)) != CG_OK)
     return st;
@@ -2291,7 +2171,7 @@ cg_status verify_pipeline(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
   hipStream_t lane[2] = {ctx->stream, dual ? ctx->hash_stream : ctx->stream};
   // Ed25519 points kernels beside the hash kernels on the first ECDSA stream when no
   // chunk has ECDSA elements (it is idle then)
-  hipStream_t pts = (!max_cnt[1] && !max_cnt[2] && ed_overlap_enabled()) ? ctx->ec_stream[0] : nullptr;
+  hipStream_t pts = (!max_cnt[1] && !max_cnt[2] && ed_overlap_enabled(ctx)) ? ctx->ec_stream[0] : nullptr;
   struct StreamRestore {
     cg_ctx* c;
     hipStream_t main;
@@ -2416,8 +2296,17 @@ cg_status cg_verify_batch(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
       c->call_begin = nullptr;
     }
   } call_span_end{ctx};
-  const bool copy_bound = verify_copy_bound(n, msg_bytes, 12 + pk_stride + sig_stride + (sig_len ? 4 : 0));
-  const std::vector<size_t> cb = verify_chunk_bounds(n, copy_bound);
+  // the call's plan (cg_plan.h): copy-bound or compute-bound by bytes per element, chunk
+  // bounds; a one-chunk call's own choices are made in create_batch once the partition
+  // has found the scheme mix
+  cg::VerifyShape shape;
+  shape.n = n;
+  shape.msg_bytes = msg_bytes;
+  shape.pk_stride = pk_stride;
+  shape.sig_stride = sig_stride;
+  shape.sig_len = sig_len != nullptr;
+  const cg::VerifyPlan plan = cg::plan_verify(shape, ctx->opts);
+  const std::vector<size_t>& cb = plan.chunks;
   if (cb.size() == 2) {  // one chunk: stage, then verify, with one host sync at the end
     MsgSrc m;
     m.host = msg;
@@ -2425,10 +2314,7 @@ cg_status cg_verify_batch(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
     m.off_host = msg_off;
     m.len_host = msg_len;
     m.keep_raw = true;
-    // latency mode only up to where it beats the balanced path with split points (r05z:
-    // 32 B ids 24,576 0.84 vs 0.81 ms, 40,000 0.97 vs 0.83; 1 KB 32,768 1.21 vs 1.33, 40,000
-    // 1.65 vs 1.49)
-    m.pair_max = copy_bound ? kEdPairMaxCopyBound : kEdPairMaxCompute;
+    m.pair_max = plan.pair_max;
     cg_batch* b = nullptr;
     cg_status st = create_batch(ctx, n, scheme_id, pk, pk_stride, sig, sig_stride, sig_len, m, &b);
     if (st != CG_OK) return st;
@@ -2581,6 +2467,16 @@ cg_status cg_set_debug(cg_ctx* ctx, int option, int64_t value) {
   CG_API_END(ctx)
 }
 
+cg_status cg_set_option(cg_ctx* ctx, const char* key, const char* value) {
+  CG_API_BEGIN
+  if (!ctx) return CG_E_INVALID_ARGUMENT;
+  const int o = cg::Options::find(key);
+  if (o < 0) return fail(ctx, CG_E_INVALID_ARGUMENT, std::string("unknown option ") + (key ? key : "(null)"));
+  ctx->opts.assign(o, value);
+  return CG_OK;
+  CG_API_END(ctx)
+}
+
 }  // extern "C"
 
 namespace {
@@ -2694,13 +2590,14 @@ cg_status tx_pipeline(cg_ctx* ctx, int mode, size_t n_tx, const uint8_t* arena, 
   // remain) is short, few enough that each chunk's signature subsets still fill the
   // device (CORDA_AMD_TX_CHUNKS / CORDA_AMD_TX_MIN_CHUNK override, for tuning and tests)
   size_t kmax = 6, min_chunk = 65536;
-  if (const char* e = std::getenv("CORDA_AMD_TX_CHUNKS")) kmax = std::max(1, std::atoi(e));
-  if (const char* e = std::getenv("CORDA_AMD_TX_MIN_CHUNK")) min_chunk = std::max(1, std::atoi(e));
+  const cg::Options& o = ctx->opts;
+  if (o.has(cg::OPT_TX_CHUNKS)) kmax = std::max(1, o.i(cg::OPT_TX_CHUNKS, 6));
+  if (o.has(cg::OPT_TX_MIN_CHUNK)) min_chunk = std::max(1, o.i(cg::OPT_TX_MIN_CHUNK, 65536));
   const size_t K = std::max<size_t>(1, std::min<size_t>(kmax, n_tx / min_chunk));
   // The last chunk's kernels run after the last upload, unhidden: it gets `tail` of
   // a regular chunk's transactions (CORDA_AMD_TX_TAIL, default 1 = even split).
   double tail = 1.0;
-  if (const char* e = std::getenv("CORDA_AMD_TX_TAIL")) tail = std::min(1.0, std::max(0.1, std::atof(e)));
+  if (o.has(cg::OPT_TX_TAIL)) tail = std::min(1.0, std::max(0.1, o.d(cg::OPT_TX_TAIL, 1.0)));
   std::vector<size_t> tb(K + 1);
   const double wsum = (double)(K - 1) + tail;
   for (size_t k = 0; k <= K; ++k)
@@ -2798,10 +2695,8 @@ cg_status tx_pipeline(cg_ctx* ctx, int mode, size_t n_tx, const uint8_t* arena, 
     hipStream_t saved;
     ~CurveStream() { c->ec_stream[1] = saved; }
   } curve_stream{ctx, ctx->ec_stream[1]};
-  {
-    const char* e = std::getenv("CORDA_AMD_TX_CURVE_ON_HASH");
-    if (ctx->ec_stream[1] == ctx->ec_stream[0] && (!e || std::atoi(e) != 0)) ctx->ec_stream[1] = ctx->hash_stream;
-  }
+  if (ctx->ec_stream[1] == ctx->ec_stream[0] && ctx->opts.on(cg::OPT_TX_CURVE_ON_HASH, true))
+    ctx->ec_stream[1] = ctx->hash_stream;
   // Merkle ids on hash_stream (after compute_txids' metadata uploads and tx_index on
   // ctx->stream), so chunk k+1's hashing runs beside chunk k's signature kernels; the
   // signature kernels of chunk k wait for its ids (the ECDSA fork inherits that).
@@ -3072,12 +2967,13 @@ cg_status ftx_pipeline(cg_ctx* ctx, size_t n_ftx, const uint8_t* arena, size_t a
                        uint32_t*& roots_d, uint8_t*& status_d, std::vector<uint32_t*>& stacks,
                        std::vector<hipEvent_t>& ev) {
   size_t kmax = 6, min_chunk = 65536;
-  if (const char* e = std::getenv("CORDA_AMD_FTX_CHUNKS")) kmax = std::max(1, std::atoi(e));
-  if (const char* e = std::getenv("CORDA_AMD_FTX_MIN_CHUNK")) min_chunk = std::max(1, std::atoi(e));
+  const cg::Options& o = ctx->opts;
+  if (o.has(cg::OPT_FTX_CHUNKS)) kmax = std::max(1, o.i(cg::OPT_FTX_CHUNKS, 6));
+  if (o.has(cg::OPT_FTX_MIN_CHUNK)) min_chunk = std::max(1, o.i(cg::OPT_FTX_MIN_CHUNK, 65536));
   const size_t K = std::max<size_t>(1, std::min<size_t>(kmax, n_ftx / min_chunk));
   // the last chunk's kernels run after the last byte: it gets `tail` of a regular chunk
   double tail = 0.5;
-  if (const char* e = std::getenv("CORDA_AMD_FTX_TAIL")) tail = std::min(1.0, std::max(0.1, std::atof(e)));
+  if (o.has(cg::OPT_FTX_TAIL)) tail = std::min(1.0, std::max(0.1, o.d(cg::OPT_FTX_TAIL, 0.5)));
   std::vector<size_t> tb(K + 1);
   const double wsum = (double)(K - 1) + (K > 1 ? tail : 1.0);
   for (size_t k = 0; k <= K; ++k) tb[k] = k == K ? n_ftx : (size_t)((double)n_ftx * (double)k / wsum);

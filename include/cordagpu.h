@@ -73,7 +73,7 @@
 extern "C" {
 #endif
 
-#define CG_ABI_VERSION 3
+#define CG_ABI_VERSION 4  /* 4: cg_set_option; the CORDA_AMD_* knobs read once, at cg_open */
 
 typedef int32_t cg_status;
 enum {
@@ -317,6 +317,18 @@ cg_status cg_reset_stats(cg_ctx* ctx);
  */
 enum { CG_DEBUG_FORCE_FULL_LENGTH = 1, CG_DEBUG_FAIL_ALLOC = 2, CG_DEBUG_THROW = 3, CG_DEBUG_FORCE_GLV_FALLBACK = 4 };
 cg_status cg_set_debug(cg_ctx* ctx, int option, int64_t value);
+
+/* Run-time options of a context: the CORDA_AMD_* tuning knobs — plan
+ * thresholds, chunk counts, stream placement — none of which changes a verdict.  cg_open
+ * reads each from the environment ONCE; cg_set_option(ctx, "CORDA_AMD_VERIFY_CHUNKS", "4")
+ * changes one for this context only (value NULL: unset, the library default).  No verify
+ * call reads the environment, so a JVM process may run contexts with different settings
+ * side by side.  Not thread-safe against a call in flight on the same context (as every
+ * entry point of a context).  Returns CG_E_INVALID_ARGUMENT for a key that is not an
+ * option (the message names it).  Reference: none (the JVM path has no such knobs); the
+ * per-node configuration pattern it follows is NodeConfiguration.kt:98-101
+ * (verifierType = InMemory | OutOfProcess). */
+cg_status cg_set_option(cg_ctx* ctx, const char* key, const char* value);
 
 #ifdef __cplusplus
 }

@@ -47,6 +47,10 @@ class CordaGpu(device: Int = 0) : AutoCloseable {
 
     private fun check(rc: Int) = check(rc == 0) { "libcordagpu error $rc: ${nativeLastError(handle)}" }
 
+    /** A CORDA_AMD_* tuning knob of this context (cg_set_option; null: the library default). The
+     *  library reads the environment only when the context opens; no knob changes a verdict. */
+    fun setOption(key: String, value: String?) = check(nativeSetOption(handle, key, value))
+
     /**
      * Batch form of [Crypto.isValid] (Crypto.kt:534-541) / [Crypto.doVerify] (Crypto.kt:472-483):
      * one verdict byte per element.  Buffers are direct ByteBuffers in the C-ABI layout (see [pack]).
@@ -113,6 +117,7 @@ class CordaGpu(device: Int = 0) : AutoCloseable {
         @JvmStatic external fun nativeOpen(device: Int): Long
         @JvmStatic external fun nativeClose(handle: Long)
         @JvmStatic external fun nativeLastError(handle: Long): String
+        @JvmStatic external fun nativeSetOption(handle: Long, key: String, value: String?): Int
         @JvmStatic external fun nativeVerify(handle: Long, n: Int, mode: Int, scheme: ByteBuffer, pk: ByteBuffer,
                                              pkStride: Int, sig: ByteBuffer, sigStride: Int, sigLen: ByteBuffer,
                                              msg: ByteBuffer, msgOff: ByteBuffer, msgLen: ByteBuffer,

@@ -7,6 +7,7 @@
  *   nativeTxVerifyExcept    cg_tx_verify_signatures_except  verifySignaturesExcept (:41-47, 72-77)
  *   nativeFtxVerify         cg_ftx_verify_batch      FilteredTransaction.verify (MerkleTransaction.kt:173-178)
  *   nativeCompositeEval     cg_composite_eval_batch  isFulfilledBy / CompositeSignature (CompositeKey.kt:186-209)
+ *   nativeSetOption         cg_set_option            a context's CORDA_AMD_* tuning knobs
  *
  * Build on a JVM host against the JDK's jni.h:
  *   gcc -O2 -shared -fPIC -I$JAVA_HOME/include -I$JAVA_HOME/include/linux -I../../include \
@@ -39,6 +40,18 @@ JNIEXPORT void JNICALL Java_net_corda_core_crypto_gpu_CordaGpu_nativeClose(JNIEn
 
 JNIEXPORT jstring JNICALL Java_net_corda_core_crypto_gpu_CordaGpu_nativeLastError(JNIEnv* env, jclass cls, jlong h) {
   return (*env)->NewStringUTF(env, cg_last_error(h > 0 ? CTX(h) : 0));
+}
+
+/* key / value as Java Strings (value null: unset); the modified-UTF-8 bytes of an ASCII
+ * option name are its C string */
+JNIEXPORT jint JNICALL Java_net_corda_core_crypto_gpu_CordaGpu_nativeSetOption(JNIEnv* env, jclass cls, jlong h,
+                                                                               jstring key, jstring value) {
+  const char* k = key ? (*env)->GetStringUTFChars(env, key, 0) : 0;
+  const char* v = value ? (*env)->GetStringUTFChars(env, value, 0) : 0;
+  const cg_status st = cg_set_option(h > 0 ? CTX(h) : 0, k, v);
+  if (v) (*env)->ReleaseStringUTFChars(env, value, v);
+  if (k) (*env)->ReleaseStringUTFChars(env, key, k);
+  return st;
 }
 
 JNIEXPORT jint JNICALL Java_net_corda_core_crypto_gpu_CordaGpu_nativeVerify(

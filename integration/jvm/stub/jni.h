@@ -27,6 +27,8 @@ struct JNINativeInterface_ {
   void* (*GetDirectBufferAddress)(JNIEnv* env, jobject buf);
   jlong (*GetDirectBufferCapacity)(JNIEnv* env, jobject buf);
   jstring (*NewStringUTF)(JNIEnv* env, const char* utf);
+  const char* (*GetStringUTFChars)(JNIEnv* env, jstring str, jboolean* is_copy);
+  void (*ReleaseStringUTFChars)(JNIEnv* env, jstring str, const char* utf);
 };
 
 #endif

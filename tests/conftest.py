@@ -79,6 +79,29 @@ def gpu_ctx():
     ctx.close()
 
 
+@pytest.fixture
+def knobs(gpu_ctx):
+    """The session context's CORDA_AMD_* run-time options (cg_set_option), with
+    monkeypatch's setenv / delenv names; every option a test touched is unset again after
+    it.  The library reads the environment only at cg_open, never per call."""
+    class Knobs:
+        def __init__(self):
+            self.touched = set()
+
+        def setenv(self, key, value):
+            gpu_ctx.set_option(key, value)
+            self.touched.add(key)
+
+        def delenv(self, key, raising=False):
+            gpu_ctx.set_option(key, None)
+            self.touched.add(key)
+
+    k = Knobs()
+    yield k
+    for key in k.touched:
+        gpu_ctx.set_option(key, None)
+
+
 def _der_with(r: int, s: int, pad_r: bool = False) -> bytes:
     def integer(v, pad=False):
         b = v.to_bytes(max(1, (v.bit_length() + 8) // 8), "big")  # minimal two's complement (v >= 0)

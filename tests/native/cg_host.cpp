@@ -456,3 +456,35 @@ extern "C" void cgh_bounds26_report(int64_t* max_limb, double* log2_max_col, int
   *max_top = cg_bounds26().max_top;
 }
 #endif
+
+// ------------------------------------------------------------------ host plan
+// cg_verify_batch's plan (cg_plan.h, the very functions cordagpu.cpp calls) for a call
+// shape and an options string "KEY=VALUE;..." (tests/test_plan.py).  out[13] =
+// {copy_bound, chunks, pair_max, defer_arena, defer_meta, async_arena, rows_direct,
+//  needs_key_sample, early_parts, split_points, key_dedupe, lanes, grouped_msm};
+// bounds[0..min(chunks + 1, max_bounds)) = the chunk boundaries.  Returns the number of
+// chunk boundaries, or -1 for an unknown option.
+#include "cg_plan.h"
+extern "C" int cgh_plan_verify(uint64_t n, uint64_t n_ed, uint64_t msg_bytes, uint64_t pk_stride, uint64_t sig_stride,
+                               int sig_len, int ecdsa, int ed_in_order, int keys_repeat, const char* opts,
+                               uint64_t* out, uint64_t* bounds, int max_bounds) {
+  cg::Options o;
+  if (!o.parse(opts)) return -1;
+  cg::VerifyShape s;
+  s.n = n;
+  s.n_ed = n_ed;
+  s.msg_bytes = msg_bytes;
+  s.pk_stride = pk_stride;
+  s.sig_stride = sig_stride;
+  s.sig_len = sig_len != 0;
+  s.ecdsa = ecdsa != 0;
+  s.ed_in_order = ed_in_order != 0;
+  s.keys_repeat = keys_repeat;
+  const cg::VerifyPlan p = cg::plan_verify(s, o);
+  const uint64_t v[13] = {p.copy_bound, p.chunks.size() - 1, p.pair_max, p.defer_arena, p.defer_meta, p.async_arena,
+                          p.rows_direct, p.needs_key_sample, p.early_parts, p.split_points, p.key_dedupe, p.lanes,
+                          p.grouped_msm};
+  memcpy(out, v, sizeof v);
+  for (int i = 0; i < max_bounds && i < (int)p.chunks.size(); ++i) bounds[i] = p.chunks[i];
+  return (int)p.chunks.size();
+}

@@ -24,7 +24,10 @@ static jstring new_string(JNIEnv* env, const char* s) {
   last_string = s;
   return (jstring)0;
 }
-static const struct JNINativeInterface_ kIface = {buf_addr, buf_cap, new_string};
+/* a fake Java String is its C string */
+static const char* get_utf(JNIEnv* env, jstring s, jboolean* is_copy) { return (const char*)s; }
+static void release_utf(JNIEnv* env, jstring s, const char* utf) {}
+static const struct JNINativeInterface_ kIface = {buf_addr, buf_cap, new_string, get_utf, release_utf};
 
 /* the glue's entry points (no header on the JVM side: the JVM resolves them by name) */
 jlong Java_net_corda_core_crypto_gpu_CordaGpu_nativeOpen(JNIEnv*, jclass, jint);
@@ -38,6 +41,8 @@ jlong Java_net_corda_core_crypto_gpu_CordaGpu_nativeBatchCreate(JNIEnv*, jclass,
 jint Java_net_corda_core_crypto_gpu_CordaGpu_nativeBatchVerify(JNIEnv*, jclass, jlong, jlong, jint, jobject,
                                                                jobject);
 void Java_net_corda_core_crypto_gpu_CordaGpu_nativeBatchDestroy(JNIEnv*, jclass, jlong, jlong);
+jint Java_net_corda_core_crypto_gpu_CordaGpu_nativeSetOption(JNIEnv*, jclass, jlong, jstring, jstring);
+#define JSTR(s) ((jstring)(s))
 
 static int failures;
 #define CHECK(c, m)                                   \
@@ -66,6 +71,9 @@ int main(int argc, char** argv) {
     Java_net_corda_core_crypto_gpu_CordaGpu_nativeLastError(env, 0, h);
     CHECK(last_string && strcmp(last_string, "null context") == 0, "last error of a failed open");
     Java_net_corda_core_crypto_gpu_CordaGpu_nativeClose(env, 0, h); /* ignored, no crash */
+    CHECK(Java_net_corda_core_crypto_gpu_CordaGpu_nativeSetOption(env, 0, h, JSTR("CORDA_AMD_ED_PAIR_MAX"),
+                                                                   JSTR("0")) == CG_E_INVALID_ARGUMENT,
+          "nativeSetOption without a context");
   } else {
     CHECK(h > 0, "nativeOpen");
     uint8_t scheme[2] = {4, 4}, pk[128], sig[128], msg[1] = {0x72}, verdict[2];
@@ -97,6 +105,18 @@ int main(int argc, char** argv) {
     CHECK(bad == CG_E_INVALID_ARGUMENT, "null pk buffer -> CG_E_INVALID_ARGUMENT as the handle");
     Java_net_corda_core_crypto_gpu_CordaGpu_nativeLastError(env, 0, h);
     CHECK(last_string && strlen(last_string) > 0, "error message");
+    CHECK(Java_net_corda_core_crypto_gpu_CordaGpu_nativeSetOption(env, 0, h, JSTR("CORDA_AMD_ED_PAIR_MAX"), JSTR("0")) ==
+              CG_OK, "nativeSetOption");
+    memset(verdict, 9, 2);
+    rc = Java_net_corda_core_crypto_gpu_CordaGpu_nativeVerify(env, 0, h, 2, CG_MODE_IS_VALID, &bs, &bpk, 64, &bsig, 64,
+                                                              &bsl, &bmsg, &bmo, &bml, &bv, 0);
+    CHECK(rc == CG_OK && verdict[0] == CG_ACCEPT && verdict[1] == CG_REJECT, "nativeVerify after nativeSetOption");
+    CHECK(Java_net_corda_core_crypto_gpu_CordaGpu_nativeSetOption(env, 0, h, JSTR("CORDA_AMD_ED_PAIR_MAX"), 0) == CG_OK,
+          "nativeSetOption unset");
+    CHECK(Java_net_corda_core_crypto_gpu_CordaGpu_nativeSetOption(env, 0, h, JSTR("NO_SUCH"), JSTR("1")) ==
+              CG_E_INVALID_ARGUMENT, "nativeSetOption unknown key");
+    Java_net_corda_core_crypto_gpu_CordaGpu_nativeLastError(env, 0, h);
+    CHECK(last_string && strstr(last_string, "NO_SUCH"), "unknown option named in the error");
     Java_net_corda_core_crypto_gpu_CordaGpu_nativeClose(env, 0, h);
   }
   printf("jni_harness %s: %s\n", gpu ? "gpu" : "cpu", failures ? "FAILED" : "ok");

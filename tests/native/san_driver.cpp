@@ -14,6 +14,9 @@
 //   H h                   half-size scalars (TB 128 and the key-reuse TB 192)
 //   J scheme u1 u2 qx qy  joint multiplication u1 G + u2 Q (GLV on secp256k1)
 //   T msg tail            SHA-256(msg || tail) as the Merkle leaf kernel streams it
+//   Q n n_ed bytes pks sgs sl ec ord keys opts
+//                         cg_verify_batch's host plan (cg_plan.h) for that shape and options
+//                         ("-" = none): its 13 fields and the chunk boundaries
 //   X                     negative control: a deliberate heap overread (must be reported)
 #include <stdint.h>
 #include <stdio.h>
@@ -48,6 +51,9 @@ void cgh_f26_op(int scheme, int op, const uint32_t* a, const uint32_t* b, uint32
 int cgh_ecdsa_joint(int scheme, const uint32_t* u1, const uint32_t* u2, const uint32_t* qx, const uint32_t* qy,
                     uint32_t* out, uint32_t force_nd);
 void cgh_sha256_tail(const uint8_t* msg, uint32_t n, const uint8_t* tail, uint32_t tail_n, uint8_t* out);
+int cgh_plan_verify(uint64_t n, uint64_t n_ed, uint64_t msg_bytes, uint64_t pk_stride, uint64_t sig_stride, int sig_len,
+                    int ecdsa, int ed_in_order, int keys_repeat, const char* opts, uint64_t* out, uint64_t* bounds,
+                    int max_bounds);
 }
 
 namespace {
@@ -133,9 +139,9 @@ int main() {
   oracle_ed25519_init();
   static char line[1 << 22];
   while (fgets(line, sizeof line, stdin)) {
-    char* f[8] = {nullptr};
+    char* f[12] = {nullptr};
     int nf = 0;
-    for (char* t = strtok(line, " \n"); t && nf < 8; t = strtok(nullptr, " \n")) f[nf++] = t;
+    for (char* t = strtok(line, " \n"); t && nf < 12; t = strtok(nullptr, " \n")) f[nf++] = t;
     if (nf == 0) continue;
     switch (f[0][0]) {
       case 'E':
@@ -203,6 +209,23 @@ int main() {
         cgh_sha256_tail(msg.p, msg.n(), tail.p, tail.n(), out);
         printf("T ");
         for (int i = 0; i < 32; ++i) printf("%02x", out[i]);
+        printf("\n");
+        break;
+      }
+      case 'Q': {  // host plan: n n_ed bytes pk_stride sig_stride sig_len ecdsa in_order keys_repeat opts
+        if (nf < 10) {
+          printf("Q skip\n");
+          break;
+        }
+        uint64_t out[13] = {0}, bounds[16] = {0};
+        const char* opts = nf > 10 && strcmp(f[10], "-") ? f[10] : "";
+        const int nb = cgh_plan_verify(strtoull(f[1], nullptr, 10), strtoull(f[2], nullptr, 10),
+                                       strtoull(f[3], nullptr, 10), strtoull(f[4], nullptr, 10),
+                                       strtoull(f[5], nullptr, 10), atoi(f[6]), atoi(f[7]), atoi(f[8]), atoi(f[9]),
+                                       opts, out, bounds, 16);
+        printf("Q %d", nb);
+        for (int i = 0; i < 13; ++i) printf(" %llu", (unsigned long long)out[i]);
+        for (int i = 0; i < nb && i < 16; ++i) printf(" %llu", (unsigned long long)bounds[i]);
         printf("\n");
         break;
       }

@@ -43,7 +43,7 @@ def test_python_binding_covers_header():
 def test_abi_version_and_no_fallback_without_gpu():
     from corda_amd import _lib
     lib = _lib.load()
-    assert lib.cg_abi_version() == _lib.ABI_VERSION == 3
+    assert lib.cg_abi_version() == _lib.ABI_VERSION == 4
     if lib.cg_device_count() > 0:
         pytest.skip("a GPU is present")
     h = ctypes.c_void_p()

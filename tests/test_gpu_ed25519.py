@@ -225,7 +225,7 @@ def test_forced_full_length_fallback_vs_oracle(gpu_ctx, oracle, golden_ed25519, 
 
 @pytest.mark.parametrize("bucket_min", ["0", "1", None])
 @pytest.mark.parametrize("mixed", [False, True])
-def test_grouped_msm_vs_oracle(gpu_ctx, oracle, golden_ed25519, monkeypatch, bucket_min, mixed):
+def test_grouped_msm_vs_oracle(gpu_ctx, oracle, golden_ed25519, knobs, bucket_min, mixed):
     """The balanced MSM over lanes grouped by digit count (cg_ed25519_bucket; round 6)
     against the oracle: off ('0'), from 4,096 signatures ('1'), and
     the default threshold (every piece of at least 4,096 grouped with '1').  Latency lanes off so the balanced MSM runs; every 97th lane
@@ -233,9 +233,9 @@ def test_grouped_msm_vs_oracle(gpu_ctx, oracle, golden_ed25519, monkeypatch, buc
     hash- and points-phase verdicts (written by the bucket kernel) among them; the mixed
     batch scatters the Ed25519 verdicts through the scheme partition's index."""
     from corda_amd._lib import DEBUG_FORCE_FULL_LENGTH
-    monkeypatch.setenv("CORDA_AMD_ED_PAIR_MAX", "0")
+    knobs.setenv("CORDA_AMD_ED_PAIR_MAX", "0")
     if bucket_min is not None:
-        monkeypatch.setenv("CORDA_AMD_ED_BUCKET_MIN", bucket_min)
+        knobs.setenv("CORDA_AMD_ED_BUCKET_MIN", bucket_min)
     g = golden_ed25519
     gb = crypto.pack(crypto.EDDSA_ED25519_SHA512, [bytes.fromhex(e["pk"]) for e in g],
                      [bytes.fromhex(e["sig"]) for e in g], [bytes.fromhex(e["msg"]) for e in g])
@@ -262,13 +262,13 @@ def test_grouped_msm_vs_oracle(gpu_ctx, oracle, golden_ed25519, monkeypatch, buc
 
 
 @pytest.fixture
-def key_reuse(monkeypatch, request):
+def key_reuse(knobs, request):
     """CORDA_AMD_KEY_REUSE: '1' forces the key-reuse path, '0' the balanced one,
     unset = automatic (distinct keys <= n / 8)."""
     if request.param is None:
-        monkeypatch.delenv("CORDA_AMD_KEY_REUSE", raising=False)
+        knobs.delenv("CORDA_AMD_KEY_REUSE", raising=False)
     else:
-        monkeypatch.setenv("CORDA_AMD_KEY_REUSE", request.param)
+        knobs.setenv("CORDA_AMD_KEY_REUSE", request.param)
     return request.param
 
 
@@ -333,7 +333,7 @@ def test_key_reuse_prepared_batch_bitmap(gpu_ctx, oracle, key_reuse):
                                                           ("9", "700", "0.3", "upload_on_caller"),
                                                           ("9", "700", "0.3", "ring"),
                                                           ("4", "700", "0.4", "pinned_in")])
-def test_host_verify_pipeline_small_chunks_vs_oracle(gpu_ctx, oracle, monkeypatch, chunks, min_chunk, tail, variant):
+def test_host_verify_pipeline_small_chunks_vs_oracle(gpu_ctx, oracle, knobs, chunks, min_chunk, tail, variant):
     """cg_verify_batch's pipeline (chunk k's upload on the copy stream beside chunk k-1's
     kernels) forced onto small, ragged chunks: a mixed batch — Ed25519 from distinct and
     from 12 repeated signers (the key-reuse path inside a chunk), secp256k1, P-256, an
@@ -349,19 +349,19 @@ def test_host_verify_pipeline_small_chunks_vs_oracle(gpu_ctx, oracle, monkeypatc
     DMAs; the pageable verdict buffers then come back through the bounce buffer)."""
     from corda_amd import dist as D
     from corda_amd._lib import KEY_INVALID, UNSUPPORTED
-    monkeypatch.setenv("CORDA_AMD_VERIFY_CHUNKS", chunks)
-    monkeypatch.setenv("CORDA_AMD_VERIFY_MIN_CHUNK", min_chunk)
-    monkeypatch.setenv("CORDA_AMD_VERIFY_TAIL", tail)
+    knobs.setenv("CORDA_AMD_VERIFY_CHUNKS", chunks)
+    knobs.setenv("CORDA_AMD_VERIFY_MIN_CHUNK", min_chunk)
+    knobs.setenv("CORDA_AMD_VERIFY_TAIL", tail)
     if variant in ("one_dma_off", "small_slices"):  # (ring staging options)
-        monkeypatch.setenv("CORDA_AMD_VERIFY_RING", "1")
+        knobs.setenv("CORDA_AMD_VERIFY_RING", "1")
     if variant == "one_dma_off":
-        monkeypatch.setenv("CORDA_AMD_VERIFY_ONE_DMA", "0")
+        knobs.setenv("CORDA_AMD_VERIFY_ONE_DMA", "0")
     if variant == "upload_on_caller":
-        monkeypatch.setenv("CORDA_AMD_VERIFY_UPLOAD_THREAD", "0")
+        knobs.setenv("CORDA_AMD_VERIFY_UPLOAD_THREAD", "0")
     if variant == "ring":
-        monkeypatch.setenv("CORDA_AMD_VERIFY_RING", "1")
+        knobs.setenv("CORDA_AMD_VERIFY_RING", "1")
     if variant == "small_slices":
-        monkeypatch.setenv("CORDA_AMD_VERIFY_SLICE_KB", "4")
+        knobs.setenv("CORDA_AMD_VERIFY_SLICE_KB", "4")
     sch = np.random.default_rng(12).choice(np.array([2, 3, 4, 4, 4], np.uint8), size=5200)
     w = datagen.make_batch(len(sch), msg_bytes=70, scheme=sch, seed=23, key_base=620_000)
     w = datagen.add_ecdsa_adversarial(w, frac=0.2, seed=4)
@@ -414,7 +414,7 @@ def test_host_verify_pipeline_small_chunks_vs_oracle(gpu_ctx, oracle, monkeypatc
 
 
 @pytest.mark.parametrize("beside", [None, "0"])
-def test_one_chunk_large_arena_and_pinned_outputs_vs_oracle(gpu_ctx, oracle, monkeypatch, beside):
+def test_one_chunk_large_arena_and_pinned_outputs_vs_oracle(gpu_ctx, oracle, knobs, beside):
     """The one-chunk host verify with an arena large enough (8,192 x 1 KB) that its deferred
     copy runs on its own stream beside the staging and points kernels (and with that
     turned off, CORDA_AMD_ARENA_BESIDE=0), 25 % mutated, in both modes; then the same call
@@ -422,7 +422,7 @@ def test_one_chunk_large_arena_and_pinned_outputs_vs_oracle(gpu_ctx, oracle, mon
     the bounce buffer) — verdicts and bitmap against the oracle."""
     from corda_amd import dist as D
     if beside is not None:
-        monkeypatch.setenv("CORDA_AMD_ARENA_BESIDE", beside)
+        knobs.setenv("CORDA_AMD_ARENA_BESIDE", beside)
     w = datagen.add_ed25519_adversarial(datagen.make_batch(8192, msg_bytes=1024, seed=83, key_base=970_000),
                                         frac=0.25, seed=13)
     assert len(w.msg) >= 6 << 20
@@ -446,14 +446,14 @@ def test_one_chunk_large_arena_and_pinned_outputs_vs_oracle(gpu_ctx, oracle, mon
 
 
 @pytest.mark.parametrize("chunks", [None, "5"])
-def test_compact_ed25519_layout_vs_oracle(gpu_ctx, oracle, monkeypatch, chunks):
+def test_compact_ed25519_layout_vs_oracle(gpu_ctx, oracle, knobs, chunks):
     """The layout an Ed25519-only JVM caller packs (and bench.py's end-to-end line times):
     scheme_id NULL, 32-byte key rows, 64-byte R||S rows and sig_len NULL — and the same
     with sig_len given when some rows are ragged (E12: 0 / 63 / 65 bytes, sig_stride 68).
     Verdicts in both modes against the oracle on the full-layout rows."""
     if chunks:
-        monkeypatch.setenv("CORDA_AMD_VERIFY_CHUNKS", chunks)
-        monkeypatch.setenv("CORDA_AMD_VERIFY_MIN_CHUNK", "300")
+        knobs.setenv("CORDA_AMD_VERIFY_CHUNKS", chunks)
+        knobs.setenv("CORDA_AMD_VERIFY_MIN_CHUNK", "300")
     w = datagen.add_ed25519_adversarial(datagen.make_batch(4000, msg_bytes=200, seed=41, key_base=700_000),
                                         frac=0.2, seed=13)
     sl = w.sig_len[:w.n].astype(np.uint32)
@@ -478,14 +478,14 @@ def test_compact_ed25519_layout_vs_oracle(gpu_ctx, oracle, monkeypatch, chunks):
 
 
 @pytest.mark.parametrize("split,overlap,signers", [("2", "1", 0), ("3", "0", 0), ("2", "1", 40)])
-def test_prepared_batch_split_and_overlap_vs_oracle(gpu_ctx, oracle, monkeypatch, split, overlap, signers):
+def test_prepared_batch_split_and_overlap_vs_oracle(gpu_ctx, oracle, knobs, split, overlap, signers):
     """cg_batch_verify's scheduling variants on one prepared batch: the Ed25519 subset as
     index pieces on two streams (CORDA_AMD_ED_SPLIT, pieces >= 65,536), the points kernel
     beside the hash kernel or after it (CORDA_AMD_ED_OVERLAP), distinct signers and 40
     repeated ones (the key-reuse path: both lanes wait for the per-key tables) — verdicts
     and accept bitmap identical to the oracle's, verified twice."""
-    monkeypatch.setenv("CORDA_AMD_ED_SPLIT", split)
-    monkeypatch.setenv("CORDA_AMD_ED_OVERLAP", overlap)
+    knobs.setenv("CORDA_AMD_ED_SPLIT", split)
+    knobs.setenv("CORDA_AMD_ED_OVERLAP", overlap)
     n = 3 * 65536 + 777
     w = datagen.make_batch(n, msg_bytes=32, seed=51, key_base=800_000, key_reuse=signers)
     w = datagen.add_ed25519_adversarial(w, frac=0.02, seed=19)
@@ -504,7 +504,7 @@ def test_prepared_batch_split_and_overlap_vs_oracle(gpu_ctx, oracle, monkeypatch
 
 @pytest.mark.parametrize("lanes", [1, 2, 4, 8])
 @pytest.mark.parametrize("mode", [MODE_IS_VALID, MODE_DO_VERIFY])
-def test_latency_mode_on_and_off_vs_oracle(gpu_ctx, oracle, golden_ed25519, monkeypatch, lanes, mode):
+def test_latency_mode_on_and_off_vs_oracle(gpu_ctx, oracle, golden_ed25519, knobs, lanes, mode):
     """The latency mode (cg_ed25519_points_lanes / cg_ed25519_msm_lanes: two, four or eight
     lanes per signature, used for small pieces, CORDA_AMD_ED_PAIR_MAX / _QUAD_MAX / _OCT_MAX)
     forced on for every size with 2, 4 and 8 lanes, and forced off: every golden class
@@ -513,9 +513,9 @@ def test_latency_mode_on_and_off_vs_oracle(gpu_ctx, oracle, golden_ed25519, monk
     loops beside ~33-window ones in one wave).  The library's per-kernel counters confirm
     which MSM kernel ran."""
     from corda_amd._lib import DEBUG_FORCE_FULL_LENGTH
-    monkeypatch.setenv("CORDA_AMD_ED_PAIR_MAX", "0" if lanes == 1 else "1000000")
-    monkeypatch.setenv("CORDA_AMD_ED_QUAD_MAX", "1000000" if lanes >= 4 else "0")
-    monkeypatch.setenv("CORDA_AMD_ED_OCT_MAX", "1000000" if lanes == 8 else "0")
+    knobs.setenv("CORDA_AMD_ED_PAIR_MAX", "0" if lanes == 1 else "1000000")
+    knobs.setenv("CORDA_AMD_ED_QUAD_MAX", "1000000" if lanes >= 4 else "0")
+    knobs.setenv("CORDA_AMD_ED_OCT_MAX", "1000000" if lanes == 8 else "0")
     msm = {1: "ed25519_msm", 2: "ed25519_msm_pair", 4: "ed25519_msm_quad", 8: "ed25519_msm_oct"}[lanes]
     gpu_ctx.set_profiling(True)
     gpu_ctx.reset_stats()
@@ -545,7 +545,7 @@ def test_latency_mode_on_and_off_vs_oracle(gpu_ctx, oracle, golden_ed25519, monk
 
 
 @pytest.mark.parametrize("path", ["auto", "lanes1", "key_reuse"])
-def test_reference_ed25519_artefacts(gpu_ctx, oracle, ref_ed25519_cases, monkeypatch, path):
+def test_reference_ed25519_artefacts(gpu_ctx, oracle, ref_ed25519_cases, knobs, path):
     """The reference's own Ed25519 artefacts (tests/golden/ref_ed25519_vectors.json): the
     tutorial's two signatures over its tx id (docs/source/tutorial-cordapp.rst:472-476), the
     four Kryo-wire keys (trade.json:3,25 = entropyToKeyPair(1)/(2); tutorial-cordapp.rst:498-499)
@@ -558,9 +558,9 @@ def test_reference_ed25519_artefacts(gpu_ctx, oracle, ref_ed25519_cases, monkeyp
     from conftest import REF_ED_EXPECT
     if path == "lanes1":
         for v in ("CORDA_AMD_ED_PAIR_MAX", "CORDA_AMD_ED_QUAD_MAX", "CORDA_AMD_ED_OCT_MAX"):
-            monkeypatch.setenv(v, "0")
+            knobs.setenv(v, "0")
     elif path == "key_reuse":
-        monkeypatch.setenv("CORDA_AMD_KEY_REUSE", "1")
+        knobs.setenv("CORDA_AMD_KEY_REUSE", "1")
     cases = ref_ed25519_cases
     b = crypto.pack(crypto.EDDSA_ED25519_SHA512, [c["pk"] for c in cases], [c["sig"] for c in cases],
                     [c["msg"] for c in cases])
@@ -598,14 +598,14 @@ def test_reference_ed25519_artefacts(gpu_ctx, oracle, ref_ed25519_cases, monkeyp
 
 
 @pytest.mark.parametrize("split", ["2", "3"])
-def test_one_chunk_verify_split_pieces_vs_oracle(gpu_ctx, oracle, monkeypatch, split):
+def test_one_chunk_verify_split_pieces_vs_oracle(gpu_ctx, oracle, knobs, split):
     """cg_verify_batch as ONE chunk (CORDA_AMD_VERIFY_CHUNKS=1) of an Ed25519-only batch —
     whose message arena is uploaded late, from launch_verify — with the index pieces on two
     streams (CORDA_AMD_ED_SPLIT): the arena must be on the device before any piece's hash
     kernel runs on the second stream (round-4 advisor finding).  Verdicts against the oracle
     on the mutated subset and a stride sample; every untouched signature accepts."""
-    monkeypatch.setenv("CORDA_AMD_VERIFY_CHUNKS", "1")
-    monkeypatch.setenv("CORDA_AMD_ED_SPLIT", split)
+    knobs.setenv("CORDA_AMD_VERIFY_CHUNKS", "1")
+    knobs.setenv("CORDA_AMD_ED_SPLIT", split)
     n = 2 * 65536 + 8191 if split == "2" else 3 * 65536 + 100
     w = datagen.add_ed25519_adversarial(datagen.make_batch(n, msg_bytes=256, seed=93, key_base=1_300_000),
                                         frac=0.02, seed=23)
@@ -622,7 +622,7 @@ def test_one_chunk_verify_split_pieces_vs_oracle(gpu_ctx, oracle, monkeypatch, s
                                                      (50_000, True, "", 32),
                                                      (20_000, False, "", 32), (6_000, True, "", 1024),
                                                      (12_000, True, "", 1024), (12_000, False, "CORDA_AMD_ASYNC_ARENA=0", 1024)])
-def test_compute_bound_one_chunk_deferred_offsets_vs_oracle(gpu_ctx, oracle, monkeypatch, n, reverse, env, msg_bytes):
+def test_compute_bound_one_chunk_deferred_offsets_vs_oracle(gpu_ctx, oracle, knobs, n, reverse, env, msg_bytes):
     """A compute-bound host-buffer call (32-byte tx ids: ~140 B per element) runs as ONE chunk
     up to 2^20 elements, and for an Ed25519-only in-order batch its offsets and lengths go
     up with the arena, after the key and signature rows (the points kernel starts first,
@@ -639,7 +639,7 @@ def test_compute_bound_one_chunk_deferred_offsets_vs_oracle(gpu_ctx, oracle, mon
     the same with the arena and its offsets / lengths issued from the upload thread beside
     the row copies (async arena; ASYNC_ARENA=0: after them)."""
     for kv in filter(None, env.split(",")):
-        monkeypatch.setenv(*kv.split("=", 1))
+        knobs.setenv(*kv.split("=", 1))
     w = datagen.add_ed25519_adversarial(datagen.make_batch(n, msg_bytes=msg_bytes, seed=101, key_base=1_700_000),
                                         frac=0.2, seed=31)
     ln = w.msg_len[:n].astype(np.uint64)
@@ -666,7 +666,7 @@ def test_compute_bound_one_chunk_deferred_offsets_vs_oracle(gpu_ctx, oracle, mon
 
 
 @pytest.mark.parametrize("upload_thread", ["1", "0"])
-def test_pipeline_errors_then_recovery(gpu_ctx, oracle, monkeypatch, upload_thread):
+def test_pipeline_errors_then_recovery(gpu_ctx, oracle, knobs, upload_thread):
     """A chunked host-buffer call (forced into six chunks) whose fifth chunk holds a message
     outside the arena returns CG_E_INVALID_ARGUMENT: the chunk's inputs are checked on the
     calling thread before its kernels go out, the upload thread (CORDA_AMD_VERIFY_UPLOAD_THREAD)
@@ -675,9 +675,9 @@ def test_pipeline_errors_then_recovery(gpu_ctx, oracle, monkeypatch, upload_thre
     call's last allocation, nothing).  After every failure the same context verifies the
     intact batch against the oracle."""
     from corda_amd._lib import DEBUG_FAIL_ALLOC, CordaGpuError
-    monkeypatch.setenv("CORDA_AMD_VERIFY_CHUNKS", "6")
-    monkeypatch.setenv("CORDA_AMD_VERIFY_MIN_CHUNK", "500")
-    monkeypatch.setenv("CORDA_AMD_VERIFY_UPLOAD_THREAD", upload_thread)
+    knobs.setenv("CORDA_AMD_VERIFY_CHUNKS", "6")
+    knobs.setenv("CORDA_AMD_VERIFY_MIN_CHUNK", "500")
+    knobs.setenv("CORDA_AMD_VERIFY_UPLOAD_THREAD", upload_thread)
     n = 4000
     w = datagen.add_ed25519_adversarial(datagen.make_batch(n, msg_bytes=96, seed=77, key_base=1_900_000),
                                         frac=0.2, seed=13)
@@ -702,11 +702,13 @@ def test_pipeline_errors_then_recovery(gpu_ctx, oracle, monkeypatch, upload_thre
         assert np.array_equal(crypto.verify_packed(gpu_ctx, good, MODE_IS_VALID), exp), k
 
 
-@pytest.mark.parametrize("n,msg_bytes", [(1, 32), (63, 1024), (65, 32), (257, 1024), (40_001, 32), (65_537, 32),
+@pytest.mark.parametrize("n,msg_bytes", [(1, 32), (63, 1024), (65, 32), (257, 1024), (20_480, 32), (20_481, 32),
+                                         (32_768, 1024), (32_769, 1024), (40_001, 32), (65_537, 32),
                                          (131_073, 32), (131_073, 1024), (262_145, 1024), ((1 << 20) + 1, 32)])
 def test_host_verify_plan_boundaries_vs_oracle(gpu_ctx, oracle, n, msg_bytes):
     """cg_verify_batch from pageable host buffers at sizes one past each plan boundary:
-    the latency-mode thresholds (40,000), the early-points part size (65,536), the
+    the latency-mode thresholds (one-chunk calls: 20,480 for 32 B ids, 32,768 for 1 KB
+    messages — each at and one past; pieces: 40,000), the early-points part size (65,536), the
     pipeline's start for copy-bound calls (2^17) and for compute-bound ones (2^20: 2^20 + 1
     32-byte ids run as eight chunks), and small ragged calls; 32 B ids and 1 KB messages, 2 %
     mutated, every verdict against the oracle."""
@@ -716,3 +718,40 @@ def test_host_verify_plan_boundaries_vs_oracle(gpu_ctx, oracle, n, msg_bytes):
     got = gpu_verdicts(gpu_ctx, w, MODE_IS_VALID)
     bad = np.flatnonzero(got != exp)
     assert bad.size == 0, [(w.classes[i], int(got[i]), int(exp[i])) for i in bad[:10]]
+
+
+def test_options_are_read_at_open_and_set_per_context(gpu_ctx, oracle, knobs):
+    """The CORDA_AMD_* knobs (cg_plan.h Options): an environment change after cg_open has
+    no effect on the open context, cg_set_option has (the library's per-kernel counters say
+    which MSM ran), an unknown key is an error naming it, and the verdicts never change."""
+    from corda_amd._lib import CordaGpuError
+    w = datagen.add_ed25519_adversarial(datagen.make_batch(1000, msg_bytes=32, seed=8, key_base=2_600_000), frac=0.1,
+                                        seed=4)
+    exp = oracle_verdicts(oracle, w, MODE_IS_VALID)
+
+    def msm_kernels():
+        gpu_ctx.set_profiling(True)
+        gpu_ctx.reset_stats()
+        try:
+            assert np.array_equal(gpu_verdicts(gpu_ctx, w, MODE_IS_VALID), exp)
+            return {k for k in ("ed25519_msm", "ed25519_msm_pair", "ed25519_msm_quad", "ed25519_msm_oct")
+                    if gpu_ctx.kernel_stats(k)[1]}
+        finally:
+            gpu_ctx.set_profiling(False)
+
+    assert msm_kernels() == {"ed25519_msm_oct"}  # 1,000 signatures: eight lanes per signature
+    old = os.environ.get("CORDA_AMD_ED_PAIR_MAX")
+    os.environ["CORDA_AMD_ED_PAIR_MAX"] = "0"
+    try:
+        assert msm_kernels() == {"ed25519_msm_oct"}  # read at cg_open only
+    finally:
+        if old is None:
+            os.environ.pop("CORDA_AMD_ED_PAIR_MAX")
+        else:
+            os.environ["CORDA_AMD_ED_PAIR_MAX"] = old
+    knobs.setenv("CORDA_AMD_ED_PAIR_MAX", "0")
+    assert msm_kernels() == {"ed25519_msm"}
+    knobs.setenv("CORDA_AMD_ED_PAIR_MAX", None)
+    assert msm_kernels() == {"ed25519_msm_oct"}
+    with pytest.raises(CordaGpuError, match="CORDA_AMD_NO_SUCH_KNOB"):
+        gpu_ctx.set_option("CORDA_AMD_NO_SUCH_KNOB", "1")

@@ -56,12 +56,12 @@ def run_tx_verify(ctx, w, mode=MODE_DO_VERIFY):
 
 
 @pytest.fixture(params=["1", "5"], ids=["one_chunk", "pipelined_5_chunks"])
-def tx_chunks(request, monkeypatch):
+def tx_chunks(request, knobs):
     """cg_tx_verify_batch as one chunk, and streamed through the copy-stream pipeline
     in 5 tx-range chunks (the arena pieces, per-chunk hashing and signature subsets
     of tx_pipeline in cordagpu.cpp) at this small size."""
-    monkeypatch.setenv("CORDA_AMD_TX_CHUNKS", request.param)
-    monkeypatch.setenv("CORDA_AMD_TX_MIN_CHUNK", "1000")
+    knobs.setenv("CORDA_AMD_TX_CHUNKS", request.param)
+    knobs.setenv("CORDA_AMD_TX_MIN_CHUNK", "1000")
     return int(request.param)
 
 
@@ -176,12 +176,12 @@ def _ftx_call(ctx, a, n):
 
 
 @pytest.fixture(params=[None, ("5", "3")], ids=["ftx-default-chunks", "ftx-5-chunks"])
-def ftx_chunks(request, monkeypatch):
+def ftx_chunks(request, knobs):
     """cg_ftx_verify_batch's upload/kernel pipeline: library defaults, and forced onto
     5 small ftx-index chunks (CORDA_AMD_FTX_CHUNKS / _MIN_CHUNK)."""
     if request.param:
-        monkeypatch.setenv("CORDA_AMD_FTX_CHUNKS", request.param[0])
-        monkeypatch.setenv("CORDA_AMD_FTX_MIN_CHUNK", request.param[1])
+        knobs.setenv("CORDA_AMD_FTX_CHUNKS", request.param[0])
+        knobs.setenv("CORDA_AMD_FTX_MIN_CHUNK", request.param[1])
     return request.param
 
 

@@ -4,8 +4,8 @@ pipeline settings, on the GPU box:
     python tools/e2e_sweep.py [--out gpurun_out/e2e_sweep.json]
 
 For each batch size (config-2 elements: Ed25519, 1 KB messages, distinct keys) and
-each setting of CORDA_AMD_VERIFY_CHUNKS / _MIN_CHUNK / _HEAD / _TAIL / _RING (read by the
-library on every call), the p50 of 15 calls after 3 warm-ups; also the same with the
+each setting of CORDA_AMD_VERIFY_CHUNKS / _MIN_CHUNK / _HEAD / _TAIL / _RING (set on the
+context with cg_set_option), the p50 of 15 calls after 3 warm-ups; also the same with the
 input buffers page-locked (cg_register_host) and the raw pageable / pinned H2D rates,
 so every p50 can be put against the PCIe bound of its bytes.
 """
@@ -68,6 +68,9 @@ def main():
     ap.add_argument("--msg-bytes", type=int, default=1024, help="message length (32: the production tx-id shape)")
     ap.add_argument("--spans", action="store_true", help="also one profiled call per row: bench.e2e_spans")
     ap.add_argument("--timeline", action="store_true", help="with --spans: every span of that call, in start order")
+    ap.add_argument("--bench-layout", action="store_true",
+                    help="the driver bench line's layout: 1 %% adversarial (E1-E12), ragged E12 rows with sig_len, "
+                         "signature stride 68 (bench.py e2e_record_32b / latency)")
     a = ap.parse_args()
     if a.spans:
         import tempfile
@@ -79,23 +82,32 @@ def main():
     from corda_amd._lib import ACCEPT, MODE_IS_VALID
     sizes = [int(x) for x in a.sizes.split(",")]
     w = datagen.make_batch(max(sizes), msg_bytes=a.msg_bytes, seed=42, key_base=0, ref_seed_stride=4096)
+    if a.bench_layout:
+        w = datagen.add_ed25519_adversarial(w, frac=0.01, seed=77)
     res = {"h2d_GBps": h2d_rates(), "runs": a.runs, "rows": []}
     with Context(0) as ctx:
         for n in sizes:
             s = w.subset(np.arange(n))
-            b = crypto.PackedBatch(s.n, None, np.ascontiguousarray(s.pk[:, :32]), 32,
-                                   np.ascontiguousarray(s.sig[:, :64]), 64, None, s.msg, s.msg_off, s.msg_len)
-            nbytes = sum(x.nbytes for x in (b.pk, b.sig, b.msg, b.msg_off, b.msg_len))
+            sl = s.sig_len[:n].astype(np.uint32)
+            ragged = a.bench_layout and bool((sl != 64).any())
+            ss = max(64, (int(sl.max()) + 3) // 4 * 4) if ragged else 64
+            sg = np.zeros((n, ss), dtype=np.uint8)
+            sg[:, :min(ss, s.sig_stride)] = s.sig[:n, :min(ss, s.sig_stride)]
+            b = crypto.PackedBatch(s.n, None, np.ascontiguousarray(s.pk[:, :32]), 32, sg, ss,
+                                   np.ascontiguousarray(sl) if ragged else None, s.msg, s.msg_off, s.msg_len)
+            nbytes = sum(x.nbytes for x in (b.pk, b.sig, b.msg, b.msg_off, b.msg_len)) + (sl.nbytes if ragged else 0)
             for pinned in ((False,) if a.pageable_only else (False, True)):
                 if pinned:
                     ctx.register_host(b.pk, b.sig, b.msg, b.msg_off, b.msg_len)
                 for st in settings:
-                    for k in set(KEYS).union(*settings):
-                        os.environ.pop(k, None)
-                    os.environ.update(st)
+                    for k in set(KEYS).union(*settings):  # (cg_set_option: the context's knobs)
+                        ctx.set_option(k, None)
+                    for k, v in st.items():
+                        ctx.set_option(k, v)
                     for _ in range(3):
                         v = crypto.verify_packed(ctx, b, MODE_IS_VALID)
-                    ok = bool((v == ACCEPT).all())
+                    ok = bool((v == ACCEPT).all()) if not a.bench_layout else \
+                        bool((v[np.array([c == "valid" for c in s.classes[:n]])] == ACCEPT).all())
                     ts = []
                     for _ in range(a.runs):
                         t0 = time.perf_counter()
@@ -118,8 +130,6 @@ def main():
                     print(json.dumps(row), flush=True)
                 if pinned:
                     ctx.unregister_host(b.pk, b.sig, b.msg, b.msg_off, b.msg_len)
-    for k in set(KEYS).union(*settings):
-        os.environ.pop(k, None)
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
     with open(a.out, "w") as f:
         json.dump(res, f, indent=1)
