@@ -79,19 +79,22 @@ CG_HD void ed25519_abyte(uint32_t ab[8], const uint32_t pk[8]) {
 // chunks over per-key tables, |c1| < 2^66, B digits over four tables 2^(64 t) B;
 // ndig then carries the number of low windows in which chunk 3 (digits 48..63 of
 // c0) is nonzero, plus 32 when c1 needs a 17th digit (ed_status_* decode it).
-template <bool FULL_LENGTH = false, bool REUSE = false>
-CG_HD uint32_t ed25519_hash_stage(const uint32_t pk[8], const uint32_t sig[16], uint32_t sig_len, const uint8_t* msg,
-                                  uint32_t msg_len, uint32_t mode, uint32_t dig[kDigitWords], uint32_t& ndig,
-                                  uint32_t& rneg, bool force_full = false) {
+// R = the signature's words 0..7; loadS(s[8]) supplies words 8..15 (S) when they are
+// needed — after the half-size reduction, so the kernel need not hold them (8 VGPRs)
+// through SHA-512 and the reduction (round 6: the hash kernel spilled at its 128-VGPR
+// four-wave shape).
+template <bool FULL_LENGTH = false, bool REUSE = false, typename LoadS>
+CG_HD uint32_t ed25519_hash_stage_r(const uint32_t pk[8], const uint32_t r[8], LoadS&& loadS, uint32_t sig_len,
+                                    const uint8_t* msg, uint32_t msg_len, uint32_t mode, uint32_t dig[kDigitWords],
+                                    uint32_t& ndig, uint32_t& rneg, bool force_full = false) {
   ndig = kMinDigits;
   rneg = 0;
   const uint32_t pre = ed25519_precheck_sig(sig_len, msg_len, mode);
   if (pre != V_COMPUTE) return pre;
   uint32_t ab[8], hd[16], h[8], s[8], c0[8], c1[8], b[8];
   ed25519_abyte(ab, pk);
-  sha512_ed25519(hd, sig, ab, msg, msg_len);
+  sha512_ed25519(hd, r, ab, msg, msg_len);
   sc_reduce512(h, hd);
-  sc_effective_s(s, sig + 8);
   uint32_t c1neg = 0;
   if (FULL_LENGTH || force_full) {
     CG_UNROLL for (int w = 0; w < 8; ++w) {
@@ -102,6 +105,11 @@ CG_HD uint32_t ed25519_hash_stage(const uint32_t pk[8], const uint32_t sig[16], 
     ed25519_half_scalars<192, 66>(h, c0, c1, c1neg);
   } else {
     ed25519_half_scalars(h, c0, c1, c1neg);
+  }
+  {
+    uint32_t sw[8];
+    loadS(sw);
+    sc_effective_s(s, sw);
   }
   // [c1 S mod L] B + [c0](-A) + [c1](-R) = 0, with c1 = (-1)^c1neg |c1|
   sc_mul_mod(b, c1, s);
@@ -135,6 +143,18 @@ CG_HD uint32_t ed25519_hash_stage(const uint32_t pk[8], const uint32_t sig[16], 
   }
   ndig = nd;
   return V_COMPUTE;
+}
+
+// The same from the signature's 16 words (host builds, tests).
+template <bool FULL_LENGTH = false, bool REUSE = false>
+CG_HD uint32_t ed25519_hash_stage(const uint32_t pk[8], const uint32_t sig[16], uint32_t sig_len, const uint8_t* msg,
+                                  uint32_t msg_len, uint32_t mode, uint32_t dig[kDigitWords], uint32_t& ndig,
+                                  uint32_t& rneg, bool force_full = false) {
+  return ed25519_hash_stage_r<FULL_LENGTH, REUSE>(
+      pk, sig, [&](uint32_t sw[8]) CG_LINLINE {
+        CG_UNROLL for (int w = 0; w < 8; ++w) sw[w] = sig[8 + w];
+      },
+      sig_len, msg, msg_len, mode, dig, ndig, rneg, force_full);
 }
 
 // Strict decode of R on top of the i2p decode: canonical y (< p), a square root

@@ -114,27 +114,22 @@ CG_HD uint32_t sc_bit(const uint32_t u[8], int pos) {
 // bit-serial emulation below only runs for such (adversarial) scalars.
 CG_HD uint32_t slide_drops_carry(const uint32_t s[8]) {
   if (!(s[7] >> 31)) return 0;
-  uint32_t u[8];
-  CG_UNROLL for (int i = 0; i < 8; ++i) u[i] = s[i];
-  uint32_t drop = 0;
-  int pos = 0;
-  CG_NOUNROLL while (pos < 256) {
-    if (!sc_bit(u, pos)) { ++pos; continue; }
-    if (pos + 4 < 256 && sc_bit(u, pos + 4)) {
-      // u += 2^(pos+4)
-      const int p = pos + 4;
-      uint64_t c = 0;
-      CG_UNROLL for (int i = 0; i < 8; ++i) {
-        const uint32_t add = ((p >> 5) == i) ? (1u << (p & 31)) : 0u;
-        const uint64_t t = (uint64_t)u[i] + add + c;
-        u[i] = (uint32_t)t;
-        c = t >> 32;
-      }
-      drop |= (uint32_t)c;
-    }
-    pos += 4;
+  // The scan as a 6-state automaton over the ORIGINAL bits, LSB first (a carry only
+  // ever clears the run of ones above a window's check bit and sets the zero after it,
+  // where the next window starts, so no later step reads a modified bit):
+  //   0 idle (looking for a set bit)   1..3 window, 3..1 bits left to absorb
+  //   4 check bit i+4 (set: +2^(i+4))  5 carry rippling through ones (a zero: next window)
+  // next = kNext[2 state + bit], 4 bits per entry; drop <=> still carrying past bit 255.
+  // Round 6: fully unrolled, ~5 instructions per bit; the bit-serial loop it replaces
+  // (dynamic word selects, a 256-bit add per window) stretched a latency-mode hash wave
+  // holding one such scalar by ~40 us (E6 rows, r06f/g).
+  constexpr uint64_t kNext = 0x515044332210ull;  // entries 0..11: 0 1 2 2 3 3 4 4 0 5 1 5
+  uint32_t st = 0;
+  CG_UNROLL for (int w = 0; w < 8; ++w) {
+    const uint32_t x = s[w];
+    CG_UNROLL for (int k = 0; k < 32; ++k) st = (uint32_t)(kNext >> (8 * st + 4 * ((x >> k) & 1u))) & 7u;
   }
-  return drop;
+  return st == 5u;
 }
 
 // Signed radix-16 digits of k < 2^253: d_i in [-8, 7] (d_63 in [0, 2]), packed
@@ -210,7 +205,10 @@ CG_HD void sc_effective_s(uint32_t out[8], const uint32_t s[8]) {
   const uint32_t c256[8] = CG_C256_WORDS;
   uint32_t adj[8];
   sc_sub_mod(adj, sm, c256);
-  CG_UNROLL for (int i = 0; i < 8; ++i) out[i] = drop ? adj[i] : sm[i];
+  // (a mask, not `drop ? adj[i] : sm[i]`: LLVM turned that array select into a select of
+  // pointers to two scratch copies, 64 B of private memory per lane)
+  const uint32_t m = 0u - drop;
+  CG_UNROLL for (int i = 0; i < 8; ++i) out[i] = (adj[i] & m) | (sm[i] & ~m);
 }
 
 }  // namespace cg

@@ -322,6 +322,13 @@ hipEvent_t take_event(cg_ctx* ctx) {
   return e;
 }
 
+// Profiling span events that will not be pushed as a span (their copy or kernel failed
+// or never ran): back to the pool, never to hipEventElapsedTime unrecorded.
+void give_back_events(cg_ctx* ctx, hipEvent_t a, hipEvent_t b) {
+  if (a) ctx->event_pool.push_back(a);
+  if (b) ctx->event_pool.push_back(b);
+}
+
 // RAII timing scope around one kernel launch on the context stream (or `s`).
 struct Timed {
   cg_ctx* ctx;
@@ -607,6 +614,7 @@ void batch_free(cg_ctx* ctx, cg_batch* b) {
   if (b->arena_job) {  // (a call that ended before launch_verify joined the arena copy)
     b->arena_job->wait();
     (void)hipStreamSynchronize(ctx->hash_stream);
+    give_back_events(ctx, b->arena_job->span[0], b->arena_job->span[1]);
   }
   if (b->verdict_owned) dfree(ctx, b->verdict);
   dfree(ctx, b->bitmap);
@@ -1508,6 +1516,7 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = 
         if (b->arena_job) {  // (never with split pieces: cg_plan.h's static_assert; kept safe anyway)
           b->arena_job->wait();
           const hipError_t e2 = b->arena_job->err;
+          give_back_events(ctx, b->arena_job->span[0], b->arena_job->span[1]);
           b->arena_job.reset();
           CG_TRY(ctx, e2, "upload arena");
           CG_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_arena, 0), "wait arena");
@@ -1606,9 +1615,11 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = 
           if (b->arena_job) {  // issued by the upload thread: the hash kernel waits for ev_arena
             b->arena_job->wait();
             const hipError_t e2 = b->arena_job->err;
-            if (b->arena_job->span[0] && b->arena_job->span[1]) {
+            if (e2 == hipSuccess && b->arena_job->span[0] && b->arena_job->span[1]) {
               ctx->pending.push_back({"h2d_arena", {b->arena_job->span[0], b->arena_job->span[1]}});
               ctx->stats["h2d_arena"].items += b->arena_job->bytes;
+            } else {
+              give_back_events(ctx, b->arena_job->span[0], b->arena_job->span[1]);
             }
             b->arena_job.reset();
             CG_TRY(ctx, e2, "upload arena");
@@ -2025,7 +2036,8 @@ cg_status verify_pipeline(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
     if (cst != CG_OK) return cst;
     hipEvent_t a = ctx->profiling ? take_event(ctx) : nullptr, b = ctx->profiling ? take_event(ctx) : nullptr;
     const hipError_t e = issue_chunk(k, a, b);
-    chunk_span(k, a, b);
+    if (e == hipSuccess) chunk_span(k, a, b);
+    else give_back_events(ctx, a, b);
     return e == hipSuccess ? CG_OK : hip_fail(ctx, e, "upload chunk");
   };
   // Asynchronous copies (pinned or staged) run one chunk ahead of the kernels, so the
@@ -2063,10 +2075,14 @@ cg_status verify_pipeline(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
       started = false;
     }
   } up;
-  struct UploaderJoin {
+  struct UploaderJoin {  // on every exit: the job joined; span events not handed to chunk_span go back
     Uploader& u;
-    ~UploaderJoin() { u.finish(); }
-  } up_join{up};
+    cg_ctx* c;
+    ~UploaderJoin() {
+      u.finish();
+      for (auto& sp : u.spans) give_back_events(c, sp.first, sp.second);
+    }
+  } up_join{up, ctx};
   auto upload_through = [&](size_t k) -> cg_status {  // enqueue copies of chunks < min(k, K)
     for (; uploaded < std::min(k, K); ++uploaded) {
       if (!thread_up) {
@@ -2223,6 +2239,7 @@ cg_status verify_pipeline(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
   if (up.started) {  // (every chunk is issued by now)
     up.finish();
     for (size_t k = 0; k < up.spans.size(); ++k) chunk_span(k, up.spans[k].first, up.spans[k].second);
+    up.spans.clear();
   }
   return CG_OK;
 }

@@ -100,12 +100,16 @@ __global__ __launch_bounds__(256) CG_HASH_ATTR void cg_ed25519_hash(const uint32
   CG_WAVE_PRIO(CG_HASH_PRIO);
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  uint32_t pkw[8], sw[16], dig[kDigitWords], ndig, rneg;
+  uint32_t pkw[8], rw[8], dig[kDigitWords], ndig, rneg;
   CG_UNROLL for (int w = 0; w < 8; ++w) pkw[w] = pk[(size_t)w * cap + i];
-  CG_UNROLL for (int w = 0; w < 16; ++w) sw[w] = sig[(size_t)w * cap + i];
+  CG_UNROLL for (int w = 0; w < 8; ++w) rw[w] = sig[(size_t)w * cap + i];
   const bool force_full = full_mod != 0 && (index_base + i) % full_mod == 0;  // cg_set_debug test hook
-  const uint32_t pre = ed25519_hash_stage<false, REUSE>(pkw, sw, sig_len[i], arena + msg_off[i], msg_len[i], mode, dig,
-                                                       ndig, rneg, force_full);
+  // S (signature words 8..15) is loaded after the half-size reduction (ed25519_hash_stage_r)
+  const uint32_t pre = ed25519_hash_stage_r<false, REUSE>(
+      pkw, rw, [&](uint32_t sw[8]) CG_LINLINE {
+        CG_UNROLL for (int w = 0; w < 8; ++w) sw[w] = sig[(size_t)(8 + w) * cap + i];
+      },
+      sig_len[i], arena + msg_off[i], msg_len[i], mode, dig, ndig, rneg, force_full);
   status[i] = pre | ndig << 8 | rneg << 16;
   if (pre != V_COMPUTE) return;
   CG_UNROLL for (int w = 0; w < kDigitWords; ++w) digits[(size_t)w * scap + i] = dig[w];

@@ -87,6 +87,32 @@ def test_scalar_ops(host):
         assert sum((((pk >> (4 * i)) & 15) - 8) * 16**i for i in range(64)) == k
 
 
+def test_slide_drop_automaton_vs_i2p_slide(host):
+    """slide_drops_carry (cg_sc25519.h, round 6: a 6-state automaton over the original bits)
+    against the Python twin's slide() on scalars with bit 255 set (the only ones that can
+    drop a carry): random, long top runs of ones, runs ending at every bit near the top,
+    and sparse / dense patterns."""
+    rnd = random.Random(17)
+    cases = [rnd.getrandbits(256) | 1 << 255 for _ in range(6000)]
+    for top in range(240, 256):  # ones from `top` to 255, random below, a zero at top - 1
+        for _ in range(40):
+            lo = rnd.getrandbits(top - 1) if top > 1 else 0
+            cases.append(((2**256 - 1) >> top << top) | lo)
+    for q in range(200):
+        dense = 2**256 - 1
+        for _ in range(rnd.randrange(1, 12)):
+            dense &= ~(1 << rnd.randrange(256))
+        cases.append(dense | 1 << 255)
+        cases.append(sum(1 << rnd.randrange(256) for _ in range(rnd.randrange(1, 40))) | 1 << 255)
+    drops = 0
+    for s in cases:
+        sv = ED.slide_value(s.to_bytes(32, "little"))
+        got = bool(host.cgh_slide_drop(w8(s)))
+        assert got == (sv != s), hex(s)
+        drops += got
+    assert 0 < drops < len(cases)
+
+
 def test_sha512_alignment(host):
     rnd = random.Random(3)
     buf = rnd.randbytes(1500)

@@ -71,6 +71,10 @@ def main():
     ap.add_argument("--bench-layout", action="store_true",
                     help="the driver bench line's layout: 1 %% adversarial (E1-E12), ragged E12 rows with sig_len, "
                          "signature stride 68 (bench.py e2e_record_32b / latency)")
+    ap.add_argument("--adversarial", type=float, default=None, help="with --bench-layout: this fraction instead of 1 %%")
+    ap.add_argument("--adv-classes", default=None, help="with --bench-layout: keep only these classes mutated "
+                                                        "(comma-separated, e.g. E12); the other mutated rows are re-signed valid")
+    ap.add_argument("--force-ragged", action="store_true", help="sig_len array and stride 68 even if every row is 64 B")
     a = ap.parse_args()
     if a.spans:
         import tempfile
@@ -83,14 +87,27 @@ def main():
     sizes = [int(x) for x in a.sizes.split(",")]
     w = datagen.make_batch(max(sizes), msg_bytes=a.msg_bytes, seed=42, key_base=0, ref_seed_stride=4096)
     if a.bench_layout:
-        w = datagen.add_ed25519_adversarial(w, frac=0.01, seed=77)
+        clean = datagen.make_batch(max(sizes), msg_bytes=a.msg_bytes, seed=42, key_base=0, ref_seed_stride=4096) \
+            if a.adv_classes else None
+        w = datagen.add_ed25519_adversarial(w, frac=0.01 if a.adversarial is None else a.adversarial, seed=77)
+        if a.adv_classes:  # restore every mutated row outside the kept classes
+            keep = set(a.adv_classes.split(","))
+            for i, c in enumerate(w.classes):
+                if c != "valid" and c not in keep:
+                    w.pk[i], w.sig[i], w.sig_len[i] = clean.pk[i], clean.sig[i], clean.sig_len[i]
+                    o = int(w.msg_off[i])
+                    w.msg[o:o + a.msg_bytes] = clean.msg[o:o + a.msg_bytes]
+                    w.msg_len[i] = a.msg_bytes
+                    w.classes[i] = "valid"
     res = {"h2d_GBps": h2d_rates(), "runs": a.runs, "rows": []}
     with Context(0) as ctx:
         for n in sizes:
             s = w.subset(np.arange(n))
             sl = s.sig_len[:n].astype(np.uint32)
-            ragged = a.bench_layout and bool((sl != 64).any())
+            ragged = (a.bench_layout and bool((sl != 64).any())) or a.force_ragged
             ss = max(64, (int(sl.max()) + 3) // 4 * 4) if ragged else 64
+            if a.force_ragged:
+                ss = max(ss, 68)
             sg = np.zeros((n, ss), dtype=np.uint8)
             sg[:, :min(ss, s.sig_stride)] = s.sig[:n, :min(ss, s.sig_stride)]
             b = crypto.PackedBatch(s.n, None, np.ascontiguousarray(s.pk[:, :32]), 32, sg, ss,
