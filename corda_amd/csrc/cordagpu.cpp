@@ -1510,8 +1510,18 @@ cg_status launch_verify(cg_ctx* ctx, cg_batch* b, int mode, bool join_streams = 
         split = std::min<uint32_t>(split, b->n_ed / kEdSplitMin);
       }
       hipStream_t ed_lane[2] = {ctx->stream, ctx->hash_stream};
-      // prepared-batch verify (this call owns the streams): points beside hash on the idle copy stream
-      hipStream_t pts = pts_stream ? pts_stream : (join_streams && ed_overlap_enabled(ctx) ? ctx->copy_stream : nullptr);
+      // Points kernel beside the hash kernel on the idle copy stream (this call owns the
+      // streams) when the call still waits on host copies — a one-chunk host-buffer call:
+      // the points kernel reads the raw rows while the arena goes up.  A resident batch runs
+      // it after the hash kernel: side by side the two VALU-bound kernels took longer than
+      // one after the other once the hash kernel stopped spilling (r06i, config 2: 99.7 ->
+      // 100.9 M/s over three interleaved pairs).  CORDA_AMD_ED_OVERLAP=0: never beside, 2:
+      // always (the round-5 plan).
+      const int overlap = ctx->opts.i(cg::OPT_ED_OVERLAP, 1);
+      const bool copies_pending = b->rows_event || b->points_early || b->arena_pending || b->arena_job;
+      hipStream_t pts = pts_stream ? pts_stream
+                                   : (join_streams && (overlap >= 2 || (overlap == 1 && copies_pending)) ? ctx->copy_stream
+                                                                                                         : nullptr);
       if (split > 1) {
         if (b->arena_job) {  // (never with split pieces: cg_plan.h's static_assert; kept safe anyway)
           b->arena_job->wait();

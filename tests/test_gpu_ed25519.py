@@ -477,11 +477,13 @@ def test_compact_ed25519_layout_vs_oracle(gpu_ctx, oracle, knobs, chunks):
         assert np.array_equal(got, exp), np.flatnonzero(got != exp)[:10]
 
 
-@pytest.mark.parametrize("split,overlap,signers", [("2", "1", 0), ("3", "0", 0), ("2", "1", 40)])
+@pytest.mark.parametrize("split,overlap,signers", [("2", "1", 0), ("3", "0", 0), ("2", "2", 40), ("1", "2", 0),
+                                                   ("1", "1", 0)])
 def test_prepared_batch_split_and_overlap_vs_oracle(gpu_ctx, oracle, knobs, split, overlap, signers):
     """cg_batch_verify's scheduling variants on one prepared batch: the Ed25519 subset as
     index pieces on two streams (CORDA_AMD_ED_SPLIT, pieces >= 65,536), the points kernel
-    beside the hash kernel or after it (CORDA_AMD_ED_OVERLAP), distinct signers and 40
+    after the hash kernel (CORDA_AMD_ED_OVERLAP 0, and 1 — the default — for a resident
+    batch) or beside it (2), distinct signers and 40
     repeated ones (the key-reuse path: both lanes wait for the per-key tables) — verdicts
     and accept bitmap identical to the oracle's, verified twice."""
     knobs.setenv("CORDA_AMD_ED_SPLIT", split)
