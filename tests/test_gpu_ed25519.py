@@ -704,6 +704,38 @@ def test_pipeline_errors_then_recovery(gpu_ctx, oracle, knobs, upload_thread):
         assert np.array_equal(crypto.verify_packed(gpu_ctx, good, MODE_IS_VALID), exp), k
 
 
+@pytest.mark.parametrize("n,msg_bytes", [(32_767, 32), (32_768, 32), (65_536, 32), (40_000, 1024), (262_144, 32)])
+def test_host_verify_arena_bounds_beside_row_copies(gpu_ctx, oracle, n, msg_bytes):
+    """One-chunk Ed25519-only host calls from 32,768 elements check msg_off / msg_len against
+    the arena on the upload thread while the rows go up and the points kernels run
+    (create_batch's BoundsBeside): an element outside the arena — first, middle or last,
+    offset past the end or length over it — still returns CG_E_INVALID_ARGUMENT naming that
+    element (as the synchronous check below 32,768 does), and the same context then
+    verifies the intact batch against the oracle."""
+    from corda_amd._lib import CordaGpuError
+    w = datagen.add_ed25519_adversarial(datagen.make_batch(n, msg_bytes=msg_bytes, seed=n % 997 + 3,
+                                                           key_base=3_400_000 + n % 7919), frac=0.02, seed=31)
+    sl = w.sig_len[:n].astype(np.uint32)
+    ss = max(64, (int(sl.max()) + 3) // 4 * 4)
+    sg = np.zeros((n, ss), dtype=np.uint8)
+    sg[:, :min(ss, w.sig_stride)] = w.sig[:n, :min(ss, w.sig_stride)]
+    mk = lambda off, ln: crypto.PackedBatch(n, None, np.ascontiguousarray(w.pk[:n, :32]), 32, sg, ss, sl, w.msg,
+                                            off, ln)
+    off0, len0 = w.msg_off[:n].astype(np.uint64), w.msg_len[:n].astype(np.uint32)
+    exp = oracle_verdicts(oracle, w, MODE_IS_VALID)
+    for i, kind in ((0, "off"), (n // 2, "len"), (n - 1, "off")):
+        off, ln = off0.copy(), len0.copy()
+        if kind == "off":
+            off[i] = np.uint64(len(w.msg) + 1)
+        else:
+            ln[i] = np.uint32(len(w.msg) - int(off[i]) + 1)
+        with pytest.raises(CordaGpuError, match=f"element {i}$"):
+            crypto.verify_packed(gpu_ctx, mk(off, ln), MODE_IS_VALID)
+        got = crypto.verify_packed(gpu_ctx, mk(off0, len0), MODE_IS_VALID)
+        bad = np.flatnonzero(got != exp)
+        assert bad.size == 0, (i, [(w.classes[j], int(got[j]), int(exp[j])) for j in bad[:10]])
+
+
 @pytest.mark.parametrize("n,msg_bytes", [(1, 32), (63, 1024), (65, 32), (257, 1024), (20_480, 32), (20_481, 32),
                                          (32_768, 1024), (32_769, 1024), (40_001, 32), (65_537, 32),
                                          (131_073, 32), (131_073, 1024), (262_145, 1024), ((1 << 20) + 1, 32)])
