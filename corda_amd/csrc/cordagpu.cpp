@@ -1038,6 +1038,21 @@ cg_status ensure_key_scratch(cg_ctx* ctx, uint32_t n_keys) {
   return CG_OK;
 }
 
+// A scheme array that names Ed25519 for every element is the batch scheme_id NULL
+// describes (include/cordagpu.h): one vectorised pass (~n / 16 ns) lets such a call take
+// the Ed25519-only host path — no per-element partition and checks (~3 ns per element:
+// 0.2 ms at 65,536), the arena bounds beside the row copies.  Returns the array to use.
+const uint8_t* ed25519_only(const uint8_t* scheme_id, size_t n) {
+  if (!scheme_id) return nullptr;
+  for (size_t i = 0; i < n; i += 4096) {  // (blocks: a mixed batch usually stops at the first)
+    const size_t e = std::min(n, i + 4096);
+    uint8_t acc = 0;
+    for (size_t j = i; j < e; ++j) acc |= (uint8_t)(scheme_id[j] ^ CG_SCHEME_EDDSA_ED25519_SHA512);
+    if (acc) return scheme_id;
+  }
+  return nullptr;
+}
+
 // create_batch's arena-bounds pass on the upload thread (see there).  Every exit of
 // create_batch waits for a posted pass (the job reads the caller's arrays and this object).
 constexpr size_t kBoundsBesideMin = 32768;  // below: ~18 us of pass, less than the thread hand-off saves
@@ -2324,6 +2339,7 @@ cg_status cg_batch_create(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const
                           const uint8_t* sig, size_t sig_stride, const uint32_t* sig_len, const uint8_t* msg,
                           size_t msg_bytes, const uint64_t* msg_off, const uint32_t* msg_len, cg_batch** out) {
   CG_API_BEGIN
+  scheme_id = ed25519_only(scheme_id, n);
   MsgSrc m;
   m.host = msg;
   m.bytes = msg_bytes;
@@ -2378,6 +2394,7 @@ cg_status cg_verify_batch(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
   if (n == 0) return CG_OK;
   if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, CG_E_DEVICE, "hipSetDevice");
   begin_call_span(ctx);
+  scheme_id = ed25519_only(scheme_id, n);
   struct CallSpanEnd {  // an early error return drops the span
     cg_ctx* c;
     ~CallSpanEnd() {

@@ -736,6 +736,33 @@ def test_host_verify_arena_bounds_beside_row_copies(gpu_ctx, oracle, n, msg_byte
         assert bad.size == 0, (i, [(w.classes[j], int(got[j]), int(exp[j])) for j in bad[:10]])
 
 
+@pytest.mark.parametrize("n", [4096, 65_536])
+def test_all_ed25519_scheme_array_equals_null(gpu_ctx, oracle, n):
+    """A scheme array naming Ed25519 for every element takes the scheme_id = NULL host path
+    (cordagpu.cpp ed25519_only); the verdicts equal the oracle's with the array, without it,
+    and with one element flagged CG_SCHEME_FLAG_KEY_INVALID (which keeps the per-element
+    path: that element KEY_INVALID, the rest unchanged); an out-of-arena message is the same
+    error either way."""
+    from corda_amd._lib import CordaGpuError
+    w = datagen.add_ed25519_adversarial(datagen.make_batch(n, msg_bytes=1024, seed=n % 991 + 7,
+                                                           key_base=3_700_000 + n % 7919), frac=0.02, seed=37)
+    exp = oracle_verdicts(oracle, w, MODE_IS_VALID)
+    mk = lambda sch, off=None: crypto.PackedBatch(n, sch, w.pk, w.pk_stride, w.sig, w.sig_stride, w.sig_len, w.msg,
+                                                  w.msg_off if off is None else off, w.msg_len)
+    assert np.array_equal(crypto.verify_packed(gpu_ctx, mk(w.scheme), MODE_IS_VALID), exp)
+    assert np.array_equal(crypto.verify_packed(gpu_ctx, mk(None), MODE_IS_VALID), exp)
+    flagged = w.scheme.copy()
+    flagged[n // 3] |= 0x80  # CG_SCHEME_FLAG_KEY_INVALID
+    want = exp.copy()
+    want[n // 3] = 3  # CG_KEY_INVALID
+    assert np.array_equal(crypto.verify_packed(gpu_ctx, mk(flagged), MODE_IS_VALID), want)
+    off = w.msg_off.astype(np.uint64).copy()
+    off[n - 2] = np.uint64(len(w.msg) + 5)
+    for sch in (w.scheme, None):
+        with pytest.raises(CordaGpuError, match=f"element {n - 2}$"):
+            crypto.verify_packed(gpu_ctx, mk(sch, off), MODE_IS_VALID)
+
+
 @pytest.mark.parametrize("n,msg_bytes", [(1, 32), (63, 1024), (65, 32), (257, 1024), (20_480, 32), (20_481, 32),
                                          (32_768, 1024), (32_769, 1024), (40_001, 32), (65_537, 32),
                                          (131_073, 32), (131_073, 1024), (262_145, 1024), ((1 << 20) + 1, 32)])
