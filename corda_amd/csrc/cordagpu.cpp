@@ -1903,6 +1903,13 @@ cg_status download_verdicts(cg_ctx* ctx, uint8_t* verdict_out, const uint8_t* ve
 // A chunk's per-element arrays inside VerifyRun::rows (and inside its ring slot, after
 // the arena piece, in the same layout): msg_off, msg_len, key rows, signature rows,
 // signature lengths, each 256-byte aligned.
+// CG_ROWS_FIRST (pageable pipeline calls): the row arrays (offsets, lengths, keys,
+// signatures, signature lengths) live whole-call on the device, chunk 0's slices go up
+// with chunk 0 and every later chunk's in one copy per array with chunk 1; chunks 2.. send
+// only their arena piece.  Per chunk they were five or six more pageable copies each.
+#ifndef CG_ROWS_FIRST
+#define CG_ROWS_FIRST 1
+#endif
 struct ChunkRows {
   size_t off, len, pk, sig, sl, bytes;  // byte offsets from the chunk's base; total size
   ChunkRows(size_t cnt, size_t pk_stride, size_t sig_stride, bool has_sl) {
@@ -2020,6 +2027,21 @@ cg_status verify_pipeline(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
     ring = ctx->ring_cap >= slot;
   }
   const bool one_dma = ctx->opts.on(cg::OPT_VERIFY_ONE_DMA, true);
+  // whole-call row arrays (CG_ROWS_FIRST; the ring stages each chunk's rows in its layout)
+  const bool soa = CG_ROWS_FIRST && !ring && K > 1;
+  const ChunkRows all_rows(n, pk_stride, sig_stride, sig_len);  // (fits: <= rows_at[K], one pad per array)
+  struct RowPtrs {
+    uint8_t *off, *len, *pk, *sig, *sl;
+  };
+  auto row_ptrs = [&](size_t k) -> RowPtrs {  // chunk k's rows on the device
+    const size_t lo = cb[k];
+    if (soa)
+      return {r.rows + all_rows.off + lo * 8, r.rows + all_rows.len + lo * 4, r.rows + all_rows.pk + lo * pk_stride,
+              r.rows + all_rows.sig + lo * sig_stride, r.rows + all_rows.sl + lo * 4};
+    const ChunkRows cr(cb[k + 1] - lo, pk_stride, sig_stride, sig_len);
+    uint8_t* const rb = r.rows + rows_at[k];
+    return {rb + cr.off, rb + cr.len, rb + cr.pk, rb + cr.sig, rb + cr.sl};
+  };
   // staging slice size (ring only); CORDA_AMD_VERIFY_SLICE_KB overrides (0: whole chunks)
   size_t slice_bytes = (size_t)12 << 20;
   if (ctx->opts.has(cg::OPT_VERIFY_SLICE_KB)) slice_bytes = (size_t)std::max(0, ctx->opts.i(cg::OPT_VERIFY_SLICE_KB, 0)) << 10;
@@ -2037,16 +2059,18 @@ cg_status verify_pipeline(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
   };
   // (device destination, host source, bytes) of chunk k: its arena piece and rows
   auto chunk_pieces = [&](size_t k) {
-    const size_t lo = cb[k], hi = cb[k + 1];
-    const ChunkRows cr(hi - lo, pk_stride, sig_stride, sig_len);
-    uint8_t* const rb = r.rows + rows_at[k];
-    std::vector<CopyPool::Piece> pieces = {
-        {r.arena + aend[k], msg + aend[k], (size_t)(aend[k + 1] - aend[k])},
-        {rb + cr.off, msg_off + lo, (hi - lo) * 8},
-        {rb + cr.len, msg_len + lo, (hi - lo) * 4},
-        {rb + cr.pk, pk + lo * pk_stride, (hi - lo) * pk_stride},
-        {rb + cr.sig, sig + lo * sig_stride, (hi - lo) * sig_stride}};
-    if (sig_len) pieces.push_back({rb + cr.sl, sig_len + lo, (hi - lo) * 4});
+    size_t lo = cb[k], hi = cb[k + 1];
+    std::vector<CopyPool::Piece> pieces = {{r.arena + aend[k], msg + aend[k], (size_t)(aend[k + 1] - aend[k])}};
+    if (soa) {  // chunk 0: its own rows; chunk 1: every later chunk's; the rest: none
+      if (k > 1) return pieces;
+      if (k == 1) hi = n;
+    }
+    const RowPtrs rp = row_ptrs(k);
+    pieces.push_back({rp.off, msg_off + lo, (hi - lo) * 8});
+    pieces.push_back({rp.len, msg_len + lo, (hi - lo) * 4});
+    pieces.push_back({rp.pk, pk + lo * pk_stride, (hi - lo) * pk_stride});
+    pieces.push_back({rp.sig, sig + lo * sig_stride, (hi - lo) * sig_stride});
+    if (sig_len) pieces.push_back({rp.sl, sig_len + lo, (hi - lo) * 4});
     return pieces;
   };
   // Issues chunk k's copies on the copy stream and records ev[k] (and the profiling span
@@ -2294,13 +2318,12 @@ cg_status verify_pipeline(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
     MsgSrc m;
     m.dev = r.arena;
     m.bytes = msg_bytes;
-    const ChunkRows cr(hi - lo, pk_stride, sig_stride, sig_len);
-    uint8_t* const rb = r.rows + rows_at[k];
-    m.off_dev = reinterpret_cast<uint64_t*>(rb + cr.off);
-    m.len_dev = reinterpret_cast<uint32_t*>(rb + cr.len);
-    m.pk_dev = rb + cr.pk;
-    m.sig_dev = rb + cr.sig;
-    m.sl_dev = sig_len ? reinterpret_cast<const uint32_t*>(rb + cr.sl) : nullptr;
+    const RowPtrs rp = row_ptrs(k);
+    m.off_dev = reinterpret_cast<uint64_t*>(rp.off);
+    m.len_dev = reinterpret_cast<uint32_t*>(rp.len);
+    m.pk_dev = rp.pk;
+    m.sig_dev = rp.sig;
+    m.sl_dev = sig_len ? reinterpret_cast<const uint32_t*>(rp.sl) : nullptr;
     m.raw_ready = r.ev[k];
     m.verdict_dev = r.verdict + lo;
     m.async = true;
