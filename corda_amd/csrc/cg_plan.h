@@ -58,6 +58,12 @@ constexpr uint32_t kEarlyPartMin = 65536;
 // parts it would slow (r05x: 65,536 x 1 KB 2.19 -> 2.11 ms, 16,384 x 1 KB 0.79 -> 0.77;
 // but 4,096 x 1 KB 0.47 -> 0.56, the thread hand-off, and 2^17-2^18 x 32 B +0.05-0.15).
 constexpr size_t kAsyncArenaMin = (size_t)8 << 20;
+// From kBoundsBesideMin elements the arena-bounds pass runs on the upload thread
+// (cordagpu.cpp BoundsBeside), so the thread is awake and an arena from 1 MB goes up from
+// it too, with no hand-off wait (r06v, 32 B ids: 40,001 0.857 -> 0.83 ms, 65,536 0.945 ->
+// 0.90; 100,000 equal).
+constexpr size_t kBoundsBesideMin = 32768;
+constexpr size_t kAsyncArenaSmallMin = (size_t)1 << 20;
 // The async arena's copies run on hash_stream from the upload thread with no wait on the
 // split pieces' fork: it must never coexist with a split (> 1 piece) prepared batch, which
 // needs at least 2 * kEdSplitMin Ed25519 elements (advisor r05).
@@ -301,7 +307,9 @@ inline VerifyPlan plan_verify(const VerifyShape& s, const Options& o) {
   const int forced = key_reuse_forced(o);
   p.defer_arena = s.msg_bytes && !s.ecdsa && s.n_ed;
   p.defer_meta = p.defer_arena && s.ed_in_order;
-  p.async_arena = p.defer_arena && s.msg_bytes >= kAsyncArenaMin && s.n < 2 * (size_t)kEarlyPartMin &&
+  p.async_arena = p.defer_arena &&
+                  (s.msg_bytes >= kAsyncArenaMin || (s.msg_bytes >= kAsyncArenaSmallMin && s.n >= kBoundsBesideMin)) &&
+                  s.n < 2 * (size_t)kEarlyPartMin &&
                   async_arena_enabled(o) && !o.has(OPT_ED_SPLIT);
   p.rows_direct = s.ed_in_order && s.pk_stride % 4 == 0 && s.sig_stride % 4 == 0;
   if (p.rows_direct && s.n > pair_max && s.n <= kEdChunk && ed_overlap_enabled(o) && !o.has(OPT_ED_SPLIT)) {

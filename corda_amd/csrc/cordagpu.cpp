@@ -1055,7 +1055,6 @@ const uint8_t* ed25519_only(const uint8_t* scheme_id, size_t n) {
 
 // create_batch's arena-bounds pass on the upload thread (see there).  Every exit of
 // create_batch waits for a posted pass (the job reads the caller's arrays and this object).
-constexpr size_t kBoundsBesideMin = 32768;  // below: ~18 us of pass, less than the thread hand-off saves
 struct BoundsBeside {
   std::mutex m;
   std::condition_variable cv;
@@ -1094,7 +1093,8 @@ cg_status create_batch(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const ui
                        cg_batch** out) {
   if (!out) return fail(ctx, CG_E_INVALID_ARGUMENT, "null out");
   *out = nullptr;
-  // A one-chunk host call of Ed25519 rows (no scheme ids, n >= kBoundsBesideMin): the
+  // A one-chunk host call of Ed25519 rows (no scheme ids, n >= cg::kBoundsBesideMin: below it
+// the pass is ~18 us, less than the thread hand-off would save): the
   // arena-bounds pass over msg_off / msg_len (~0.55 ns per element: 0.15 ms at 2^18, all of
   // it before the first copy) runs on the upload thread while this thread copies the rows
   // and launches the points kernels, which read no message.  The batch is handed out only
@@ -1102,7 +1102,7 @@ cg_status create_batch(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const ui
   // launched later, by launch_verify); a failure returns the same status and message as the
   // synchronous check, after draining what was launched.
   BoundsBeside beside;
-  const bool bounds_beside = !scheme_id && m.keep_raw && !m.dev && m.off_host && m.len_host && n >= kBoundsBesideMin;
+  const bool bounds_beside = !scheme_id && m.keep_raw && !m.dev && m.off_host && m.len_host && n >= cg::kBoundsBesideMin;
   cg_status st = check_inputs(ctx, n, scheme_id, pk, pk_stride, sig, sig_stride, sig_len, m, !bounds_beside);
   if (st != CG_OK) return st;
   if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, CG_E_DEVICE, "hipSetDevice");

@@ -66,11 +66,14 @@ CASES = [
     ((32768, 1024), dict(ONE, copy_bound=1, lanes=4, split_points=0, async_arena=1, grouped_msm=0)),
     ((32769, 1024), dict(ONE, copy_bound=1, lanes=1, split_points=1, async_arena=1, grouped_msm=1)),
     ((40000, 32), dict(ONE, lanes=1, split_points=1)),
-    ((40001, 32), dict(ONE, lanes=1, split_points=1, async_arena=0, grouped_msm=1)),
+    ((40001, 32), dict(ONE, lanes=1, split_points=1, async_arena=1, grouped_msm=1)),
+    # an arena from 1 MB goes up from the upload thread once the bounds pass runs there (n >= 32,768)
+    ((32767, 32), dict(ONE, lanes=1, async_arena=0)),
+    ((32768, 32), dict(ONE, lanes=1, async_arena=1)),
     # the early-points part size (65,536): one part is split points, two parts early points
-    ((65536, 32), dict(ONE, lanes=1, early_parts=1, split_points=1)),
+    ((65536, 32), dict(ONE, lanes=1, early_parts=1, split_points=1, async_arena=1)),
     ((65537, 32), dict(ONE, lanes=1, early_parts=1, split_points=1)),
-    ((131071, 32), dict(ONE, lanes=1, early_parts=1, split_points=1, async_arena=0)),
+    ((131071, 32), dict(ONE, lanes=1, early_parts=1, split_points=1, async_arena=1)),
     ((131073, 32), dict(ONE, lanes=1, early_parts=2, split_points=0, async_arena=0)),
     # copy-bound calls from 2^17 run the chunked pipeline
     ((131071, 1024), dict(ONE, copy_bound=1, lanes=1, early_parts=1, split_points=1, async_arena=1)),
