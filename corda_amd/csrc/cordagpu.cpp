@@ -671,6 +671,7 @@ struct MsgSrc {
   // after the call's final sync) instead of a host sync at the end of staging
   bool keep_raw = false;
   uint32_t pair_max = 0;  // the batch's latency-mode threshold (0: kEdPairMaxDefault)
+  size_t index_base = 0;  // the batch's first element in the caller's (a pipeline chunk): error messages
 };
 
 // First element whose message lies outside an arena of `bytes` bytes, or n: a
@@ -688,9 +689,11 @@ std::string out_of_arena_message(size_t i) { return "message out of arena bounds
 
 // arena_bounds = false: the caller runs the all-Ed25519 arena-bounds pass itself (create_batch's
 // BoundsBeside, on the upload thread beside the row copies)
+// index_base: the first element's index in the caller's batch (a pipeline chunk), so an
+// error names the caller's element.
 cg_status check_inputs(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const uint8_t* pk, size_t pk_stride,
                        const uint8_t* sig, size_t sig_stride, const uint32_t* sig_len, const MsgSrc& m,
-                       bool arena_bounds = true) {
+                       bool arena_bounds = true, size_t index_base = 0) {
   if (!ctx) return CG_E_INVALID_ARGUMENT;
   if (n > 0xFFFFFFF0ull) return fail(ctx, CG_E_INVALID_ARGUMENT, "batch larger than 2^32 - 16 elements");
   if (n == 0) return CG_OK;
@@ -701,7 +704,7 @@ cg_status check_inputs(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const ui
   if (!scheme_id) {  // all Ed25519: only the arena bounds
     if (m.off_host && arena_bounds) {
       const size_t i = first_out_of_arena(m.off_host, m.len_host, n, m.bytes);
-      if (i < n) return fail(ctx, CG_E_INVALID_ARGUMENT, out_of_arena_message(i));
+      if (i < n) return fail(ctx, CG_E_INVALID_ARGUMENT, out_of_arena_message(index_base + i));
     }
     if (pk_stride < 32 || sig_stride < 64)
       return fail(ctx, CG_E_INVALID_ARGUMENT, "Ed25519 needs pk_stride >= 32 and sig_stride >= 64");
@@ -711,14 +714,15 @@ cg_status check_inputs(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const ui
     const uint8_t s = scheme_id[i];
     // off > bytes || len > bytes - off: the sum off + len could wrap for a huge off
     if (m.off_host && (m.off_host[i] > m.bytes || m.len_host[i] > m.bytes - m.off_host[i]))
-      return fail(ctx, CG_E_INVALID_ARGUMENT, out_of_arena_message(i));
+      return fail(ctx, CG_E_INVALID_ARGUMENT, out_of_arena_message(index_base + i));
     if (s & CG_SCHEME_FLAG_KEY_INVALID) continue;  // never read beyond its verdict
     if (s == CG_SCHEME_EDDSA_ED25519_SHA512) has_ed = true;
     if (s == CG_SCHEME_ECDSA_SECP256K1_SHA256 || s == CG_SCHEME_ECDSA_SECP256R1_SHA256) {
       has_ec = true;
       const uint32_t l = sig_len ? sig_len[i] : (uint32_t)sig_stride;
       if (l > sig_stride)
-        return fail(ctx, CG_E_INVALID_ARGUMENT, "ECDSA signature longer than sig_stride at element " + std::to_string(i));
+        return fail(ctx, CG_E_INVALID_ARGUMENT,
+                    "ECDSA signature longer than sig_stride at element " + std::to_string(index_base + i));
     }
   }
   if (has_ed && (pk_stride < 32 || sig_stride < 64))
@@ -1103,7 +1107,8 @@ cg_status create_batch(cg_ctx* ctx, size_t n, const uint8_t* scheme_id, const ui
   // synchronous check, after draining what was launched.
   BoundsBeside beside;
   const bool bounds_beside = !scheme_id && m.keep_raw && !m.dev && m.off_host && m.len_host && n >= cg::kBoundsBesideMin;
-  cg_status st = check_inputs(ctx, n, scheme_id, pk, pk_stride, sig, sig_stride, sig_len, m, !bounds_beside);
+  cg_status st = check_inputs(ctx, n, scheme_id, pk, pk_stride, sig, sig_stride, sig_len, m, !bounds_beside,
+                              m.index_base);
   if (st != CG_OK) return st;
   if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, CG_E_DEVICE, "hipSetDevice");
   if (bounds_beside && !beside.post(ctx, m.off_host, m.len_host, n, m.bytes)) {
@@ -2055,7 +2060,7 @@ cg_status verify_pipeline(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
     mc.off_host = msg_off + lo;
     mc.len_host = msg_len + lo;
     return check_inputs(ctx, hi - lo, scheme_id ? scheme_id + lo : nullptr, pk + lo * pk_stride, pk_stride,
-                        sig + lo * sig_stride, sig_stride, sig_len ? sig_len + lo : nullptr, mc);
+                        sig + lo * sig_stride, sig_stride, sig_len ? sig_len + lo : nullptr, mc, true, lo);
   };
   // (device destination, host source, bytes) of chunk k: its arena piece and rows
   auto chunk_pieces = [&](size_t k) {
@@ -2327,6 +2332,7 @@ cg_status verify_pipeline(cg_ctx* ctx, size_t n, int mode, const uint8_t* scheme
     m.raw_ready = r.ev[k];
     m.verdict_dev = r.verdict + lo;
     m.async = true;
+    m.index_base = lo;
     cg_batch* b = nullptr;
     st = create_batch(ctx, hi - lo, scheme_id ? scheme_id + lo : nullptr, pk + lo * pk_stride, pk_stride,
                       sig + lo * sig_stride, sig_stride, sig_len ? sig_len + lo : nullptr, m, &b);
@@ -2850,6 +2856,7 @@ cg_status tx_pipeline(cg_ctx* ctx, int mode, size_t n_tx, const uint8_t* arena, 
       m.raw_ready = ev[k];
       m.verdict_dev = verdict_d + s0;
       m.async = true;
+      m.index_base = s0;
       cg_batch* b = nullptr;
       st = create_batch(ctx, s1 - s0, scheme_id ? scheme_id + s0 : nullptr, pk + s0 * pk_stride, pk_stride,
                         sig + s0 * sig_stride, sig_stride, sig_len ? sig_len + s0 : nullptr, m, &b);
