@@ -571,7 +571,7 @@ def run_ed25519(args, dist):
         ks = kstats(ctx, ED_KERNELS + ED_REUSE_KERNELS + ED_AUX_KERNELS)
         ctx.set_profiling(False)
     split_note = ("kernels / roofline: 3 extra steps with the options CORDA_AMD_ED_SPLIT=1 CORDA_AMD_ED_OVERLAP=0 (each kernel "
-                  "alone over the whole batch); kernels_in_step: the timed steps' own spans (points beside hash)")
+                  "alone over the whole batch); kernels_in_step: the timed steps' own spans (a resident batch runs the points kernel after the hash kernel)")
 
     # verdict check (outside the timed region): untouched elements must accept
     verdict = pb.verify(MODE_IS_VALID)
