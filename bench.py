@@ -788,11 +788,12 @@ def config4_subrecord(args, dist, n_tx=1 << 20):
     tampered), host buffers in, per-tx first failing signature out — timed exactly as
     --workload tx times it, with its PCIe roofline (host-to-device bytes per step against
     the box's measured pinned copy rate) and CPU baseline (the C port's tx ids + per-
-    signature verify on a 32,768-tx sample, ids and first-bad indices compared)."""
+    signature verify on a 98,304-tx sample — ~20 s of CPU work on 16 threads — ids and
+    first-bad indices compared)."""
     sub = argparse.Namespace(**vars(args))
     sub.batch, sub.pool, sub.pool_set, sub.msg_bytes, sub.key_reuse = n_tx, 131072, False, None, 0
     sub.steps, sub.warmup = 5, 2
-    sub.no_cpu_baseline, sub.cpu_sample = args.no_cpu_baseline, 32768
+    sub.no_cpu_baseline, sub.cpu_sample = args.no_cpu_baseline, 98304
     return _subrecord(run_tx(sub, dist), sub)
 
 
