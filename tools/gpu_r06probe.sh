@@ -3,6 +3,6 @@
 set -o pipefail
 O=gpurun_out/r06probe
 mkdir -p $O
-AB_REPS=3 timeout -k 10 700 bash tools/ab_bench.sh new fake > $O/ab.log 2>&1 || exit 2
-mv gpurun_out/ab.txt $O/ab_fake_table.txt
+AB_REPS=3 timeout -k 10 700 bash tools/ab_bench.sh new ${AB_VARIANT:-fake} > $O/ab.log 2>&1 || exit 2
+mv gpurun_out/ab.txt $O/ab_${AB_VARIANT:-fake}_table.txt
 echo done
