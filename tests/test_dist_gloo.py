@@ -249,9 +249,10 @@ def _run_resilient(world, n, fail_ranks, fail_again=-1, fail_kind="gpu"):
     return [p.exitcode for p in procs], res
 
 
-@pytest.mark.parametrize("world,n,fail", [(3, 3000, (1,)), (3, 2017, (2,)), (3, 4096 + 33, (0, 2)), (2, 777, ())])
+@pytest.mark.parametrize("world,n,fail", [(3, 3000, (1,)), (3, 2017, (2,)), (3, 4096 + 33, (0, 2)), (2, 777, ()),
+                                         (8, 20_000 + 17, (3, 6))])
 def test_shard_failure_redistributes_to_survivors(world, n, fail):
-    """verify_sharded_resilient at world 3 (and 2) over gloo with one or two ranks whose
+    """verify_sharded_resilient at world 3 (and 2, and the driver's 8) over gloo with one or two ranks whose
     verify fails (the CordaGpuError a cg_batch_verify returning < 0 raises, as
     CG_DEBUG_FAIL_ALLOC injects on the GPU): each failed range is re-split over the
     survivors, the gathered bitmap equals the oracle's for the whole batch on EVERY rank,
