@@ -158,13 +158,23 @@ CG_DEV void store_slot(const LaneTab& lt, int p, int k, const ge_cached& c) {
   if (k == 0) return;
   store_cached(lt.entry(p * kSlotsPerPoint + k - 1), c);
 }
+// Lane-table entries are read through the global address space: the select between a
+// lane's entry and the shared identity entry left a generic pointer, and the MSM issued
+// flat loads (r06bb: global loads, msm 6.50-6.77 -> 6.41-6.54 ms, config 2 +1 %; the same
+// loads marked nontemporal measured 9 % slower).
+CG_DEV int4 gload(const int4* p, int q) {
+  typedef int v4i __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(1))) const v4i* gv4p;
+  const v4i t = ((gv4p)p)[q];
+  return make_int4(t.x, t.y, t.z, t.w);
+}
 CG_DEV void fetch_slot(const LaneTab& lt, int p, uint32_t k, RawEntry& r) {
   const int4* src = k ? lt.entry(p * kSlotsPerPoint + k - 1) : g_ident_entry;
-  CG_UNROLL for (int q = 0; q < kTabLimbs / 4; ++q) r.q[q] = src[q];
+  CG_UNROLL for (int q = 0; q < kTabLimbs / 4; ++q) r.q[q] = gload(src, q);
 }
 CG_DEV void load_entry(const int4* src, ge_cached& c) {
   RawEntry r;
-  CG_UNROLL for (int q = 0; q < kTabLimbs / 4; ++q) r.q[q] = src[q];
+  CG_UNROLL for (int q = 0; q < kTabLimbs / 4; ++q) r.q[q] = gload(src, q);
   unpack_entry(r, c);
 }
 CG_DEV void load_slot(const LaneTab& lt, int p, uint32_t k, ge_cached& c) {
